@@ -1,0 +1,527 @@
+// pybind11 bindings: torch tensors -> raw-pointer launchers of csrc/kernels/*.hip.
+//
+// Compiled by the host compiler against torch's headers; every op enqueues on the current HIP
+// stream of the calling thread (at::hip::getCurrentHIPStream) and allocates its outputs with the
+// torch caching allocator, so ops compose with torch streams and can be captured in a hipGraph.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPGuard.h>
+
+#include <vector>
+
+#include "pde_kernels.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+void check(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "pde native op '", what, "' failed: ", hipGetErrorString(e));
+}
+
+#define CHECK_DEV(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bf16")
+#define CHECK_F32(x) TORCH_CHECK((x).scalar_type() == at::kFloat, #x " must be fp32")
+#define CHECK_IN(x) \
+  CHECK_DEV(x);     \
+  CHECK_CONTIG(x)
+
+inline uint16_t* u16(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+inline const uint16_t* cu16(const optional<Tensor>& t) {
+  return t.has_value() && t->defined() ? reinterpret_cast<const uint16_t*>(t->data_ptr()) : nullptr;
+}
+inline const float* cf32(const optional<Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
+}
+inline float* f32(const optional<Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
+}
+
+pde::Operand dense(const Tensor& t, long ld_r, long ld_k) {
+  pde::Operand o{};
+  o.ptr = t.data_ptr();
+  o.kind = 0;
+  o.ld_r = ld_r;
+  o.ld_k = ld_k;
+  return o;
+}
+
+pde::Operand gather(const Tensor& t, int kind, int N, int H, int W, int C, int R, int S, int stride, int pad,
+                    int Ho, int Wo) {
+  pde::Operand o{};
+  o.ptr = t.data_ptr();
+  o.kind = kind;
+  o.g = pde::ConvGeom{N, H, W, C, R, S, stride, pad, Ho, Wo};
+  return o;
+}
+
+void run_gemm(pde::GemmArgs& a, const Tensor& like, int max_split) {
+  Tensor ws;
+  a.workspace = nullptr;
+  a.splitk = 1;
+  if (max_split > 1) {
+    ws = at::empty({static_cast<long>(max_split) * a.M * a.N}, like.options().dtype(at::kFloat));
+    a.workspace = ws.data_ptr<float>();
+    a.splitk = max_split;
+  }
+  check(pde::gemm_bf16(a, cur_stream()), "gemm");
+}
+
+// ------------------------------------------------------------------------------------------------
+// Dense GEMMs (nn.Linear)
+// ------------------------------------------------------------------------------------------------
+Tensor linear_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, bool relu, bool out_f32) {
+  CHECK_IN(x); CHECK_IN(w); CHECK_BF16(x); CHECK_BF16(w);
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "linear_fwd: shape mismatch");
+  Tensor out = at::empty({M, N}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  pde::GemmArgs a{};
+  a.M = M; a.N = N; a.K = K;
+  a.a = dense(x, K, 1);
+  a.b = dense(w, K, 1);
+  a.out = out.data_ptr(); a.ldo = N;
+  a.bias = cf32(bias);
+  a.nbias = a.bias ? static_cast<int>(bias->numel()) : 0;
+  a.epi = (a.bias ? pde::EPI_BIAS : 0) | (relu ? pde::EPI_RELU : 0) | (out_f32 ? pde::EPI_OUT_F32 : 0);
+  run_gemm(a, x, 1);
+  return out;
+}
+
+// dx[M,K] = dy[M,N] . w[N,K]  (optionally * (aux > 0): fused ReLU backward of the producer)
+Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const optional<Tensor>& aux) {
+  CHECK_IN(dy); CHECK_IN(w); CHECK_BF16(dy); CHECK_BF16(w);
+  const int M = dy.size(0), N = dy.size(1), K = w.size(1);
+  TORCH_CHECK(w.size(0) == N, "linear_dgrad: shape mismatch");
+  Tensor dx = at::empty({M, K}, dy.options());
+  pde::GemmArgs a{};
+  a.M = M; a.N = K; a.K = N;
+  a.a = dense(dy, N, 1);
+  a.b = dense(w, 1, K);
+  a.out = dx.data_ptr(); a.ldo = K;
+  a.aux = cu16(aux); a.ldaux = K;
+  a.epi = a.aux ? pde::EPI_DRELU : 0;
+  run_gemm(a, dy, 1);
+  return dx;
+}
+
+// dW[N,K] = dy[M,N]^T . x[M,K]   (fp32, split-K over the batch when the tile grid is small)
+Tensor linear_wgrad(const Tensor& dy, const Tensor& x) {
+  CHECK_IN(dy); CHECK_IN(x); CHECK_BF16(dy); CHECK_BF16(x);
+  const int M = dy.size(0), N = dy.size(1), K = x.size(1);
+  TORCH_CHECK(x.size(0) == M, "linear_wgrad: shape mismatch");
+  Tensor dw = at::empty({N, K}, dy.options().dtype(at::kFloat));
+  pde::GemmArgs a{};
+  a.M = N; a.N = K; a.K = M;
+  a.a = dense(dy, 1, N);
+  a.b = dense(x, 1, K);
+  a.out = dw.data_ptr(); a.ldo = K;
+  a.epi = pde::EPI_OUT_F32;
+  run_gemm(a, dy, M >= 1024 ? 16 : 1);
+  return dw;
+}
+
+// ------------------------------------------------------------------------------------------------
+// NHWC implicit-GEMM convolution
+// ------------------------------------------------------------------------------------------------
+Tensor conv_fwd(const Tensor& x, const Tensor& wf, const optional<Tensor>& bias, int R, int S, int stride, int pad,
+                bool relu, bool out_f32) {
+  CHECK_IN(x); CHECK_IN(wf); CHECK_BF16(x); CHECK_BF16(wf);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 8 == 0, "conv_fwd: input channels must be padded to a multiple of 8");
+  const int Co = wf.size(0);
+  TORCH_CHECK(wf.size(1) == R * S * C, "conv_fwd: weight must be [Co, R*S*C]");
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  Tensor y = at::empty({N, Ho, Wo, Co}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  pde::GemmArgs a{};
+  a.M = N * Ho * Wo; a.N = Co; a.K = R * S * C;
+  a.a = gather(x, 1, N, H, W, C, R, S, stride, pad, Ho, Wo);
+  a.b = dense(wf, a.K, 1);
+  a.out = y.data_ptr(); a.ldo = Co;
+  a.bias = cf32(bias);
+  a.nbias = a.bias ? static_cast<int>(bias->numel()) : 0;
+  a.epi = (a.bias ? pde::EPI_BIAS : 0) | (relu ? pde::EPI_RELU : 0) | (out_f32 ? pde::EPI_OUT_F32 : 0);
+  run_gemm(a, x, 1);
+  return y;
+}
+
+// dx[N,H,W,Ci] from dy[N,Ho,Wo,Co] and wd = [Ci, R*S*Co]
+Tensor conv_dgrad(const Tensor& dy, const Tensor& wd, int H, int W, int R, int S, int stride, int pad,
+                  const optional<Tensor>& aux) {
+  CHECK_IN(dy); CHECK_IN(wd); CHECK_BF16(dy); CHECK_BF16(wd);
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
+  TORCH_CHECK(Co % 8 == 0, "conv_dgrad: Cout must be a multiple of 8");
+  const int Ci = wd.size(0);
+  TORCH_CHECK(wd.size(1) == R * S * Co, "conv_dgrad: weight must be [Ci, R*S*Co]");
+  Tensor dx = at::empty({N, H, W, Ci}, dy.options());
+  pde::GemmArgs a{};
+  a.M = N * H * W; a.N = Ci; a.K = R * S * Co;
+  a.a = gather(dy, 3, N, Ho, Wo, Co, R, S, stride, pad, H, W);
+  a.b = dense(wd, a.K, 1);
+  a.out = dx.data_ptr(); a.ldo = Ci;
+  a.aux = cu16(aux); a.ldaux = Ci;
+  a.epi = a.aux ? pde::EPI_DRELU : 0;
+  run_gemm(a, dy, 1);
+  return dx;
+}
+
+// dW[Co, R*S*C] fp32 from dy[N,Ho,Wo,Co] and x[N,H,W,C]
+Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int R, int S, int stride, int pad) {
+  CHECK_IN(dy); CHECK_IN(x); CHECK_BF16(dy); CHECK_BF16(x);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
+  TORCH_CHECK(C % 8 == 0, "conv_wgrad: input channels must be a multiple of 8");
+  Tensor dw = at::empty({Co, R * S * C}, dy.options().dtype(at::kFloat));
+  pde::GemmArgs a{};
+  a.M = Co; a.N = R * S * C; a.K = N * Ho * Wo;
+  a.a = dense(dy, 1, Co);
+  a.b = gather(x, 2, N, H, W, C, R, S, stride, pad, Ho, Wo);
+  a.out = dw.data_ptr(); a.ldo = a.N;
+  a.epi = pde::EPI_OUT_F32;
+  run_gemm(a, dy, 16);
+  return dw;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Elementwise / layout
+// ------------------------------------------------------------------------------------------------
+Tensor cast_bf16(const Tensor& x) {
+  CHECK_IN(x); CHECK_F32(x);
+  Tensor y = at::empty(x.sizes(), x.options().dtype(at::kBFloat16));
+  check(pde::cast_f32_bf16(x.data_ptr<float>(), u16(y), x.numel(), cur_stream()), "cast_bf16");
+  return y;
+}
+void cast_bf16_into(const Tensor& x, Tensor& y) {
+  CHECK_IN(x); CHECK_F32(x); CHECK_IN(y); CHECK_BF16(y);
+  TORCH_CHECK(x.numel() == y.numel(), "cast_bf16_into: size mismatch");
+  check(pde::cast_f32_bf16(x.data_ptr<float>(), u16(y), x.numel(), cur_stream()), "cast_bf16_into");
+}
+Tensor cast_f32(const Tensor& x) {
+  CHECK_IN(x); CHECK_BF16(x);
+  Tensor y = at::empty(x.sizes(), x.options().dtype(at::kFloat));
+  check(pde::cast_bf16_f32(u16(x), y.data_ptr<float>(), x.numel(), cur_stream()), "cast_f32");
+  return y;
+}
+Tensor nchw_to_nhwc(const Tensor& x, int Cp) {
+  CHECK_IN(x); CHECK_F32(x);
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(Cp % 8 == 0 && Cp >= C, "nchw_to_nhwc: bad channel padding");
+  Tensor y = at::empty({N, H, W, Cp}, x.options().dtype(at::kBFloat16));
+  check(pde::nchw_f32_to_nhwc_bf16(x.data_ptr<float>(), u16(y), N, C, H, W, Cp, cur_stream()), "nchw_to_nhwc");
+  return y;
+}
+// [Co, Ci, R, S] fp32 -> [Cop, R*S*Cp] bf16 (zero padded channels)
+Tensor conv_w_fwd(const Tensor& w, int Cp, int Cop) {
+  CHECK_IN(w); CHECK_F32(w);
+  const int Co = w.size(0), Ci = w.size(1), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(Cp >= Ci && Cop >= Co, "conv_w_fwd: padding smaller than channels");
+  Tensor y = at::empty({Cop, R * S * Cp}, w.options().dtype(at::kBFloat16));
+  check(pde::conv_weight_fwd_layout(w.data_ptr<float>(), u16(y), Co, Ci, R, S, Cp, Cop, cur_stream()), "conv_w_fwd");
+  return y;
+}
+// [Co, Ci, R, S] fp32 -> [Cip, R*S*Cop] bf16
+Tensor conv_w_dgrad(const Tensor& w, int Cip, int Cop) {
+  CHECK_IN(w); CHECK_F32(w);
+  const int Co = w.size(0), Ci = w.size(1), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(Cip >= Ci && Cop >= Co, "conv_w_dgrad: padding smaller than channels");
+  Tensor y = at::empty({Cip, R * S * Cop}, w.options().dtype(at::kBFloat16));
+  check(pde::conv_weight_dgrad_layout(w.data_ptr<float>(), u16(y), Co, Ci, R, S, Cip, Cop, cur_stream()),
+        "conv_w_dgrad");
+  return y;
+}
+// [Cop, R*S*Cp] fp32 (wgrad GEMM output) -> [Co, Ci, R, S] fp32
+Tensor conv_wgrad_oihw(const Tensor& g, int Co, int Ci, int R, int S) {
+  CHECK_IN(g); CHECK_F32(g);
+  TORCH_CHECK(g.size(0) >= Co, "conv_wgrad_oihw: rows");
+  const int Cp = g.size(1) / (R * S);
+  Tensor y = at::empty({Co, Ci, R, S}, g.options());
+  check(pde::conv_wgrad_to_oihw(g.data_ptr<float>(), y.data_ptr<float>(), Co, Ci, R, S, Cp, 0, cur_stream()),
+        "conv_wgrad_oihw");
+  return y;
+}
+Tensor colsum(const Tensor& x) {
+  CHECK_IN(x); CHECK_BF16(x);
+  const int N = x.size(-1);
+  const int M = x.numel() / N;
+  Tensor y = at::empty({N}, x.options().dtype(at::kFloat));
+  check(pde::colsum_bf16(u16(x), y.data_ptr<float>(), M, N, 0, cur_stream()), "colsum");
+  return y;
+}
+Tensor relu_bwd(const Tensor& dy, const Tensor& y) {
+  CHECK_IN(dy); CHECK_IN(y); CHECK_BF16(dy); CHECK_BF16(y);
+  Tensor dx = at::empty_like(dy);
+  check(pde::relu_bwd_bf16(u16(dy), u16(y), u16(dx), dy.numel(), cur_stream()), "relu_bwd");
+  return dx;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Losses
+// ------------------------------------------------------------------------------------------------
+std::vector<Tensor> ce_fwd(const Tensor& x, const Tensor& tgt, int mode) {
+  CHECK_IN(x); CHECK_IN(tgt);
+  TORCH_CHECK(tgt.scalar_type() == at::kLong, "targets must be int64");
+  const int B = x.size(0), V = x.size(1);
+  TORCH_CHECK(B <= 1 << 20, "batch too large for the single-block reduction");
+  const bool f = x.scalar_type() == at::kFloat;
+  Tensor loss = at::empty({}, x.options().dtype(at::kFloat));
+  Tensor lse = at::empty({B}, x.options().dtype(at::kFloat));
+  check(pde::ce_fwd(x.data_ptr(), f, tgt.data_ptr<int64_t>(), B, V, mode, loss.data_ptr<float>(),
+                    mode == 0 ? lse.data_ptr<float>() : nullptr, cur_stream()),
+        "ce_fwd");
+  return {loss, lse};
+}
+Tensor ce_bwd(const Tensor& x, const Tensor& tgt, const Tensor& lse, const Tensor& gout, int mode, bool dx_f32) {
+  CHECK_IN(x); CHECK_IN(tgt); CHECK_IN(gout);
+  const int B = x.size(0), V = x.size(1);
+  const bool f = x.scalar_type() == at::kFloat;
+  Tensor dx = at::empty({B, V}, x.options().dtype(dx_f32 ? at::kFloat : at::kBFloat16));
+  check(pde::ce_bwd(x.data_ptr(), f, tgt.data_ptr<int64_t>(), lse.data_ptr<float>(), gout.data_ptr<float>(), B, V,
+                    mode, dx.data_ptr(), dx_f32, cur_stream()),
+        "ce_bwd");
+  return dx;
+}
+Tensor log_softmax_fwd(const Tensor& x) {
+  CHECK_IN(x);
+  const int B = x.size(0), V = x.size(1);
+  Tensor y = at::empty({B, V}, x.options().dtype(at::kFloat));
+  check(pde::log_softmax_fwd(x.data_ptr(), x.scalar_type() == at::kFloat, B, V, y.data_ptr<float>(), cur_stream()),
+        "log_softmax_fwd");
+  return y;
+}
+Tensor log_softmax_bwd(const Tensor& dy, const Tensor& y, bool dx_f32) {
+  CHECK_IN(dy); CHECK_IN(y); CHECK_F32(dy); CHECK_F32(y);
+  const int B = y.size(0), V = y.size(1);
+  Tensor dx = at::empty({B, V}, y.options().dtype(dx_f32 ? at::kFloat : at::kBFloat16));
+  check(pde::log_softmax_bwd(dy.data_ptr<float>(), y.data_ptr<float>(), B, V, dx.data_ptr(), dx_f32, cur_stream()),
+        "log_softmax_bwd");
+  return dx;
+}
+Tensor mse_fwd(const Tensor& p, const Tensor& t) {
+  CHECK_IN(p); CHECK_IN(t); CHECK_F32(t);
+  Tensor loss = at::empty({}, p.options().dtype(at::kFloat));
+  check(pde::mse_fwd(p.data_ptr(), p.scalar_type() == at::kFloat, t.data_ptr<float>(), p.numel(),
+                     loss.data_ptr<float>(), cur_stream()),
+        "mse_fwd");
+  return loss;
+}
+Tensor mse_bwd(const Tensor& p, const Tensor& t, const Tensor& gout, bool dx_f32) {
+  CHECK_IN(p); CHECK_IN(t); CHECK_IN(gout);
+  Tensor dx = at::empty(p.sizes(), p.options().dtype(dx_f32 ? at::kFloat : at::kBFloat16));
+  check(pde::mse_bwd(p.data_ptr(), p.scalar_type() == at::kFloat, t.data_ptr<float>(), gout.data_ptr<float>(),
+                     p.numel(), dx.data_ptr(), dx_f32, cur_stream()),
+        "mse_bwd");
+  return dx;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused multi-tensor optimiser
+// ------------------------------------------------------------------------------------------------
+// Build the device table for a parameter set; returns (table bytes tensor on device, total elems).
+std::tuple<Tensor, int64_t> optim_table(const std::vector<Tensor>& params, const std::vector<Tensor>& grads,
+                                        const std::vector<Tensor>& exp_avg, const std::vector<Tensor>& exp_avg_sq,
+                                        const std::vector<Tensor>& bf16_copies) {
+  const size_t n = params.size();
+  TORCH_CHECK(grads.size() == n, "optim_table: grads size");
+  std::vector<pde::OptimEntry> tab(n);
+  long off = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const Tensor& p = params[i];
+    CHECK_IN(p); CHECK_F32(p);
+    pde::OptimEntry& e = tab[i];
+    e.param = p.data_ptr<float>();
+    e.grad = grads[i].defined() ? grads[i].data_ptr<float>() : nullptr;
+    if (grads[i].defined()) { CHECK_CONTIG(grads[i]); TORCH_CHECK(grads[i].numel() == p.numel(), "grad size"); }
+    e.exp_avg = i < exp_avg.size() && exp_avg[i].defined() ? exp_avg[i].data_ptr<float>() : nullptr;
+    e.exp_avg_sq = i < exp_avg_sq.size() && exp_avg_sq[i].defined() ? exp_avg_sq[i].data_ptr<float>() : nullptr;
+    e.bf16_copy = i < bf16_copies.size() && bf16_copies[i].defined() ? u16(bf16_copies[i]) : nullptr;
+    e.offset = off;
+    e.size = p.numel();
+    off += p.numel();
+  }
+  const long bytes = static_cast<long>(n * sizeof(pde::OptimEntry));
+  Tensor host = at::empty({bytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  std::memcpy(host.data_ptr(), tab.data(), bytes);
+  Tensor dev = at::empty({bytes}, params.empty() ? at::TensorOptions().dtype(at::kByte)
+                                                 : params[0].options().dtype(at::kByte));
+  dev.copy_(host, /*non_blocking=*/true);
+  return {dev, off};
+}
+
+void optim_step(const Tensor& table, int ntensors, int64_t total, int mode, const Tensor& hparams, Tensor& step) {
+  CHECK_IN(table); CHECK_IN(hparams); CHECK_IN(step);
+  TORCH_CHECK(hparams.numel() >= pde::HP_COUNT, "hparams size");
+  TORCH_CHECK(step.scalar_type() == at::kInt, "step must be int32");
+  check(pde::multi_tensor_optim(mode, reinterpret_cast<const pde::OptimEntry*>(table.data_ptr()), ntensors, total,
+                                hparams.data_ptr<float>(), step.data_ptr<int>(), cur_stream()),
+        "optim_step");
+}
+
+// ------------------------------------------------------------------------------------------------
+// BatchNorm / pooling / dropout / EmbeddingBag
+// ------------------------------------------------------------------------------------------------
+// Returns y, save_mean, save_invstd.
+std::vector<Tensor> bn_fwd(const Tensor& x, const optional<Tensor>& gamma, const optional<Tensor>& beta,
+                           const optional<Tensor>& running_mean, const optional<Tensor>& running_var, double eps,
+                           double momentum, const optional<Tensor>& res, bool relu) {
+  CHECK_IN(x); CHECK_BF16(x);
+  const int C = x.size(-1);
+  const int P = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "bn_fwd: C must be a multiple of 8");
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor y = at::empty_like(x);
+  Tensor mean = at::empty({C}, fo), invstd = at::empty({C}, fo), ss = at::empty({2 * C}, fo);
+  Tensor ws = at::empty({static_cast<long>(pde::bn_workspace_blocks(P, C)) * 2 * C}, fo);
+  check(pde::bn_fwd_train(u16(x), P, C, cf32(gamma), cf32(beta), static_cast<float>(eps),
+                          static_cast<float>(momentum), f32(running_mean), f32(running_var), mean.data_ptr<float>(),
+                          invstd.data_ptr<float>(), ss.data_ptr<float>(), ws.data_ptr<float>(), cu16(res), relu,
+                          u16(y), cur_stream()),
+        "bn_fwd");
+  return {y, mean, invstd};
+}
+// Inference / eval mode: y = x*scale + shift with scale/shift from running stats (computed in torch).
+Tensor bn_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, const optional<Tensor>& res, bool relu) {
+  CHECK_IN(x); CHECK_BF16(x);
+  const int C = x.size(-1);
+  const int P = x.numel() / C;
+  Tensor y = at::empty_like(x);
+  check(pde::bn_apply(u16(x), P, C, scale.data_ptr<float>(), shift.data_ptr<float>(), cu16(res), relu, u16(y),
+                      cur_stream()),
+        "bn_apply");
+  return y;
+}
+// Returns dx, dgamma, dbeta, dres (dres undefined unless want_dres)
+std::vector<Tensor> bn_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const Tensor& mean,
+                           const Tensor& invstd, const optional<Tensor>& gamma, bool relu, bool want_dres) {
+  CHECK_IN(dy); CHECK_IN(x); CHECK_IN(y); CHECK_BF16(dy);
+  const int C = x.size(-1);
+  const int P = x.numel() / C;
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor dx = at::empty_like(x);
+  Tensor dg = at::empty({C}, fo), db = at::empty({C}, fo), coef = at::empty({3 * C}, fo);
+  Tensor ws = at::empty({static_cast<long>(pde::bn_workspace_blocks(P, C)) * 2 * C}, fo);
+  Tensor dres;
+  if (want_dres) dres = at::empty_like(x);
+  check(pde::bn_bwd(u16(dy), u16(x), u16(y), mean.data_ptr<float>(), invstd.data_ptr<float>(), cf32(gamma), P, C,
+                    relu, dg.data_ptr<float>(), db.data_ptr<float>(), ws.data_ptr<float>(), coef.data_ptr<float>(),
+                    u16(dx), want_dres ? u16(dres) : nullptr, cur_stream()),
+        "bn_bwd");
+  return {dx, dg, db, dres};
+}
+std::vector<Tensor> maxpool_fwd(const Tensor& x, int k, int s, int p, bool relu) {
+  CHECK_IN(x); CHECK_BF16(x);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
+  Tensor y = at::empty({N, Ho, Wo, C}, x.options());
+  Tensor idx = at::empty({N, Ho, Wo, C}, x.options().dtype(at::kByte));
+  check(pde::maxpool_fwd(u16(x), u16(y), idx.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, k, s, p, relu, cur_stream()),
+        "maxpool_fwd");
+  return {y, idx};
+}
+Tensor maxpool_bwd(const Tensor& dy, const Tensor& y, const Tensor& idx, int H, int W, int k, int s, int p,
+                   bool relu) {
+  CHECK_IN(dy); CHECK_IN(y); CHECK_IN(idx); CHECK_BF16(dy);
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), C = dy.size(3);
+  Tensor dx = at::empty({N, H, W, C}, dy.options());
+  check(pde::maxpool_bwd(u16(dy), u16(y), idx.data_ptr<uint8_t>(), u16(dx), N, H, W, C, Ho, Wo, k, s, p, relu,
+                         cur_stream()),
+        "maxpool_bwd");
+  return dx;
+}
+Tensor avgpool_fwd(const Tensor& x) {
+  CHECK_IN(x); CHECK_BF16(x);
+  const int N = x.size(0), C = x.size(-1);
+  const int HW = x.numel() / (static_cast<long>(N) * C);
+  TORCH_CHECK(C % 8 == 0, "avgpool: C % 8");
+  Tensor y = at::empty({N, C}, x.options());
+  check(pde::avgpool_fwd(u16(x), u16(y), N, HW, C, cur_stream()), "avgpool_fwd");
+  return y;
+}
+Tensor avgpool_bwd(const Tensor& dy, int H, int W) {
+  CHECK_IN(dy); CHECK_BF16(dy);
+  const int N = dy.size(0), C = dy.size(1);
+  Tensor dx = at::empty({N, H, W, C}, dy.options());
+  check(pde::avgpool_bwd(u16(dy), u16(dx), N, H * W, C, cur_stream()), "avgpool_bwd");
+  return dx;
+}
+std::vector<Tensor> dropout_fwd(const Tensor& x, double p, int64_t seed, bool channel) {
+  CHECK_IN(x); CHECK_BF16(x);
+  Tensor y = at::empty_like(x);
+  Tensor mask = at::empty(x.sizes(), x.options().dtype(at::kByte));
+  int HW = 1, C = 1;
+  if (channel) {
+    C = x.size(-1);
+    HW = x.numel() / (x.size(0) * C);
+  }
+  check(pde::dropout_fwd(u16(x), u16(y), mask.data_ptr<uint8_t>(), x.numel(), channel ? 1 : 0, HW, C,
+                         static_cast<float>(p), static_cast<unsigned long long>(seed), cur_stream()),
+        "dropout_fwd");
+  return {y, mask};
+}
+Tensor dropout_bwd(const Tensor& dy, const Tensor& mask, double p) {
+  CHECK_IN(dy); CHECK_IN(mask);
+  Tensor dx = at::empty_like(dy);
+  check(pde::dropout_bwd(u16(dy), mask.data_ptr<uint8_t>(), u16(dx), dy.numel(), static_cast<float>(p), cur_stream()),
+        "dropout_bwd");
+  return dx;
+}
+Tensor embbag_fwd(const Tensor& w, const Tensor& idx, const Tensor& off) {
+  CHECK_IN(w); CHECK_IN(idx); CHECK_IN(off); CHECK_F32(w);
+  const int B = off.size(0), D = w.size(1);
+  Tensor out = at::empty({B, D}, w.options());
+  check(pde::embbag_fwd(w.data_ptr<float>(), idx.data_ptr<int64_t>(), off.data_ptr<int64_t>(), B, idx.numel(), D,
+                        out.data_ptr<float>(), cur_stream()),
+        "embbag_fwd");
+  return out;
+}
+Tensor embbag_bwd(const Tensor& dy, const Tensor& idx, const Tensor& off, int64_t num) {
+  CHECK_IN(dy); CHECK_IN(idx); CHECK_IN(off); CHECK_F32(dy);
+  const int B = off.size(0), D = dy.size(1);
+  Tensor dw = at::zeros({num, D}, dy.options());
+  check(pde::embbag_bwd(dy.data_ptr<float>(), idx.data_ptr<int64_t>(), off.data_ptr<int64_t>(), B, idx.numel(), D,
+                        dw.data_ptr<float>(), cur_stream()),
+        "embbag_bwd");
+  return dw;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X (gfx950) native kernels for pytorch_distributed_examples_amd";
+  m.def("linear_fwd", &linear_fwd);
+  m.def("linear_dgrad", &linear_dgrad);
+  m.def("linear_wgrad", &linear_wgrad);
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("cast_bf16", &cast_bf16);
+  m.def("cast_bf16_into", &cast_bf16_into);
+  m.def("cast_f32", &cast_f32);
+  m.def("nchw_to_nhwc", &nchw_to_nhwc);
+  m.def("conv_w_fwd", &conv_w_fwd);
+  m.def("conv_w_dgrad", &conv_w_dgrad);
+  m.def("conv_wgrad_oihw", &conv_wgrad_oihw);
+  m.def("colsum", &colsum);
+  m.def("relu_bwd", &relu_bwd);
+  m.def("ce_fwd", &ce_fwd);
+  m.def("ce_bwd", &ce_bwd);
+  m.def("log_softmax_fwd", &log_softmax_fwd);
+  m.def("log_softmax_bwd", &log_softmax_bwd);
+  m.def("mse_fwd", &mse_fwd);
+  m.def("mse_bwd", &mse_bwd);
+  m.def("optim_table", &optim_table);
+  m.def("optim_step", &optim_step);
+  m.def("bn_fwd", &bn_fwd);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd", &bn_bwd);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("dropout_fwd", &dropout_fwd);
+  m.def("dropout_bwd", &dropout_bwd);
+  m.def("embbag_fwd", &embbag_fwd);
+  m.def("embbag_bwd", &embbag_bwd);
+}

@@ -1,0 +1,141 @@
+// Host-side launcher declarations for the CDNA4 (gfx950) kernels in csrc/kernels/*.hip.
+//
+// Every launcher takes raw device pointers plus the hipStream_t it must enqueue on, does no
+// allocation and no synchronisation (so the caller may capture it into a hipGraph), and returns
+// a hipError_t from hipGetLastError() after the launch.  bindings.cpp wraps them for torch.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace pde {
+
+// ---------------------------------------------------------------------------------------------
+// GEMM / implicit-GEMM convolution (gemm.hip)
+// ---------------------------------------------------------------------------------------------
+// Epilogue flags (bitwise OR).
+enum EpiFlags : int {
+  EPI_NONE = 0,
+  EPI_BIAS = 1,       // + bias[n] (fp32)
+  EPI_RELU = 2,       // max(0, .)
+  EPI_DRELU = 4,      // * (aux[m, n] > 0)   aux: bf16 [M, ldaux] (saved post-ReLU activation)
+  EPI_OUT_F32 = 8,    // output fp32 (else bf16)
+  EPI_ACCUM = 16,     // out += result (fp32 output only)
+};
+
+// Operand description.  The GEMM computes  C[m, n] = sum_k A[m, k] * B[n, k].
+//   kind 0 (dense):   element (r, k) at ptr[r * ld_r + k * ld_k]; one of ld_r / ld_k must be 1.
+//   kind 1 (im2col):  NHWC activation gather.  r indexes output pixels (n, ho, wo), k indexes
+//                     (kh, kw, c) with c fastest.  Requires C % 8 == 0.
+//   kind 2 (im2col^T): same gather but r indexes (kh, kw, c) and k indexes output pixels
+//                     (the weight-gradient "B" operand).
+//   kind 3 (dgrad):   transposed-conv gather from dy (NHWC, C = Cout of the forward conv):
+//                     r indexes input pixels (n, h, w), k indexes (kh, kw, co); element is
+//                     dy[n, (h + pad - kh) / s, (w + pad - kw) / s, co] when divisible & in range.
+struct ConvGeom {
+  int N, H, W, C;      // gathered tensor dims (NHWC)
+  int R, S;            // kernel
+  int stride, pad;
+  int Ho, Wo;          // output spatial dims of the gather (kind 1/2: conv output; kind 3: H, W of dx)
+};
+
+struct Operand {
+  const void* ptr;
+  int kind;            // 0 dense, 1 im2col, 2 im2col^T, 3 dgrad gather
+  long ld_r, ld_k;     // dense strides (elements)
+  ConvGeom g;          // gather geometry
+};
+
+struct GemmArgs {
+  int M, N, K;
+  Operand a, b;
+  void* out; long ldo;             // out[m * ldo + n]
+  const float* bias;               // EPI_BIAS (bias[n] for n < nbias, 0 beyond: padded channels)
+  int nbias;
+  const uint16_t* aux; long ldaux; // EPI_DRELU (bf16 bits)
+  int epi;
+  int splitk;                      // >1: fp32 partial slabs in workspace, then reduce + epilogue
+  float* workspace;                // splitk * M * N fp32
+};
+
+hipError_t gemm_bf16(const GemmArgs& args, hipStream_t stream);
+
+// ---------------------------------------------------------------------------------------------
+// Elementwise / layout (elementwise.hip)
+// ---------------------------------------------------------------------------------------------
+hipError_t cast_f32_bf16(const float* in, uint16_t* out, long n, hipStream_t s);
+hipError_t cast_bf16_f32(const uint16_t* in, float* out, long n, hipStream_t s);
+// NCHW fp32 -> NHWC bf16 with channel padding to Cp (zero fill)
+hipError_t nchw_f32_to_nhwc_bf16(const float* in, uint16_t* out, int N, int C, int H, int W, int Cp,
+                                 hipStream_t s);
+// [Cout, Cin, R, S] fp32 -> [Cop, R, S, Cp] bf16 (forward igemm B operand, K-contiguous, zero padded)
+hipError_t conv_weight_fwd_layout(const float* w, uint16_t* out, int Co, int Ci, int R, int S, int Cp, int Cop,
+                                  hipStream_t s);
+// [Cout, Cin, R, S] fp32 -> [Cip, R, S, Cop] bf16 (dgrad B operand: n = ci, k = (r, s, co), zero padded)
+hipError_t conv_weight_dgrad_layout(const float* w, uint16_t* out, int Co, int Ci, int R, int S, int Cip, int Cop,
+                                    hipStream_t s);
+// dW gemm output [Cout, R*S*Cp] fp32 -> [Cout, Cin, R, S] fp32 (optionally accumulate)
+hipError_t conv_wgrad_to_oihw(const float* in, float* out, int Co, int Ci, int R, int S, int Cp, int accum,
+                              hipStream_t s);
+// column sums of a bf16 [M, N] matrix into fp32 [N] (bias gradient); accum adds to out
+hipError_t colsum_bf16(const uint16_t* x, float* out, int M, int N, int accum, hipStream_t s);
+hipError_t relu_bwd_bf16(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n, hipStream_t s);
+
+// ---------------------------------------------------------------------------------------------
+// Losses (loss.hip).  mode 0 = cross-entropy on logits, mode 1 = NLL on log-probabilities.
+// ---------------------------------------------------------------------------------------------
+hipError_t ce_fwd(const void* x, int x_f32, const int64_t* tgt, int B, int V, int mode, float* loss, float* lse,
+                  hipStream_t s);
+hipError_t ce_bwd(const void* x, int x_f32, const int64_t* tgt, const float* lse, const float* gout, int B, int V,
+                  int mode, void* dx, int dx_f32, hipStream_t s);
+hipError_t log_softmax_fwd(const void* x, int x_f32, int B, int V, float* y, hipStream_t s);
+hipError_t log_softmax_bwd(const float* dy, const float* y, int B, int V, void* dx, int dx_f32, hipStream_t s);
+hipError_t mse_fwd(const void* p, int p_f32, const float* t, long n, float* loss, hipStream_t s);
+hipError_t mse_bwd(const void* p, int p_f32, const float* t, const float* gout, long n, void* dx, int dx_f32,
+                   hipStream_t s);
+
+// ---------------------------------------------------------------------------------------------
+// Optimisers (optim.hip): one launch over every tensor of a parameter set.
+// ---------------------------------------------------------------------------------------------
+struct OptimEntry {
+  float* param;          // fp32 master weight
+  const float* grad;     // fp32 gradient (nullptr: treated as zero)
+  float* exp_avg;        // Adam/AdamW m, SGD momentum buffer
+  float* exp_avg_sq;     // Adam/AdamW v
+  uint16_t* bf16_copy;   // optional bf16 compute copy written after the update
+  long offset;           // prefix offset in the concatenated element space
+  long size;
+};
+enum HParam { HP_LR = 0, HP_BETA1, HP_BETA2, HP_EPS, HP_WD, HP_MOMENTUM, HP_GRAD_SCALE, HP_COUNT };
+// mode 0 SGD, 1 Adam, 2 AdamW.  dev_hparams: float[HP_COUNT]; dev_step: int (steps taken so far,
+// incremented on device after the update).
+hipError_t multi_tensor_optim(int mode, const OptimEntry* dev_table, int ntensors, long total_elems,
+                              const float* dev_hparams, int* dev_step, hipStream_t s);
+
+// ---------------------------------------------------------------------------------------------
+// BatchNorm / pooling / dropout / EmbeddingBag (norm_pool.hip).  Activations NHWC bf16, [P = N*H*W][C].
+// ---------------------------------------------------------------------------------------------
+int bn_workspace_blocks(int P, int C);  // ws needs bn_workspace_blocks * 2 * C floats
+hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, const float* beta, float eps,
+                        float momentum, float* running_mean, float* running_var, float* save_mean,
+                        float* save_invstd, float* scale_shift, float* ws, const uint16_t* res, int relu,
+                        uint16_t* y, hipStream_t s);
+hipError_t bn_apply(const uint16_t* x, int P, int C, const float* scale, const float* shift, const uint16_t* res,
+                    int relu, uint16_t* y, hipStream_t s);
+hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
+                  const float* gamma, int P, int C, int relu, float* dgamma, float* dbeta, float* ws, float* coef,
+                  uint16_t* dx, uint16_t* dres, hipStream_t s);
+hipError_t maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
+                       int k, int st, int p, int relu, hipStream_t s);
+hipError_t maxpool_bwd(const uint16_t* dy, const uint16_t* y, const uint8_t* idx, uint16_t* dx, int N, int H, int W,
+                       int C, int Ho, int Wo, int k, int st, int p, int relu, hipStream_t s);
+hipError_t avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s);
+hipError_t avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t s);
+hipError_t dropout_fwd(const uint16_t* x, uint16_t* y, uint8_t* mask, long n, int mode, int HW, int C, float p,
+                       unsigned long long seed, hipStream_t s);
+hipError_t dropout_bwd(const uint16_t* dy, const uint8_t* mask, uint16_t* dx, long n, float p, hipStream_t s);
+hipError_t embbag_fwd(const float* w, const int64_t* idx, const int64_t* off, int B, long L, int D, float* out,
+                      hipStream_t s);
+hipError_t embbag_bwd(const float* dy, const int64_t* idx, const int64_t* off, int B, long L, int D, float* dw,
+                      hipStream_t s);
+
+}  // namespace pde

@@ -1,0 +1,45 @@
+// Shared device helpers for the gfx950 kernels: bf16 conversion, vector types, wave reductions.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace pde {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(uint16_t b) {
+  return __uint_as_float(static_cast<uint32_t>(b) << 16);
+}
+// Round-to-nearest-even via the native cast (hipcc emits v_cvt_pk_bf16_f32; NaN stays NaN).
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 h = static_cast<__bf16>(f);
+  return __builtin_bit_cast(uint16_t, h);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+inline int ceil_div(long a, long b) { return static_cast<int>((a + b - 1) / b); }
+
+// Grid size for a grid-stride memory-bound kernel: enough blocks to fill 256 CUs, capped.
+inline int stream_grid(long n, int block, int per_thread = 1) {
+  long blocks = (n + static_cast<long>(block) * per_thread - 1) / (static_cast<long>(block) * per_thread);
+  if (blocks < 1) blocks = 1;
+  if (blocks > 2048) blocks = 2048;
+  return static_cast<int>(blocks);
+}
+
+}  // namespace pde

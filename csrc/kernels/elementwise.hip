@@ -1,0 +1,201 @@
+// Memory-bound layout / cast / reduction kernels (gfx950).  All loads are vectorised (8 x bf16 or
+// 4 x f32 per lane, cdna_hip_programming.md Guideline 13) and grids are capped grid-stride loops
+// (Guideline 11).
+#include "common.cuh"
+#include "pde_kernels.h"
+
+namespace pde {
+
+namespace {
+
+__global__ void k_cast_f32_bf16(const float* __restrict__ in, uint16_t* __restrict__ out, long n) {
+  const long nv = n / 8;
+  const long stride = static_cast<long>(gridDim.x) * blockDim.x;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < nv; i += stride) {
+    const f32x4 a = reinterpret_cast<const f32x4*>(in)[2 * i];
+    const f32x4 b = reinterpret_cast<const f32x4*>(in)[2 * i + 1];
+    u16x8 o;
+    o[0] = f2bf(a[0]); o[1] = f2bf(a[1]); o[2] = f2bf(a[2]); o[3] = f2bf(a[3]);
+    o[4] = f2bf(b[0]); o[5] = f2bf(b[1]); o[6] = f2bf(b[2]); o[7] = f2bf(b[3]);
+    reinterpret_cast<u16x8*>(out)[i] = o;
+  }
+  for (long i = nv * 8 + blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < n; i += stride)
+    out[i] = f2bf(in[i]);
+}
+
+__global__ void k_cast_bf16_f32(const uint16_t* __restrict__ in, float* __restrict__ out, long n) {
+  const long nv = n / 8;
+  const long stride = static_cast<long>(gridDim.x) * blockDim.x;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < nv; i += stride) {
+    const u16x8 v = reinterpret_cast<const u16x8*>(in)[i];
+    f32x4 a, b;
+    a[0] = bf2f(v[0]); a[1] = bf2f(v[1]); a[2] = bf2f(v[2]); a[3] = bf2f(v[3]);
+    b[0] = bf2f(v[4]); b[1] = bf2f(v[5]); b[2] = bf2f(v[6]); b[3] = bf2f(v[7]);
+    reinterpret_cast<f32x4*>(out)[2 * i] = a;
+    reinterpret_cast<f32x4*>(out)[2 * i + 1] = b;
+  }
+  for (long i = nv * 8 + blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < n; i += stride)
+    out[i] = bf2f(in[i]);
+}
+
+// One thread per output 8-channel group of one pixel.
+__global__ void k_nchw_to_nhwc(const float* __restrict__ in, uint16_t* __restrict__ out, int N, int C,
+                               int H, int W, int Cp) {
+  const int groups = Cp / 8;
+  const long total = static_cast<long>(N) * H * W * groups;
+  const long HW = static_cast<long>(H) * W;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int g = static_cast<int>(i % groups);
+    const long pix = i / groups;
+    const int n = static_cast<int>(pix / HW);
+    const long hw = pix - n * HW;
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = g * 8 + j;
+      o[j] = c < C ? f2bf(in[(static_cast<long>(n) * C + c) * HW + hw]) : uint16_t(0);
+    }
+    reinterpret_cast<u16x8*>(out)[i] = o;
+  }
+}
+
+__global__ void k_conv_w_fwd(const float* __restrict__ w, uint16_t* __restrict__ out, int Co, int Ci,
+                             int R, int S, int Cp, int Cop) {
+  const long total = static_cast<long>(Cop) * R * S * Cp;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int c = static_cast<int>(i % Cp);
+    long t = i / Cp;
+    const int s = static_cast<int>(t % S);
+    t /= S;
+    const int r = static_cast<int>(t % R);
+    const int co = static_cast<int>(t / R);
+    out[i] = (c < Ci && co < Co) ? f2bf(w[((static_cast<long>(co) * Ci + c) * R + r) * S + s]) : uint16_t(0);
+  }
+}
+
+// out[ci][r][s][co] = w[co][ci][r][s]   (padded to [Cip][R][S][Cop] with zeros)
+__global__ void k_conv_w_dgrad(const float* __restrict__ w, uint16_t* __restrict__ out, int Co, int Ci,
+                               int R, int S, int Cip, int Cop) {
+  const long total = static_cast<long>(Cop) * R * S * Cip;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int co = static_cast<int>(i % Cop);
+    long t = i / Cop;
+    const int s = static_cast<int>(t % S);
+    t /= S;
+    const int r = static_cast<int>(t % R);
+    const int ci = static_cast<int>(t / R);
+    out[i] = (co < Co && ci < Ci) ? f2bf(w[((static_cast<long>(co) * Ci + ci) * R + r) * S + s]) : uint16_t(0);
+  }
+}
+
+__global__ void k_wgrad_to_oihw(const float* __restrict__ in, float* __restrict__ out, int Co, int Ci,
+                                int R, int S, int Cp, int accum) {
+  const long total = static_cast<long>(Co) * Ci * R * S;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int s = static_cast<int>(i % S);
+    long t = i / S;
+    const int r = static_cast<int>(t % R);
+    t /= R;
+    const int ci = static_cast<int>(t % Ci);
+    const int co = static_cast<int>(t / Ci);
+    const float v = in[((static_cast<long>(co) * R + r) * S + s) * Cp + ci];
+    out[i] = accum ? out[i] + v : v;
+  }
+}
+
+// Column sums of bf16 [M, N] (bias gradient): each block owns a strip of 64 columns x
+// (M / gridDim.y) rows; 4 waves stride the rows, partials meet in LDS, then one fp32 atomic per
+// column per block (or a plain store when a single block covers all rows).
+__global__ void k_colsum_bf16(const uint16_t* __restrict__ x, float* __restrict__ out, int M, int N,
+                              int rows_per_block, int accum) {
+  __shared__ float part[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int wid = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  float acc = 0.f;
+  if (col < N)
+    for (int r = r0 + wid; r < r1; r += 4) acc += bf2f(x[static_cast<long>(r) * N + col]);
+  part[wid][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (wid == 0 && col < N) {
+    const float v = part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x];
+    if (gridDim.y == 1)
+      out[col] = accum ? out[col] + v : v;
+    else
+      atomicAdd(out + col, v);
+  }
+}
+
+__global__ void k_relu_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+                           uint16_t* __restrict__ dx, long n) {
+  const long nv = n / 8;
+  const long stride = static_cast<long>(gridDim.x) * blockDim.x;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < nv; i += stride) {
+    const u16x8 g = reinterpret_cast<const u16x8*>(dy)[i];
+    const u16x8 a = reinterpret_cast<const u16x8*>(y)[i];
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = bf2f(a[j]) > 0.f ? g[j] : uint16_t(0);
+    reinterpret_cast<u16x8*>(dx)[i] = o;
+  }
+  for (long i = nv * 8 + blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < n; i += stride)
+    dx[i] = bf2f(y[i]) > 0.f ? dy[i] : uint16_t(0);
+}
+
+}  // namespace
+
+hipError_t cast_f32_bf16(const float* in, uint16_t* out, long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_cast_f32_bf16, dim3(stream_grid(n, 256, 8)), dim3(256), 0, s, in, out, n);
+  return hipGetLastError();
+}
+hipError_t cast_bf16_f32(const uint16_t* in, float* out, long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_cast_bf16_f32, dim3(stream_grid(n, 256, 8)), dim3(256), 0, s, in, out, n);
+  return hipGetLastError();
+}
+hipError_t nchw_f32_to_nhwc_bf16(const float* in, uint16_t* out, int N, int C, int H, int W, int Cp,
+                                 hipStream_t s) {
+  const long total = static_cast<long>(N) * H * W * (Cp / 8);
+  hipLaunchKernelGGL(k_nchw_to_nhwc, dim3(stream_grid(total, 256)), dim3(256), 0, s, in, out, N, C, H, W, Cp);
+  return hipGetLastError();
+}
+hipError_t conv_weight_fwd_layout(const float* w, uint16_t* out, int Co, int Ci, int R, int S, int Cp, int Cop,
+                                  hipStream_t s) {
+  const long total = static_cast<long>(Cop) * R * S * Cp;
+  hipLaunchKernelGGL(k_conv_w_fwd, dim3(stream_grid(total, 256)), dim3(256), 0, s, w, out, Co, Ci, R, S, Cp, Cop);
+  return hipGetLastError();
+}
+hipError_t conv_weight_dgrad_layout(const float* w, uint16_t* out, int Co, int Ci, int R, int S, int Cip, int Cop,
+                                    hipStream_t s) {
+  const long total = static_cast<long>(Cop) * R * S * Cip;
+  hipLaunchKernelGGL(k_conv_w_dgrad, dim3(stream_grid(total, 256)), dim3(256), 0, s, w, out, Co, Ci, R, S, Cip,
+                     Cop);
+  return hipGetLastError();
+}
+hipError_t conv_wgrad_to_oihw(const float* in, float* out, int Co, int Ci, int R, int S, int Cp, int accum,
+                              hipStream_t s) {
+  const long total = static_cast<long>(Co) * Ci * R * S;
+  hipLaunchKernelGGL(k_wgrad_to_oihw, dim3(stream_grid(total, 256)), dim3(256), 0, s, in, out, Co, Ci, R, S,
+                     Cp, accum);
+  return hipGetLastError();
+}
+hipError_t colsum_bf16(const uint16_t* x, float* out, int M, int N, int accum, hipStream_t s) {
+  // accum is handled by the caller zeroing/keeping out; with a single row-block we overwrite.
+  const int col_blocks = ceil_div(N, 64);
+  int row_blocks = 1;
+  while (row_blocks < 64 && col_blocks * row_blocks < 512 && M / (row_blocks * 2) >= 64) row_blocks *= 2;
+  const int rpb = ceil_div(M, row_blocks);
+  if (row_blocks > 1 && !accum) (void)hipMemsetAsync(out, 0, sizeof(float) * N, s);
+  hipLaunchKernelGGL(k_colsum_bf16, dim3(col_blocks, row_blocks), dim3(256), 0, s, x, out, M, N, rpb, accum);
+  return hipGetLastError();
+}
+hipError_t relu_bwd_bf16(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_relu_bwd, dim3(stream_grid(n, 256, 8)), dim3(256), 0, s, dy, y, dx, n);
+  return hipGetLastError();
+}
+
+}  // namespace pde

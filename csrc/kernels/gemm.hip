@@ -1,0 +1,368 @@
+// bf16 MFMA GEMM / implicit-GEMM convolution for gfx950 (CDNA4).
+//
+//   C[m, n] = epilogue( sum_k A[m, k] * B[n, k] )
+//
+// One kernel template serves every matmul-shaped op of the suite: nn.Linear
+// forward / dgrad / wgrad, and NHWC implicit-GEMM convolution forward / dgrad / wgrad (the
+// operands are gathered from the activation on the fly -- no im2col buffer in HBM).
+//
+// Structure (cdna_hip_programming.md §5 "standard MFMA GEMM main loop"):
+//   * 256 threads = 4 wave64s arranged WM x WN, each wave owns a (BM/WM) x (BN/WN) sub-tile made
+//     of 16x16 fragments computed with v_mfma_f32_16x16x32_bf16 (fp32 accumulate).
+//   * A and B tiles are staged global -> registers -> LDS, double-buffered: the global loads of
+//     K-tile t+1 are issued before the MFMAs of tile t and written to the other LDS buffer after
+//     them (async-STAGE split, T14), one barrier per K-tile.
+//   * LDS images are K-contiguous rows padded by 16 B so MFMA fragments are single ds_read_b128.
+//     Operands that are contiguous along the row (M/N) dimension -- the transposed operands of
+//     dgrad / wgrad -- are loaded 16 B along the row and scattered into the K-contiguous image.
+//   * Tiles are mapped XCD-aware (T1): consecutive tile ids go to the same XCD group so tiles
+//     sharing A rows / B columns hit the same L2.
+//   * Split-K writes fp32 partial slabs, reduced by gemm_splitk_reduce (which applies the fused
+//     epilogue), so wgrad GEMMs with a huge reduction (N*H*W) still fill 256 CUs.
+#include "common.cuh"
+#include "pde_kernels.h"
+
+namespace pde {
+
+namespace {
+
+constexpr int kThreads = 256;
+
+// Load 8 consecutive K elements of row r (K-contiguous operand).
+__device__ __forceinline__ u16x8 load_kc(const Operand& op, int rows, int K, int r, int k0,
+                                         bool vec_ok) {
+  u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (r >= rows || k0 >= K) return v;
+  const uint16_t* p = static_cast<const uint16_t*>(op.ptr);
+  if (op.kind == 0) {
+    const long base = static_cast<long>(r) * op.ld_r;
+    if (vec_ok && k0 + 8 <= K) {
+      v = *reinterpret_cast<const u16x8*>(p + base + k0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (k0 + i < K) v[i] = p[base + static_cast<long>(k0 + i) * op.ld_k];
+    }
+    return v;
+  }
+  const ConvGeom& g = op.g;
+  // k0 -> (kh, kw, c0); C % 8 == 0 so the 8 elements share (kh, kw)
+  const int c0 = k0 % g.C;
+  const int rs = k0 / g.C;
+  const int kw = rs % g.S;
+  const int kh = rs / g.S;
+  const int HWo = g.Ho * g.Wo;
+  const int n = r / HWo;
+  const int rem = r - n * HWo;
+  const int oy = rem / g.Wo;
+  const int ox = rem - oy * g.Wo;
+  int iy, ix;
+  if (op.kind == 1) {
+    iy = oy * g.stride - g.pad + kh;
+    ix = ox * g.stride - g.pad + kw;
+  } else {  // kind 3: transposed-conv gather (dgrad). (oy, ox) are dx coords, dy has dims H x W.
+    int ty = oy + g.pad - kh;
+    int tx = ox + g.pad - kw;
+    if (ty < 0 || tx < 0) return v;
+    if (g.stride > 1) {
+      if ((ty % g.stride) != 0 || (tx % g.stride) != 0) return v;
+      ty /= g.stride;
+      tx /= g.stride;
+    }
+    iy = ty;
+    ix = tx;
+  }
+  if (iy < 0 || iy >= g.H || ix < 0 || ix >= g.W) return v;
+  v = *reinterpret_cast<const u16x8*>(p + ((static_cast<long>(n) * g.H + iy) * g.W + ix) * g.C + c0);
+  return v;
+}
+
+// Load 8 consecutive ROW elements r0..r0+7 at reduction index k (row-contiguous operand).
+__device__ __forceinline__ u16x8 load_rc(const Operand& op, int rows, int K, int r0, int k,
+                                         bool vec_ok) {
+  u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (r0 >= rows || k >= K) return v;
+  const uint16_t* p = static_cast<const uint16_t*>(op.ptr);
+  if (op.kind == 0) {
+    const long base = static_cast<long>(k) * op.ld_k;
+    if (vec_ok && r0 + 8 <= rows) {
+      v = *reinterpret_cast<const u16x8*>(p + base + r0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (r0 + i < rows) v[i] = p[base + static_cast<long>(r0 + i) * op.ld_r];
+    }
+    return v;
+  }
+  // kind 2: rows are (kh, kw, c) of the conv, k is the output pixel (n, oy, ox)
+  const ConvGeom& g = op.g;
+  const int c0 = r0 % g.C;
+  const int rs = r0 / g.C;
+  const int kw = rs % g.S;
+  const int kh = rs / g.S;
+  const int HWo = g.Ho * g.Wo;
+  const int n = k / HWo;
+  const int rem = k - n * HWo;
+  const int oy = rem / g.Wo;
+  const int ox = rem - oy * g.Wo;
+  const int iy = oy * g.stride - g.pad + kh;
+  const int ix = ox * g.stride - g.pad + kw;
+  if (iy < 0 || iy >= g.H || ix < 0 || ix >= g.W) return v;
+  v = *reinterpret_cast<const u16x8*>(p + ((static_cast<long>(n) * g.H + iy) * g.W + ix) * g.C + c0);
+  return v;
+}
+
+template <int BROWS, int BK, bool KC>
+struct TileLoader {
+  static constexpr int kVecs = BROWS * BK / 8;
+  static constexpr int kPer = (kVecs + kThreads - 1) / kThreads;
+  u16x8 regs[kPer];
+
+  __device__ __forceinline__ void load(const Operand& op, int rows, int K, int row0, int k0,
+                                       bool vec_ok) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      if (v < kVecs) {
+        if constexpr (KC) {
+          const int row = v / (BK / 8);
+          const int kv = v - row * (BK / 8);
+          regs[i] = load_kc(op, rows, K, row0 + row, k0 + kv * 8, vec_ok);
+        } else {
+          const int kk = v / (BROWS / 8);
+          const int rv = v - kk * (BROWS / 8);
+          regs[i] = load_rc(op, rows, K, row0 + rv * 8, k0 + kk, vec_ok);
+        }
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(uint16_t* lds) {  // lds: [BROWS][BK + 8]
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      if (v < kVecs) {
+        if constexpr (KC) {
+          const int row = v / (BK / 8);
+          const int kv = v - row * (BK / 8);
+          *reinterpret_cast<u16x8*>(lds + row * (BK + 8) + kv * 8) = regs[i];
+        } else {
+          const int kk = v / (BROWS / 8);
+          const int rv = v - kk * (BROWS / 8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) lds[(rv * 8 + j) * (BK + 8) + kk] = regs[i][j];
+        }
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ float apply_epi(float v, int epi, int m, int n, const GemmArgs& a) {
+  if ((epi & EPI_BIAS) && n < a.nbias) v += a.bias[n];
+  if (epi & EPI_DRELU) v = (bf2f(a.aux[static_cast<long>(m) * a.ldaux + n]) > 0.f) ? v : 0.f;
+  if (epi & EPI_RELU) v = fmaxf(v, 0.f);
+  return v;
+}
+
+__device__ __forceinline__ void store_out(float v, int epi, int m, int n, const GemmArgs& a) {
+  const long off = static_cast<long>(m) * a.ldo + n;
+  if (epi & EPI_OUT_F32) {
+    float* o = static_cast<float*>(a.out);
+    if (epi & EPI_ACCUM) v += o[off];
+    o[off] = v;
+  } else {
+    static_cast<uint16_t*>(a.out)[off] = f2bf(v);
+  }
+}
+
+template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC>
+__global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles_m, int tiles_n,
+                                                        int k_per_split, int a_vec, int b_vec) {
+  static_assert(WM * WN == 4, "4 waves per block");
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int LDS_A = BM * (BK + 8), LDS_B = BN * (BK + 8);
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (LDS_A + LDS_B)];
+
+  // XCD-aware tile id remap (bijective; see cdna_hip_programming.md §5 "XCD swizzle").
+  const int ntiles = tiles_m * tiles_n;
+  const int orig = blockIdx.x;
+  int tile = orig;
+  if (ntiles > 8) {
+    const int q = ntiles / 8, r = ntiles % 8, xcd = orig % 8;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  }
+  // group tiles along M in bands of 8 so co-resident tiles reuse B columns
+  constexpr int GROUP = 8;
+  const int group_sz = GROUP * tiles_n;
+  const int gid = tile / group_sz;
+  const int first_m = gid * GROUP;
+  const int gm = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (tile % group_sz) % gm;
+  const int tn = (tile % group_sz) / gm;
+
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kz = blockIdx.z;
+  const int kbeg = kz * k_per_split;
+  const int kend = min(args.K, kbeg + k_per_split);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  TileLoader<BM, BK, AKC> la;
+  TileLoader<BN, BK, BKC> lb;
+  const bool avec = a_vec != 0, bvec = b_vec != 0;
+  // Reduction bound for the loaders is kend (zero fill past the split's end).
+  if (nk > 0) {
+    la.load(args.a, args.M, kend, m0, kbeg, avec);
+    lb.load(args.b, args.N, kend, n0, kbeg, bvec);
+    la.store(smem);
+    lb.store(smem + LDS_A);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      la.load(args.a, args.M, kend, m0, kbeg + (kt + 1) * BK, avec);
+      lb.load(args.b, args.N, kend, n0, kbeg + (kt + 1) * BK, bvec);
+    }
+    const uint16_t* As = smem + cur * (LDS_A + LDS_B);
+    const uint16_t* Bs = As + LDS_A;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(
+            As + (wm * WTM + i * 16 + (lane & 15)) * (BK + 8) + kk * 32 + (lane >> 4) * 8);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(
+            Bs + (wn * WTN + j * 16 + (lane & 15)) * (BK + 8) + kk * 32 + (lane >> 4) * 8);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      uint16_t* nxt = smem + (cur ^ 1) * (LDS_A + LDS_B);
+      la.store(nxt);
+      lb.store(nxt + LDS_A);
+    }
+    __syncthreads();
+  }
+
+  // Epilogue. C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + reg.
+  const bool split = gridDim.z > 1;
+  float* ws = args.workspace;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * WTN + j * 16 + (lane & 15);
+      if (n >= args.N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+        if (m >= args.M) continue;
+        float v = acc[i][j][r];
+        if (split) {
+          ws[(static_cast<long>(kz) * args.M + m) * args.N + n] = v;
+        } else {
+          v = apply_epi(v, args.epi, m, n, args);
+          store_out(v, args.epi, m, n, args);
+        }
+      }
+    }
+  }
+}
+
+__global__ void gemm_splitk_reduce(GemmArgs args, int splits) {
+  const long total = static_cast<long>(args.M) * args.N;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    float v = 0.f;
+    for (int z = 0; z < splits; ++z) v += args.workspace[z * total + i];
+    const int m = static_cast<int>(i / args.N);
+    const int n = static_cast<int>(i - static_cast<long>(m) * args.N);
+    v = apply_epi(v, args.epi, m, n, args);
+    store_out(v, args.epi, m, n, args);
+  }
+}
+
+template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC>
+hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
+  const int tm = ceil_div(a.M, BM), tn = ceil_div(a.N, BN);
+  int kps = ceil_div(a.K, splitk);
+  kps = ceil_div(kps, BK) * BK;
+  splitk = ceil_div(a.K, kps);
+  // Vector (16 B) loads are legal when the contiguous dimension and the other stride keep
+  // every 8-element group 16-byte aligned.
+  auto vec_ok = [](const Operand& o, bool kc, int rows, int K) {
+    if (o.kind != 0) return 1;
+    if (kc) return (o.ld_k == 1 && o.ld_r % 8 == 0 && (reinterpret_cast<uintptr_t>(o.ptr) & 15) == 0) ? 1 : 0;
+    return (o.ld_r == 1 && o.ld_k % 8 == 0 && (reinterpret_cast<uintptr_t>(o.ptr) & 15) == 0) ? 1 : 0;
+  };
+  const int av = vec_ok(a.a, AKC, a.M, a.K), bv = vec_ok(a.b, BKC, a.N, a.K);
+  dim3 grid(tm * tn, 1, splitk);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AKC, BKC>), grid, dim3(kThreads), 0, s, a, tm, tn,
+                     kps, av, bv);
+  if (splitk > 1) {
+    const long total = static_cast<long>(a.M) * a.N;
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(stream_grid(total, 256)), dim3(256), 0, s, a, splitk);
+  }
+  return hipGetLastError();
+}
+
+template <bool AKC, bool BKC>
+hipError_t dispatch_tiles(const GemmArgs& a, hipStream_t s) {
+  const long t128 = static_cast<long>(ceil_div(a.M, 128)) * ceil_div(a.N, 128);
+  const long t64 = static_cast<long>(ceil_div(a.M, 64)) * ceil_div(a.N, 64);
+  // Split-K only where a workspace was provided and the tile grid cannot fill the chip.
+  auto pick_split = [&](long tiles, int bk) {
+    if (a.workspace == nullptr || a.splitk <= 1) return 1;
+    int sk = 1;
+    while (sk < a.splitk && tiles * sk < 512 && a.K / (sk * 2) >= 4 * bk) sk *= 2;
+    return sk;
+  };
+  if (a.N <= 32) {
+    const long t = static_cast<long>(ceil_div(a.M, 128)) * ceil_div(a.N, 32);
+    return launch_cfg<128, 32, 32, 4, 1, AKC, BKC>(a, s, pick_split(t, 32));
+  }
+  if (a.M <= 32) {
+    const long t = static_cast<long>(ceil_div(a.M, 32)) * ceil_div(a.N, 128);
+    return launch_cfg<32, 128, 32, 1, 4, AKC, BKC>(a, s, pick_split(t, 32));
+  }
+  if (t128 >= 256) return launch_cfg<128, 128, 32, 2, 2, AKC, BKC>(a, s, pick_split(t128, 32));
+  return launch_cfg<64, 64, 32, 2, 2, AKC, BKC>(a, s, pick_split(t64, 32));
+}
+
+bool is_kc(const Operand& o) {
+  if (o.kind == 1 || o.kind == 3) return true;
+  if (o.kind == 2) return false;
+  return o.ld_k == 1;
+}
+
+}  // namespace
+
+hipError_t gemm_bf16(const GemmArgs& a, hipStream_t s) {
+  if (a.M <= 0 || a.N <= 0) return hipSuccess;
+  const bool akc = is_kc(a.a), bkc = is_kc(a.b);
+  if (akc && bkc) return dispatch_tiles<true, true>(a, s);
+  if (akc && !bkc) return dispatch_tiles<true, false>(a, s);
+  if (!akc && bkc) return dispatch_tiles<false, true>(a, s);
+  return dispatch_tiles<false, false>(a, s);
+}
+
+}  // namespace pde

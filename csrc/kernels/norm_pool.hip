@@ -1,0 +1,509 @@
+// BatchNorm (training, NHWC bf16), max/avg pooling, dropout and EmbeddingBag kernels (gfx950).
+//
+// BatchNorm follows SURVEY.md §2.5 / §7.4 H2: per-micro-batch batch statistics in fp32, bf16
+// activations.  Forward = shifted-sum partials per block -> per-channel finalize (fixed order,
+// deterministic; running-stat update with unbiased variance) -> fused normalize(+residual)(+ReLU).
+// Backward = partials of (sum dy, sum dy*xhat) with the ReLU mask applied on the fly -> finalize ->
+// fused dx (+ residual grad).  Every pass streams 16 B (8 channels) per lane.
+#include "common.cuh"
+#include "pde_kernels.h"
+
+namespace pde {
+
+namespace {
+
+// Thread -> (row-in-iteration, 8-channel group) mapping for [P][C] streaming reductions.
+struct RowGroupMap {
+  int G, rows_per_iter, r, g;
+  bool active;
+  __device__ RowGroupMap(int C) {
+    G = C / 8;
+    const int gg = G < 256 ? G : 256;
+    rows_per_iter = 256 / gg;
+    r = threadIdx.x / gg;
+    g = threadIdx.x % gg;
+    active = r < rows_per_iter;
+  }
+};
+
+__device__ __forceinline__ void load8(const uint16_t* p, float (&v)[8]) {
+  const u16x8 u = *reinterpret_cast<const u16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf2f(u[j]);
+}
+
+// Partial shifted sums: ws[blk][0][c] = sum(x - K_c), ws[blk][1][c] = sum((x - K_c)^2), K_c = x[0][c].
+__global__ __launch_bounds__(256) void k_bn_stats(const uint16_t* __restrict__ x, int P, int C, int rows_per_block,
+                                                  float* __restrict__ ws) {
+  const RowGroupMap mp(C);
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(P, r0 + rows_per_block);
+  for (int gbase = 0; gbase < mp.G; gbase += 256 / mp.rows_per_iter) {
+    const int g = gbase + mp.g;
+    float s1[8], s2[8], piv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+    const bool ok = mp.active && g < mp.G;
+    if (ok) {
+      load8(x + g * 8, piv);
+      for (int r = r0 + mp.r; r < r1; r += mp.rows_per_iter) {
+        float v[8];
+        load8(x + static_cast<long>(r) * C + g * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float d = v[j] - piv[j]; s1[j] += d; s2[j] += d * d; }
+      }
+    }
+    // reduce over the rows_per_iter threads sharing g via LDS
+    __shared__ float red[2][256][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { red[0][threadIdx.x][j] = s1[j]; red[1][threadIdx.x][j] = s2[j]; }
+    __syncthreads();
+    if (mp.r == 0 && ok) {
+      const int gg = 256 / mp.rows_per_iter;
+      for (int rr = 1; rr < mp.rows_per_iter; ++rr) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { s1[j] += red[0][rr * gg + mp.g][j]; s2[j] += red[1][rr * gg + mp.g][j]; }
+      }
+      float* o = ws + static_cast<long>(blockIdx.x) * 2 * C;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { o[g * 8 + j] = s1[j]; o[C + g * 8 + j] = s2[j]; }
+    }
+    __syncthreads();
+  }
+}
+
+// Per channel: combine partials -> mean, invstd, scale/shift; update running stats.
+__global__ void k_bn_finalize(const uint16_t* __restrict__ x, const float* __restrict__ ws, int nblk, int P, int C,
+                              const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                              float momentum, float* __restrict__ running_mean, float* __restrict__ running_var,
+                              float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                              float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    s1 += ws[static_cast<long>(b) * 2 * C + c];
+    s2 += ws[static_cast<long>(b) * 2 * C + C + c];
+  }
+  const float piv = bf2f(x[c]);
+  const double n = static_cast<double>(P);
+  const double mean_s = s1 / n;
+  double var = s2 / n - mean_s * mean_s;
+  if (var < 0.0) var = 0.0;
+  const float mean = static_cast<float>(mean_s) + piv;
+  const float invstd = rsqrtf(static_cast<float>(var) + eps);
+  save_mean[c] = mean;
+  save_invstd[c] = invstd;
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  scale[c] = g * invstd;
+  shift[c] = b - mean * g * invstd;
+  if (running_mean) {
+    const float unbiased = P > 1 ? static_cast<float>(var * n / (n - 1.0)) : static_cast<float>(var);
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+  }
+}
+
+// y = x * scale + shift (+ res) (relu) ; bf16 out
+__global__ void k_bn_apply(const uint16_t* __restrict__ x, const float* __restrict__ scale,
+                           const float* __restrict__ shift, const uint16_t* __restrict__ res, uint16_t* __restrict__ y,
+                           long nvec, int C, int relu) {
+  const int G = C / 8;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < nvec;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int g = static_cast<int>(i % G);
+    float v[8];
+    load8(x + i * 8, v);
+    float rv[8];
+    if (res) load8(res + i * 8, rv);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = v[j] * scale[g * 8 + j] + shift[g * 8 + j];
+      if (res) t += rv[j];
+      if (relu) t = fmaxf(t, 0.f);
+      o[j] = f2bf(t);
+    }
+    reinterpret_cast<u16x8*>(y)[i] = o;
+  }
+}
+
+// Backward partials: ws[blk][0][c] = sum dyr, ws[blk][1][c] = sum dyr * (x - mean) * invstd,
+// dyr = dy * (relu ? y > 0 : 1)
+__global__ __launch_bounds__(256) void k_bn_bwd_reduce(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                                                       const uint16_t* __restrict__ y, const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd, int P, int C,
+                                                       int rows_per_block, int relu, float* __restrict__ ws) {
+  const RowGroupMap mp(C);
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(P, r0 + rows_per_block);
+  for (int gbase = 0; gbase < mp.G; gbase += 256 / mp.rows_per_iter) {
+    const int g = gbase + mp.g;
+    float s1[8], s2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+    const bool ok = mp.active && g < mp.G;
+    if (ok) {
+      float mu[8], is[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { mu[j] = mean[g * 8 + j]; is[j] = invstd[g * 8 + j]; }
+      for (int r = r0 + mp.r; r < r1; r += mp.rows_per_iter) {
+        const long off = static_cast<long>(r) * C + g * 8;
+        float d[8], xv[8];
+        load8(dy + off, d);
+        load8(x + off, xv);
+        if (relu) {
+          float yv[8];
+          load8(y + off, yv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { s1[j] += d[j]; s2[j] += d[j] * (xv[j] - mu[j]) * is[j]; }
+      }
+    }
+    __shared__ float red[2][256][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { red[0][threadIdx.x][j] = s1[j]; red[1][threadIdx.x][j] = s2[j]; }
+    __syncthreads();
+    if (mp.r == 0 && ok) {
+      const int gg = 256 / mp.rows_per_iter;
+      for (int rr = 1; rr < mp.rows_per_iter; ++rr) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { s1[j] += red[0][rr * gg + mp.g][j]; s2[j] += red[1][rr * gg + mp.g][j]; }
+      }
+      float* o = ws + static_cast<long>(blockIdx.x) * 2 * C;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { o[g * 8 + j] = s1[j]; o[C + g * 8 + j] = s2[j]; }
+    }
+    __syncthreads();
+  }
+}
+
+// Per channel: dgamma, dbeta (written / accumulated) and the dx coefficients.
+__global__ void k_bn_bwd_finalize(const float* __restrict__ ws, int nblk, int P, int C, const float* __restrict__ gamma,
+                                  const float* __restrict__ invstd, float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                  float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int b = 0; b < nblk; ++b) {
+    s1 += ws[static_cast<long>(b) * 2 * C + c];
+    s2 += ws[static_cast<long>(b) * 2 * C + C + c];
+  }
+  if (dgamma) dgamma[c] = s2;
+  if (dbeta) dbeta[c] = s1;
+  const float a = (gamma ? gamma[c] : 1.f) * invstd[c];
+  coef[c] = a;                                   // a
+  coef[C + c] = a * s1 / static_cast<float>(P);  // b
+  coef[2 * C + c] = a * s2 / static_cast<float>(P);  // c
+}
+
+// dx = a*dyr - b - c*xhat ; dres = dyr (if requested)
+__global__ void k_bn_bwd_apply(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                               const uint16_t* __restrict__ y, const float* __restrict__ mean,
+                               const float* __restrict__ invstd, const float* __restrict__ coef, long nvec, int C,
+                               int relu, uint16_t* __restrict__ dx, uint16_t* __restrict__ dres) {
+  const int G = C / 8;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < nvec;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int g = static_cast<int>(i % G);
+    float d[8], xv[8];
+    load8(dy + i * 8, d);
+    load8(x + i * 8, xv);
+    if (relu) {
+      float yv[8];
+      load8(y + i * 8, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+    }
+    u16x8 o, orr;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = g * 8 + j;
+      const float xh = (xv[j] - mean[c]) * invstd[c];
+      o[j] = f2bf(coef[c] * d[j] - coef[C + c] - coef[2 * C + c] * xh);
+      orr[j] = f2bf(d[j]);
+    }
+    reinterpret_cast<u16x8*>(dx)[i] = o;
+    if (dres) reinterpret_cast<u16x8*>(dres)[i] = orr;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Max pooling, NHWC, any C (scalar channel loop for C % 8 != 0, the MNIST CNN's 10 / 20 channels).
+// Saves the argmax window index (uint8) for the backward gather.
+__global__ void k_maxpool_fwd(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, uint8_t* __restrict__ idx,
+                              int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p, int relu) {
+  const long total = static_cast<long>(N) * Ho * Wo * C;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int c = static_cast<int>(i % C);
+    long t = i / C;
+    const int ox = static_cast<int>(t % Wo);
+    t /= Wo;
+    const int oy = static_cast<int>(t % Ho);
+    const int n = static_cast<int>(t / Ho);
+    float best = -INFINITY;
+    int bi = 0;
+    for (int ky = 0; ky < k; ++ky) {
+      const int iy = oy * s - p + ky;
+      if (iy < 0 || iy >= H) continue;
+      for (int kx = 0; kx < k; ++kx) {
+        const int ix = ox * s - p + kx;
+        if (ix < 0 || ix >= W) continue;
+        const float v = bf2f(x[((static_cast<long>(n) * H + iy) * W + ix) * C + c]);
+        if (v > best) { best = v; bi = ky * k + kx; }
+      }
+    }
+    if (relu) best = fmaxf(best, 0.f);
+    y[i] = f2bf(best);
+    idx[i] = static_cast<uint8_t>(bi);
+  }
+}
+
+// Gather form: each input element sums the grads of the outputs whose argmax it is (deterministic).
+__global__ void k_maxpool_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+                              const uint8_t* __restrict__ idx, uint16_t* __restrict__ dx, int N, int H, int W, int C,
+                              int Ho, int Wo, int k, int s, int p, int relu) {
+  const long total = static_cast<long>(N) * H * W * C;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int c = static_cast<int>(i % C);
+    long t = i / C;
+    const int ix = static_cast<int>(t % W);
+    t /= W;
+    const int iy = static_cast<int>(t % H);
+    const int n = static_cast<int>(t / H);
+    float acc = 0.f;
+    // outputs oy with oy*s - p <= iy <= oy*s - p + k - 1
+    const int oy_lo = max(0, (iy + p - k + s) / s), oy_hi = min(Ho - 1, (iy + p) / s);
+    const int ox_lo = max(0, (ix + p - k + s) / s), ox_hi = min(Wo - 1, (ix + p) / s);
+    for (int oy = oy_lo; oy <= oy_hi; ++oy) {
+      const int ky = iy + p - oy * s;
+      if (ky < 0 || ky >= k) continue;
+      for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+        const int kx = ix + p - ox * s;
+        if (kx < 0 || kx >= k) continue;
+        const long o = ((static_cast<long>(n) * Ho + oy) * Wo + ox) * C + c;
+        if (idx[o] == ky * k + kx) {
+          if (!relu || bf2f(y[o]) > 0.f) acc += bf2f(dy[o]);
+        }
+      }
+    }
+    dx[i] = f2bf(acc);
+  }
+}
+
+// Global average pool NHWC [N][HW][C] -> [N][C] (bf16 out), one thread per (n, c-group of 8).
+__global__ void k_avgpool_fwd(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int N, int HW, int C) {
+  const int G = C / 8;
+  const long total = static_cast<long>(N) * G;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int g = static_cast<int>(i % G);
+    const int n = static_cast<int>(i / G);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int q = 0; q < HW; ++q) {
+      float v[8];
+      load8(x + (static_cast<long>(n) * HW + q) * C + g * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+    u16x8 o;
+    const float inv = 1.f / static_cast<float>(HW);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j] * inv);
+    reinterpret_cast<u16x8*>(y)[i] = o;
+  }
+}
+
+__global__ void k_avgpool_bwd(const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx, int N, int HW, int C) {
+  const int G = C / 8;
+  const long total = static_cast<long>(N) * HW * G;
+  const float inv = 1.f / static_cast<float>(HW);
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int g = static_cast<int>(i % G);
+    const int n = static_cast<int>(i / (static_cast<long>(HW) * G));
+    float v[8];
+    load8(dy + static_cast<long>(n) * C + g * 8, v);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j] * inv);
+    reinterpret_cast<u16x8*>(dx)[i] = o;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Dropout.  Counter-based hash RNG (splitmix64 of seed ^ element id): deterministic for a given
+// (seed, offset), no state.  Channel mode (Dropout2d): one draw per (n, c) of an NHWC tensor.
+__device__ __forceinline__ float uniform01(unsigned long long seed, unsigned long long id) {
+  unsigned long long z = seed + 0x9E3779B97F4A7C15ULL * (id + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  z ^= z >> 31;
+  return static_cast<float>(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// mode 0: elementwise on [n_elems]; mode 1: channel mask over NHWC with (HW, C).
+// mask out (uint8) is written so backward is a pure multiply.
+__global__ void k_dropout_fwd(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, uint8_t* __restrict__ mask,
+                              long n, int mode, int HW, int C, float p, unsigned long long seed) {
+  const float scale = 1.f / (1.f - p);
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    unsigned long long id;
+    if (mode == 0) {
+      id = static_cast<unsigned long long>(i);
+    } else {
+      const long c = i % C;
+      const long nimg = i / (static_cast<long>(HW) * C);
+      id = static_cast<unsigned long long>(nimg * C + c);
+    }
+    const bool keep = uniform01(seed, id) >= p;
+    mask[i] = keep ? 1 : 0;
+    y[i] = keep ? f2bf(bf2f(x[i]) * scale) : uint16_t(0);
+  }
+}
+
+__global__ void k_dropout_bwd(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
+                              uint16_t* __restrict__ dx, long n, float p) {
+  const float scale = 1.f / (1.f - p);
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<long>(gridDim.x) * blockDim.x)
+    dx[i] = mask[i] ? f2bf(bf2f(dy[i]) * scale) : uint16_t(0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// EmbeddingBag (mode=sum): one wave per bag, lanes over the embedding dim.
+__global__ void k_embbag_fwd(const float* __restrict__ w, const int64_t* __restrict__ idx,
+                             const int64_t* __restrict__ off, int B, long L, int D, float* __restrict__ out) {
+  const int bag = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (bag >= B) return;
+  const long s = off[bag];
+  const long e = bag + 1 < B ? off[bag + 1] : L;
+  for (int d = lane; d < D; d += 64) {
+    float acc = 0.f;
+    for (long j = s; j < e; ++j) acc += w[idx[j] * D + d];
+    out[static_cast<long>(bag) * D + d] = acc;
+  }
+}
+
+// dW[idx[j], :] += dy[bag(j), :]  (fp32 atomics; the table is tiny and rows are 64 B)
+__global__ void k_embbag_bwd(const float* __restrict__ dy, const int64_t* __restrict__ idx,
+                             const int64_t* __restrict__ off, int B, long L, int D, float* __restrict__ dw) {
+  const int bag = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (bag >= B) return;
+  const long s = off[bag];
+  const long e = bag + 1 < B ? off[bag + 1] : L;
+  for (long j = s; j < e; ++j)
+    for (int d = lane; d < D; d += 64) atomicAdd(dw + idx[j] * D + d, dy[static_cast<long>(bag) * D + d]);
+}
+
+int bn_blocks(int P, int C, int& rows_per_block) {
+  const int G = C / 8;
+  const int rpi = 256 / (G < 256 ? G : 256);
+  // aim for ~16 row-iterations per block, at most 512 blocks
+  int nblk = ceil_div(P, rpi * 16);
+  if (nblk > 512) nblk = 512;
+  if (nblk < 1) nblk = 1;
+  rows_per_block = ceil_div(P, nblk);
+  nblk = ceil_div(P, rows_per_block);
+  return nblk;
+}
+
+}  // namespace
+
+int bn_workspace_blocks(int P, int C) {
+  int rpb;
+  return bn_blocks(P, C, rpb);
+}
+
+hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, const float* beta, float eps,
+                        float momentum, float* running_mean, float* running_var, float* save_mean,
+                        float* save_invstd, float* scale_shift, float* ws, const uint16_t* res, int relu,
+                        uint16_t* y, hipStream_t s) {
+  int rpb;
+  const int nblk = bn_blocks(P, C, rpb);
+  hipLaunchKernelGGL(k_bn_stats, dim3(nblk), dim3(256), 0, s, x, P, C, rpb, ws);
+  hipLaunchKernelGGL(k_bn_finalize, dim3(ceil_div(C, 256)), dim3(256), 0, s, x, ws, nblk, P, C, gamma, beta, eps,
+                     momentum, running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C);
+  const long nvec = static_cast<long>(P) * C / 8;
+  hipLaunchKernelGGL(k_bn_apply, dim3(stream_grid(nvec, 256)), dim3(256), 0, s, x, scale_shift, scale_shift + C,
+                     res, y, nvec, C, relu);
+  return hipGetLastError();
+}
+
+hipError_t bn_apply(const uint16_t* x, int P, int C, const float* scale, const float* shift, const uint16_t* res,
+                    int relu, uint16_t* y, hipStream_t s) {
+  const long nvec = static_cast<long>(P) * C / 8;
+  hipLaunchKernelGGL(k_bn_apply, dim3(stream_grid(nvec, 256)), dim3(256), 0, s, x, scale, shift, res, y, nvec, C,
+                     relu);
+  return hipGetLastError();
+}
+
+hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
+                  const float* gamma, int P, int C, int relu, float* dgamma, float* dbeta, float* ws, float* coef,
+                  uint16_t* dx, uint16_t* dres, hipStream_t s) {
+  int rpb;
+  const int nblk = bn_blocks(P, C, rpb);
+  hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(nblk), dim3(256), 0, s, dy, x, y, mean, invstd, P, C, rpb, relu, ws);
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(ceil_div(C, 256)), dim3(256), 0, s, ws, nblk, P, C, gamma, invstd,
+                     dgamma, dbeta, coef);
+  const long nvec = static_cast<long>(P) * C / 8;
+  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(stream_grid(nvec, 256)), dim3(256), 0, s, dy, x, y, mean, invstd, coef,
+                     nvec, C, relu, dx, dres);
+  return hipGetLastError();
+}
+
+hipError_t maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
+                       int k, int st, int p, int relu, hipStream_t s) {
+  const long total = static_cast<long>(N) * Ho * Wo * C;
+  hipLaunchKernelGGL(k_maxpool_fwd, dim3(stream_grid(total, 256)), dim3(256), 0, s, x, y, idx, N, H, W, C, Ho, Wo,
+                     k, st, p, relu);
+  return hipGetLastError();
+}
+hipError_t maxpool_bwd(const uint16_t* dy, const uint16_t* y, const uint8_t* idx, uint16_t* dx, int N, int H, int W,
+                       int C, int Ho, int Wo, int k, int st, int p, int relu, hipStream_t s) {
+  const long total = static_cast<long>(N) * H * W * C;
+  hipLaunchKernelGGL(k_maxpool_bwd, dim3(stream_grid(total, 256)), dim3(256), 0, s, dy, y, idx, dx, N, H, W, C, Ho,
+                     Wo, k, st, p, relu);
+  return hipGetLastError();
+}
+hipError_t avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s) {
+  const long total = static_cast<long>(N) * (C / 8);
+  hipLaunchKernelGGL(k_avgpool_fwd, dim3(stream_grid(total, 256)), dim3(256), 0, s, x, y, N, HW, C);
+  return hipGetLastError();
+}
+hipError_t avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t s) {
+  const long total = static_cast<long>(N) * HW * (C / 8);
+  hipLaunchKernelGGL(k_avgpool_bwd, dim3(stream_grid(total, 256)), dim3(256), 0, s, dy, dx, N, HW, C);
+  return hipGetLastError();
+}
+hipError_t dropout_fwd(const uint16_t* x, uint16_t* y, uint8_t* mask, long n, int mode, int HW, int C, float p,
+                       unsigned long long seed, hipStream_t s) {
+  hipLaunchKernelGGL(k_dropout_fwd, dim3(stream_grid(n, 256)), dim3(256), 0, s, x, y, mask, n, mode, HW, C, p, seed);
+  return hipGetLastError();
+}
+hipError_t dropout_bwd(const uint16_t* dy, const uint8_t* mask, uint16_t* dx, long n, float p, hipStream_t s) {
+  hipLaunchKernelGGL(k_dropout_bwd, dim3(stream_grid(n, 256)), dim3(256), 0, s, dy, mask, dx, n, p);
+  return hipGetLastError();
+}
+hipError_t embbag_fwd(const float* w, const int64_t* idx, const int64_t* off, int B, long L, int D, float* out,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_embbag_fwd, dim3(ceil_div(B, 4)), dim3(256), 0, s, w, idx, off, B, L, D, out);
+  return hipGetLastError();
+}
+hipError_t embbag_bwd(const float* dy, const int64_t* idx, const int64_t* off, int B, long L, int D, float* dw,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_embbag_bwd, dim3(ceil_div(B, 4)), dim3(256), 0, s, dy, idx, off, B, L, D, dw);
+  return hipGetLastError();
+}
+
+}  // namespace pde

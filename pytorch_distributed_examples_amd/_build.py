@@ -1,0 +1,120 @@
+"""In-tree native build: hipcc (gfx950) for csrc/**/*.hip, the host compiler for the C++ runtime and
+bindings, linked into ``pytorch_distributed_examples_amd/_C*.so`` against the HIP runtime and RCCL that
+torch itself loads (torch ships its own libamdhip64.so.7 / librccl.so.1 with the same
+sonames as /opt/rocm, so the extension binds to the already-loaded copies).
+
+No hipify step runs: sources are written in HIP directly, and ``torch.utils.cpp_extension`` is not
+used to compile them (it would hipify on ROCm).  Objects are rebuilt only when their source or a header
+changed.  ``python -m pytorch_distributed_examples_amd._build`` builds from the command line.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO = PKG_DIR.parent
+CSRC = REPO / "csrc"
+BUILD = REPO / "build" / "native"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = os.environ.get("PDE_OFFLOAD_ARCH", "gfx950")
+
+EXTENSIONS = {
+    # module name -> (hip sources, host C++ sources)
+    "_C": (
+        ["kernels/gemm.hip", "kernels/elementwise.hip", "kernels/loss.hip", "kernels/optim.hip",
+         "kernels/norm_pool.hip"],
+        ["bindings.cpp"],
+    ),
+}
+
+
+def _torch_paths():
+    import torch  # noqa: WPS433
+
+    tdir = Path(torch.__file__).resolve().parent
+    return tdir, tdir / "include", tdir / "lib", bool(torch._C._GLIBCXX_USE_CXX11_ABI)
+
+
+def _ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _headers() -> list[Path]:
+    return sorted(CSRC.rglob("*.h")) + sorted(CSRC.rglob("*.cuh"))
+
+
+def _stale(obj: Path, src: Path, headers: list[Path]) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    if src.stat().st_mtime > t:
+        return True
+    return any(h.stat().st_mtime > t for h in headers)
+
+
+def _run(cmd: list[str]) -> None:
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("native build failed:\n  " + " ".join(cmd) + "\n" + res.stdout + res.stderr)
+
+
+def build(verbose: bool = False, jobs: int | None = None) -> list[Path]:
+    """Compile every extension; returns the paths of the built shared objects."""
+    tdir, tinc, tlib, cxx11 = _torch_paths()
+    hipcc = shutil.which("hipcc") or str(ROCM / "bin" / "hipcc")
+    cxx = os.environ.get("CXX", "g++")
+    py_inc = sysconfig.get_paths()["include"]
+    BUILD.mkdir(parents=True, exist_ok=True)
+    headers = _headers()
+    abi = f"-D_GLIBCXX_USE_CXX11_ABI={1 if cxx11 else 0}"
+    common_inc = [f"-I{CSRC / 'include'}", f"-I{CSRC / 'kernels'}", f"-I{CSRC / 'comm'}"]
+    torch_inc = [f"-I{tinc}", f"-I{tinc / 'torch/csrc/api/include'}", f"-I{py_inc}", f"-I{ROCM / 'include'}"]
+
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    outputs = []
+    for name, (hip_srcs, cpp_srcs) in EXTENSIONS.items():
+        objs: list[Path] = []
+        tasks = []
+        for rel in hip_srcs:
+            src = CSRC / rel
+            obj = BUILD / (rel.replace("/", "_") + ".o")
+            objs.append(obj)
+            if _stale(obj, src, headers):
+                tasks.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", abi,
+                              "-munsafe-fp-atomics", *common_inc, *([f"-I{ROCM / 'include'}"]),
+                              "-c", str(src), "-o", str(obj)])
+        for rel in cpp_srcs:
+            src = CSRC / rel
+            obj = BUILD / (rel.replace("/", "_") + ".o")
+            objs.append(obj)
+            if _stale(obj, src, headers):
+                tasks.append([cxx, "-O2", "-std=c++17", "-fPIC", abi, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+                              f"-DTORCH_EXTENSION_NAME={name}", "-DTORCH_API_INCLUDE_EXTENSION_H",
+                              "-Wno-deprecated-declarations", *common_inc, *torch_inc, "-c", str(src), "-o", str(obj)])
+        if tasks:
+            with cf.ThreadPoolExecutor(jobs) as ex:
+                for cmd in tasks:
+                    if verbose:
+                        print(" ".join(cmd), flush=True)
+                list(ex.map(_run, tasks))
+        so = PKG_DIR / f"{name}{_ext_suffix()}"
+        if not so.exists() or any(o.stat().st_mtime > so.stat().st_mtime for o in objs):
+            link = [cxx, "-shared", "-o", str(so), *map(str, objs), f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch",
+                    "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64", "-lrccl",
+                    f"-Wl,-rpath,{tlib}", "-Wl,--no-as-needed"]
+            if verbose:
+                print(" ".join(link), flush=True)
+            _run(link)
+        outputs.append(so)
+    return outputs
+
+
+if __name__ == "__main__":
+    for p in build(verbose="-v" in sys.argv):
+        print(p)

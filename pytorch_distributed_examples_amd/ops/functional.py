@@ -1,0 +1,396 @@
+"""Autograd functions over the gfx950 HIP kernels (``_C``), with a plain-PyTorch CPU path.
+
+Device policy
+-------------
+* GPU tensors take the native path: activations are bf16, convolutions are NHWC (channels padded to a
+  multiple of 8 with zeros), every matmul-shaped op runs on the MFMA implicit-GEMM kernel and the
+  element-wise/normalisation work on the fused kernels of ``csrc/kernels``.  The extension is required;
+  a missing build raises (``_native.NativeUnavailable``) instead of silently using ATen.
+* CPU tensors take the reference path (fp32 NCHW ``torch.nn.functional``), which is what the
+  reference scripts run (every reference workload is CPU/gloo) and what the CPU/gloo
+  config of BASELINE.json (config 0) measures.
+
+Parameters always stay in PyTorch's fp32 layout (``Linear.weight`` [out, in], ``Conv2d.weight``
+[Co, Ci, R, S]) so ``state_dict``s interoperate with the reference's snapshot format
+(pytorch_elastic/mnist_ddp_elastic.py:95-104).  The bf16 / re-laid-out compute copies are produced by
+small layout kernels and cached per (parameter version, optimiser generation).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .. import _native
+
+# ---------------------------------------------------------------------------------------------
+# compute-copy cache
+# ---------------------------------------------------------------------------------------------
+_GEN = [0]
+_FORCE_RECOMPUTE = [False]
+
+
+def bump_weight_generation() -> None:
+    """Invalidate all cached bf16 compute copies (called by the fused optimiser after a step)."""
+    _GEN[0] += 1
+
+
+class recompute_weight_copies:
+    """Context manager: never reuse cached copies (used while capturing a hipGraph so the layout
+    kernels become part of the graph and see every replay's updated weights)."""
+
+    def __enter__(self):
+        self._old = _FORCE_RECOMPUTE[0]
+        _FORCE_RECOMPUTE[0] = True
+
+    def __exit__(self, *exc):
+        _FORCE_RECOMPUTE[0] = self._old
+
+
+def _cached(p: torch.Tensor, kind, fn):
+    if _FORCE_RECOMPUTE[0]:
+        return fn()
+    key = (p._version, _GEN[0])
+    cache = p.__dict__.setdefault("_pde_cache", {})
+    ent = cache.get(kind)
+    if ent is None or ent[0] != key:
+        ent = (key, fn())
+        cache[kind] = ent
+    return ent[1]
+
+
+def pad8(c: int) -> int:
+    return (c + 7) // 8 * 8
+
+
+def _C():
+    return _native.C()
+
+
+def _bf16_weight(w: torch.Tensor) -> torch.Tensor:
+    return _cached(w, "bf16", lambda: _C().cast_bf16(w.detach().contiguous()))
+
+
+# ---------------------------------------------------------------------------------------------
+# Linear (+ bias, + ReLU): y = relu?(x W^T + b)
+# ---------------------------------------------------------------------------------------------
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu, out_f32, consumer_masks, mask_input_grad):
+        wb = _bf16_weight(weight)
+        y = _C().linear_fwd(x, wb, bias.detach() if bias is not None else None, relu, out_f32)
+        ctx.relu = relu and not consumer_masks
+        ctx.mask_input_grad = mask_input_grad
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, wb, y if ctx.relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb, y = ctx.saved_tensors
+        dy = dy.contiguous()
+        if dy.dtype != torch.bfloat16:
+            dy = _C().cast_bf16(dy.float().contiguous())
+        if ctx.relu:
+            dy = _C().relu_bwd(dy, y)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _C().linear_dgrad(dy, wb, x if ctx.mask_input_grad else None)
+        if ctx.needs_input_grad[1]:
+            dw = _C().linear_wgrad(dy, x)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = _C().colsum(dy)
+        return dx, dw, db, None, None, None, None
+
+
+def linear(x, weight, bias=None, relu=False, out_f32=False, consumer_masks=False, mask_input_grad=False):
+    """Fused linear layer.
+
+    GPU: bf16 MFMA GEMM with bias/ReLU fused in the epilogue.  ``consumer_masks`` declares that the
+    next layer's backward already applies this layer's ReLU mask (its ``mask_input_grad``), which
+    fuses threshold_backward into the dgrad GEMM epilogue (SURVEY.md §2.5 MLP table).
+    """
+    if not x.is_cuda:
+        y = F.linear(x, weight, bias)
+        return F.relu(y) if relu else y
+    if x.dtype != torch.bfloat16:
+        x = _C().cast_bf16(x.float().contiguous())
+    return _LinearFn.apply(x.contiguous(), weight, bias, relu, out_f32, consumer_masks, mask_input_grad)
+
+
+# ---------------------------------------------------------------------------------------------
+# NHWC implicit-GEMM convolution
+# ---------------------------------------------------------------------------------------------
+class _Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, pad, relu):
+        co, ci, r, s = weight.shape
+        cp = x.shape[3]
+        cop = pad8(co)
+        wf = _cached(weight, ("conv_fwd", cp, cop), lambda: _C().conv_w_fwd(weight.detach().contiguous(), cp, cop))
+        y = _C().conv_fwd(x, wf, bias.detach() if bias is not None else None, r, s, stride, pad, relu, False)
+        ctx.geom = (co, ci, r, s, stride, pad, cp, cop, x.shape[1], x.shape[2])
+        ctx.relu = relu
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, weight, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, y = ctx.saved_tensors
+        co, ci, r, s, stride, pad, cp, cop, h, w = ctx.geom
+        dy = dy.contiguous()
+        if ctx.relu:
+            dy = _C().relu_bwd(dy, y)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wd = _cached(weight, ("conv_dgrad", cp, cop),
+                         lambda: _C().conv_w_dgrad(weight.detach().contiguous(), cp, cop))
+            dx = _C().conv_dgrad(dy, wd, h, w, r, s, stride, pad, None)
+        if ctx.needs_input_grad[1]:
+            g = _C().conv_wgrad(dy, x, r, s, stride, pad)
+            dw = _C().conv_wgrad_oihw(g, co, ci, r, s)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = _C().colsum(dy)[:co]
+        return dx, dw, db, None, None, None
+
+
+def conv2d(x, weight, bias=None, stride=1, padding=0, relu=False):
+    """2-D convolution.  GPU: ``x`` is NHWC bf16 with C padded to a multiple of 8; output NHWC with
+    Cout padded to a multiple of 8 (padded channels are exactly zero).  CPU: NCHW fp32 F.conv2d."""
+    if not x.is_cuda:
+        y = F.conv2d(x, weight, bias, stride=stride, padding=padding)
+        return F.relu(y) if relu else y
+    return _Conv2dFn.apply(x.contiguous(), weight, bias, int(stride), int(padding), relu)
+
+
+def to_native_image(x: torch.Tensor) -> torch.Tensor:
+    """NCHW fp32 input batch -> the device's native activation layout (NHWC bf16 padded on GPU)."""
+    if not x.is_cuda:
+        return x
+    return _C().nchw_to_nhwc(x.float().contiguous(), pad8(x.shape[1]))
+
+
+# ---------------------------------------------------------------------------------------------
+# BatchNorm2d (train: batch statistics; eval: running statistics), fused residual add + ReLU
+# ---------------------------------------------------------------------------------------------
+class _BatchNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, running_mean, running_var, residual, eps, momentum, relu):
+        y, mean, invstd = _C().bn_fwd(x, gamma.detach() if gamma is not None else None,
+                                      beta.detach() if beta is not None else None, running_mean, running_var,
+                                      eps, momentum, residual, relu)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, y, mean, invstd, gamma)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, invstd, gamma = ctx.saved_tensors
+        dx, dg, db, dres = _C().bn_bwd(dy.contiguous(), x, y, mean, invstd,
+                                       gamma.detach() if gamma is not None else None, ctx.relu, ctx.has_res)
+        return dx, dg, db, None, None, (dres if ctx.has_res else None), None, None, None
+
+
+def batch_norm(x, weight, bias, running_mean, running_var, training, momentum=0.1, eps=1e-5, residual=None,
+               relu=False):
+    """BatchNorm2d with optional fused residual add and ReLU:  relu?(bn(x) + residual)."""
+    if not x.is_cuda:
+        y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if relu else y
+    x = x.contiguous()
+    if training:
+        return _BatchNormFn.apply(x, weight, bias, running_mean, running_var,
+                                  residual.contiguous() if residual is not None else None, eps, momentum, relu)
+    invstd = torch.rsqrt(running_var + eps)
+    scale = (weight * invstd if weight is not None else invstd).float().contiguous()
+    shift = ((bias if bias is not None else 0) - running_mean * scale).float().contiguous()
+    return _C().bn_apply(x, scale, shift, residual.contiguous() if residual is not None else None, relu)
+
+
+# ---------------------------------------------------------------------------------------------
+# Pooling
+# ---------------------------------------------------------------------------------------------
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p, relu):
+        y, idx = _C().maxpool_fwd(x, k, s, p, relu)
+        ctx.cfg = (x.shape[1], x.shape[2], k, s, p, relu)
+        ctx.save_for_backward(y, idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, idx = ctx.saved_tensors
+        h, w, k, s, p, relu = ctx.cfg
+        return _C().maxpool_bwd(dy.contiguous(), y, idx, h, w, k, s, p, relu), None, None, None, None
+
+
+def max_pool2d(x, kernel_size, stride=None, padding=0, relu=False):
+    """Max pooling (optionally fused with a following ReLU: relu(maxpool(x)))."""
+    stride = kernel_size if stride is None else stride
+    if not x.is_cuda:
+        y = F.max_pool2d(x, kernel_size, stride, padding)
+        return F.relu(y) if relu else y
+    return _MaxPoolFn.apply(x.contiguous(), int(kernel_size), int(stride), int(padding), relu)
+
+
+class _AvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.hw = (x.shape[1], x.shape[2])
+        return _C().avgpool_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _C().avgpool_bwd(dy.contiguous(), *ctx.hw)
+
+
+def global_avg_pool_flat(x):
+    """AdaptiveAvgPool2d((1, 1)) + flatten -> [N, C]."""
+    if not x.is_cuda:
+        return torch.flatten(F.adaptive_avg_pool2d(x, (1, 1)), 1)
+    return _AvgPoolFn.apply(x.contiguous())
+
+
+def flatten_nchw(x, channels):
+    """Flatten an activation in NCHW order ([N, C*H*W], the reference's ``x.view(-1, 320)``).
+    GPU input is NHWC with padded channels; the real ``channels`` are kept."""
+    if not x.is_cuda:
+        return x.reshape(x.shape[0], -1)
+    return x[..., :channels].permute(0, 3, 1, 2).reshape(x.shape[0], -1).contiguous()
+
+
+# ---------------------------------------------------------------------------------------------
+# Dropout
+# ---------------------------------------------------------------------------------------------
+class _DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, channel, seed):
+        y, mask = _C().dropout_fwd(x, p, seed, channel)
+        ctx.p = p
+        ctx.save_for_backward(mask)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (mask,) = ctx.saved_tensors
+        return _C().dropout_bwd(dy.contiguous(), mask, ctx.p), None, None, None
+
+
+def _seed() -> int:
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+def dropout(x, p=0.5, training=True, channel=False):
+    """Dropout (``channel=True``: Dropout2d, one draw per (sample, channel))."""
+    if not training or p == 0.0:
+        return x
+    if not x.is_cuda:
+        return F.dropout2d(x, p, training) if channel else F.dropout(x, p, training)
+    if x.dtype != torch.bfloat16:
+        x = _C().cast_bf16(x.float().contiguous())
+    return _DropoutFn.apply(x.contiguous(), float(p), channel, _seed())
+
+
+# ---------------------------------------------------------------------------------------------
+# Losses / log_softmax
+# ---------------------------------------------------------------------------------------------
+class _CrossEntropyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, mode):
+        loss, lse = _C().ce_fwd(logits, target, mode)
+        ctx.mode = mode
+        ctx.out_f32 = logits.dtype == torch.float32
+        ctx.save_for_backward(logits, target, lse)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, target, lse = ctx.saved_tensors
+        dx = _C().ce_bwd(logits, target, lse, g.float().contiguous().reshape(1), ctx.mode, ctx.out_f32)
+        return dx, None, None
+
+
+def cross_entropy(logits, target):
+    """Mean cross-entropy (log_softmax + NLL fused)."""
+    if not logits.is_cuda:
+        return F.cross_entropy(logits.float(), target)
+    return _CrossEntropyFn.apply(logits.contiguous(), target.contiguous(), 0)
+
+
+def nll_loss(logp, target):
+    """Mean NLL over log-probabilities."""
+    if not logp.is_cuda:
+        return F.nll_loss(logp, target)
+    return _CrossEntropyFn.apply(logp.contiguous(), target.contiguous(), 1)
+
+
+class _LogSoftmaxFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y = _C().log_softmax_fwd(x)
+        ctx.in_f32 = x.dtype == torch.float32
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        return _C().log_softmax_bwd(dy.float().contiguous(), y, ctx.in_f32)
+
+
+def log_softmax(x, dim=1):
+    if not x.is_cuda:
+        return F.log_softmax(x, dim=dim)
+    assert dim in (1, -1) and x.dim() == 2
+    return _LogSoftmaxFn.apply(x.contiguous())
+
+
+class _MSEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, target):
+        ctx.out_f32 = pred.dtype == torch.float32
+        ctx.save_for_backward(pred, target)
+        return _C().mse_fwd(pred, target)
+
+    @staticmethod
+    def backward(ctx, g):
+        pred, target = ctx.saved_tensors
+        return _C().mse_bwd(pred, target, g.float().contiguous().reshape(1), ctx.out_f32), None
+
+
+def mse_loss(pred, target):
+    if not pred.is_cuda:
+        return F.mse_loss(pred.float(), target)
+    return _MSEFn.apply(pred.contiguous(), target.float().contiguous())
+
+
+# ---------------------------------------------------------------------------------------------
+# EmbeddingBag (sum)
+# ---------------------------------------------------------------------------------------------
+class _EmbBagFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, weight, indices, offsets):
+        ctx.num = weight.shape[0]
+        ctx.save_for_backward(indices, offsets)
+        return _C().embbag_fwd(weight.detach().contiguous(), indices, offsets)
+
+    @staticmethod
+    def backward(ctx, dy):
+        indices, offsets = ctx.saved_tensors
+        return _C().embbag_bwd(dy.float().contiguous(), indices, offsets, ctx.num), None, None
+
+
+def embedding_bag_sum(weight, indices, offsets):
+    if not weight.is_cuda:
+        return F.embedding_bag(indices, weight, offsets, mode="sum")
+    return _EmbBagFn.apply(weight, indices.contiguous().long(), offsets.contiguous().long())
+
+
+def kaiming_uniform_(t, a=math.sqrt(5)):
+    return torch.nn.init.kaiming_uniform_(t, a=a)

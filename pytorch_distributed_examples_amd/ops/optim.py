@@ -1,0 +1,157 @@
+"""Fused multi-tensor optimisers: SGD, Adam, AdamW.
+
+GPU parameters are updated by ONE ``multi_tensor_optim`` launch per param group (csrc/kernels/optim.hip)
+whose hyper-parameters and step counter live in device memory, so the update is hipGraph-capturable
+and an LR change between replays (Horovod-elastic ``on_state_reset``, horovod_mnist_elastic.py:80-82)
+is honoured.  CPU parameters use the same math in plain torch (the reference's CPU configuration).
+
+The per-parameter state uses torch's key names (``step``, ``exp_avg``, ``exp_avg_sq``,
+``momentum_buffer``) so ``state_dict()`` round-trips with ``torch.optim`` and with the elastic
+``TorchState`` commit/restore.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+from . import functional as OF
+
+_MODES = {"sgd": 0, "adam": 1, "adamw": 2}
+
+
+class _FusedBase(torch.optim.Optimizer):
+    KIND = "adam"
+
+    def __init__(self, params, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, momentum=0.0,
+                 grad_scale=1.0):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, momentum=momentum,
+                        grad_scale=grad_scale)
+        super().__init__(params, defaults)
+        self._dev = {}  # id(group) -> dict(table, sig, hp, hp_key, step)
+
+    # -- GPU -----------------------------------------------------------------------------------
+    def _group_dev(self, gi, group, params):
+        C = _native.C()
+        st = self._dev.get(gi)
+        dev = params[0].device
+        if st is None:
+            st = {"sig": None, "hp_key": None,
+                  "hp": torch.zeros(8, dtype=torch.float32, device=dev),
+                  "step": torch.zeros(1, dtype=torch.int32, device=dev)}
+            # resume a step count restored from a state_dict
+            s0 = self.state[params[0]].get("step") if params else None
+            if s0 is not None:
+                st["step"].fill_(int(s0))
+            self._dev[gi] = st
+        need_avg = self.KIND in ("adam", "adamw") or group["momentum"] != 0.0
+        for p in params:
+            state = self.state[p]
+            if self.KIND in ("adam", "adamw"):
+                if "exp_avg" not in state:
+                    state["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+            elif need_avg and "momentum_buffer" not in state:
+                state["momentum_buffer"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+        grads = [p.grad for p in params]
+        if self.KIND in ("adam", "adamw"):
+            m = [self.state[p]["exp_avg"] for p in params]
+            v = [self.state[p]["exp_avg_sq"] for p in params]
+        else:
+            m = [self.state[p]["momentum_buffer"] for p in params] if need_avg else []
+            v = []
+        sig = tuple((p.data_ptr(), g.data_ptr(), g.is_contiguous()) for p, g in zip(params, grads)) + \
+            tuple(t.data_ptr() for t in m) + tuple(t.data_ptr() for t in v)
+        if st["sig"] != sig:
+            grads_c = [g if g.is_contiguous() else g.contiguous() for g in grads]
+            table, total = C.optim_table([p.data for p in params], grads_c, m, v, [])
+            st.update(sig=sig, table=table, total=total, n=len(params), grads_keep=grads_c)
+        b1, b2 = group["betas"]
+        hp_key = (group["lr"], b1, b2, group["eps"], group["weight_decay"], group["momentum"], group["grad_scale"])
+        if st["hp_key"] != hp_key:
+            st["hp"].copy_(torch.tensor(list(hp_key) + [0.0], dtype=torch.float32), non_blocking=False)
+            st["hp_key"] = hp_key
+        return st
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        C = None
+        for gi, group in enumerate(self.param_groups):
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
+                continue
+            if params[0].is_cuda:
+                C = C or _native.C()
+                st = self._group_dev(gi, group, params)
+                C.optim_step(st["table"], st["n"], st["total"], _MODES[self.KIND], st["hp"], st["step"])
+                for p in params:
+                    self.state[p]["step"] = self.state[p].get("step", 0) + 1
+            else:
+                self._cpu_step(group, params)
+        OF.bump_weight_generation()
+        return loss
+
+    # -- CPU reference math (torch.optim semantics) ---------------------------------------------
+    def _cpu_step(self, group, params):
+        lr, (b1, b2), eps = group["lr"], group["betas"], group["eps"]
+        wd, mom, gs = group["weight_decay"], group["momentum"], group["grad_scale"]
+        for p in params:
+            g = p.grad if gs == 1.0 else p.grad * gs
+            state = self.state[p]
+            state["step"] = state.get("step", 0) + 1
+            t = state["step"]
+            if self.KIND == "sgd":
+                if wd != 0:
+                    g = g.add(p, alpha=wd)
+                if mom != 0:
+                    buf = state.get("momentum_buffer")
+                    if buf is None or t == 1:
+                        buf = g.clone()
+                    else:
+                        buf.mul_(mom).add_(g)
+                    state["momentum_buffer"] = buf
+                    g = buf
+                p.add_(g, alpha=-lr)
+                continue
+            if self.KIND == "adamw":
+                p.mul_(1 - lr * wd)
+            elif wd != 0:
+                g = g.add(p, alpha=wd)
+            if "exp_avg" not in state:
+                state["exp_avg"] = torch.zeros_like(p)
+                state["exp_avg_sq"] = torch.zeros_like(p)
+            m, v = state["exp_avg"], state["exp_avg_sq"]
+            m.lerp_(g, 1 - b1)
+            v.mul_(b2).addcmul_(g, g, value=1 - b2)
+            bc1 = 1 - b1 ** t
+            bc2 = 1 - b2 ** t
+            denom = (v.sqrt() / (bc2 ** 0.5)).add_(eps)
+            p.addcdiv_(m, denom, value=-lr / bc1)
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._dev = {}
+
+
+class FusedSGD(_FusedBase):
+    KIND = "sgd"
+
+    def __init__(self, params, lr, momentum=0.0, weight_decay=0.0, grad_scale=1.0):
+        super().__init__(params, lr=lr, momentum=momentum, weight_decay=weight_decay, grad_scale=grad_scale)
+
+
+class FusedAdam(_FusedBase):
+    KIND = "adam"
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, grad_scale=1.0):
+        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, grad_scale=grad_scale)
+
+
+class FusedAdamW(_FusedBase):
+    KIND = "adamw"
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, grad_scale=1.0):
+        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, grad_scale=grad_scale)

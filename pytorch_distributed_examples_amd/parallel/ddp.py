@@ -1,0 +1,196 @@
+"""Data-parallel wrapper with xGMI-sized gradient buckets (SURVEY.md P1, §2.6 DDP rows, §5.8).
+
+Mirrors ``torch.nn.parallel.DistributedDataParallel`` as used by the reference
+(pytorch_elastic/mnist_ddp_elastic.py:58, rpc/server_model_data_parallel.py:41):
+
+* construction broadcasts parameters and buffers from rank 0 -- coalesced into ONE flat broadcast;
+* gradients live in one flat fp32 buffer laid out in bucket order (``param.grad`` are views into it), so
+  a bucket is a single contiguous tensor and ``zero_grad`` is a single fill;
+* a post-accumulate-grad hook counts down each bucket; full buckets are all-reduced asynchronously, in
+  bucket order (the same on every rank), while the rest of backward runs -- RCCL runs them on its own
+  stream, ordered after the producing kernels;
+* RCCL averages in-collective (``ReduceOp.AVG``), so no separate divide kernel runs (gloo: SUM then a
+  scale);
+* bucket sizes follow :mod:`.xgmi` (sized for 7 point-to-point links, not DDP's 25 MiB default);
+* ``overlap=False`` skips the hooks and reduces every bucket in :meth:`sync_gradients` -- the form used
+  inside a captured hipGraph step;
+* ``grad_dtype=torch.bfloat16`` halves the bytes on the wire (bucket cast -> all-reduce -> cast back).
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from . import xgmi
+
+
+def _flat_broadcast(tensors, src, group):
+    if not tensors:
+        return
+    by_dtype: dict = {}
+    for t in tensors:
+        by_dtype.setdefault((t.dtype, t.device), []).append(t)
+    for (dtype, device), ts in by_dtype.items():
+        flat = torch.cat([t.detach().reshape(-1) for t in ts])
+        dist.broadcast(flat, src, group=group)
+        off = 0
+        with torch.no_grad():
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[off:off + n].view_as(t))
+                off += n
+
+
+class DistributedDataParallel(nn.Module):
+    def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float | None = None,
+                 broadcast_buffers: bool = True, overlap: bool = True, grad_dtype: torch.dtype | None = None,
+                 src_rank: int = 0):
+        super().__init__()
+        self.module = module
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.broadcast_buffers = broadcast_buffers
+        self.overlap = overlap
+        self.grad_dtype = grad_dtype
+        self.src = src_rank
+        self._params = [p for p in module.parameters() if p.requires_grad]
+        dev = self._params[0].device if self._params else torch.device("cpu")
+        self._use_avg = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
+        if self.world > 1:
+            _flat_broadcast(list(module.parameters()) + list(module.buffers()), src_rank, process_group)
+
+        # bucket plan over parameters in reverse registration order (~ gradient ready order)
+        order = list(reversed(self._params))
+        sizes = [p.numel() * (2 if grad_dtype == torch.bfloat16 else 4) for p in order]
+        cap = int(bucket_cap_mb * 2 ** 20) if bucket_cap_mb else None
+        plan = xgmi.plan_buckets(sizes, self.world, cap)
+        total = sum(p.numel() for p in order)
+        self.flat_grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        self._views = {}
+        self._bucket_of = {}
+        self._bucket_ranges = []
+        off = 0
+        for bi, idxs in enumerate(plan):
+            start = off
+            for i in idxs:
+                p = order[i]
+                n = p.numel()
+                self._views[p] = self.flat_grad[off:off + n].view_as(p)
+                self._bucket_of[p] = bi
+                off += n
+            self._bucket_ranges.append((start, off))
+        self._bucket_sizes = [len(idxs) for idxs in plan]
+        for p in self._params:
+            p.grad = self._views[p]
+        self._bucket_flat = [self.flat_grad[s:e] for s, e in self._bucket_ranges]
+        self._bf16_bufs = [torch.empty(e - s, dtype=torch.bfloat16, device=dev) for s, e in self._bucket_ranges] \
+            if grad_dtype == torch.bfloat16 else None
+        self._sync = True
+        self._reset_state()
+        self._hooks = []
+        if overlap and self.world > 1:
+            for p in self._params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(p)))
+
+    # ------------------------------------------------------------------------------------------
+    def _reset_state(self):
+        self._pending = list(self._bucket_sizes)
+        self._next = 0
+        self._works = []
+        self._callback_queued = False
+
+    def _make_hook(self, p):
+        view = self._views[p]
+
+        def hook(param):
+            if not self._sync:
+                return
+            if param.grad is None or param.grad.data_ptr() != view.data_ptr():
+                # someone replaced .grad (e.g. zero_grad(set_to_none=True)): fold it back into the bucket
+                if param.grad is not None:
+                    view.copy_(param.grad)
+                param.grad = view
+            if not self._callback_queued:
+                self._callback_queued = True
+                torch.autograd.Variable._execution_engine.queue_callback(self._finalize_overlap)
+            b = self._bucket_of[param]
+            self._pending[b] -= 1
+            self._launch_ready()
+
+        return hook
+
+    def _launch(self, b: int):
+        if self._bf16_bufs is not None:
+            buf = self._bf16_bufs[b]
+            buf.copy_(self._bucket_flat[b])
+        else:
+            buf = self._bucket_flat[b]
+        op = dist.ReduceOp.AVG if self._use_avg else dist.ReduceOp.SUM
+        work = dist.all_reduce(buf, op=op, group=self.pg, async_op=True)
+        self._works.append((b, work))
+
+    def _launch_ready(self):
+        while self._next < len(self._pending) and self._pending[self._next] <= 0:
+            self._launch(self._next)
+            self._next += 1
+
+    def _complete(self):
+        for b, work in self._works:
+            work.wait()
+            if self._bf16_bufs is not None:
+                self._bucket_flat[b].copy_(self._bf16_bufs[b])
+        if not self._use_avg and self.world > 1:
+            self.flat_grad.mul_(1.0 / self.world)
+        self._reset_state()
+
+    def _finalize_overlap(self):
+        # buckets whose params got no gradient this step (unused parameters) still reduce
+        while self._next < len(self._pending):
+            self._launch(self._next)
+            self._next += 1
+        self._complete()
+
+    # ------------------------------------------------------------------------------------------
+    def sync_gradients(self):
+        """Reduce all buckets now (non-overlapped mode / after ``no_sync`` accumulation)."""
+        if self.world <= 1:
+            return
+        for b in range(len(self._bucket_ranges)):
+            self._launch(b)
+        self._complete()
+
+    def forward(self, *args, **kwargs):
+        if self.broadcast_buffers and self.world > 1 and self.module.training:
+            bufs = [b for b in self.module.buffers() if b.is_floating_point()]
+            if bufs:
+                _flat_broadcast(bufs, self.src, self.pg)
+        return self.module(*args, **kwargs)
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.flat_grad.zero_()
+        for p in self._params:
+            if p.grad is None or p.grad.data_ptr() != self._views[p].data_ptr():
+                p.grad = self._views[p]
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self._sync
+        self._sync = False
+        try:
+            yield
+        finally:
+            self._sync = old
+
+    @property
+    def bucket_bytes(self):
+        mult = 2 if self.grad_dtype == torch.bfloat16 else 4
+        return [(e - s) * mult for s, e in self._bucket_ranges]
+
+    def state_dict(self, *a, **k):
+        return self.module.state_dict(*a, **k)
+
+    def load_state_dict(self, *a, **k):
+        return self.module.load_state_dict(*a, **k)

@@ -1,0 +1,233 @@
+"""Numerics of every gfx950 kernel against a plain PyTorch fp32 reference of the same op.
+
+Inputs are random and asymmetric (cdna_hip_programming.md §3: an asymmetric operand catches swapped
+C/D layouts); tolerances are set for bf16 operands with fp32 accumulation.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from pytorch_distributed_examples_amd.ops import functional as OF
+
+pytestmark = pytest.mark.gpu
+
+
+def bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def rel_err(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("M,K,N", [(128, 784, 1024), (128, 1024, 10), (1000, 320, 50), (37, 50, 10),
+                                   (2048, 2048, 1000), (8, 64, 128)])
+def test_linear_fwd_bwd(gpu, M, K, N):
+    C = OF._C()
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=gpu)
+    w = torch.randn(N, K, device=gpu) * 0.05
+    b = torch.randn(N, device=gpu)
+    xb, wb = x.bfloat16(), w.bfloat16()
+    y = C.linear_fwd(xb, wb, b, True, True)
+    ref = torch.relu(bf(x) @ bf(w).t() + b)
+    assert rel_err(y, ref) < 1e-2
+    dy = torch.randn(M, N, device=gpu).bfloat16()
+    dx = C.linear_dgrad(dy, wb, None)
+    assert rel_err(dx, dy.float() @ bf(w)) < 1e-2
+    aux = torch.randn(M, K, device=gpu).bfloat16()
+    dxm = C.linear_dgrad(dy, wb, aux)
+    assert rel_err(dxm, (dy.float() @ bf(w)) * (aux.float() > 0)) < 1e-2
+    dw = C.linear_wgrad(dy, xb)
+    assert rel_err(dw, dy.float().t() @ bf(x)) < 1e-2
+
+
+def test_linear_identity_asymmetric(gpu):
+    """A = I with an asymmetric B catches a transposed C write."""
+    C = OF._C()
+    n = 64
+    eye = torch.eye(n, device=gpu).bfloat16()
+    B = (torch.arange(n * n, device=gpu).reshape(n, n) % 61).float().bfloat16()
+    y = C.linear_fwd(eye, B, None, False, True)
+    assert torch.equal(y, B.float().t())
+
+
+CONV_CFGS = [
+    # N, Cin, H, Cout, k, stride, pad
+    (4, 3, 128, 64, 7, 2, 3),     # ResNet stem
+    (4, 64, 32, 64, 3, 1, 1),
+    (4, 64, 32, 256, 1, 1, 0),
+    (4, 128, 32, 128, 3, 2, 1),
+    (4, 256, 32, 512, 1, 2, 0),
+    (4, 512, 4, 2048, 1, 1, 0),
+    (8, 1, 28, 10, 5, 1, 0),      # MNIST conv1
+    (8, 10, 12, 20, 5, 1, 0),     # MNIST conv2
+]
+
+
+@pytest.mark.parametrize("cfg", CONV_CFGS)
+def test_conv_fwd_bwd(gpu, cfg):
+    n, ci, h, co, k, s, p = cfg
+    torch.manual_seed(1)
+    x = torch.randn(n, ci, h, h, device=gpu)
+    w = (torch.randn(co, ci, k, k, device=gpu) * (1.0 / (ci * k * k) ** 0.5)).requires_grad_()
+    b = torch.randn(co, device=gpu).requires_grad_()
+    xr = bf(x).requires_grad_()
+    yr = F.conv2d(xr, bf(w.detach()).requires_grad_(), b, stride=s, padding=p)
+    # native
+    xn = OF.to_native_image(x).requires_grad_()
+    yn = OF.conv2d(xn, w, b, s, p)
+    y_nchw = yn[..., :co].permute(0, 3, 1, 2).float()
+    assert rel_err(y_nchw, yr) < 1.5e-2
+    g = torch.randn_like(yr)
+    gn = torch.zeros_like(yn, dtype=torch.float32)
+    gn[..., :co] = g.permute(0, 2, 3, 1)
+    (yn.float() * gn).sum().backward()
+    wr = bf(w.detach()).requires_grad_()
+    xr2 = bf(x).requires_grad_()
+    F.conv2d(xr2, wr, b.detach(), stride=s, padding=p).backward(g)
+    assert rel_err(w.grad, wr.grad) < 2e-2
+    assert rel_err(b.grad, g.sum((0, 2, 3))) < 1e-2
+    dx = xn.grad[..., :ci].permute(0, 3, 1, 2)
+    assert rel_err(dx, xr2.grad) < 2e-2
+    assert xn.grad[..., ci:].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
+def test_batchnorm(gpu, relu, res):
+    torch.manual_seed(2)
+    n, c, h = 8, 64, 16
+    x = torch.randn(n, c, h, h, device=gpu) * 3 + 1
+    gamma = (torch.rand(c, device=gpu) + 0.5).requires_grad_()
+    beta = torch.randn(c, device=gpu).requires_grad_()
+    r = torch.randn(n, c, h, h, device=gpu) if res else None
+    rm, rv = torch.zeros(c, device=gpu), torch.ones(c, device=gpu)
+    xn = bf(x).permute(0, 2, 3, 1).contiguous().bfloat16().requires_grad_()
+    rn = bf(r).permute(0, 2, 3, 1).contiguous().bfloat16().requires_grad_() if res else None
+    y = OF.batch_norm(xn, gamma, beta, rm, rv, True, 0.1, 1e-5, rn, relu)
+    # reference
+    xr = bf(x).requires_grad_()
+    g2, b2 = gamma.detach().clone().requires_grad_(), beta.detach().clone().requires_grad_()
+    rm2, rv2 = torch.zeros(c, device=gpu), torch.ones(c, device=gpu)
+    rr = bf(r).requires_grad_() if res else None
+    yr = F.batch_norm(xr, rm2, rv2, g2, b2, True, 0.1, 1e-5)
+    if res:
+        yr = yr + rr
+    if relu:
+        yr = torch.relu(yr)
+    assert rel_err(y.permute(0, 3, 1, 2), yr) < 1e-2
+    assert rel_err(rm, rm2) < 1e-3 and rel_err(rv, rv2) < 1e-3
+    gy = torch.randn_like(yr)
+    yr.backward(gy)
+    y.float().backward(gy.permute(0, 2, 3, 1))
+    assert rel_err(xn.grad.permute(0, 3, 1, 2), xr.grad) < 2e-2
+    assert rel_err(gamma.grad, g2.grad) < 2e-2
+    assert rel_err(beta.grad, b2.grad) < 2e-2
+    if res:
+        assert rel_err(rn.grad.permute(0, 3, 1, 2), rr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("k,s,p,relu", [(3, 2, 1, False), (2, 2, 0, True)])
+def test_maxpool(gpu, k, s, p, relu):
+    torch.manual_seed(3)
+    x = torch.randn(4, 16, 12, 12, device=gpu)
+    xn = bf(x).permute(0, 2, 3, 1).contiguous().bfloat16().requires_grad_()
+    y = OF.max_pool2d(xn, k, s, p, relu)
+    xr = bf(x).requires_grad_()
+    yr = F.max_pool2d(xr, k, s, p)
+    if relu:
+        yr = torch.relu(yr)
+    assert torch.allclose(y.permute(0, 3, 1, 2).float(), yr)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    y.float().backward(g.permute(0, 2, 3, 1))
+    assert rel_err(xn.grad.permute(0, 3, 1, 2), xr.grad) < 1e-2
+
+
+def test_avgpool_and_losses(gpu):
+    torch.manual_seed(4)
+    x = torch.randn(8, 4, 4, 64, device=gpu).bfloat16().requires_grad_()
+    y = OF.global_avg_pool_flat(x)
+    assert rel_err(y, x.float().mean((1, 2))) < 1e-2
+    y.float().sum().backward()
+    assert torch.allclose(x.grad.float(), torch.full_like(x.float(), 1 / 16), atol=1e-3)
+
+    logits = torch.randn(300, 10, device=gpu, requires_grad=True)
+    tgt = torch.randint(0, 10, (300,), device=gpu)
+    loss = OF.cross_entropy(logits, tgt)
+    l2 = logits.detach().clone().requires_grad_()
+    ref = F.cross_entropy(l2, tgt)
+    assert abs(loss.item() - ref.item()) < 1e-4
+    loss.backward()
+    ref.backward()
+    assert rel_err(logits.grad, l2.grad) < 1e-4
+
+    lp = OF.log_softmax(logits.detach().clone().requires_grad_())
+    assert rel_err(lp, F.log_softmax(logits.detach(), 1)) < 1e-5
+    nl = OF.nll_loss(lp, tgt)
+    assert abs(nl.item() - ref.item()) < 1e-4
+
+    pred = torch.randn(32, 1000, device=gpu, requires_grad=True)
+    t = torch.randn(32, 1000, device=gpu)
+    m = OF.mse_loss(pred, t)
+    p2 = pred.detach().clone().requires_grad_()
+    mr = F.mse_loss(p2, t)
+    assert abs(m.item() - mr.item()) < 1e-4
+    m.backward()
+    mr.backward()
+    assert rel_err(pred.grad, p2.grad) < 1e-5
+
+
+def test_dropout(gpu):
+    x = torch.ones(64, 4, 4, 32, device=gpu).bfloat16().requires_grad_()
+    y = OF.dropout(x, 0.5, True, channel=True)
+    keep = (y.float() != 0)
+    # channel mode: constant over spatial positions of one (n, c)
+    assert torch.equal(keep, keep[:, :1, :1, :].expand_as(keep))
+    frac = keep.float().mean().item()
+    assert 0.4 < frac < 0.6
+    assert torch.allclose(y.float()[keep], torch.full_like(y.float()[keep], 2.0))
+    y.float().sum().backward()
+    assert torch.equal(x.grad.float() != 0, keep)
+
+
+def test_embedding_bag(gpu):
+    torch.manual_seed(5)
+    w = torch.randn(100, 16, device=gpu, requires_grad=True)
+    idx = torch.randint(0, 100, (40,), device=gpu)
+    off = torch.tensor([0, 3, 9, 20, 31], device=gpu)
+    y = OF.embedding_bag_sum(w, idx, off)
+    w2 = w.detach().clone().requires_grad_()
+    yr = F.embedding_bag(idx, w2, off, mode="sum")
+    assert rel_err(y, yr) < 1e-5
+    g = torch.randn_like(yr)
+    y.backward(g)
+    yr.backward(g)
+    assert rel_err(w.grad, w2.grad) < 1e-5
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adam", "adamw"])
+def test_fused_optimizers(gpu, kind):
+    from pytorch_distributed_examples_amd.ops import optim as O
+
+    torch.manual_seed(6)
+    shapes = [(1024, 784), (1024,), (10, 1024), (10,), (7, 3, 5, 5)]
+    ps = [torch.randn(*s, device=gpu) for s in shapes]
+    ref = [p.detach().clone().requires_grad_() for p in ps]
+    mine = [p.detach().clone().requires_grad_() for p in ps]
+    if kind == "sgd":
+        o1, o2 = O.FusedSGD(mine, lr=0.05, momentum=0.9), torch.optim.SGD(ref, lr=0.05, momentum=0.9)
+    elif kind == "adam":
+        o1, o2 = O.FusedAdam(mine, lr=1e-3), torch.optim.Adam(ref, lr=1e-3)
+    else:
+        o1, o2 = O.FusedAdamW(mine, lr=1e-2), torch.optim.AdamW(ref, lr=1e-2)
+    for _ in range(3):
+        gs = [torch.randn_like(p) for p in ps]
+        for p, g in zip(mine, gs):
+            p.grad = g.clone()
+        for p, g in zip(ref, gs):
+            p.grad = g.clone()
+        o1.step()
+        o2.step()
+    for a, b in zip(mine, ref):
+        assert rel_err(a, b) < 1e-5

@@ -1,0 +1,83 @@
+"""Model-level GPU checks: one forward/backward of each model family on the native path against the
+CPU fp32 reference path of the SAME module (same weights), and loss decrease over a few steps."""
+import copy
+
+import pytest
+import torch
+
+from pytorch_distributed_examples_amd.models.cnn import Net
+from pytorch_distributed_examples_amd.models.mlp import MLP
+from pytorch_distributed_examples_amd.models.resnet import ResNetShard1, ResNetShard2
+from pytorch_distributed_examples_amd.ops import functional as OF
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_err(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def test_mlp_step_matches_cpu(gpu):
+    torch.manual_seed(0)
+    m_cpu = MLP(hidden_layers=5, features=1024)
+    m_gpu = copy.deepcopy(m_cpu).to(gpu)
+    x = torch.randn(128, 1, 28, 28)
+    y = torch.randint(0, 10, (128,))
+    l_cpu = OF.cross_entropy(m_cpu(x), y)
+    l_cpu.backward()
+    l_gpu = OF.cross_entropy(m_gpu(x.to(gpu)), y.to(gpu))
+    l_gpu.backward()
+    assert abs(l_cpu.item() - l_gpu.item()) < 2e-2
+    for (n, p1), p2 in zip(m_cpu.named_parameters(), m_gpu.parameters()):
+        assert rel_err(p2.grad.cpu(), p1.grad) < 5e-2, n
+
+
+def test_cnn_step_matches_cpu(gpu):
+    torch.manual_seed(0)
+    m_cpu = Net().eval()  # eval: dropout off so both paths are deterministic
+    m_gpu = copy.deepcopy(m_cpu).to(gpu).eval()
+    x = torch.randn(64, 1, 28, 28)
+    y = torch.randint(0, 10, (64,))
+    l_cpu = OF.nll_loss(m_cpu(x), y)
+    l_cpu.backward()
+    l_gpu = OF.nll_loss(m_gpu(x.to(gpu)), y.to(gpu))
+    l_gpu.backward()
+    assert abs(l_cpu.item() - l_gpu.item()) < 2e-2
+    for (n, p1), p2 in zip(m_cpu.named_parameters(), m_gpu.parameters()):
+        assert rel_err(p2.grad.cpu(), p1.grad) < 5e-2, n
+
+
+def test_resnet_shards_match_cpu(gpu):
+    torch.manual_seed(0)
+    s1, s2 = ResNetShard1(), ResNetShard2()
+    g1, g2 = copy.deepcopy(s1).to(gpu), copy.deepcopy(s2).to(gpu)
+    x = torch.randn(4, 3, 128, 128)
+    t = torch.randn(4, 1000)
+    out_cpu = s2(s1(x))
+    out_gpu = g2(g1(x.to(gpu)))
+    assert out_gpu.shape == (4, 1000)
+    assert rel_err(out_gpu.cpu(), out_cpu) < 5e-2
+    OF.mse_loss(out_cpu, t).backward()
+    OF.mse_loss(out_gpu, t.to(gpu)).backward()
+    for (n, p1), p2 in zip(list(s1.named_parameters())[:6] + list(s2.named_parameters())[-4:],
+                           list(g1.parameters())[:6] + list(g2.parameters())[-4:]):
+        assert rel_err(p2.grad.cpu(), p1.grad) < 0.1, n
+
+
+def test_cnn_trains(gpu):
+    from pytorch_distributed_examples_amd.data.synthetic import SyntheticMNIST
+    from pytorch_distributed_examples_amd.ops.optim import FusedSGD
+
+    torch.manual_seed(0)
+    m = Net().to(gpu)
+    opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9)
+    data = SyntheticMNIST(4096, device=gpu, seed=1)
+    losses = []
+    for i in range(30):
+        x, y = data.batch(i, 256)
+        opt.zero_grad(set_to_none=False)
+        loss = OF.nll_loss(m(x), y)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert sum(losses[-5:]) / 5 < losses[0] * 0.7, losses
