@@ -89,6 +89,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", default="cnn", choices=["cnn", "mlp", "resnet50"])
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch")
+    ap.add_argument("--no-graph", action="store_true", help="run the step eagerly (no hipGraph capture)")
+    ap.add_argument("--generic", action="store_true", help="CNN: layer-by-layer kernels instead of the fused step")
     args = ap.parse_args()
     batch = args.batch or {"cnn": 1024, "mlp": 128, "resnet50": 32}[args.model]
 
@@ -96,15 +98,47 @@ def main():
     from pytorch_distributed_examples_amd.parallel.ddp import DistributedDataParallel
 
     model, opt, batch_fn, loss_fn = build(args.model, ctx.device, batch)
-    ddp = DistributedDataParallel(model)
+    use_graph = not args.no_graph
+    fused = None
+    if args.model == "cnn" and not args.generic:
+        # whole-network fused kernel (csrc/kernels/cnn_fused.hip): gradients land directly in the
+        # DDP flat buffer (forward layout), then one RCCL all-reduce and one fused SGD launch.
+        from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
 
-    def step(i):
+        fused = FusedCNN(model)
+        ddp = DistributedDataParallel(model, overlap=False, param_order="forward")
+    else:
+        ddp = DistributedDataParallel(model, overlap=not use_graph)
+
+    def train_step(x, y):
+        if fused is not None:
+            loss = fused.forward_backward(x, y, grad_out=ddp.flat_grad)
+            ddp.sync_gradients()
+            opt.step()
+            return loss
         ddp.zero_grad()
-        x, y = batch_fn(i)
         loss = loss_fn(ddp(x), y)
         loss.backward()
+        if use_graph:
+            ddp.sync_gradients()
         opt.step()
         return loss
+
+    graphed = None
+    if use_graph:
+        from pytorch_distributed_examples_amd.utils.graph import CapturedStep
+
+        try:
+            graphed = CapturedStep(train_step, batch_fn(0), warmup=3).capture()
+        except Exception as exc:  # capture unsupported (e.g. collective in capture): run eagerly
+            if ctx.rank == 0:
+                print(f"[bench] hipGraph capture failed, running eagerly: {exc}", file=sys.stderr)
+            use_graph = False
+            ddp = DistributedDataParallel(model, overlap=True)
+
+    def step(i):
+        x, y = batch_fn(i)
+        return graphed(x, y) if graphed is not None else train_step(x, y)
 
     for i in range(args.warmup):
         step(i)
@@ -133,13 +167,14 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / base, 2) if base else None,
-            "dtype": "bf16",
+            "dtype": "fp32" if fused is not None else "bf16",
             "data": "synthetic",
             "config": {"model": {"cnn": "mnist_cnn_Net", "mlp": "mnist_mlp_5x1024",
                                  "resnet50": "resnet50_128px"}[args.model],
                        "global_batch": batch * ctx.world_size, "seq_len": None,
                        "image": "1x28x28" if args.model != "resnet50" else "3x128x128",
-                       "parallelism": f"dp{ctx.world_size}", "final_loss": round(final_loss, 4)},
+                       "parallelism": f"dp{ctx.world_size}", "final_loss": round(final_loss, 4),
+                       "hipgraph": graphed is not None, "fused_step": fused is not None},
         }), flush=True)
     pdist.shutdown()
 

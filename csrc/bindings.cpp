@@ -59,10 +59,21 @@ pde::Operand gather(const Tensor& t, int kind, int N, int H, int W, int C, int R
   return o;
 }
 
+// Split-K cap for a GEMM with reduction length K: at most 512 slabs, each >= 256 long, and the fp32
+// slab workspace bounded to 128 MiB (the kernel picks the actual split from the tile count).
+int split_cap(const pde::GemmArgs& a) {
+  long cap = a.K / 128;
+  const long by_mem = (128L << 20) / (4L * a.M * a.N);
+  if (cap > by_mem) cap = by_mem;
+  if (cap > 512) cap = 512;
+  return cap < 1 ? 1 : static_cast<int>(cap);
+}
+
 void run_gemm(pde::GemmArgs& a, const Tensor& like, int max_split) {
   Tensor ws;
   a.workspace = nullptr;
   a.splitk = 1;
+  if (max_split < 0) max_split = split_cap(a);
   if (max_split > 1) {
     ws = at::empty({static_cast<long>(max_split) * a.M * a.N}, like.options().dtype(at::kFloat));
     a.workspace = ws.data_ptr<float>();
@@ -87,7 +98,7 @@ Tensor linear_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias
   a.bias = cf32(bias);
   a.nbias = a.bias ? static_cast<int>(bias->numel()) : 0;
   a.epi = (a.bias ? pde::EPI_BIAS : 0) | (relu ? pde::EPI_RELU : 0) | (out_f32 ? pde::EPI_OUT_F32 : 0);
-  run_gemm(a, x, 1);
+  run_gemm(a, x, -1);
   return out;
 }
 
@@ -104,7 +115,7 @@ Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const optional<Tensor>& a
   a.out = dx.data_ptr(); a.ldo = K;
   a.aux = cu16(aux); a.ldaux = K;
   a.epi = a.aux ? pde::EPI_DRELU : 0;
-  run_gemm(a, dy, 1);
+  run_gemm(a, dy, -1);
   return dx;
 }
 
@@ -120,7 +131,7 @@ Tensor linear_wgrad(const Tensor& dy, const Tensor& x) {
   a.b = dense(x, 1, K);
   a.out = dw.data_ptr(); a.ldo = K;
   a.epi = pde::EPI_OUT_F32;
-  run_gemm(a, dy, M >= 1024 ? 16 : 1);
+  run_gemm(a, dy, -1);
   return dw;
 }
 
@@ -144,7 +155,7 @@ Tensor conv_fwd(const Tensor& x, const Tensor& wf, const optional<Tensor>& bias,
   a.bias = cf32(bias);
   a.nbias = a.bias ? static_cast<int>(bias->numel()) : 0;
   a.epi = (a.bias ? pde::EPI_BIAS : 0) | (relu ? pde::EPI_RELU : 0) | (out_f32 ? pde::EPI_OUT_F32 : 0);
-  run_gemm(a, x, 1);
+  run_gemm(a, x, -1);
   return y;
 }
 
@@ -164,7 +175,7 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wd, int H, int W, int R, int S
   a.out = dx.data_ptr(); a.ldo = Ci;
   a.aux = cu16(aux); a.ldaux = Ci;
   a.epi = a.aux ? pde::EPI_DRELU : 0;
-  run_gemm(a, dy, 1);
+  run_gemm(a, dy, -1);
   return dx;
 }
 
@@ -181,7 +192,7 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int R, int S, int stride, i
   a.b = gather(x, 2, N, H, W, C, R, S, stride, pad, Ho, Wo);
   a.out = dw.data_ptr(); a.ldo = a.N;
   a.epi = pde::EPI_OUT_F32;
-  run_gemm(a, dy, 16);
+  run_gemm(a, dy, -1);
   return dw;
 }
 
@@ -247,7 +258,10 @@ Tensor colsum(const Tensor& x) {
   const int N = x.size(-1);
   const int M = x.numel() / N;
   Tensor y = at::empty({N}, x.options().dtype(at::kFloat));
-  check(pde::colsum_bf16(u16(x), y.data_ptr<float>(), M, N, 0, cur_stream()), "colsum");
+  const int ws_blocks = 512;
+  Tensor ws = at::empty({static_cast<long>(ws_blocks) * N}, x.options().dtype(at::kFloat));
+  check(pde::colsum_bf16_ws(u16(x), y.data_ptr<float>(), M, N, 0, ws.data_ptr<float>(), ws_blocks, cur_stream()),
+        "colsum");
   return y;
 }
 Tensor relu_bwd(const Tensor& dy, const Tensor& y) {
@@ -446,8 +460,10 @@ Tensor avgpool_bwd(const Tensor& dy, int H, int W) {
   check(pde::avgpool_bwd(u16(dy), u16(dx), N, H * W, C, cur_stream()), "avgpool_bwd");
   return dx;
 }
-std::vector<Tensor> dropout_fwd(const Tensor& x, double p, int64_t seed, bool channel) {
-  CHECK_IN(x); CHECK_BF16(x);
+// counter: device int64[1] RNG counter (advanced on device after the draw); salt: per-call constant.
+std::vector<Tensor> dropout_fwd(const Tensor& x, double p, Tensor& counter, int64_t salt, bool channel) {
+  CHECK_IN(x); CHECK_BF16(x); CHECK_IN(counter);
+  TORCH_CHECK(counter.scalar_type() == at::kLong && counter.numel() >= 1, "counter must be int64[1]");
   Tensor y = at::empty_like(x);
   Tensor mask = at::empty(x.sizes(), x.options().dtype(at::kByte));
   int HW = 1, C = 1;
@@ -456,7 +472,8 @@ std::vector<Tensor> dropout_fwd(const Tensor& x, double p, int64_t seed, bool ch
     HW = x.numel() / (x.size(0) * C);
   }
   check(pde::dropout_fwd(u16(x), u16(y), mask.data_ptr<uint8_t>(), x.numel(), channel ? 1 : 0, HW, C,
-                         static_cast<float>(p), static_cast<unsigned long long>(seed), cur_stream()),
+                         static_cast<float>(p), reinterpret_cast<unsigned long long*>(counter.data_ptr()),
+                         static_cast<unsigned long long>(salt), cur_stream()),
         "dropout_fwd");
   return {y, mask};
 }
@@ -486,9 +503,53 @@ Tensor embbag_bwd(const Tensor& dy, const Tensor& idx, const Tensor& off, int64_
   return dw;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Fused MNIST CNN training step
+// ------------------------------------------------------------------------------------------------
+// Launches forward+loss+backward for the whole batch; returns (loss scalar, slabs).  The caller reduces
+// the slabs into a gradient buffer with cnn_reduce (possibly the DDP flat gradient).
+std::vector<Tensor> cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, Tensor& rng,
+                              double p_drop2, double p_drop1, bool training, int64_t nwg,
+                              const optional<Tensor>& stamps) {
+  CHECK_IN(images); CHECK_IN(tgt); CHECK_IN(params); CHECK_IN(rng); CHECK_F32(images); CHECK_F32(params);
+  TORCH_CHECK(params.numel() == pde::cnn_num_params(), "cnn_train: params must be the flat Net parameters");
+  TORCH_CHECK(images.numel() == tgt.numel() * 28 * 28, "cnn_train: images must be [B,1,28,28]");
+  TORCH_CHECK(tgt.scalar_type() == at::kLong && rng.scalar_type() == at::kLong, "cnn_train: dtypes");
+  const int B = tgt.numel();
+  (void)nwg;  // the kernel trains cnn_images_per_workgroup() images per workgroup
+  const int ni = pde::cnn_images_per_workgroup();
+  const int n = (B + ni - 1) / ni;
+  auto fo = images.options();
+  Tensor slabs = at::empty({static_cast<long>(n) * pde::cnn_num_params()}, fo);
+  Tensor part = at::empty({n}, fo);
+  Tensor loss = at::empty({}, fo);
+  check(pde::cnn_train_fused(images.data_ptr<float>(), tgt.data_ptr<int64_t>(), B, params.data_ptr<float>(),
+                             reinterpret_cast<unsigned long long*>(rng.data_ptr()), static_cast<float>(p_drop2),
+                             static_cast<float>(p_drop1), training ? 1 : 0, slabs.data_ptr<float>(),
+                             part.data_ptr<float>(), n, loss.data_ptr<float>(), cur_stream(),
+                             stamps.has_value() && stamps->defined()
+                                 ? reinterpret_cast<unsigned long long*>(stamps->data_ptr())
+                                 : nullptr),
+        "cnn_train");
+  return {loss, slabs};
+}
+
+void cnn_reduce(const Tensor& slabs, const optional<Tensor>& gscale, Tensor& grads, bool accumulate) {
+  CHECK_IN(slabs); CHECK_IN(grads); CHECK_F32(grads);
+  TORCH_CHECK(grads.numel() == pde::cnn_num_params(), "cnn_reduce: grads size");
+  const int nwg = slabs.numel() / pde::cnn_num_params();
+  check(pde::cnn_reduce_grads(slabs.data_ptr<float>(), nwg, cf32(gscale), grads.data_ptr<float>(), accumulate,
+                              cur_stream()),
+        "cnn_reduce");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("cnn_train", &cnn_train);
+  m.def("cnn_reduce", &cnn_reduce);
+  m.def("cnn_num_params", &pde::cnn_num_params);
+  m.def("cnn_smem_bytes", &pde::cnn_smem_bytes);
   m.doc() = "MI355X (gfx950) native kernels for pytorch_distributed_examples_amd";
   m.def("linear_fwd", &linear_fwd);
   m.def("linear_dgrad", &linear_dgrad);

@@ -78,6 +78,9 @@ hipError_t conv_wgrad_to_oihw(const float* in, float* out, int Co, int Ci, int R
                               hipStream_t s);
 // column sums of a bf16 [M, N] matrix into fp32 [N] (bias gradient); accum adds to out
 hipError_t colsum_bf16(const uint16_t* x, float* out, int M, int N, int accum, hipStream_t s);
+// Vectorised deterministic variant for N % 8 == 0; ws holds ws_blocks * N floats (falls back otherwise).
+hipError_t colsum_bf16_ws(const uint16_t* x, float* out, int M, int N, int accum, float* ws, int ws_blocks,
+                          hipStream_t s);
 hipError_t relu_bwd_bf16(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n, hipStream_t s);
 
 // ---------------------------------------------------------------------------------------------
@@ -131,10 +134,25 @@ hipError_t maxpool_bwd(const uint16_t* dy, const uint16_t* y, const uint8_t* idx
 hipError_t avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t s);
 hipError_t avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t s);
 hipError_t dropout_fwd(const uint16_t* x, uint16_t* y, uint8_t* mask, long n, int mode, int HW, int C, float p,
-                       unsigned long long seed, hipStream_t s);
+                       unsigned long long* counter, unsigned long long salt, hipStream_t s);
 hipError_t dropout_bwd(const uint16_t* dy, const uint8_t* mask, uint16_t* dx, long n, float p, hipStream_t s);
 hipError_t embbag_fwd(const float* w, const int64_t* idx, const int64_t* off, int B, long L, int D, float* out,
                       hipStream_t s);
+// ---------------------------------------------------------------------------------------------
+// Fused MNIST-CNN training step (cnn_fused.hip): forward + NLL + backward of horovod/mnist_horovod.py's
+// Net per image in LDS.  params: flat fp32 in torch parameter order (cnn_num_params() floats).
+// slabs: nwg * cnn_num_params() floats; loss_part: nwg floats.
+// ---------------------------------------------------------------------------------------------
+int cnn_num_params();
+size_t cnn_smem_bytes();
+int cnn_images_per_workgroup();
+hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, const float* params,
+                           unsigned long long* rng, float p_drop2, float p_drop1, int training, float* slabs,
+                           float* loss_part, int nwg, float* loss, hipStream_t s,
+                           unsigned long long* stamps = nullptr);
+hipError_t cnn_reduce_grads(const float* slabs, int nwg, const float* gscale, float* grads, int accumulate,
+                            hipStream_t s);
+
 hipError_t embbag_bwd(const float* dy, const int64_t* idx, const int64_t* off, int B, long L, int D, float* dw,
                       hipStream_t s);
 

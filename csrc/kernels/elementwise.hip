@@ -131,6 +131,50 @@ __global__ void k_colsum_bf16(const uint16_t* __restrict__ x, float* __restrict_
   }
 }
 
+// Narrow-matrix column sums (N % 8 == 0): thread = (row-in-iteration, 8-column group), 16-byte loads,
+// fixed-order partials per block -> ws[blk][N], summed by k_colsum_final.  Deterministic.
+__global__ __launch_bounds__(256) void k_colsum_vec(const uint16_t* __restrict__ x, int M, int N, int rows_per_block,
+                                                    float* __restrict__ ws) {
+  const int G = N / 8;
+  const int gg = G < 256 ? G : 256;
+  const int rpi = 256 / gg;
+  const int rr = threadIdx.x / gg, g0 = threadIdx.x % gg;
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  __shared__ float red[256][8];
+  for (int gb = 0; gb < G; gb += gg) {
+    const int g = gb + g0;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (rr < rpi && g < G)
+      for (int r = r0 + rr; r < r1; r += rpi) {
+        const u16x8 v = *reinterpret_cast<const u16x8*>(x + static_cast<long>(r) * N + g * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[j]);
+      }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = acc[j];
+    __syncthreads();
+    if (rr == 0 && g < G) {
+      for (int q = 1; q < rpi; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += red[q * gg + g0][j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ws[static_cast<long>(blockIdx.x) * N + g * 8 + j] = acc[j];
+    }
+    __syncthreads();
+  }
+}
+
+// One wave per column: lanes stride the block partials, then a wave reduction.
+__global__ void k_colsum_final(const float* __restrict__ ws, int nblk, int N, float* __restrict__ out, int accum) {
+  const int col = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (col >= N) return;
+  float v = 0.f;
+  for (int b = lane; b < nblk; b += 64) v += ws[static_cast<long>(b) * N + col];
+  v = wave_sum(v);
+  if (lane == 0) out[col] = accum ? out[col] + v : v;
+}
+
 __global__ void k_relu_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
                            uint16_t* __restrict__ dx, long n) {
   const long nv = n / 8;
@@ -183,6 +227,23 @@ hipError_t conv_wgrad_to_oihw(const float* in, float* out, int Co, int Ci, int R
                      Cp, accum);
   return hipGetLastError();
 }
+hipError_t colsum_bf16_ws(const uint16_t* x, float* out, int M, int N, int accum, float* ws, int ws_blocks,
+                          hipStream_t s) {
+  if (N % 8 == 0 && ws != nullptr) {
+    const int G = N / 8;
+    const int rpi = 256 / (G < 256 ? G : 256);
+    int nblk = ceil_div(M, rpi * 8);
+    if (nblk > ws_blocks) nblk = ws_blocks;
+    if (nblk < 1) nblk = 1;
+    const int rpb = ceil_div(M, nblk);
+    nblk = ceil_div(M, rpb);
+    hipLaunchKernelGGL(k_colsum_vec, dim3(nblk), dim3(256), 0, s, x, M, N, rpb, ws);
+    hipLaunchKernelGGL(k_colsum_final, dim3(ceil_div(N, 4)), dim3(256), 0, s, ws, nblk, N, out, accum);
+    return hipGetLastError();
+  }
+  return colsum_bf16(x, out, M, N, accum, s);
+}
+
 hipError_t colsum_bf16(const uint16_t* x, float* out, int M, int N, int accum, hipStream_t s) {
   // accum is handled by the caller zeroing/keeping out; with a single row-block we overwrite.
   const int col_blocks = ceil_div(N, 64);

@@ -333,7 +333,8 @@ hipError_t dispatch_tiles(const GemmArgs& a, hipStream_t s) {
   auto pick_split = [&](long tiles, int bk) {
     if (a.workspace == nullptr || a.splitk <= 1) return 1;
     int sk = 1;
-    while (sk < a.splitk && tiles * sk < 512 && a.K / (sk * 2) >= 4 * bk) sk *= 2;
+    // target >= 4 blocks per CU (1024) while every split keeps >= 8 K-tiles of work
+    while (sk < a.splitk && tiles * sk < 1024 && a.K / (sk * 2) >= 4 * bk) sk *= 2;
     return sk;
   };
   if (a.N <= 32) {

@@ -78,13 +78,17 @@ __global__ void k_bn_finalize(const uint16_t* __restrict__ x, const float* __res
                               float momentum, float* __restrict__ running_mean, float* __restrict__ running_var,
                               float* __restrict__ save_mean, float* __restrict__ save_invstd,
                               float* __restrict__ scale, float* __restrict__ shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  // one wave per channel: lanes stride the block partials (fixed order -> deterministic)
+  const int c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int b = 0; b < nblk; ++b) {
-    s1 += ws[static_cast<long>(b) * 2 * C + c];
-    s2 += ws[static_cast<long>(b) * 2 * C + C + c];
+  float p1 = 0.f, p2 = 0.f;
+  for (int b = lane; b < nblk; b += 64) {
+    p1 += ws[static_cast<long>(b) * 2 * C + c];
+    p2 += ws[static_cast<long>(b) * 2 * C + C + c];
   }
+  const double s1 = wave_sum(p1), s2 = wave_sum(p2);
+  if (lane != 0) return;
   const float piv = bf2f(x[c]);
   const double n = static_cast<double>(P);
   const double mean_s = s1 / n;
@@ -185,13 +189,16 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const uint16_t* __restric
 __global__ void k_bn_bwd_finalize(const float* __restrict__ ws, int nblk, int P, int C, const float* __restrict__ gamma,
                                   const float* __restrict__ invstd, float* __restrict__ dgamma, float* __restrict__ dbeta,
                                   float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (c >= C) return;
-  float s1 = 0.f, s2 = 0.f;
-  for (int b = 0; b < nblk; ++b) {
-    s1 += ws[static_cast<long>(b) * 2 * C + c];
-    s2 += ws[static_cast<long>(b) * 2 * C + C + c];
+  float p1 = 0.f, p2 = 0.f;
+  for (int b = lane; b < nblk; b += 64) {
+    p1 += ws[static_cast<long>(b) * 2 * C + c];
+    p2 += ws[static_cast<long>(b) * 2 * C + C + c];
   }
+  const float s1 = wave_sum(p1), s2 = wave_sum(p2);
+  if (lane != 0) return;
   if (dgamma) dgamma[c] = s2;
   if (dbeta) dbeta[c] = s1;
   const float a = (gamma ? gamma[c] : 1.f) * invstd[c];
@@ -350,9 +357,13 @@ __device__ __forceinline__ float uniform01(unsigned long long seed, unsigned lon
 }
 
 // mode 0: elementwise on [n_elems]; mode 1: channel mask over NHWC with (HW, C).
-// mask out (uint8) is written so backward is a pure multiply.
+// mask out (uint8) is written so backward is a pure multiply.  The seed is (*counter, salt): the
+// counter lives in device memory and is advanced by k_rng_advance after every call, so a captured
+// hipGraph draws fresh masks on every replay.
 __global__ void k_dropout_fwd(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, uint8_t* __restrict__ mask,
-                              long n, int mode, int HW, int C, float p, unsigned long long seed) {
+                              long n, int mode, int HW, int C, float p, const unsigned long long* counter,
+                              unsigned long long salt) {
+  const unsigned long long seed = counter[0] * 0xD1B54A32D192ED03ULL + salt;
   const float scale = 1.f / (1.f - p);
   for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < n;
        i += static_cast<long>(gridDim.x) * blockDim.x) {
@@ -369,6 +380,8 @@ __global__ void k_dropout_fwd(const uint16_t* __restrict__ x, uint16_t* __restri
     y[i] = keep ? f2bf(bf2f(x[i]) * scale) : uint16_t(0);
   }
 }
+
+__global__ void k_rng_advance(unsigned long long* counter) { counter[0] += 1; }
 
 __global__ void k_dropout_bwd(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
                               uint16_t* __restrict__ dx, long n, float p) {
@@ -432,7 +445,7 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
   int rpb;
   const int nblk = bn_blocks(P, C, rpb);
   hipLaunchKernelGGL(k_bn_stats, dim3(nblk), dim3(256), 0, s, x, P, C, rpb, ws);
-  hipLaunchKernelGGL(k_bn_finalize, dim3(ceil_div(C, 256)), dim3(256), 0, s, x, ws, nblk, P, C, gamma, beta, eps,
+  hipLaunchKernelGGL(k_bn_finalize, dim3(ceil_div(C, 4)), dim3(256), 0, s, x, ws, nblk, P, C, gamma, beta, eps,
                      momentum, running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C);
   const long nvec = static_cast<long>(P) * C / 8;
   hipLaunchKernelGGL(k_bn_apply, dim3(stream_grid(nvec, 256)), dim3(256), 0, s, x, scale_shift, scale_shift + C,
@@ -454,7 +467,7 @@ hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, cons
   int rpb;
   const int nblk = bn_blocks(P, C, rpb);
   hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(nblk), dim3(256), 0, s, dy, x, y, mean, invstd, P, C, rpb, relu, ws);
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(ceil_div(C, 256)), dim3(256), 0, s, ws, nblk, P, C, gamma, invstd,
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(ceil_div(C, 4)), dim3(256), 0, s, ws, nblk, P, C, gamma, invstd,
                      dgamma, dbeta, coef);
   const long nvec = static_cast<long>(P) * C / 8;
   hipLaunchKernelGGL(k_bn_bwd_apply, dim3(stream_grid(nvec, 256)), dim3(256), 0, s, dy, x, y, mean, invstd, coef,
@@ -487,8 +500,10 @@ hipError_t avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, h
   return hipGetLastError();
 }
 hipError_t dropout_fwd(const uint16_t* x, uint16_t* y, uint8_t* mask, long n, int mode, int HW, int C, float p,
-                       unsigned long long seed, hipStream_t s) {
-  hipLaunchKernelGGL(k_dropout_fwd, dim3(stream_grid(n, 256)), dim3(256), 0, s, x, y, mask, n, mode, HW, C, p, seed);
+                       unsigned long long* counter, unsigned long long salt, hipStream_t s) {
+  hipLaunchKernelGGL(k_dropout_fwd, dim3(stream_grid(n, 256)), dim3(256), 0, s, x, y, mask, n, mode, HW, C, p,
+                     counter, salt);
+  hipLaunchKernelGGL(k_rng_advance, dim3(1), dim3(1), 0, s, counter);
   return hipGetLastError();
 }
 hipError_t dropout_bwd(const uint16_t* dy, const uint8_t* mask, uint16_t* dx, long n, float p, hipStream_t s) {

@@ -28,7 +28,7 @@ EXTENSIONS = {
     # module name -> (hip sources, host C++ sources)
     "_C": (
         ["kernels/gemm.hip", "kernels/elementwise.hip", "kernels/loss.hip", "kernels/optim.hip",
-         "kernels/norm_pool.hip"],
+         "kernels/norm_pool.hip", "kernels/cnn_fused.hip"],
         ["bindings.cpp"],
     ),
 }

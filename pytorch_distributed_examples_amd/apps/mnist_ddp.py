@@ -1,0 +1,182 @@
+"""Elastic DDP MNIST trainer (reference: pytorch_elastic/mnist_ddp_elastic.py).
+
+Launched by torchrun exactly like the reference (docstring at :1-7):
+
+    torchrun --nnodes=1:2 --nproc_per_node=N --rdzv_backend=c10d --rdzv_endpoint=127.0.0.1:29603 \
+        --max-restarts=3 pytorch_elastic/mnist_ddp_elastic.py 10 5 [--batch_size 128]
+
+Behaviour kept from the reference: positional ``total_epochs save_every``, ``--batch_size`` (default 128;
+the reference's help text says 32, :207), the MLP 5x1024 + Adam(1e-3) + CrossEntropy (:162-175), one
+DistributedSampler shard per rank with ``set_epoch`` (:89), a per-rank test pass on the rank's test shard
+after every epoch (:117-130; we also print the all-reduced global accuracy, Q6), snapshot every
+``save_every`` epochs with the reference's keys and resume from it (Q4 semantics kept), the printed
+lines, and ``Execution time``.
+
+MI355X-first differences: RCCL (``nccl``) over xGMI on GPUs -- gloo on CPU -- with the xGMI bucket
+policy; bf16 MFMA kernels; HBM-resident synthetic MNIST; atomic snapshot by global rank 0 only;
+``--model cnn`` runs BASELINE config 1's CNN through the same plumbing; ``--rewire`` keeps the worker
+alive across membership changes (in-process RCCL communicator re-wire, :mod:`..elastic.rewire`).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import time
+
+import torch
+
+from ..data.loader import ShardedLoader
+from ..data.synthetic import mnist_splits
+from ..elastic import fault
+from ..elastic.snapshot import load_snapshot, save_snapshot
+from ..ops import functional as OF
+from ..ops.optim import FusedAdam, FusedSGD
+from ..parallel import dist as pdist
+from ..parallel.ddp import DistributedDataParallel
+from ..utils.log import RankLogger, MetricsWriter
+
+
+def load_train_objs(model_name: str, device, train_size: int, test_size: int):
+    train_set, test_set = mnist_splits(device=device, train=train_size, test=test_size)
+    if model_name == "cnn":
+        from ..models.cnn import Net
+
+        model = Net()
+        loss = OF.nll_loss
+        make_opt = lambda params: FusedSGD(params, lr=0.01)  # noqa: E731  (mnist_horovod.py:50)
+    else:
+        from ..models.mlp import reference_mlp
+
+        model = reference_mlp()
+        loss = OF.cross_entropy
+        make_opt = lambda params: FusedAdam(params, lr=1e-3)  # noqa: E731  (mnist_ddp_elastic.py:173)
+    return train_set, test_set, model, make_opt, loss
+
+
+class Trainer:
+    def __init__(self, ctx, model, train_data, test_data, make_opt, criterion, save_every, snapshot_path,
+                 log, metrics=None, save_optimizer=True):
+        self.ctx = ctx
+        self.global_rank = int(os.environ.get("RANK", ctx.rank))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", ctx.local_rank))
+        self.model = model.to(ctx.device)
+        self.train_data, self.test_data = train_data, test_data
+        self.criterion = criterion
+        self.save_every = save_every
+        self.snapshot_path = snapshot_path
+        self.epochs_run = 0
+        self.log = log
+        self.metrics = metrics
+        self.save_optimizer = save_optimizer
+        self.optimizer = make_opt(self.model.parameters())
+        self.global_step = 0
+        if os.path.exists(snapshot_path):
+            log.print("Loading snapshot")
+            self._load_snapshot(snapshot_path)
+        self.ddp = DistributedDataParallel(self.model)
+
+    def _load_snapshot(self, path):
+        snap = load_snapshot(path)
+        self.model.load_state_dict(snap["MODEL_STATE"])
+        if "OPTIMIZER_STATE" in snap:
+            self.optimizer.load_state_dict(snap["OPTIMIZER_STATE"])
+        self.epochs_run = snap["EPOCHS_RUN"]
+        self.log.print(f"Resuming training from snapshot at Epoch {self.epochs_run}")
+
+    def _run_batch(self, source, targets):
+        self.ddp.zero_grad()
+        output = self.ddp(source)
+        loss = self.criterion(output, targets)
+        loss.backward()
+        self.optimizer.step()
+        fault.maybe_fault(self.global_step, self.global_rank)
+        self.global_step += 1
+        return loss
+
+    def _run_epoch(self, epoch):
+        self.model.train()
+        b_sz = self.train_data.batch_size
+        self.log.print(f"Local Rank: {self.local_rank} | Global Rank: {self.global_rank} | Epoch {epoch} | "
+                       f"Batchsize: {b_sz} | Steps: {len(self.train_data)}", all_ranks=True)
+        self.train_data.set_epoch(epoch)
+        t0 = time.perf_counter()
+        n = 0
+        loss = None
+        for source, targets in self.train_data:
+            loss = self._run_batch(source, targets)
+            n += source.shape[0]
+        if self.ctx.device.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        img_s = pdist.sum_over_ranks(n / dt, self.ctx.device)
+        if self.metrics is not None:
+            self.metrics.write(epoch=epoch, images_per_s=img_s, epoch_s=dt,
+                               loss=float(loss.item()) if loss is not None else None)
+        self.log.print(f"Epoch {epoch} | train {dt:.2f}s | {img_s:.0f} images/s (node)")
+        self.test()
+
+    def _save_snapshot(self, epoch):
+        save_snapshot(self.snapshot_path, self.model.state_dict(), epoch,
+                      self.optimizer.state_dict() if self.save_optimizer else None)
+        self.log.print(f"Epoch {epoch} | Training snapshot saved at {self.snapshot_path}")
+
+    def train(self, max_epochs: int):
+        for epoch in range(self.epochs_run, max_epochs):
+            self._run_epoch(epoch)
+            if self.global_rank == 0 and epoch % self.save_every == 0:
+                self._save_snapshot(epoch)
+
+    @torch.no_grad()
+    def test(self):
+        # The reference never calls model.eval() (:117-130); we evaluate in eval mode (dropout off).
+        was = self.model.training
+        self.model.eval()
+        correct = torch.zeros((), dtype=torch.long, device=self.ctx.device)
+        total = 0
+        for images, labels in self.test_data:
+            outputs = self.model(images)
+            predicted = outputs.float().argmax(1)
+            total += labels.size(0)
+            correct += (predicted == labels).sum()
+        c = int(correct.item())
+        self.log.print(f"Test accuracy: {(c / max(1, total)) * 100:.2f}%", all_ranks=True)
+        gc = pdist.sum_over_ranks(c, self.ctx.device)
+        gt = pdist.sum_over_ranks(total, self.ctx.device)
+        self.log.print(f"Global test accuracy: {(gc / max(1, gt)) * 100:.2f}%")
+        self.model.train(was)
+
+
+def main(argv=None):
+    parser = argparse.ArgumentParser(description="simple distributed training job")
+    parser.add_argument("total_epochs", type=int, help="Total epochs to train the model")
+    parser.add_argument("save_every", type=int, help="How often to save a snapshot")
+    parser.add_argument("--batch_size", default=128, type=int, help="Input batch size on each device (default: 128)")
+    parser.add_argument("--model", default="mlp", choices=["mlp", "cnn"])
+    parser.add_argument("--device", default="auto", choices=["auto", "cpu", "gpu"])
+    parser.add_argument("--snapshot_path", default="snapshot.pt")
+    parser.add_argument("--train_size", type=int, default=60000)
+    parser.add_argument("--test_size", type=int, default=10000)
+    parser.add_argument("--metrics", default=None, help="JSONL metrics file (rank 0)")
+    parser.add_argument("--rewire", action="store_true",
+                        help="survive membership changes in-process (RCCL communicator re-wire)")
+    args = parser.parse_args(argv)
+
+    start = time.time()
+    if args.rewire:
+        from ..elastic.rewire import run_elastic
+
+        run_elastic(args)
+    else:
+        ctx = pdist.init_distributed(device="cpu" if args.device == "cpu" else None)
+        log = RankLogger(ctx.rank)
+        metrics = MetricsWriter(args.metrics) if args.metrics and ctx.rank == 0 else None
+        train_set, test_set, model, make_opt, criterion = load_train_objs(args.model, ctx.device, args.train_size,
+                                                                          args.test_size)
+        train_data = ShardedLoader(train_set, args.batch_size, ctx.world_size, ctx.rank, shuffle=True)
+        test_data = ShardedLoader(test_set, args.batch_size, ctx.world_size, ctx.rank, shuffle=False)
+        trainer = Trainer(ctx, model, train_data, test_data, make_opt, criterion, args.save_every,
+                          args.snapshot_path, log, metrics)
+        trainer.train(args.total_epochs)
+        pdist.shutdown()
+    end = time.time()
+    print(f"Execution time: {end - start}")

@@ -60,6 +60,28 @@ def _cached(p: torch.Tensor, kind, fn):
     return ent[1]
 
 
+_EMU = [False]
+
+
+class emulate_bf16_on_cpu:
+    """Context manager for numerics tests: the CPU reference path rounds weights, inputs and outputs of
+    every op to bf16 like the GPU kernels store them (fp32 math in between), so GPU-vs-CPU differences
+    isolate kernel bugs from bf16 storage noise."""
+
+    def __enter__(self):
+        self._old = _EMU[0]
+        _EMU[0] = True
+
+    def __exit__(self, *exc):
+        _EMU[0] = self._old
+
+
+def _emu(t):
+    if t is None or not _EMU[0]:
+        return t
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
 def pad8(c: int) -> int:
     return (c + 7) // 8 * 8
 
@@ -112,8 +134,9 @@ def linear(x, weight, bias=None, relu=False, out_f32=False, consumer_masks=False
     fuses threshold_backward into the dgrad GEMM epilogue (SURVEY.md §2.5 MLP table).
     """
     if not x.is_cuda:
-        y = F.linear(x, weight, bias)
-        return F.relu(y) if relu else y
+        y = F.linear(_emu(x), _emu(weight), bias)
+        y = F.relu(y) if relu else y
+        return y if out_f32 else _emu(y)
     if x.dtype != torch.bfloat16:
         x = _C().cast_bf16(x.float().contiguous())
     return _LinearFn.apply(x.contiguous(), weight, bias, relu, out_f32, consumer_masks, mask_input_grad)
@@ -160,15 +183,15 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, relu=False):
     """2-D convolution.  GPU: ``x`` is NHWC bf16 with C padded to a multiple of 8; output NHWC with
     Cout padded to a multiple of 8 (padded channels are exactly zero).  CPU: NCHW fp32 F.conv2d."""
     if not x.is_cuda:
-        y = F.conv2d(x, weight, bias, stride=stride, padding=padding)
-        return F.relu(y) if relu else y
+        y = F.conv2d(_emu(x), _emu(weight), bias, stride=stride, padding=padding)
+        return _emu(F.relu(y) if relu else y)
     return _Conv2dFn.apply(x.contiguous(), weight, bias, int(stride), int(padding), relu)
 
 
 def to_native_image(x: torch.Tensor) -> torch.Tensor:
     """NCHW fp32 input batch -> the device's native activation layout (NHWC bf16 padded on GPU)."""
     if not x.is_cuda:
-        return x
+        return _emu(x)
     return _C().nchw_to_nhwc(x.float().contiguous(), pad8(x.shape[1]))
 
 
@@ -201,7 +224,7 @@ def batch_norm(x, weight, bias, running_mean, running_var, training, momentum=0.
         y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
         if residual is not None:
             y = y + residual
-        return F.relu(y) if relu else y
+        return _emu(F.relu(y) if relu else y)
     x = x.contiguous()
     if training:
         return _BatchNormFn.apply(x, weight, bias, running_mean, running_var,
@@ -253,7 +276,7 @@ class _AvgPoolFn(torch.autograd.Function):
 def global_avg_pool_flat(x):
     """AdaptiveAvgPool2d((1, 1)) + flatten -> [N, C]."""
     if not x.is_cuda:
-        return torch.flatten(F.adaptive_avg_pool2d(x, (1, 1)), 1)
+        return _emu(torch.flatten(F.adaptive_avg_pool2d(x, (1, 1)), 1))
     return _AvgPoolFn.apply(x.contiguous())
 
 
@@ -270,8 +293,8 @@ def flatten_nchw(x, channels):
 # ---------------------------------------------------------------------------------------------
 class _DropoutFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, p, channel, seed):
-        y, mask = _C().dropout_fwd(x, p, seed, channel)
+    def forward(ctx, x, p, channel, salt):
+        y, mask = _C().dropout_fwd(x, p, _rng_counter(x.device), salt, channel)
         ctx.p = p
         ctx.save_for_backward(mask)
         return y
@@ -282,8 +305,25 @@ class _DropoutFn(torch.autograd.Function):
         return _C().dropout_bwd(dy.contiguous(), mask, ctx.p), None, None, None
 
 
+_RNG: dict = {}
+_SALT = [0]
+
+
+def _rng_counter(device) -> torch.Tensor:
+    """Per-device int64 RNG counter in device memory, seeded from torch's generator once and advanced by
+    the dropout kernels themselves (so hipGraph replays draw new masks)."""
+    key = (device.type, device.index)
+    t = _RNG.get(key)
+    if t is None:
+        t = torch.randint(0, 2 ** 40, (1,), dtype=torch.long).to(device)
+        _RNG[key] = t
+    return t
+
+
 def _seed() -> int:
-    return int(torch.randint(0, 2 ** 62, (1,)).item())
+    """Per-call-site salt (distinct streams for distinct dropout calls within a step)."""
+    _SALT[0] = (_SALT[0] + 0x9E3779B97F4A7C15) % (2 ** 62)
+    return _SALT[0]
 
 
 def dropout(x, p=0.5, training=True, channel=False):
@@ -291,7 +331,7 @@ def dropout(x, p=0.5, training=True, channel=False):
     if not training or p == 0.0:
         return x
     if not x.is_cuda:
-        return F.dropout2d(x, p, training) if channel else F.dropout(x, p, training)
+        return _emu(F.dropout2d(x, p, training) if channel else F.dropout(x, p, training))
     if x.dtype != torch.bfloat16:
         x = _C().cast_bf16(x.float().contiguous())
     return _DropoutFn.apply(x.contiguous(), float(p), channel, _seed())

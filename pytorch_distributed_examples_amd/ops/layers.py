@@ -75,10 +75,25 @@ class BatchNorm2d(nn.Module):
         self.register_buffer("running_mean", torch.zeros(num_features))
         self.register_buffer("running_var", torch.ones(num_features))
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+        self._nbt_pending = 0
+
+    def _flush_nbt(self):
+        # GPU path counts batches on the host and folds them into the buffer lazily: one less kernel
+        # launch per BN layer per step, same state_dict value.
+        if self._nbt_pending:
+            self.num_batches_tracked.add_(self._nbt_pending)
+            self._nbt_pending = 0
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        self._flush_nbt()
+        super()._save_to_state_dict(destination, prefix, keep_vars)
 
     def forward(self, x, residual=None, relu=False):
         if self.training:
-            self.num_batches_tracked.add_(1)
+            if x.is_cuda:
+                self._nbt_pending += 1
+            else:
+                self.num_batches_tracked.add_(1)
         return OF.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
                              self.momentum, self.eps, residual, relu)
 

@@ -47,7 +47,7 @@ def _flat_broadcast(tensors, src, group):
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float | None = None,
                  broadcast_buffers: bool = True, overlap: bool = True, grad_dtype: torch.dtype | None = None,
-                 src_rank: int = 0):
+                 src_rank: int = 0, param_order: str = "reverse"):
         super().__init__()
         self.module = module
         self.pg = process_group
@@ -62,8 +62,10 @@ class DistributedDataParallel(nn.Module):
         if self.world > 1:
             _flat_broadcast(list(module.parameters()) + list(module.buffers()), src_rank, process_group)
 
-        # bucket plan over parameters in reverse registration order (~ gradient ready order)
-        order = list(reversed(self._params))
+        # bucket plan over parameters in reverse registration order (~ gradient ready order).
+        # param_order="forward" lays the flat gradient out in registration order instead, so a fused
+        # whole-model kernel that produces all gradients at once can write it directly.
+        order = list(reversed(self._params)) if param_order == "reverse" else list(self._params)
         sizes = [p.numel() * (2 if grad_dtype == torch.bfloat16 else 4) for p in order]
         cap = int(bucket_cap_mb * 2 ** 20) if bucket_cap_mb else None
         plan = xgmi.plan_buckets(sizes, self.world, cap)

@@ -1,0 +1,53 @@
+"""Whole-training-step hipGraph capture (the MNIST nets are launch-bound).
+
+A training step of this suite is a fixed sequence of HIP kernels: layout/cast kernels, MFMA GEMMs,
+fused epilogues, BN/pool/loss kernels, the RCCL all-reduce of the flat gradient buffer and ONE fused
+optimizer kernel whose hyper-parameters/step live in device memory.  :class:`CapturedStep` records that
+sequence once into a ``torch.cuda.CUDAGraph`` (a hipGraph on ROCm) and replays it with a single launch
+per step; the batch is copied into static input buffers before each replay.
+
+Capture rules honoured by the ops layer:
+* no host synchronisation inside the step (no ``.item()``; loss stays a device tensor);
+* weight compute-copies are re-derived inside the graph (``recompute_weight_copies``) so replays see the
+  optimizer's updates;
+* dropout draws from a device-resident counter advanced by the kernels (new masks every replay);
+* the DDP wrapper runs in ``overlap=False`` mode (bucket all-reduces issued after backward on the
+  capturing stream) -- RCCL collectives are capturable.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import functional as OF
+
+
+class CapturedStep:
+    def __init__(self, step_fn, example_inputs, warmup: int = 3):
+        self.step_fn = step_fn
+        self.static_inputs = [t.clone() for t in example_inputs]
+        self.graph = None
+        self.static_out = None
+        self._warmup = warmup
+
+    def capture(self):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(self._warmup):
+                self.step_fn(*self.static_inputs)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with OF.recompute_weight_copies():
+            with torch.cuda.graph(g):
+                self.static_out = self.step_fn(*self.static_inputs)
+        torch.cuda.synchronize()
+        self.graph = g
+        return self
+
+    def __call__(self, *inputs):
+        for dst, src in zip(self.static_inputs, inputs):
+            if dst.data_ptr() != src.data_ptr():
+                dst.copy_(src, non_blocking=True)
+        self.graph.replay()
+        return self.static_out

@@ -1,0 +1,26 @@
+"""Diagnostic: per-phase time of the fused CNN kernel from in-kernel wall_clock64 stamps (100 MHz)."""
+import torch
+
+from pytorch_distributed_examples_amd.models.cnn import Net
+from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
+
+dev = torch.device("cuda")
+net = Net().to(dev).train()
+f = FusedCNN(net)
+B = 1024
+x = torch.randn(B, 1, 28, 28, device=dev)
+y = torch.randint(0, 10, (B,), device=dev)
+for _ in range(5):
+    f.forward_backward(x, y)
+nwg = B // 4
+f.stamps = torch.zeros(nwg, 16, dtype=torch.long, device=dev)
+f.forward_backward(x, y)
+torch.cuda.synchronize()
+st = f.stamps.cpu().double()
+d = (st[:, 1:12] - st[:, 0:11]) / 100.0  # us
+names = ["P0 load", "P1 conv1", "P2 conv2", "P3 fc1", "P4a fc2", "P4b loss", "P5 fc2bwd", "P6 fc1bwd",
+         "P7a c2wgrad", "P7b c2dgrad", "P9 conv1wgrad"]
+for i, n in enumerate(names):
+    print(f"{n:14s} median {d[:, i].median().item():7.2f} us  max {d[:, i].max().item():7.2f} us")
+print("total median", (st[:, 11] - st[:, 0]).median().item() / 100.0, "us")
+print("span (first start -> last stamp)", (st[:, 11].max() - st[:, 0].min()).item() / 100.0, "us")

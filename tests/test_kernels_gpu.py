@@ -90,7 +90,8 @@ def test_conv_fwd_bwd(gpu, cfg):
     assert rel_err(b.grad, g.sum((0, 2, 3))) < 1e-2
     dx = xn.grad[..., :ci].permute(0, 3, 1, 2)
     assert rel_err(dx, xr2.grad) < 2e-2
-    assert xn.grad[..., ci:].abs().max().item() == 0.0
+    if xn.shape[-1] > ci:
+        assert xn.grad[..., ci:].abs().max().item() == 0.0
 
 
 @pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])

@@ -23,8 +23,9 @@ def test_mlp_step_matches_cpu(gpu):
     m_gpu = copy.deepcopy(m_cpu).to(gpu)
     x = torch.randn(128, 1, 28, 28)
     y = torch.randint(0, 10, (128,))
-    l_cpu = OF.cross_entropy(m_cpu(x), y)
-    l_cpu.backward()
+    with OF.emulate_bf16_on_cpu():
+        l_cpu = OF.cross_entropy(m_cpu(x), y)
+        l_cpu.backward()
     l_gpu = OF.cross_entropy(m_gpu(x.to(gpu)), y.to(gpu))
     l_gpu.backward()
     assert abs(l_cpu.item() - l_gpu.item()) < 2e-2
@@ -38,8 +39,9 @@ def test_cnn_step_matches_cpu(gpu):
     m_gpu = copy.deepcopy(m_cpu).to(gpu).eval()
     x = torch.randn(64, 1, 28, 28)
     y = torch.randint(0, 10, (64,))
-    l_cpu = OF.nll_loss(m_cpu(x), y)
-    l_cpu.backward()
+    with OF.emulate_bf16_on_cpu():
+        l_cpu = OF.nll_loss(m_cpu(x), y)
+        l_cpu.backward()
     l_gpu = OF.nll_loss(m_gpu(x.to(gpu)), y.to(gpu))
     l_gpu.backward()
     assert abs(l_cpu.item() - l_gpu.item()) < 2e-2
@@ -53,11 +55,13 @@ def test_resnet_shards_match_cpu(gpu):
     g1, g2 = copy.deepcopy(s1).to(gpu), copy.deepcopy(s2).to(gpu)
     x = torch.randn(4, 3, 128, 128)
     t = torch.randn(4, 1000)
-    out_cpu = s2(s1(x))
+    with OF.emulate_bf16_on_cpu():
+        out_cpu = s2(s1(x))
     out_gpu = g2(g1(x.to(gpu)))
     assert out_gpu.shape == (4, 1000)
     assert rel_err(out_gpu.cpu(), out_cpu) < 5e-2
-    OF.mse_loss(out_cpu, t).backward()
+    with OF.emulate_bf16_on_cpu():
+        OF.mse_loss(out_cpu, t).backward()
     OF.mse_loss(out_gpu, t.to(gpu)).backward()
     for (n, p1), p2 in zip(list(s1.named_parameters())[:6] + list(s2.named_parameters())[-4:],
                            list(g1.parameters())[:6] + list(g2.parameters())[-4:]):
@@ -80,4 +84,45 @@ def test_cnn_trains(gpu):
         loss.backward()
         opt.step()
         losses.append(loss.item())
+    assert sum(losses[-5:]) / 5 < losses[0] * 0.7, losses
+
+
+def test_fused_cnn_matches_reference(gpu):
+    """Fused whole-network kernel (fp32) vs the fp32 CPU reference, dropout off (eval)."""
+    from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
+
+    torch.manual_seed(0)
+    m_cpu = Net().eval()
+    m_gpu = copy.deepcopy(m_cpu).to(gpu).eval()
+    fused = FusedCNN(m_gpu)
+    x = torch.randn(300, 1, 28, 28)
+    y = torch.randint(0, 10, (300,))
+    l_cpu = OF.nll_loss(m_cpu(x), y)
+    l_cpu.backward()
+    g = torch.zeros(fused.flat.numel(), device=gpu)
+    loss = fused.forward_backward(x.to(gpu), y.to(gpu), grad_out=g)
+    assert abs(loss.item() - l_cpu.item()) < 1e-4
+    off = 0
+    for n, p in m_cpu.named_parameters():
+        k = p.numel()
+        assert rel_err(g[off:off + k].cpu().view_as(p), p.grad) < 1e-3, n
+        off += k
+
+
+def test_fused_cnn_trains_with_dropout(gpu):
+    from pytorch_distributed_examples_amd.data.synthetic import SyntheticMNIST
+    from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
+    from pytorch_distributed_examples_amd.ops.optim import FusedSGD
+
+    torch.manual_seed(0)
+    m = Net().to(gpu).train()
+    fused = FusedCNN(m)
+    fused.grad_buffer()
+    opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9)
+    data = SyntheticMNIST(4096, device=gpu, seed=1)
+    losses = []
+    for i in range(40):
+        x, y = data.batch(i, 256)
+        losses.append(fused.forward_backward(x, y).item())
+        opt.step()
     assert sum(losses[-5:]) / 5 < losses[0] * 0.7, losses
