@@ -1,0 +1,127 @@
+// pybind11 module `_comm`: RCCL communicator manager + Horovod-style fusion engine.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "comm_manager.h"
+#include "fusion_engine.h"
+
+namespace {
+
+using pde::FusionEngine;
+using pde::RcclComm;
+
+int code_of(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return 0;
+    case at::kBFloat16: return 1;
+    case at::kHalf: return 2;
+    case at::kDouble: return 3;
+    case at::kInt: return 4;
+    case at::kLong: return 5;
+    case at::kByte: return 6;
+    default: TORCH_CHECK(false, "rccl: unsupported dtype");
+  }
+  return -1;
+}
+
+hipStream_t cur(const at::Tensor& t) { return at::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+void check_gpu(const at::Tensor& t) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "rccl ops need contiguous GPU tensors");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X communication runtime: RCCL communicator manager and tensor-fusion engine";
+  m.def("rccl_unique_id", []() { return py::bytes(pde::rccl_unique_id()); });
+  m.def("rccl_version", &pde::rccl_version);
+
+  py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def(py::init<>())
+      .def("init",
+           [](RcclComm& c, py::bytes uid, int rank, int size, int device, bool blocking) {
+             std::string u = uid;
+             py::gil_scoped_release nogil;
+             c.init(u, rank, size, device, blocking);
+           },
+           py::arg("uid"), py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("blocking") = true)
+      .def("abort", [](RcclComm& c) { py::gil_scoped_release nogil; c.abort(); })
+      .def("destroy", [](RcclComm& c) { py::gil_scoped_release nogil; c.destroy(); })
+      .def_property_readonly("valid", &RcclComm::valid)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("size", &RcclComm::size)
+      .def_property_readonly("device", &RcclComm::device)
+      .def("async_error", &RcclComm::async_error)
+      // tensor-level collectives, enqueued on the caller's CURRENT torch stream (stream-ordered with
+      // the producing kernels; no host synchronisation)
+      .def("allreduce_",
+           [](RcclComm& c, at::Tensor& t, int op) {
+             check_gpu(t);
+             c.allreduce(t.data_ptr(), t.data_ptr(), t.numel(), code_of(t), op, cur(t));
+             return t;
+           },
+           py::arg("tensor"), py::arg("op") = 0)
+      .def("broadcast_",
+           [](RcclComm& c, at::Tensor& t, int root) {
+             check_gpu(t);
+             c.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), code_of(t), root, cur(t));
+             return t;
+           })
+      .def("allgather",
+           [](RcclComm& c, const at::Tensor& t) {
+             check_gpu(t);
+             std::vector<int64_t> shape = t.sizes().vec();
+             if (shape.empty()) shape.push_back(1);
+             shape[0] *= c.size();
+             at::Tensor out = at::empty(shape, t.options());
+             c.allgather(t.data_ptr(), out.data_ptr(), t.numel(), code_of(t), cur(t));
+             return out;
+           })
+      .def("reduce_scatter",
+           [](RcclComm& c, const at::Tensor& t, int op) {
+             check_gpu(t);
+             TORCH_CHECK(t.numel() % c.size() == 0, "reduce_scatter: numel must divide by size");
+             at::Tensor out = at::empty({t.numel() / c.size()}, t.options());
+             c.reduce_scatter(t.data_ptr(), out.data_ptr(), out.numel(), code_of(t), op, cur(t));
+             return out;
+           })
+      .def("alltoall",
+           [](RcclComm& c, const at::Tensor& t) {
+             check_gpu(t);
+             TORCH_CHECK(t.numel() % c.size() == 0, "alltoall: numel must divide by size");
+             at::Tensor out = at::empty_like(t);
+             c.alltoall(t.data_ptr(), out.data_ptr(), t.numel() / c.size(), code_of(t), cur(t));
+             return out;
+           })
+      .def("send",
+           [](RcclComm& c, const at::Tensor& t, int peer) {
+             check_gpu(t);
+             c.send(t.data_ptr(), t.numel(), code_of(t), peer, cur(t));
+           })
+      .def("recv",
+           [](RcclComm& c, at::Tensor& t, int peer) {
+             check_gpu(t);
+             c.recv(t.data_ptr(), t.numel(), code_of(t), peer, cur(t));
+             return t;
+           })
+      .def("group_start", &RcclComm::group_start)
+      .def("group_end", &RcclComm::group_end);
+
+  py::class_<FusionEngine, std::shared_ptr<FusionEngine>>(m, "FusionEngine")
+      .def(py::init<int, int, int64_t, const std::string&>(), py::arg("rank"), py::arg("size"),
+           py::arg("fusion_bytes"), py::arg("timeline_path") = "")
+      .def("set_rccl", &FusionEngine::set_rccl)
+      .def("set_py_backend", &FusionEngine::set_py_backend)
+      .def("allreduce", &FusionEngine::allreduce, py::arg("tensor"), py::arg("output"), py::arg("name"),
+           py::arg("op"), py::arg("prescale") = 1.0, py::arg("postscale") = 1.0, py::arg("compress") = false)
+      .def("broadcast", &FusionEngine::broadcast)
+      .def("allgather", &FusionEngine::allgather)
+      .def("flush", &FusionEngine::flush)
+      .def("poll", &FusionEngine::poll)
+      .def("wait", &FusionEngine::wait)
+      .def("shutdown", &FusionEngine::shutdown)
+      .def("stats", &FusionEngine::stats)
+      .def_property("fusion_bytes", &FusionEngine::fusion_bytes, &FusionEngine::set_fusion_bytes);
+}

@@ -31,6 +31,10 @@ EXTENSIONS = {
          "kernels/norm_pool.hip", "kernels/cnn_fused.hip"],
         ["bindings.cpp"],
     ),
+    "_comm": (
+        ["comm/pack.hip"],
+        ["comm/comm_manager.cpp", "comm/fusion_engine.cpp", "comm/comm_bindings.cpp"],
+    ),
 }
 
 

@@ -1,0 +1,410 @@
+"""Horovod-compatible core API on the MI355X runtime.
+
+``init()`` joins the job (torchrun env, the elastic driver's rendezvous, or a 1-process world), creates
+the c10d process group used for control messages and -- on GPUs -- an RCCL communicator of our own
+(:class:`_comm.RcclComm`, unique id exchanged through the c10d store) driving the C++ tensor-fusion
+engine (:class:`_comm.FusionEngine`).  On CPU the same engine batches tensors and calls the gloo group.
+
+Collectives return handles; ``synchronize(handle)`` orders the caller's stream after the collective (GPU)
+or blocks (CPU).  Environment knobs (Horovod names where one exists):
+
+    HOROVOD_FUSION_THRESHOLD   fusion buffer bytes (default: xGMI policy, 64 MiB cap)
+    HOROVOD_TIMELINE           Chrome-trace file written by the engine
+    PDE_HVD_TIMEOUT            seconds before a stuck collective is declared failed (GPU, default 300)
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import threading
+import time
+
+import torch
+import torch.distributed as dist
+
+from .. import _native
+from ..elastic import rendezvous
+from ..parallel import xgmi
+from .exceptions import HorovodInternalError
+
+
+class ReduceOp:
+    Sum = 0
+    Average = 1
+    Min = 2
+    Max = 3
+    Product = 4
+    Adasum = 10
+
+
+Average, Sum, Adasum, Min, Max, Product = (ReduceOp.Average, ReduceOp.Sum, ReduceOp.Adasum, ReduceOp.Min,
+                                            ReduceOp.Max, ReduceOp.Product)
+
+_DIST_OPS = {ReduceOp.Sum: dist.ReduceOp.SUM, ReduceOp.Min: dist.ReduceOp.MIN, ReduceOp.Max: dist.ReduceOp.MAX,
+             ReduceOp.Product: dist.ReduceOp.PRODUCT}
+
+
+class _Ctx:
+    def __init__(self):
+        self.initialized = False
+        self.rank = 0
+        self.size = 1
+        self.local_rank = 0
+        self.local_size = 1
+        self.device = torch.device("cpu")
+        self.engine = None
+        self.comm = None
+        self.group = None
+        self.rdzv = None
+        self.generation = 0
+        self.names: dict = {}
+        self.lock = threading.Lock()
+
+
+_ctx = _Ctx()
+
+
+def _fusion_bytes(world: int) -> int:
+    env = os.environ.get("HOROVOD_FUSION_THRESHOLD")
+    if env:
+        return int(env)
+    # one fusion buffer carries >= the xGMI bucket floor; Horovod's 64 MiB default as the cap
+    return max(xgmi.bucket_floor(max(world, 2)), min(xgmi.MAX_BUCKET_BYTES, 64 * 2 ** 20))
+
+
+def _py_allreduce(t, op):
+    group = _ctx.group
+    if op == ReduceOp.Average:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        t.div_(_ctx.size)
+    else:
+        dist.all_reduce(t, op=_DIST_OPS[op], group=group)
+
+
+def _py_broadcast(t, root):
+    dist.broadcast(t, root, group=_ctx.group)
+
+
+def _py_allgather(t, out):
+    dist.all_gather_into_tensor(out, t, group=_ctx.group)
+
+
+def init(comm=None, device: str | None = None):
+    """Initialise (or re-initialise after an elastic reset) the job."""
+    if _ctx.initialized:
+        return
+    use_gpu = device != "cpu" and torch.cuda.is_available()
+    backend = "nccl" if use_gpu else "gloo"
+    timeout = datetime.timedelta(seconds=int(os.environ.get("PDE_HVD_TIMEOUT", "300")))
+    if rendezvous.elastic_env():
+        if _ctx.rdzv is None:
+            _ctx.rdzv = rendezvous.RendezvousClient()
+        rnd, rank, size = _ctx.rdzv.join()
+        local_rank = int(os.environ.get("LOCAL_RANK", os.environ.get("PDE_WORKER_ID", "0")))
+        if use_gpu:
+            torch.cuda.set_device(local_rank % torch.cuda.device_count())
+        store = _ctx.rdzv.pg_store()
+        dist.init_process_group(backend, store=store, rank=rank, world_size=size, timeout=timeout)
+        _ctx.generation = rnd
+    else:
+        from ..parallel import dist as pdist
+
+        ctx = pdist.init_distributed(backend=backend, device="cpu" if not use_gpu else None,
+                                     timeout_s=int(timeout.total_seconds()))
+        rank, size, local_rank = ctx.rank, ctx.world_size, ctx.local_rank
+        store = dist.distributed_c10d._get_default_store()
+    _ctx.rank, _ctx.size = dist.get_rank(), dist.get_world_size()
+    _ctx.local_rank = local_rank
+    _ctx.local_size = int(os.environ.get("LOCAL_WORLD_SIZE", str(_ctx.size)))
+    _ctx.device = torch.device("cuda", torch.cuda.current_device()) if use_gpu else torch.device("cpu")
+    _ctx.group = dist.group.WORLD
+    C = _native.comm()
+    tl = os.environ.get("HOROVOD_TIMELINE", "")
+    if tl and _ctx.size > 1:
+        tl = f"{tl}.rank{_ctx.rank}"
+    eng = C.FusionEngine(_ctx.rank, _ctx.size, _fusion_bytes(_ctx.size), tl)
+    eng.set_py_backend(_py_allreduce, _py_broadcast, _py_allgather)
+    if use_gpu:
+        key = f"pde/hvd/rccl_uid/{_ctx.generation}"
+        if _ctx.rank == 0:
+            store.set(key, C.rccl_unique_id())
+        uid = store.get(key)
+        comm = C.RcclComm()
+        comm.init(uid, _ctx.rank, _ctx.size, _ctx.device.index, True)
+        eng.set_rccl(comm)
+        _ctx.comm = comm
+    _ctx.engine = eng
+    _ctx.names = {}
+    _ctx.initialized = True
+
+
+def shutdown(abort: bool = False):
+    """Tear down the engine, communicator and process group (in-process; used by elastic reset)."""
+    if not _ctx.initialized:
+        return
+    try:
+        _ctx.engine.shutdown()
+    except Exception:  # noqa: BLE001 - a failed peer may leave the engine in an error state
+        pass
+    if _ctx.comm is not None:
+        if abort:
+            _ctx.comm.abort()
+        else:
+            try:
+                _ctx.comm.destroy()
+            except Exception:  # noqa: BLE001
+                _ctx.comm.abort()
+    _ctx.engine = None
+    _ctx.comm = None
+    try:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        pass
+    _ctx.initialized = False
+
+
+def is_initialized() -> bool:
+    return _ctx.initialized
+
+
+def _need():
+    if not _ctx.initialized:
+        raise ValueError("Horovod has not been initialized; use hvd.init().")
+
+
+def size() -> int:
+    _need()
+    return _ctx.size
+
+
+def rank() -> int:
+    _need()
+    return _ctx.rank
+
+
+def local_rank() -> int:
+    _need()
+    return _ctx.local_rank
+
+
+def local_size() -> int:
+    _need()
+    return _ctx.local_size
+
+
+def cross_rank() -> int:
+    return rank() // max(1, local_size())
+
+
+def cross_size() -> int:
+    return max(1, size() // max(1, local_size()))
+
+
+def is_homogeneous() -> bool:
+    return True
+
+
+def rocm_built() -> bool:
+    return torch.version.hip is not None
+
+
+def nccl_built() -> bool:  # RCCL == NCCL API on ROCm
+    return True
+
+
+def mpi_built() -> bool:
+    return False
+
+
+def gloo_built() -> bool:
+    return True
+
+
+def gpu_available(framework: str = "torch") -> bool:
+    return torch.cuda.is_available()
+
+
+# ---------------------------------------------------------------------------------------------
+# handles / collectives
+# ---------------------------------------------------------------------------------------------
+class _Handle:
+    __slots__ = ("h", "output", "post")
+
+    def __init__(self, h, output, post=None):
+        self.h, self.output, self.post = h, output, post
+
+
+def _auto_name(prefix: str, name: str | None) -> str:
+    if name is not None:
+        return name
+    with _ctx.lock:
+        n = _ctx.names.get(prefix, 0)
+        _ctx.names[prefix] = n + 1
+    return f"{prefix}.noname.{n}"
+
+
+def _resolve_op(average, op):
+    if op is None:
+        op = ReduceOp.Average if (average is None or average) else ReduceOp.Sum
+    if op == ReduceOp.Adasum:
+        raise NotImplementedError("Adasum is not supported; use Average or Sum")
+    return op
+
+
+def allreduce_async_(tensor, average=None, name=None, op=None, prescale_factor=1.0, postscale_factor=1.0,
+                     compression_bf16: bool = False):
+    _need()
+    op = _resolve_op(average, op)
+    t = tensor if tensor.is_contiguous() else tensor.contiguous()
+    h = _ctx.engine.allreduce(t, t, _auto_name("allreduce", name), op, float(prescale_factor),
+                              float(postscale_factor), compression_bf16)
+    post = None if t is tensor else (lambda out, tensor=tensor: tensor.copy_(out))
+    return _Handle(h, t, post)
+
+
+def allreduce_async(tensor, average=None, name=None, op=None, prescale_factor=1.0, postscale_factor=1.0):
+    _need()
+    op = _resolve_op(average, op)
+    t = tensor.contiguous()
+    out = torch.empty_like(t)
+    h = _ctx.engine.allreduce(t, out, _auto_name("allreduce", name), op, float(prescale_factor),
+                              float(postscale_factor), False)
+    return _Handle(h, out)
+
+
+def allreduce(tensor, average=None, name=None, compression=None, op=None, prescale_factor=1.0,
+              postscale_factor=1.0):
+    if compression is not None:
+        c, ctx = compression.compress(tensor)
+        out = synchronize(allreduce_async(c, average, name, op, prescale_factor, postscale_factor))
+        return compression.decompress(out, ctx)
+    return synchronize(allreduce_async(tensor, average, name, op, prescale_factor, postscale_factor))
+
+
+def allreduce_(tensor, average=None, name=None, op=None, prescale_factor=1.0, postscale_factor=1.0):
+    return synchronize(allreduce_async_(tensor, average, name, op, prescale_factor, postscale_factor))
+
+
+def grouped_allreduce(tensors, average=None, name=None, op=None):
+    hs = [allreduce_async(t, average, f"{name}.{i}" if name else None, op) for i, t in enumerate(tensors)]
+    return [synchronize(h) for h in hs]
+
+
+def allgather_async(tensor, name=None):
+    _need()
+    h = _ctx.engine.allgather(tensor.contiguous(), _auto_name("allgather", name))
+    return _Handle(h, None)
+
+
+def allgather(tensor, name=None):
+    return synchronize(allgather_async(tensor, name))
+
+
+def broadcast_async_(tensor, root_rank, name=None):
+    _need()
+    t = tensor if tensor.is_contiguous() else tensor.contiguous()
+    h = _ctx.engine.broadcast(t, int(root_rank), _auto_name("broadcast", name))
+    post = None if t is tensor else (lambda out, tensor=tensor: tensor.copy_(out))
+    return _Handle(h, t, post)
+
+
+def broadcast_async(tensor, root_rank, name=None):
+    return broadcast_async_(tensor.clone(), root_rank, name)
+
+
+def broadcast_(tensor, root_rank, name=None):
+    return synchronize(broadcast_async_(tensor, root_rank, name))
+
+
+def broadcast(tensor, root_rank, name=None):
+    return synchronize(broadcast_async(tensor, root_rank, name))
+
+
+def alltoall(tensor, splits=None, name=None):
+    """All-to-all along dim 0 (direct c10d call; RCCL's all-to-all on GPU)."""
+    _need()
+    if splits is None:
+        out = torch.empty_like(tensor)
+        dist.all_to_all_single(out, tensor.contiguous(), group=_ctx.group)
+        return out
+    splits = [int(s) for s in splits]
+    recv = torch.tensor(splits, dtype=torch.long)
+    all_splits = [torch.zeros_like(recv) for _ in range(_ctx.size)]
+    dist.all_gather(all_splits, recv, group=_ctx.group) if _ctx.device.type == "cpu" else None
+    if _ctx.device.type != "cpu":
+        g = recv.to(_ctx.device)
+        gathered = [torch.zeros_like(g) for _ in range(_ctx.size)]
+        dist.all_gather(gathered, g, group=_ctx.group)
+        all_splits = [x.cpu() for x in gathered]
+    in_splits = splits
+    out_splits = [int(s[_ctx.rank]) for s in all_splits]
+    out = tensor.new_empty((sum(out_splits),) + tuple(tensor.shape[1:]))
+    dist.all_to_all_single(out, tensor.contiguous(), out_splits, in_splits, group=_ctx.group)
+    return out
+
+
+def synchronize(handle):
+    _need()
+    if not isinstance(handle, _Handle):
+        raise ValueError("synchronize expects a handle returned by an *_async op")
+    try:
+        out = _ctx.engine.wait(handle.h)
+    except RuntimeError as exc:
+        raise HorovodInternalError(str(exc)) from exc
+    if handle.post is not None:
+        handle.post(out)
+        return handle.output if handle.output is not None else out
+    return out
+
+
+def poll(handle) -> bool:
+    _need()
+    return bool(_ctx.engine.poll(handle.h))
+
+
+def join(device=-1) -> int:
+    """Barrier; returns the last rank to join (Horovod semantics for uneven inputs, simplified)."""
+    _need()
+    t = torch.tensor([_ctx.rank], dtype=torch.float32, device=_ctx.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=_ctx.group)
+    return int(t.item())
+
+
+def barrier():
+    _need()
+    if _ctx.size > 1:
+        dist.barrier(group=_ctx.group)
+
+
+def broadcast_object(obj, root_rank=0, name=None):
+    _need()
+    if _ctx.size == 1:
+        return obj
+    lst = [obj if _ctx.rank == root_rank else None]
+    dist.broadcast_object_list(lst, src=root_rank, group=_ctx.group,
+                               device=_ctx.device if _ctx.device.type == "cuda" else None)
+    return lst[0]
+
+
+def allgather_object(obj, name=None):
+    _need()
+    out = [None] * _ctx.size
+    dist.all_gather_object(out, obj, group=_ctx.group)
+    return out
+
+
+def engine_stats() -> dict:
+    _need()
+    return dict(_ctx.engine.stats())
+
+
+def _wait_with_timeout(h, timeout_s: float):
+    t0 = time.time()
+    while not poll(h):
+        if time.time() - t0 > timeout_s:
+            if _ctx.comm is not None:
+                _ctx.comm.abort()
+            raise HorovodInternalError(f"collective timed out after {timeout_s}s")
+        time.sleep(0.0005)
+    return synchronize(h)
