@@ -55,12 +55,14 @@ class DistributedDataParallel(nn.Module):
         self.broadcast_buffers = broadcast_buffers
         self.overlap = overlap
         self.grad_dtype = grad_dtype
-        self.src = src_rank
+        # src_rank is a rank WITHIN the group; c10d broadcast wants the global rank
+        self.src = dist.get_global_rank(process_group, src_rank) if (process_group is not None and
+                                                                     dist.is_initialized()) else src_rank
         self._params = [p for p in module.parameters() if p.requires_grad]
         dev = self._params[0].device if self._params else torch.device("cpu")
         self._use_avg = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
         if self.world > 1:
-            _flat_broadcast(list(module.parameters()) + list(module.buffers()), src_rank, process_group)
+            _flat_broadcast(list(module.parameters()) + list(module.buffers()), self.src, process_group)
 
         # bucket plan over parameters in reverse registration order (~ gradient ready order).
         # param_order="forward" lays the flat gradient out in registration order instead, so a fused
