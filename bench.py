@@ -91,16 +91,23 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch")
     ap.add_argument("--no-graph", action="store_true", help="run the step eagerly (no hipGraph capture)")
     ap.add_argument("--generic", action="store_true", help="CNN: layer-by-layer kernels instead of the fused step")
+    ap.add_argument("--device", default="auto", choices=["auto", "cpu"], help="cpu: contract/plumbing check only")
     args = ap.parse_args()
     batch = args.batch or {"cnn": 1024, "mlp": 128, "resnet50": 32}[args.model]
 
-    ctx = pdist.init_distributed()
+    ctx = pdist.init_distributed(device="cpu" if args.device == "cpu" else None)
+    on_gpu = ctx.device.type == "cuda"
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
     from pytorch_distributed_examples_amd.parallel.ddp import DistributedDataParallel
 
     model, opt, batch_fn, loss_fn = build(args.model, ctx.device, batch)
-    use_graph = not args.no_graph
+    use_graph = not args.no_graph and on_gpu
     fused = None
-    if args.model == "cnn" and not args.generic:
+    if args.model == "cnn" and not args.generic and ctx.device.type == "cuda":
         # whole-network fused kernel (csrc/kernels/cnn_fused.hip): gradients land directly in the
         # DDP flat buffer (forward layout), then one RCCL all-reduce and one fused SGD launch.
         from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
@@ -143,12 +150,12 @@ def main():
     for i in range(args.warmup):
         step(i)
     pdist.barrier(ctx)
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(args.warmup + i)
     pdist.barrier(ctx)
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
     dt = pdist.max_over_ranks(dt, ctx.device)
     final_loss = float(loss.item())

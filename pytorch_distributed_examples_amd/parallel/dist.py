@@ -62,6 +62,10 @@ def init_distributed(backend: str | None = None, device: str | None = None, time
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
+    if backend == "gloo" and os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
+        # single-host gloo: bind the loopback device explicitly (the container hostname may not resolve,
+        # which otherwise makes re-formed groups after a torchrun restart fail to connect)
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
     if not dist.is_initialized():
         if init_method is None:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

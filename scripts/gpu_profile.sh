@@ -13,4 +13,5 @@ for m in $models; do
     --output-format csv -- python3 "$R/bench.py" --model "$m" --steps $steps --warmup 3 --no-graph \
     > "$R/gpurun_out/prof_$m.log" 2>&1 || { echo "profile $m failed"; tail -5 "$R/gpurun_out/prof_$m.log"; exit 1; }
   cd "$R" && python3 scripts/prof_summary.py "gpurun_out/prof_$m/${m}_kernel_stats.csv" $((steps + 6))
+  python3 scripts/prof_summary.py "gpurun_out/prof_$m/${m}_kernel_stats.csv" $((steps + 6)) --md > "gpurun_out/prof_$m.md"
 done

@@ -1,0 +1,79 @@
+"""GPU communication runtime on one MI355X: the RCCL communicator wrapper (csrc/comm/comm_manager.cpp),
+the fusion engine's GPU path (pack kernel -> RCCL all-reduce -> unpack, csrc/comm/pack.hip) and the
+Horovod-compatible API on top of it, world size 1 (multi-rank behaviour is covered on gloo by
+tests/test_hvd_cpu.py; the driver's 8-GPU bench exercises RCCL across ranks)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_rccl_comm_world1(gpu):
+    from pytorch_distributed_examples_amd import _native
+
+    C = _native.comm()
+    assert C.rccl_version() >= 22000
+    comm = C.RcclComm()
+    comm.init(C.rccl_unique_id(), 0, 1, gpu.index, True)
+    t = torch.arange(1000, device=gpu, dtype=torch.float32)
+    comm.allreduce_(t, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(t.cpu(), torch.arange(1000, dtype=torch.float32))
+    b = torch.randn(77, device=gpu, dtype=torch.bfloat16)
+    ref = b.clone()
+    comm.broadcast_(b, 0)
+    g = comm.allgather(b)
+    torch.cuda.synchronize()
+    assert torch.equal(g.view(-1), ref.view(-1))
+    comm.destroy()
+
+
+def test_hvd_gpu_fusion_world1(gpu):
+    from pytorch_distributed_examples_amd import hvd
+    from pytorch_distributed_examples_amd.models.cnn import Net
+    from pytorch_distributed_examples_amd.ops import functional as OF
+
+    hvd.init()
+    try:
+        assert hvd.size() == 1 and hvd.rocm_built()
+        # many small tensors of mixed sizes -> fused into one pack / all-reduce / unpack
+        ts = [torch.randn(n, device=gpu) for n in (3, 1000, 17, 4096, 1, 513)]
+        refs = [t.clone() for t in ts]
+        hs = [hvd.allreduce_async_(t, name=f"t{i}", op=hvd.Sum, prescale_factor=2.0, postscale_factor=0.25)
+              for i, t in enumerate(ts)]
+        for h in hs:
+            hvd.synchronize(h)
+        for t, r in zip(ts, refs):
+            assert torch.allclose(t, r * 0.5, atol=1e-6)
+        st = hvd.engine_stats()
+        assert st["fused_requests"] >= 5, st
+        # bf16 wire compression round-trips through the pack kernel's f32->bf16 path
+        x = torch.randn(2048, device=gpu)
+        y = hvd.allreduce(x, op=hvd.Average, compression=hvd.Compression.bf16)
+        assert (y - x).abs().max().item() < 1e-2
+        a, b = torch.randn(300, device=gpu), torch.randn(5000, device=gpu)
+        ra, rb = a.clone(), b.clone()
+        hs = [hvd.allreduce_async_(t, name=n, op=hvd.Sum, compression_bf16=True) for n, t in (("a", a), ("b", b))]
+        for h in hs:
+            hvd.synchronize(h)
+        assert torch.equal(a, ra.to(torch.bfloat16).float()) and torch.equal(b, rb.to(torch.bfloat16).float())
+        g = hvd.allgather(torch.ones(2, 3, device=gpu))
+        assert g.shape == (2, 3)
+        # DistributedOptimizer on the GPU == plain SGD at world 1
+        torch.manual_seed(0)
+        m = Net().to(gpu).eval()
+        ref = Net().to(gpu).eval()
+        ref.load_state_dict(m.state_dict())
+        opt = hvd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1),
+                                       named_parameters=m.named_parameters())
+        xs = torch.randn(32, 1, 28, 28, device=gpu)
+        ys = torch.randint(0, 10, (32,), device=gpu)
+        OF.nll_loss(m(xs), ys).backward()
+        opt.step()
+        ropt = torch.optim.SGD(ref.parameters(), lr=0.1)
+        OF.nll_loss(ref(xs), ys).backward()
+        ropt.step()
+        for p, q in zip(m.parameters(), ref.parameters()):
+            assert torch.allclose(p, q, atol=1e-5)
+    finally:
+        hvd.shutdown()
