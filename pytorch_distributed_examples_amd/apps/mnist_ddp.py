@@ -158,7 +158,9 @@ def main(argv=None):
     parser.add_argument("--test_size", type=int, default=10000)
     parser.add_argument("--metrics", default=None, help="JSONL metrics file (rank 0)")
     parser.add_argument("--rewire", action="store_true",
-                        help="survive membership changes in-process (RCCL communicator re-wire)")
+                        help="survive membership changes in-process (RCCL communicator re-wire); launch with "
+                             "python -m pytorch_distributed_examples_amd.launch.hvdrun")
+    parser.add_argument("--commit_every", type=int, default=10, help="--rewire: steps between in-memory commits")
     args = parser.parse_args(argv)
 
     start = time.time()

@@ -1,0 +1,321 @@
+"""In-process communicator re-wire for elastic DDP (SURVEY.md P3 / §5.3 "re-wire RCCL without a job
+restart").
+
+The reference's elastic DDP (pytorch_elastic/mnist_ddp_elastic.py, launched by torchrun ``--max-restarts``)
+survives a failure by killing and restarting EVERY worker, which then reload ``snapshot.pt``
+(mnist_ddp_elastic.py:54-56; observed in SURVEY.md §5.3).  ``mnist_ddp_elastic.py --rewire`` instead keeps
+the surviving processes -- and their device-resident model, optimizer state and data -- alive:
+
+1. workers are launched by the elastic driver (:mod:`..launch.hvdrun`), which publishes membership
+   *rounds* in a TCPStore (:mod:`.rendezvous`);
+2. each round gets a fresh gloo control group and, on GPUs, a fresh RCCL communicator of our own
+   (:class:`_comm.RcclComm`, unique id in the round's ``PrefixStore``), which DDP uses for its buckets;
+3. a dead peer surfaces as a failed gloo collective (CPU) or as an RCCL collective that does not finish
+   while the driver has already published a newer round (GPU): the communicator is ``ncclCommAbort``-ed,
+   the survivors restore their last in-memory commit and join the next round;
+4. workers added by host discovery are picked up at the next commit point: all ranks agree on the
+   driver's ``updated`` flag (MAX all-reduce), close the round cleanly and re-join together;
+5. after every (re)join rank 0 -- always a survivor holding the newest commit -- broadcasts model,
+   optimizer state and the epoch position; the sampler is re-sharded for the new world size and resumes
+   at the first batch not yet consumed by the whole group.
+
+Commits are device-resident clones (one D2D copy per tensor, 288 GB of HBM leaves plenty of room).
+"""
+from __future__ import annotations
+
+import copy
+import datetime
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+from .. import _native
+from .rendezvous import RendezvousClient
+
+
+class PeerFailure(RuntimeError):
+    """A collective of the current round failed (a member died or hung)."""
+
+
+class MembershipChanged(Exception):
+    """The driver published a new round (hosts added/removed); re-join at a commit point."""
+
+
+class _CpuWork:
+    def __init__(self, work):
+        self.work = work
+
+    def wait(self):
+        try:
+            self.work.wait()
+        except RuntimeError as exc:
+            raise PeerFailure(str(exc)) from exc
+
+
+class _GpuWork:
+    def __init__(self, comm, event):
+        self.comm, self.event = comm, event
+
+    def wait(self):
+        self.comm.wait_event(self.event)
+
+
+class RoundComm:
+    """Communicator set of one rendezvous round (see the module docstring)."""
+
+    def __init__(self, rdzv: RendezvousClient, rank: int, size: int, device: torch.device,
+                 timeout_s: float = 120.0, grace_s: float = 2.0):
+        self.rdzv, self.rank, self.size, self.device = rdzv, rank, size, device
+        self.timeout_s, self.grace_s = timeout_s, grace_s
+        store = rdzv.pg_store()
+        dist.init_process_group("gloo", store=store, rank=rank, world_size=size,
+                                timeout=datetime.timedelta(seconds=timeout_s))
+        self.rccl = None
+        if device.type == "cuda" and size > 1:
+            C = _native.comm()
+            if rank == 0:
+                store.set("rccl_uid", C.rccl_unique_id())
+            uid = store.get("rccl_uid")
+            self.rccl = C.RcclComm()
+            self.rccl.init(uid, rank, size, device.index, True)
+        self.supports_avg = self.rccl is not None
+
+    # -- data plane ------------------------------------------------------------------------------
+    def allreduce_async(self, t: torch.Tensor, avg: bool = False):
+        if self.rccl is not None:
+            self.rccl.allreduce_(t, 1 if avg else 0)
+            ev = torch.cuda.Event()
+            ev.record()
+            return _GpuWork(self, ev)
+        return _CpuWork(dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True))
+
+    def broadcast_(self, t: torch.Tensor, src: int):
+        if self.rccl is not None:
+            self.rccl.broadcast_(t, src)
+            ev = torch.cuda.Event()
+            ev.record()
+            self.wait_event(ev)
+            return t
+        try:
+            if t.device.type == "cpu":
+                dist.broadcast(t, src)
+            else:  # control plane is gloo: stage through the host
+                h = t.cpu()
+                dist.broadcast(h, src)
+                t.copy_(h)
+        except RuntimeError as exc:
+            raise PeerFailure(str(exc)) from exc
+        return t
+
+    def wait_event(self, ev):
+        """Host-side liveness wait for an RCCL collective: returns when it finished; aborts the
+        communicator and raises :class:`PeerFailure` on an RCCL async error, when the collective is
+        still pending ``grace_s`` after the driver published a newer round, or after ``timeout_s``."""
+        t0 = time.time()
+        next_check = t0 + 0.05
+        while not ev.query():
+            now = time.time()
+            if now >= next_check:
+                next_check = now + 0.05
+                err = self.rccl.async_error()
+                if err not in (0, 7):  # ncclSuccess, ncclInProgress
+                    self.abort()
+                    raise PeerFailure(f"RCCL async error {err}")
+                if now - t0 > self.grace_s and self.rdzv.hosts_updated():
+                    self.abort()
+                    raise PeerFailure("collective stalled after a membership change")
+                if now - t0 > self.timeout_s:
+                    self.abort()
+                    raise PeerFailure(f"collective timed out after {self.timeout_s}s")
+            time.sleep(0.0002)
+
+    # -- control plane ---------------------------------------------------------------------------
+    def agree(self, flag: bool) -> bool:
+        t = torch.tensor([1.0 if flag else 0.0])
+        try:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        except RuntimeError as exc:
+            raise PeerFailure(str(exc)) from exc
+        return bool(t.item() > 0)
+
+    def broadcast_object(self, obj, src: int = 0):
+        lst = [obj if self.rank == src else None]
+        try:
+            dist.broadcast_object_list(lst, src=src)
+        except RuntimeError as exc:
+            raise PeerFailure(str(exc)) from exc
+        return lst[0]
+
+    def abort(self):
+        if self.rccl is not None:
+            self.rccl.abort()
+
+    def close(self, abort: bool = False):
+        if self.rccl is not None:
+            if abort:
+                self.rccl.abort()
+            else:
+                try:
+                    self.rccl.destroy()
+                except RuntimeError:
+                    self.rccl.abort()
+            self.rccl = None
+        try:
+            if dist.is_initialized():
+                dist.destroy_process_group()
+        except Exception:  # noqa: BLE001 - a group with a dead member may fail to tear down cleanly
+            pass
+
+
+def _clone(obj):
+    if torch.is_tensor(obj):
+        return obj.detach().clone()
+    if isinstance(obj, dict):
+        return type(obj)((k, _clone(v)) for k, v in obj.items())
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_clone(v) for v in obj)
+    return copy.deepcopy(obj)
+
+
+def _to_cpu(obj):
+    if torch.is_tensor(obj):
+        return obj.detach().cpu()
+    if isinstance(obj, dict):
+        return type(obj)((k, _to_cpu(v)) for k, v in obj.items())
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_cpu(v) for v in obj)
+    return obj
+
+
+class Commit:
+    """In-memory commit of model + optimizer + position (device-resident clones)."""
+
+    def __init__(self, model, optimizer, position: dict):
+        self.model, self.optimizer = model, optimizer
+        self.position = position
+        self.save()
+
+    def save(self):
+        self._model = _clone(self.model.state_dict())
+        self._opt = _clone(self.optimizer.state_dict())
+        self._pos = dict(self.position)
+
+    def restore(self):
+        self.model.load_state_dict(self._model)
+        self.optimizer.load_state_dict(_clone(self._opt))
+        self.position.clear()
+        self.position.update(self._pos)
+
+
+def run_elastic(args):
+    """``mnist_ddp_elastic.py --rewire``: the Trainer loop of apps/mnist_ddp.py with in-process re-wire."""
+    from ..apps.mnist_ddp import load_train_objs
+    from ..data.loader import ShardedLoader
+    from ..elastic import fault
+    from ..elastic.snapshot import save_snapshot
+    from ..parallel import dist as pdist
+    from ..parallel.ddp import DistributedDataParallel
+    from ..utils.log import RankLogger
+
+    if "PDE_ELASTIC_STORE" not in os.environ:
+        raise SystemExit("--rewire needs the elastic driver: python -m pytorch_distributed_examples_amd.launch.hvdrun "
+                         "-np N --min-np M pytorch_elastic/mnist_ddp_elastic.py E S --rewire")
+    rdzv = RendezvousClient()
+    use_gpu = args.device != "cpu" and torch.cuda.is_available()
+    if use_gpu:
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        dev = torch.device("cuda", local % torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+    train_set, test_set, model, make_opt, criterion = load_train_objs(args.model, dev, args.train_size,
+                                                                      args.test_size)
+    model = model.to(dev)
+    optimizer = make_opt(model.parameters())
+    pos = {"epoch": 0, "seen": 0}  # samples of the current epoch consumed by the whole group
+    commit = Commit(model, optimizer, pos)
+    commit_every = max(1, int(getattr(args, "commit_every", 10)))
+    step = 0
+    ddp = None
+    pid = os.getpid()
+    while True:
+        rnd, rank, size = rdzv.join()
+        comm = RoundComm(rdzv, rank, size, dev)
+        log = RankLogger(rank)
+        log.print(f"[rewire] round {rnd}: rank {rank} of {size} (pid {pid})", all_ranks=True)
+        try:
+            # rank 0 is a survivor with the newest commit: everybody adopts its state
+            state = comm.broadcast_object({"pos": dict(pos), "opt": _to_cpu(optimizer.state_dict())}
+                                          if rank == 0 else None)
+            if rank != 0:
+                pos.clear()
+                pos.update(state["pos"])
+                optimizer.load_state_dict(state["opt"])
+            if ddp is not None:
+                ddp.remove_hooks()
+            ddp = DistributedDataParallel(model, comm=comm)
+            commit.save()
+            train_data = ShardedLoader(train_set, args.batch_size, size, rank, shuffle=True)
+            test_data = ShardedLoader(test_set, args.batch_size, size, rank, shuffle=False)
+            per_step = args.batch_size * size
+            since = 0
+            for epoch in range(pos["epoch"], args.total_epochs):
+                model.train()
+                train_data.set_epoch(epoch)
+                train_data.start_batch = min(pos["seen"] // per_step, len(train_data))
+                log.print(f"Local Rank: {rdzv.wid} | Global Rank: {rank} | Epoch {epoch} | Batchsize: "
+                          f"{args.batch_size} | Steps: {len(train_data)} | start batch {train_data.start_batch}",
+                          all_ranks=True)
+                for source, targets in train_data:
+                    ddp.zero_grad()
+                    loss = criterion(ddp(source), targets)
+                    loss.backward()
+                    optimizer.step()
+                    fault.maybe_fault(step, rank)
+                    step += 1
+                    pos["seen"] += per_step
+                    since += 1
+                    if since % commit_every == 0:
+                        commit.save()
+                        if comm.agree(rdzv.hosts_updated()):
+                            raise MembershipChanged()
+                pos["epoch"], pos["seen"] = epoch + 1, 0
+                commit.save()
+                _test(model, test_data, dev, comm, log)
+                if rank == 0 and epoch % args.save_every == 0:
+                    save_snapshot(args.snapshot_path, model.state_dict(), epoch, optimizer.state_dict())
+                    log.print(f"Epoch {epoch} | Training snapshot saved at {args.snapshot_path}")
+            log.print(f"[rewire] finished {args.total_epochs} epochs in round {rnd} (world {size}, pid {pid})",
+                      all_ranks=True)
+            comm.close()
+            break
+        except PeerFailure as exc:
+            log.print(f"[rewire] round {rnd}: peer failure ({str(exc).splitlines()[0][:120]}); restoring commit "
+                      f"epoch {commit._pos['epoch']} seen {commit._pos['seen']}", all_ranks=True)
+            comm.close(abort=True)
+            commit.restore()
+        except MembershipChanged:
+            log.print(f"[rewire] round {rnd}: membership changed, re-joining", all_ranks=True)
+            comm.close()
+    pdist.shutdown()
+
+
+@torch.no_grad()
+def _test(model, loader, dev, comm, log):
+    was = model.training
+    model.eval()
+    correct = torch.zeros((), dtype=torch.long, device=dev)
+    total = 0
+    for images, labels in loader:
+        correct += (model(images).float().argmax(1) == labels).sum()
+        total += labels.size(0)
+    t = torch.tensor([float(correct.item()), float(total)])
+    if comm.size > 1:
+        try:
+            dist.all_reduce(t)
+        except RuntimeError as exc:
+            raise PeerFailure(str(exc)) from exc
+    log.print(f"Global test accuracy: {t[0].item() / max(1.0, t[1].item()) * 100:.2f}%")
+    model.train(was)

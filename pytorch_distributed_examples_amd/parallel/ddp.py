@@ -14,7 +14,10 @@ Mirrors ``torch.nn.parallel.DistributedDataParallel`` as used by the reference
 * bucket sizes follow :mod:`.xgmi` (sized for 7 point-to-point links, not DDP's 25 MiB default);
 * ``overlap=False`` skips the hooks and reduces every bucket in :meth:`sync_gradients` -- the form used
   inside a captured hipGraph step;
-* ``grad_dtype=torch.bfloat16`` halves the bytes on the wire (bucket cast -> all-reduce -> cast back).
+* ``grad_dtype=torch.bfloat16`` halves the bytes on the wire (bucket cast -> all-reduce -> cast back);
+* ``comm=`` swaps the c10d group for another communicator (``size``, ``supports_avg``,
+  ``allreduce_async(t, avg) -> work``, ``broadcast_(t, src)``), e.g. the per-round RCCL communicator of
+  :mod:`..elastic.rewire` that is aborted and rebuilt in-process on a membership change.
 """
 from __future__ import annotations
 
@@ -27,7 +30,7 @@ from torch import nn
 from . import xgmi
 
 
-def _flat_broadcast(tensors, src, group):
+def _flat_broadcast(tensors, src, group, comm=None):
     if not tensors:
         return
     by_dtype: dict = {}
@@ -35,7 +38,10 @@ def _flat_broadcast(tensors, src, group):
         by_dtype.setdefault((t.dtype, t.device), []).append(t)
     for (dtype, device), ts in by_dtype.items():
         flat = torch.cat([t.detach().reshape(-1) for t in ts])
-        dist.broadcast(flat, src, group=group)
+        if comm is not None:
+            comm.broadcast_(flat, src)
+        else:
+            dist.broadcast(flat, src, group=group)
         off = 0
         with torch.no_grad():
             for t in ts:
@@ -47,22 +53,29 @@ def _flat_broadcast(tensors, src, group):
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float | None = None,
                  broadcast_buffers: bool = True, overlap: bool = True, grad_dtype: torch.dtype | None = None,
-                 src_rank: int = 0, param_order: str = "reverse"):
+                 src_rank: int = 0, param_order: str = "reverse", comm=None):
         super().__init__()
         self.module = module
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.comm = comm
+        if comm is not None:
+            self.world = comm.size
+        else:
+            self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.broadcast_buffers = broadcast_buffers
         self.overlap = overlap
         self.grad_dtype = grad_dtype
         # src_rank is a rank WITHIN the group; c10d broadcast wants the global rank
-        self.src = dist.get_global_rank(process_group, src_rank) if (process_group is not None and
+        self.src = dist.get_global_rank(process_group, src_rank) if (process_group is not None and comm is None and
                                                                      dist.is_initialized()) else src_rank
         self._params = [p for p in module.parameters() if p.requires_grad]
         dev = self._params[0].device if self._params else torch.device("cpu")
-        self._use_avg = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
+        if comm is not None:
+            self._use_avg = bool(comm.supports_avg)
+        else:
+            self._use_avg = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
         if self.world > 1:
-            _flat_broadcast(list(module.parameters()) + list(module.buffers()), self.src, process_group)
+            _flat_broadcast(list(module.parameters()) + list(module.buffers()), self.src, process_group, comm)
 
         # bucket plan over parameters in reverse registration order (~ gradient ready order).
         # param_order="forward" lays the flat gradient out in registration order instead, so a fused
@@ -132,8 +145,11 @@ class DistributedDataParallel(nn.Module):
             buf.copy_(self._bucket_flat[b])
         else:
             buf = self._bucket_flat[b]
-        op = dist.ReduceOp.AVG if self._use_avg else dist.ReduceOp.SUM
-        work = dist.all_reduce(buf, op=op, group=self.pg, async_op=True)
+        if self.comm is not None:
+            work = self.comm.allreduce_async(buf, avg=self._use_avg)
+        else:
+            op = dist.ReduceOp.AVG if self._use_avg else dist.ReduceOp.SUM
+            work = dist.all_reduce(buf, op=op, group=self.pg, async_op=True)
         self._works.append((b, work))
 
     def _launch_ready(self):
@@ -170,7 +186,7 @@ class DistributedDataParallel(nn.Module):
         if self.broadcast_buffers and self.world > 1 and self.module.training:
             bufs = [b for b in self.module.buffers() if b.is_floating_point()]
             if bufs:
-                _flat_broadcast(bufs, self.src, self.pg)
+                _flat_broadcast(bufs, self.src, self.pg, self.comm)
         return self.module(*args, **kwargs)
 
     def zero_grad(self, set_to_none: bool = False):
@@ -178,6 +194,12 @@ class DistributedDataParallel(nn.Module):
         for p in self._params:
             if p.grad is None or p.grad.data_ptr() != self._views[p].data_ptr():
                 p.grad = self._views[p]
+
+    def remove_hooks(self):
+        """Detach from the parameters (before wrapping the same module in a new DDP, e.g. per round)."""
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
 
     @contextlib.contextmanager
     def no_sync(self):

@@ -59,3 +59,44 @@ def test_elastic_ddp_restarts_after_worker_failure(tmp_path):
     assert "[fault-injector] rank 1 step 10" in out
     # the group restarted: after the fault the job resumed from the epoch-0 snapshot and finished
     assert re.search(r"Resuming training from snapshot at Epoch 0", out), out[-3000:]
+
+
+HVDRUN = ["python", "-m", "pytorch_distributed_examples_amd.launch.hvdrun"]
+
+
+def test_rewire_survives_worker_failure_in_process(tmp_path):
+    """--rewire: a worker dies mid-epoch; the survivor keeps its process (same pid across rounds), restores
+    its in-memory commit and continues with the replacement worker -- no job restart."""
+    from dist_utils import run_cmd
+
+    env = {"PDE_FAULT_AT_STEP": "40", "PDE_FAULT_RANK": "1", "PDE_FAULT_MODE": "exit",
+           "PDE_FAULT_ONCE": str(tmp_path / "once")}
+    rc, out = run_cmd(HVDRUN + ["-np", "2", "--min-np", "1", "--verbose", SCRIPT, "3", "1", "--rewire", "--device",
+                                "cpu", "--train_size", "8192", "--test_size", "512", "--snapshot_path",
+                                str(tmp_path / "s.pt")], env=env)
+    assert rc == 0, out
+    assert "[fault-injector] rank 1 step 40" in out and "peer failure" in out, out[-3000:]
+    pids0 = re.findall(r"\[rewire\] round 0: rank 0 of 2 \(pid (\d+)\)", out)
+    pids1 = re.findall(r"\[rewire\] round 1: rank 0 of \d \(pid (\d+)\)", out)
+    assert pids0 and pids1 and pids0 == pids1, out[-3000:]  # rank 0 survived in-process
+    fin = re.findall(r"\[rewire\] finished 3 epochs in round (\d+)", out)
+    assert len(fin) == 2 and set(fin) == {"1"}, out[-3000:]
+
+
+def test_rewire_scale_up_via_discovery(tmp_path):
+    """A host-discovery script that grows from 1 to 2 slots: the running worker picks the newcomer up at its
+    next commit point and both finish in the same round."""
+    from dist_utils import run_cmd
+
+    snap = tmp_path / "s.pt"
+    disc = tmp_path / "discover.sh"  # a second slot appears once the first epoch's snapshot exists
+    disc.write_text(f"#!/bin/bash\nif [ -f {snap} ]; then echo localhost:2; else echo localhost:1; fi\n")
+    disc.chmod(0o755)
+    rc, out = run_cmd(HVDRUN + ["--min-np", "1", "--max-np", "2", "--host-discovery-script", str(disc), "--verbose",
+                                SCRIPT, "4", "2", "--rewire", "--device", "cpu", "--train_size", "16384",
+                                "--test_size", "512", "--snapshot_path", str(snap)])
+    assert rc == 0, out
+    assert "membership changed, re-joining" in out, out[-3000:]
+    assert re.search(r"\[rewire\] round 1: rank 1 of 2", out), out[-3000:]
+    fin = re.findall(r"\[rewire\] finished 4 epochs in round (\d+) \(world (\d)", out)
+    assert len(fin) == 2 and all(w == "2" for _, w in fin), out[-3000:]
