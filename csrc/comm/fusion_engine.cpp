@@ -2,7 +2,7 @@
 #include "fusion_engine.h"
 
 #include <c10/hip/HIPCachingAllocator.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
 #include <sstream>
 
@@ -102,7 +102,7 @@ int64_t FusionEngine::allreduce(at::Tensor t, at::Tensor out, const std::string&
   r.t_enqueue = now();
   if (t.is_cuda()) {
     TORCH_CHECK(gpu_backend_, "fusion engine: GPU tensor but no RCCL communicator");
-    c10::hip::HIPGuard guard(t.device());
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(t.device());
     hip_ok(hipEventCreateWithFlags(&r.ready, hipEventDisableTiming), "event create");
     hip_ok(hipEventRecord(r.ready, at::hip::getCurrentHIPStream(t.device().index()).stream()), "event record");
   }
@@ -138,7 +138,7 @@ int64_t FusionEngine::broadcast(at::Tensor t, int root, const std::string& name)
   r.t_enqueue = now();
   if (t.is_cuda()) {
     TORCH_CHECK(gpu_backend_, "fusion engine: GPU tensor but no RCCL communicator");
-    c10::hip::HIPGuard guard(t.device());
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(t.device());
     hip_ok(hipEventCreateWithFlags(&r.ready, hipEventDisableTiming), "event create");
     hip_ok(hipEventRecord(r.ready, at::hip::getCurrentHIPStream(t.device().index()).stream()), "event record");
   }
@@ -169,7 +169,7 @@ int64_t FusionEngine::allgather(at::Tensor t, const std::string& name) {
   r.t_enqueue = now();
   if (t.is_cuda()) {
     TORCH_CHECK(gpu_backend_, "fusion engine: GPU tensor but no RCCL communicator");
-    c10::hip::HIPGuard guard(t.device());
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(t.device());
     hip_ok(hipEventCreateWithFlags(&r.ready, hipEventDisableTiming), "event create");
     hip_ok(hipEventRecord(r.ready, at::hip::getCurrentHIPStream(t.device().index()).stream()), "event record");
   }
