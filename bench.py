@@ -174,7 +174,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / base, 2) if base else None,
-            "dtype": "fp32" if fused is not None else "bf16",
+            "dtype": "bf16",
             "data": "synthetic",
             "config": {"model": {"cnn": "mnist_cnn_Net", "mlp": "mnist_mlp_5x1024",
                                  "resnet50": "resnet50_128px"}[args.model],

@@ -353,7 +353,7 @@ std::tuple<Tensor, int64_t> optim_table(const std::vector<Tensor>& params, const
     e.bf16_copy = i < bf16_copies.size() && bf16_copies[i].defined() ? u16(bf16_copies[i]) : nullptr;
     e.offset = off;
     e.size = p.numel();
-    off += p.numel();
+    off += (p.numel() + 3) / 4 * 4;  // groups of 4 elements never straddle two tensors
   }
   const long bytes = static_cast<long>(n * sizeof(pde::OptimEntry));
   Tensor host = at::empty({bytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
@@ -367,7 +367,7 @@ std::tuple<Tensor, int64_t> optim_table(const std::vector<Tensor>& params, const
 void optim_step(const Tensor& table, int ntensors, int64_t total, int mode, const Tensor& hparams, Tensor& step) {
   CHECK_IN(table); CHECK_IN(hparams); CHECK_IN(step);
   TORCH_CHECK(hparams.numel() >= pde::HP_COUNT, "hparams size");
-  TORCH_CHECK(step.scalar_type() == at::kInt, "step must be int32");
+  TORCH_CHECK(step.scalar_type() == at::kInt && step.numel() >= 2, "step must be int32[2]");
   check(pde::multi_tensor_optim(mode, reinterpret_cast<const pde::OptimEntry*>(table.data_ptr()), ntensors, total,
                                 hparams.data_ptr<float>(), step.data_ptr<int>(), cur_stream()),
         "optim_step");
@@ -508,17 +508,22 @@ Tensor embbag_bwd(const Tensor& dy, const Tensor& idx, const Tensor& off, int64_
 // ------------------------------------------------------------------------------------------------
 // Launches forward+loss+backward for the whole batch; returns (loss scalar, slabs).  The caller reduces
 // the slabs into a gradient buffer with cnn_reduce (possibly the DDP flat gradient).
-std::vector<Tensor> cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, Tensor& rng,
-                              double p_drop2, double p_drop1, bool training, int64_t nwg,
-                              const optional<Tensor>& stamps) {
-  CHECK_IN(images); CHECK_IN(tgt); CHECK_IN(params); CHECK_IN(rng); CHECK_F32(images); CHECK_F32(params);
+Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, Tensor& rng, double p_drop2,
+                 double p_drop1, bool training, Tensor& grads, bool accumulate, const optional<Tensor>& gscale,
+                 const optional<Tensor>& stamps) {
+  CHECK_IN(images); CHECK_IN(tgt); CHECK_IN(params); CHECK_IN(rng); CHECK_IN(grads);
+  CHECK_F32(images); CHECK_F32(params); CHECK_F32(grads);
   TORCH_CHECK(params.numel() == pde::cnn_num_params(), "cnn_train: params must be the flat Net parameters");
+  TORCH_CHECK(grads.numel() == pde::cnn_num_params(), "cnn_train: grads size");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(grads.data_ptr()) % 16 == 0, "cnn_train: grads must be 16-B aligned");
   TORCH_CHECK(images.numel() == tgt.numel() * 28 * 28, "cnn_train: images must be [B,1,28,28]");
   TORCH_CHECK(tgt.scalar_type() == at::kLong && rng.scalar_type() == at::kLong, "cnn_train: dtypes");
   const int B = tgt.numel();
-  (void)nwg;  // the kernel trains cnn_images_per_workgroup() images per workgroup
   const int ni = pde::cnn_images_per_workgroup();
   const int n = (B + ni - 1) / ni;
+  if (stamps.has_value() && stamps->defined())
+    TORCH_CHECK(stamps->numel() >= static_cast<long>(n) * 16 && stamps->scalar_type() == at::kLong,
+                "cnn_train: stamps must be int64[nwg*16]");
   auto fo = images.options();
   Tensor slabs = at::empty({static_cast<long>(n) * pde::cnn_num_params()}, fo);
   Tensor part = at::empty({n}, fo);
@@ -526,28 +531,19 @@ std::vector<Tensor> cnn_train(const Tensor& images, const Tensor& tgt, const Ten
   check(pde::cnn_train_fused(images.data_ptr<float>(), tgt.data_ptr<int64_t>(), B, params.data_ptr<float>(),
                              reinterpret_cast<unsigned long long*>(rng.data_ptr()), static_cast<float>(p_drop2),
                              static_cast<float>(p_drop1), training ? 1 : 0, slabs.data_ptr<float>(),
-                             part.data_ptr<float>(), n, loss.data_ptr<float>(), cur_stream(),
+                             part.data_ptr<float>(), n, loss.data_ptr<float>(), grads.data_ptr<float>(), cf32(gscale),
+                             accumulate ? 1 : 0, cur_stream(),
                              stamps.has_value() && stamps->defined()
                                  ? reinterpret_cast<unsigned long long*>(stamps->data_ptr())
                                  : nullptr),
         "cnn_train");
-  return {loss, slabs};
-}
-
-void cnn_reduce(const Tensor& slabs, const optional<Tensor>& gscale, Tensor& grads, bool accumulate) {
-  CHECK_IN(slabs); CHECK_IN(grads); CHECK_F32(grads);
-  TORCH_CHECK(grads.numel() == pde::cnn_num_params(), "cnn_reduce: grads size");
-  const int nwg = slabs.numel() / pde::cnn_num_params();
-  check(pde::cnn_reduce_grads(slabs.data_ptr<float>(), nwg, cf32(gscale), grads.data_ptr<float>(), accumulate,
-                              cur_stream()),
-        "cnn_reduce");
+  return loss;
 }
 
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cnn_train", &cnn_train);
-  m.def("cnn_reduce", &cnn_reduce);
   m.def("cnn_num_params", &pde::cnn_num_params);
   m.def("cnn_smem_bytes", &pde::cnn_smem_bytes);
   m.doc() = "MI355X (gfx950) native kernels for pytorch_distributed_examples_amd";

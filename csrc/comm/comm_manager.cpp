@@ -69,10 +69,10 @@ RcclComm::~RcclComm() {
     ncclCommAbort(comm_);
     comm_ = nullptr;
   }
-  if (stream_ != nullptr) {
-    (void)hipStreamDestroy(stream_);
-    stream_ = nullptr;
-  }
+  // The stream is deliberately NOT destroyed: tensors used by collectives were recordStream()-ed on it,
+  // and torch's caching allocator records events on every such stream when those tensors are freed --
+  // possibly long after this communicator is gone (elastic re-init).  A stream per communicator
+  // lifetime is a negligible leak; a destroyed one would be a use-after-free inside the allocator.
 }
 
 void RcclComm::check(ncclResult_t r, const char* what) const {

@@ -109,8 +109,9 @@ struct OptimEntry {
   long size;
 };
 enum HParam { HP_LR = 0, HP_BETA1, HP_BETA2, HP_EPS, HP_WD, HP_MOMENTUM, HP_GRAD_SCALE, HP_COUNT };
-// mode 0 SGD, 1 Adam, 2 AdamW.  dev_hparams: float[HP_COUNT]; dev_step: int (steps taken so far,
-// incremented on device after the update).
+// mode 0 SGD, 1 Adam, 2 AdamW.  dev_hparams: float[HP_COUNT]; dev_step: int[2] = {steps taken so far,
+// arrival counter (0 between launches)}; the step is advanced on device by the update itself.
+// Table offsets must be multiples of 4 (optim_table pads them).
 hipError_t multi_tensor_optim(int mode, const OptimEntry* dev_table, int ntensors, long total_elems,
                               const float* dev_hparams, int* dev_step, hipStream_t s);
 
@@ -146,12 +147,13 @@ hipError_t embbag_fwd(const float* w, const int64_t* idx, const int64_t* off, in
 int cnn_num_params();
 size_t cnn_smem_bytes();
 int cnn_images_per_workgroup();
+// Two launches: the fused training kernel (per-workgroup gradient slabs + loss partials), then the
+// deterministic slab reduction into `grads` (16-B aligned; (+)= gscale * sum) which also finalises the
+// loss and advances the dropout counter.
 hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, const float* params,
                            unsigned long long* rng, float p_drop2, float p_drop1, int training, float* slabs,
-                           float* loss_part, int nwg, float* loss, hipStream_t s,
-                           unsigned long long* stamps = nullptr);
-hipError_t cnn_reduce_grads(const float* slabs, int nwg, const float* gscale, float* grads, int accumulate,
-                            hipStream_t s);
+                           float* loss_part, int nwg, float* loss, float* grads, const float* gscale,
+                           int accumulate, hipStream_t s, unsigned long long* stamps = nullptr);
 
 hipError_t embbag_bwd(const float* dy, const int64_t* idx, const int64_t* off, int B, long L, int D, float* dw,
                       hipStream_t s);

@@ -5,20 +5,23 @@
 //
 // Why: the network is 21,840 parameters and ~1 MFLOP/image forward; at the reference batch (1024 per
 // worker) the layer-by-layer path is ~40 kernels of a few microseconds each, every one far below the
-// chip's roofline.  Here ONE workgroup (8 wave64s) trains NI=4 images end to end,
-// the 4 images side by side in every phase so each phase has 4x the independent work (ILP/TLP for a
-// latency-bound, LDS-resident pipeline):
-//   * conv1/conv2/fc2 weights are staged in LDS once per workgroup; fc1's 64 KB weight matrix is read
-//     from L2 (shared by all workgroups), each load feeding all 4 images;
-//   * pooling is computed from the conv outputs in registers (4 conv taps per pooled cell, the argmax
-//     tap kept as a byte), so no pre-pool activation is ever stored;
-//   * backward exploits the pooling sparsity: only the argmax tap of each pooled cell carries gradient,
-//     so conv2-wgrad, conv2-dgrad and conv1-wgrad do 1/4 of the dense work;
-//   * since the 4 images are processed together, every weight gradient is complete after its phase and
-//     is written straight to the workgroup's fp32 slab (no accumulators to carry); k_cnn_reduce sums the slabs in a fixed order (deterministic) straight into the flat gradient
-//     buffer (e.g. the DDP bucket).
-// Dropout masks come from a counter-based hash keyed by a device-resident counter that k_cnn_loss
-// advances, so hipGraph replays draw fresh masks.  All math is fp32.
+// chip's roofline.  Here ONE workgroup (8 wave64s) trains NI=4 images end to end:
+//   * the five convolution GEMMs -- conv1 fwd, conv2 fwd, conv2 dgrad, conv2 wgrad, conv1 wgrad -- run
+//     on the matrix cores (v_mfma_f32_16x16x32_bf16, fp32 accumulate) as implicit GEMMs whose operand
+//     fragments are gathered straight from the LDS-resident bf16 activations (im2col never exists);
+//   * the conv weights are re-laid out ONCE per workgroup into LDS in MFMA B-fragment order (one 16-byte
+//     ds_read per lane per fragment); fc1's 64 KB weight matrix is read from L2 (shared by all WGs);
+//   * the forward M dimension is ordered (pooled cell, 2x2 tap), so an MFMA lane's 4 accumulator rows
+//     are exactly the 4 taps of one pooling window: max-pool, argmax, bias, dropout2d and ReLU are done
+//     on the accumulators, and no pre-pool activation is ever stored;
+//   * backward scatters the pooled gradients to their argmax taps once (a dense bf16 plane per channel)
+//     and feeds it to the dgrad / wgrad GEMMs; small fc layers, softmax/NLL and masks stay in fp32 VALU;
+//   * every weight gradient of the 4 images is complete after its phase and is written straight to the
+//     workgroup's fp32 slab; k_cnn_reduce sums the slabs in a fixed order (deterministic) straight into
+//     the flat gradient buffer (e.g. the DDP bucket).
+// Dropout masks come from a counter-based hash keyed by a device-resident counter that k_cnn_reduce
+// advances, so hipGraph replays draw fresh masks.  Precision: bf16 MFMA operands (images, conv weights,
+// conv activations and their gradients), fp32 accumulation, fp32 fc layers / loss / gradients.
 #include "common.cuh"
 #include "pde_kernels.h"
 
@@ -26,11 +29,21 @@ namespace pde {
 
 namespace {
 
-constexpr int T = 512;   // 8 waves
-constexpr int NI = 4;    // images per workgroup, processed side by side
-constexpr int C1 = 10, C2 = 20, KS = 5, H0 = 28, P1 = 12, P2 = 4, F1 = 50, F2 = 10;
-constexpr int NX = H0 * H0, NR1 = C1 * P1 * P1, NIN = C2 * P2 * P2;  // 784, 1440, 320
+constexpr int T = 512;            // 8 waves
+constexpr int NW = T / 64;
+constexpr int NI = 4;             // images per workgroup
+constexpr int C1 = 10, C2 = 20, KS = 5, H0 = 28, O1 = 24, P1 = 12, O2 = 8, P2 = 4, F1 = 50, F2 = 10;
+constexpr int NX = H0 * H0, NC1 = P1 * P1, NR1 = C1 * NC1, NC2 = P2 * P2, NIN = C2 * NC2;  // 784 144 1440 16 320
 constexpr int W1N = C1 * KS * KS, W2N = C2 * C1 * KS * KS, FC1N = F1 * NIN, FC2N = F2 * F1;
+constexpr int K2 = C1 * KS * KS;       // 250: conv2 fwd reduction (ci,ky,kx)
+constexpr int KS2 = 8;                 // conv2 fwd k-steps of 32
+// conv2 dgrad: one k-step per filter tap (ky,kx) with K = co (20 -> 32): the gradient is kept channel-last
+// (d2n[pos][co]) so a lane's 8 k-values are one 16-byte LDS read
+constexpr int KSD = KS * KS;           // 25 k-steps
+constexpr int C2P = 32;
+constexpr int MT1 = O1 * O1 / 16;      // 36 conv1 M-tiles per image (4 cells x 4 taps each)
+constexpr int MTD = NC1 * 1 / 16;      // 9 conv2-dgrad M-tiles per image (144 r1 positions)
+constexpr int KSW1 = O1 * O1 / 32;     // 18 conv1-wgrad k-steps per image
 // parameter offsets in the flat gradient (torch parameter order of Net)
 constexpr int O_W1 = 0, O_B1 = O_W1 + W1N, O_W2 = O_B1 + C1, O_B2 = O_W2 + W2N, O_FC1W = O_B2 + C2,
               O_FC1B = O_FC1W + FC1N, O_FC2W = O_FC1B + F1, O_FC2B = O_FC2W + FC2N, NPARAM = O_FC2B + F2;
@@ -43,22 +56,37 @@ __device__ __forceinline__ float hash_u01(unsigned long long seed, unsigned long
   return static_cast<float>(z >> 40) * (1.0f / 16777216.0f);
 }
 
+__device__ __forceinline__ f32x4 mfma(const u16x8& a, const u16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+}
+
 struct CnnSmem {
-  float x[NI][NX];
-  float w1[W1N], b1[C1], w2[W2N], b2[C2];   // contiguous: staged with one loop
+  // bf16 MFMA operands
+  alignas(16) u16x8 w2f[KS2][2][64];   // conv2 fwd B fragments [kstep][ntile][lane]; P9 partials later
+  alignas(16) u16x8 w2d[KSD][64];      // conv2 dgrad B fragments [tap][lane]: B[k=co][n=ci]
+  alignas(16) u16x8 w1f[64];           // conv1 B fragment
+  // conv2-output gradient (non-zero only at the argmax taps), twice: channel-last for the dgrad A
+  // fragments (co padded to 32 with zeros) and as 8x8 planes for the wgrad A fragments
+  alignas(16) uint16_t d2n[NI][O2 * O2][C2P];
+  alignas(16) uint16_t d2[NI][C2][O2 * O2];
+  uint16_t x[NI][NX];                  // images
+  uint16_t r1[NI][NR1];                // relu(maxpool(conv1)), [ci][cell]
+  uint16_t dr1[NI][NR1];               // grad at r1 (relu'-masked) == conv1-output grad at argmax taps
+  // fp32 head
+  float b1[C1], b2[C2];
   float fc2w[FC2N], fc2b[F2];
-  float r1[NI][NR1];     // relu(maxpool(conv1))
-  float dr1[NI][NR1];    // grad wrt r1 -> grad at the argmax tap of conv1
-  float r2[NI][NIN];     // relu(maxpool(dropout2d(conv2))) == fc1 input (NCHW flatten order)
-  alignas(16) float dp2[NI][NIN];    // grad at the argmax tap of conv2 (16-B rows: f32x4 loads)
+  float r2[NI][NIN];                   // fc1 input (NCHW flatten order)
+  alignas(16) float dp2[NI][NIN];      // grad at the pooled conv2 output (dropout2d applied)
   float h1[NI][F1], m1[NI][F1], h1d[NI][F1], dh[NI][F1];
   float mc2[NI][C2];
   float logit[NI][F2], dlog[NI][F2];
   float valid[NI];
-  float gw1[W1N], gb1[C1];   // conv1 gradients (LDS atomics across the 4 images)
   unsigned char a1[NI][NR1];
-  alignas(16) unsigned char a2[NI][NIN];
+  unsigned char a2[NI][NIN];
 };
+static_assert(sizeof(CnnSmem) <= 160 * 1024, "LDS budget");
+static_assert(sizeof(u16x8) * KS2 * 2 * 64 >= NW * 2 * 64 * sizeof(f32x4), "P9 partials alias w2f");
 
 __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ images, const int64_t* __restrict__ tgt,
                                                  int B, const float* __restrict__ params,
@@ -74,22 +102,54 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   CnnSmem& S = *reinterpret_cast<CnnSmem*>(smem_raw);
   const int t = threadIdx.x;
   const int lane = t & 63, wid = t >> 6;
+  const int lr = lane & 15, lg = lane >> 4;  // fragment row/col (lane & 15) and k-group (lane >> 4)
+  const float* gW1 = params + O_W1;
+  const float* gW2 = params + O_W2;
   const float* gFC1W = params + O_FC1W;
   const float* gFC1B = params + O_FC1B;
   const int n0 = blockIdx.x * NI;
 
-  // ---- P0: stage weights, zero accumulators, load the images and dropout masks --------------------
-  for (int i = t; i < W1N + C1 + W2N + C2; i += T) (&S.w1[0])[i] = params[O_W1 + i];
+  // ---- P0: images -> bf16, weights -> bf16 MFMA fragments, fp32 head weights, dropout masks ------
+  for (int i = t; i < NI * NX / 4; i += T) {
+    const int im = (i * 4) / NX, off = i * 4 - im * NX, n = n0 + im;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (n < B) v = *reinterpret_cast<const f32x4*>(images + static_cast<long>(n) * NX + off);
+    uint16_t* dst = &S.x[im][off];
+    dst[0] = f2bf(v[0]); dst[1] = f2bf(v[1]); dst[2] = f2bf(v[2]); dst[3] = f2bf(v[3]);
+  }
+  for (int e = t; e < KS2 * 2 * 64 + KSD * 64 + 64; e += T) {
+    u16x8 f;
+    if (e < KS2 * 2 * 64) {  // conv2 fwd: B[k=(ci,ky,kx)][n=co] = w2[co][k]
+      const int ks = e >> 7, nt = (e >> 6) & 1, l = e & 63;
+      const int co = nt * 16 + (l & 15), k0 = ks * 32 + (l >> 4) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = (co < C2 && k0 + j < K2) ? f2bf(gW2[co * K2 + k0 + j]) : 0;
+      S.w2f[ks][nt][l] = f;
+    } else if (e < KS2 * 2 * 64 + KSD * 64) {  // conv2 dgrad, tap (ky,kx): B[k=co][n=ci] = w2[co][ci][ky][kx]
+      const int e2 = e - KS2 * 2 * 64, tap = e2 >> 6, l = e2 & 63;
+      const int ci = l & 15, c0 = (l >> 4) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        f[j] = (ci < C1 && c0 + j < C2) ? f2bf(gW2[(c0 + j) * K2 + ci * 25 + tap]) : 0;
+      S.w2d[tap][l] = f;
+    } else {  // conv1: B[k=(ky,kx)][n=co] = w1[co][k]
+      const int l = e - KS2 * 2 * 64 - KSD * 64;
+      const int co = l & 15, k0 = (l >> 4) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = (co < C1 && k0 + j < 25) ? f2bf(gW1[co * 25 + k0 + j]) : 0;
+      S.w1f[l] = f;
+    }
+  }
+  for (int i = t; i < NI * O2 * O2 * (C2P - 16) / 8; i += T) {  // zero the co padding (20..31) once
+    const int pos = i >> 1, h = i & 1;
+    *reinterpret_cast<u16x8*>(&S.d2n[0][pos][16 + 8 * h]) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  for (int i = t; i < C1; i += T) S.b1[i] = params[O_B1 + i];
+  for (int i = t; i < C2; i += T) S.b2[i] = params[O_B2 + i];
   for (int i = t; i < FC2N + F2; i += T) (&S.fc2w[0])[i] = params[O_FC2W + i];
-  for (int i = t; i < W1N + C1; i += T) (&S.gw1[0])[i] = 0.f;
-  float* slab = slabs + static_cast<long>(blockIdx.x) * NPARAM;
   const unsigned long long seed = rng[0] * 0xD1B54A32D192ED03ULL;
   const float keep2 = training ? 1.f / (1.f - p_drop2) : 1.f;
   const float keep1 = training ? 1.f / (1.f - p_drop1) : 1.f;
-  for (int i = t; i < NI * NX; i += T) {
-    const int im = i / NX, n = n0 + im;
-    S.x[im][i - im * NX] = n < B ? images[static_cast<long>(n) * NX + (i - im * NX)] : 0.f;
-  }
   if (t < NI * C2) {
     const int im = t / C2, c = t - im * C2;
     const unsigned long long id = static_cast<unsigned long long>(n0 + im) * C2 + c;
@@ -101,76 +161,100 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   } else if (t >= 384 && t < 384 + NI) {
     S.valid[t - 384] = (n0 + t - 384) < B ? 1.f : 0.f;
   }
+  float* slab = slabs + static_cast<long>(blockIdx.x) * NPARAM;
   __syncthreads();
   PDE_STAMP(1);
 
-  // ---- P1: conv1 + maxpool2 + relu: one pooled cell (4 conv taps) per item ----------------------
-  for (int it = t; it < NI * NR1; it += T) {
-    const int im = it / NR1, p = it - im * NR1;
-    const int co = p / (P1 * P1), rem = p - co * P1 * P1, py = rem / P1, px = rem - py * P1;
-    const float* xi = S.x[im] + (2 * py) * H0 + 2 * px;
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+  // ---- P1: conv1 (MFMA, M = (cell, tap), K = 25 -> 32, N = co) + maxpool2 + relu -------------------
+  {
+    int koff[8];
 #pragma unroll
-    for (int ky = 0; ky < KS; ++ky) {
-      float row0[6], row1[6];
+    for (int j = 0; j < 8; ++j) {
+      const int k = lg * 8 + j;
+      koff[j] = k < 25 ? (k / 5) * H0 + (k % 5) : -1;
+    }
+    const u16x8 bw = S.w1f[lane];
+    const int tap = lr & 3, dy = tap >> 1, dx = tap & 1;
+    for (int tile = wid; tile < NI * MT1; tile += NW) {
+      const int im = tile / MT1, c0 = (tile - im * MT1) * 4;
+      const int cell = c0 + (lr >> 2), py = cell / P1, px = cell - py * P1;
+      const uint16_t* xb = S.x[im] + (2 * py + dy) * H0 + 2 * px + dx;
+      u16x8 a;
 #pragma unroll
-      for (int xx = 0; xx < 6; ++xx) { row0[xx] = xi[ky * H0 + xx]; row1[xx] = xi[(ky + 1) * H0 + xx]; }
-#pragma unroll
-      for (int kx = 0; kx < KS; ++kx) {
-        const float w = S.w1[co * 25 + ky * 5 + kx];
-        acc0 += w * row0[kx];
-        acc1 += w * row0[kx + 1];
-        acc2 += w * row1[kx];
-        acc3 += w * row1[kx + 1];
+      for (int j = 0; j < 8; ++j) a[j] = koff[j] >= 0 ? xb[koff[j]] : 0;
+      const f32x4 acc = mfma(a, bw, f32x4{0.f, 0.f, 0.f, 0.f});
+      const int co = lr;
+      if (co < C1) {  // rows (lg*4 + r) = taps r of cell c0 + lg
+        int am = 0;
+        float m = acc[0];
+        if (acc[1] > m) { m = acc[1]; am = 1; }
+        if (acc[2] > m) { m = acc[2]; am = 2; }
+        if (acc[3] > m) { m = acc[3]; am = 3; }
+        const int q = co * NC1 + c0 + lg;
+        S.r1[im][q] = f2bf(fmaxf(m + S.b1[co], 0.f));
+        S.a1[im][q] = static_cast<unsigned char>(am);
       }
     }
-    int am = 0;
-    float m = acc0;
-    if (acc1 > m) { m = acc1; am = 1; }
-    if (acc2 > m) { m = acc2; am = 2; }
-    if (acc3 > m) { m = acc3; am = 3; }
-    S.r1[im][p] = fmaxf(m + S.b1[co], 0.f);
-    S.a1[im][p] = static_cast<unsigned char>(am);
   }
   __syncthreads();
   PDE_STAMP(2);
 
-  // ---- P2: conv2 + dropout2d + maxpool2 + relu -------------------------------------------------
-  for (int it = t; it < NI * NIN; it += T) {
-    const int im = it / NIN, q = it - im * NIN;
-    const int co = q / (P2 * P2), rem = q - co * P2 * P2, py = rem / P2, px = rem - py * P2;
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-    for (int ci = 0; ci < C1; ++ci) {
-      const float* r = S.r1[im] + ci * P1 * P1 + (2 * py) * P1 + 2 * px;
-      const float* w = S.w2 + (co * C1 + ci) * 25;
+  // ---- P2: conv2 (MFMA, M = (cell, tap) 64/image, K = (ci,ky,kx) 250 -> 256, N = co 20 -> 32)
+  //          + dropout2d + maxpool2 + relu.  Wave w: image w/2, M-tiles 2(w&1), 2(w&1)+1, both N-tiles.
+  {
+    const int im = wid >> 1;
+    const int tap = lr & 3, dy = tap >> 1, dx = tap & 1;
+    int rb[2];
 #pragma unroll
-      for (int ky = 0; ky < KS; ++ky) {
-        float row0[6], row1[6];
+    for (int u = 0; u < 2; ++u) {
+      const int cell = ((wid & 1) * 2 + u) * 4 + (lr >> 2), py = cell >> 2, px = cell & 3;
+      rb[u] = (2 * py + dy) * P1 + 2 * px + dx;
+    }
+    f32x4 acc[2][2];
 #pragma unroll
-        for (int xx = 0; xx < 6; ++xx) { row0[xx] = r[ky * P1 + xx]; row1[xx] = r[(ky + 1) * P1 + xx]; }
+    for (int u = 0; u < 2; ++u) acc[u][0] = acc[u][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint16_t* r1 = S.r1[im];
+    for (int ks = 0; ks < KS2; ++ks) {
+      int koff[8];
 #pragma unroll
-        for (int kx = 0; kx < KS; ++kx) {
-          const float wv = w[ky * 5 + kx];
-          acc0 += wv * row0[kx];
-          acc1 += wv * row0[kx + 1];
-          acc2 += wv * row1[kx];
-          acc3 += wv * row1[kx + 1];
+      for (int j = 0; j < 8; ++j) {
+        const int k = ks * 32 + lg * 8 + j, ci = k / 25, r = k - ci * 25, ky = r / 5, kx = r - ky * 5;
+        koff[j] = k < K2 ? ci * NC1 + ky * P1 + kx : -1;
+      }
+      const u16x8 b0 = S.w2f[ks][0][lane], b1 = S.w2f[ks][1][lane];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        u16x8 a;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = koff[j] >= 0 ? r1[rb[u] + koff[j]] : 0;
+        acc[u][0] = mfma(a, b0, acc[u][0]);
+        acc[u][1] = mfma(a, b1, acc[u][1]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int co = nt * 16 + lr;
+        if (co < C2) {
+          const f32x4 v = acc[u][nt];
+          int am = 0;
+          float m = v[0];
+          if (v[1] > m) { m = v[1]; am = 1; }
+          if (v[2] > m) { m = v[2]; am = 2; }
+          if (v[3] > m) { m = v[3]; am = 3; }
+          const int q = co * NC2 + ((wid & 1) * 2 + u) * 4 + lg;
+          S.r2[im][q] = fmaxf((m + S.b2[co]) * S.mc2[im][co], 0.f);
+          S.a2[im][q] = static_cast<unsigned char>(am);
         }
       }
     }
-    int am = 0;
-    float m = acc0;
-    if (acc1 > m) { m = acc1; am = 1; }
-    if (acc2 > m) { m = acc2; am = 2; }
-    if (acc3 > m) { m = acc3; am = 3; }
-    S.r2[im][q] = fmaxf((m + S.b2[co]) * S.mc2[im][co], 0.f);
-    S.a2[im][q] = static_cast<unsigned char>(am);
   }
   __syncthreads();
   PDE_STAMP(3);
 
   // ---- P3: fc1 + relu + dropout: wave per output row, lanes over inputs, 4 images per load ------
-  for (int j = wid; j < F1; j += T / 64) {
+  for (int j = wid; j < F1; j += NW) {
     const float* wr = gFC1W + j * NIN;
     float s[NI] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -242,7 +326,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   __syncthreads();
   PDE_STAMP(7);
 
-  // ---- P6: fc1 backward: dW, db (straight to the slab), dr2 -> grad at conv2's argmax tap ---------
+  // ---- P6: fc1 backward: dW, db (straight to the slab), dp2 = grad at the pooled conv2 output -------
   for (int idx = t; idx < FC1N; idx += T) {
     const int j = idx / NIN, i = idx - j * NIN;
     float s = 0.f;
@@ -257,7 +341,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     slab[O_FC1B + t] = s;
   }
   if (t < NIN) {
-    const int i = t, co = i / (P2 * P2);
+    const int i = t, co = i / NC2;
     float s[NI] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 10
     for (int j = 0; j < F1; ++j) {
@@ -269,146 +353,240 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     for (int im = 0; im < NI; ++im) S.dp2[im][i] = (S.r2[im][i] > 0.f) ? s[im] * S.mc2[im][co] : 0.f;
   }
   __syncthreads();
-  PDE_STAMP(8);
-
-  // ---- P7a: conv2 wgrad (sparse: one tap per pooled cell).  Item = (co, ci, ky) computing the 5 kx
-  // taps together: each (cell, image) costs 2 index loads + one 5-wide r1 row segment.
-  for (int it = t; it < C2 * C1 * KS; it += T) {
-    const int co = it / (C1 * KS), rem = it - co * C1 * KS, ci = rem / KS, ky = rem - ci * KS;
-    float s[KS] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int im = 0; im < NI; ++im) {
-      const float* r = S.r1[im] + ci * P1 * P1 + ky * P1;
-#pragma unroll 4
-      for (int c = 0; c < P2 * P2; ++c) {
-        const int q = co * 16 + c, py = c >> 2, px = c & 3;
-        const float g = S.dp2[im][q];
-        const int a = S.a2[im][q];
-        const float* rr = r + (2 * py + (a >> 1)) * P1 + 2 * px + (a & 1);
-#pragma unroll
-        for (int kx = 0; kx < KS; ++kx) s[kx] += g * rr[kx];
-      }
-    }
-    float* dst = slab + O_W2 + (co * C1 + ci) * 25 + ky * 5;
-#pragma unroll
-    for (int kx = 0; kx < KS; ++kx) dst[kx] = s[kx];
+  // scatter dp2 to the argmax taps (both layouts; every tap of every window is written); conv2 bias
+  // grad alongside
+  for (int it = t; it < NI * NIN; it += T) {
+    const int im = it / NIN, q = it - im * NIN, co = q / NC2, cell = q - co * NC2;
+    const int py = cell >> 2, px = cell & 3, a = S.a2[im][q];
+    const uint16_t g = f2bf(S.dp2[im][q]);
+    const int p00 = (2 * py) * O2 + 2 * px;
+    const uint32_t gv = g;
+    *reinterpret_cast<uint32_t*>(&S.d2[im][co][p00]) = a == 0 ? gv : (a == 1 ? gv << 16 : 0u);
+    *reinterpret_cast<uint32_t*>(&S.d2[im][co][p00 + O2]) = a == 2 ? gv : (a == 3 ? gv << 16 : 0u);
+    S.d2n[im][p00][co] = a == 0 ? g : 0;
+    S.d2n[im][p00 + 1][co] = a == 1 ? g : 0;
+    S.d2n[im][p00 + O2][co] = a == 2 ? g : 0;
+    S.d2n[im][p00 + O2 + 1][co] = a == 3 ? g : 0;
   }
   if (t >= 448 && t < 448 + C2) {
     const int co = t - 448;
     float s = 0.f;
     for (int im = 0; im < NI; ++im)
-      for (int c = 0; c < 16; ++c) s += S.dp2[im][co * 16 + c];
+      for (int c = 0; c < NC2; ++c) s += S.dp2[im][co * NC2 + c];
     slab[O_B2 + co] = s;
   }
+  __syncthreads();
+  PDE_STAMP(8);
+
+  // ---- P7a: conv2 wgrad (MFMA): dW2[co][(ci,ky,kx)] = sum_(im,y,x) d2[co][y][x] * r1[ci][y+ky][x+kx].
+  // M = co (2 tiles), N = 250 -> 16 tiles (2 per wave), K = (im, y, x) 256 = 8 k-steps.  An A fragment
+  // is one 16-byte row of the d2 plane.
+  {
+    int nb[2];
+    bool nv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int kidx = (wid * 2 + u) * 16 + lr, ci = kidx / 25, r = kidx - ci * 25, ky = r / 5, kx = r - ky * 5;
+      nv[u] = kidx < K2;
+      nb[u] = nv[u] ? ci * NC1 + ky * P1 + kx : 0;
+    }
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc[0][u] = acc[1][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < KS2; ++ks) {
+      const int im = ks >> 1, y = (ks & 1) * 4 + lg;  // this lane's 8 positions: row y, x = 0..7
+      u16x8 a[2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int co = mt * 16 + lr;
+        a[mt] = co < C2 ? *reinterpret_cast<const u16x8*>(&S.d2[im][co][y * O2]) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint16_t* src = S.r1[im] + nb[u] + y * P1;
+        u16x8 b;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = nv[u] ? src[j] : 0;
+        acc[0][u] = mfma(a[0], b, acc[0][u]);
+        acc[1][u] = mfma(a[1], b, acc[1][u]);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int kidx = (wid * 2 + u) * 16 + lr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = mt * 16 + lg * 4 + r;
+          if (co < C2 && kidx < K2) slab[O_W2 + co * K2 + kidx] = acc[mt][u][r];
+        }
+      }
+  }
   PDE_STAMP(9);
-  // ---- P7b: conv2 dgrad as a row gather (no atomics, deterministic) + relu'(r1).  Item = one row y of
-  // one (image, ci) plane; the 12 outputs stay in registers.  Only cells whose argmax tap row lies in
-  // [y-4, y] can reach row y: py in [(y-4)/2, y/2].  (A 4-lanes-per-row split with shuffle reduction
-  // measured slower: 46 vs 37 us per workgroup -- LDS weight-read conflicts across co.)
-  for (int it = t; it < NI * C1 * P1; it += T) {
-    const int im = it / (C1 * P1), rem = it - im * C1 * P1, ci = rem / P1, y = rem - ci * P1;
-    float s[P1];
+
+  // ---- P7b: conv2 dgrad (MFMA): dr1[ci][Y][X] = sum_(ky,kx) sum_co d2[Y-ky][X-kx][co] * w2[co][ci][ky][kx],
+  // then relu'(r1).  M = r1 positions (9 tiles per image, 36 total, round-robin over waves), N = ci,
+  // one k-step per filter tap with K = co: a lane's A fragment is the 16-byte co-block (lane >> 4) of
+  // channel-last position (Y-ky, X-kx), or zero when that position is outside the 8x8 conv2 output.
+  {
+    constexpr int MAXT = (NI * MTD + NW - 1) / NW;  // 5
+    f32x4 acc[MAXT];
+    int ty[MAXT], tx[MAXT], tb[MAXT];
 #pragma unroll
-    for (int xx = 0; xx < P1; ++xx) s[xx] = 0.f;
-    const int py_lo = max(0, (y - 4) >> 1), py_hi = min(P2 - 1, y >> 1);
-    for (int co = 0; co < C2; ++co) {
-      const float* w = S.w2 + (co * C1 + ci) * 25;
-      for (int py = py_lo; py <= py_hi; ++py) {
+    for (int u = 0; u < MAXT; ++u) {
+      acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int tile = wid + u * NW;
+      const int im = tile / MTD, pos = (tile % MTD) * 16 + lr;
+      ty[u] = pos / P1;
+      tx[u] = pos - ty[u] * P1;
+      tb[u] = ((im * O2 * O2) + ty[u] * O2 + tx[u]) * C2P + lg * 8;  // element offset at tap (0,0)
+    }
+    const uint16_t* base = &S.d2n[0][0][0];
+    for (int tap = 0; tap < KSD; ++tap) {
+      const int ky = tap / KS, kx = tap - ky * KS;
+      const int tofs = -(ky * O2 + kx) * C2P;
+      const u16x8 b = S.w2d[tap][lane];
 #pragma unroll
-        for (int px = 0; px < P2; ++px) {
-          const int q = co * 16 + py * 4 + px;
-          const float g = S.dp2[im][q];
-          const int a = S.a2[im][q];
-          const int ky = y - (2 * py + (a >> 1));
-          if (ky >= 0 && ky < KS && g != 0.f) {
-            const float* wr = w + ky * 5;
-            if (a & 1) {
-#pragma unroll
-              for (int kx = 0; kx < KS; ++kx) s[2 * px + 1 + kx] += g * wr[kx];
-            } else {
-#pragma unroll
-              for (int kx = 0; kx < KS; ++kx) s[2 * px + kx] += g * wr[kx];
-            }
-          }
+      for (int u = 0; u < MAXT; ++u) {
+        if (wid + u * NW < NI * MTD) {
+          const bool ok = static_cast<unsigned>(ty[u] - ky) < O2 && static_cast<unsigned>(tx[u] - kx) < O2;
+          const u16x8 a = ok ? *reinterpret_cast<const u16x8*>(base + tb[u] + tofs) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+          acc[u] = mfma(a, b, acc[u]);
         }
       }
     }
-    const float* r1 = S.r1[im] + ci * P1 * P1 + y * P1;
-    float* d = S.dr1[im] + ci * P1 * P1 + y * P1;
 #pragma unroll
-    for (int xx = 0; xx < P1; ++xx) d[xx] = r1[xx] > 0.f ? s[xx] : 0.f;
+    for (int u = 0; u < MAXT; ++u) {
+      const int tile = wid + u * NW;
+      const int ci = lr;
+      if (tile < NI * MTD && ci < C1) {
+        const int im = tile / MTD;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = ci * NC1 + (tile % MTD) * 16 + lg * 4 + r;
+          S.dr1[im][q] = S.r1[im][q] != 0 ? f2bf(acc[u][r]) : 0;  // r1 is relu'd: r1 == 0 <=> dead
+        }
+      }
+    }
   }
   __syncthreads();
   PDE_STAMP(10);
 
-  // ---- P9: conv1 wgrad at the argmax taps.  Item = (co, ky, image, half of the cells) computing the 5
-  // kx taps together; combined with LDS atomics (400 items x 5 adds).  Bias grad alongside.
-  for (int it = t; it < C1 * KS * NI * 2; it += T) {
-    const int co = it / (KS * NI * 2), rem = it - co * KS * NI * 2, ky = rem / (NI * 2), r2_ = rem - ky * NI * 2;
-    const int im = r2_ >> 1, half = r2_ & 1;
-    const float* g = S.dr1[im] + co * 144;
-    const unsigned char* am = S.a1[im] + co * 144;
-    const float* xi = S.x[im] + ky * H0;
-    float s[KS] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int c = half * 72; c < half * 72 + 72; ++c) {
-      const float gv = g[c];
-      const int py = c / P1, px = c - py * P1, a = am[c];
-      const float* xr = xi + (2 * py + (a >> 1)) * H0 + 2 * px + (a & 1);
+  // ---- P9: conv1 wgrad (MFMA): dW1[co][(ky,kx)] = sum_(im,y,x) dconv1[co][y][x] * x[y+ky][x+kx], with
+  // dconv1 = dr1 at the argmax tap of each pooling window.  M = co, N = 25 -> 2 tiles, K = (im,y,x)
+  // 2304 = 72 k-steps split over the 8 waves (9 each); partials combined in LDS in a fixed order.
+  {
+    int nb[2];
+    bool nv[2];
 #pragma unroll
-      for (int kx = 0; kx < KS; ++kx) s[kx] += gv * xr[kx];
+    for (int u = 0; u < 2; ++u) {
+      const int kidx = u * 16 + lr;
+      nv[u] = kidx < 25;
+      nb[u] = nv[u] ? (kidx / 5) * H0 + kidx % 5 : 0;
     }
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    const int co = lr;
+    for (int ks = wid; ks < NI * KSW1; ks += NW) {
+      const int im = ks / KSW1, p0 = (ks - im * KSW1) * 32 + lg * 8;
+      const int y = p0 / O1, x0 = p0 - y * O1;  // 8 positions: row y, x0..x0+7 (x0 % 8 == 0)
+      u16x8 a = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (co < C1) {
+        const int cbase = co * NC1 + (y >> 1) * P1 + (x0 >> 1);
+        const int ty = (y & 1) * 2;
 #pragma unroll
-    for (int kx = 0; kx < KS; ++kx) atomicAdd(&S.gw1[co * 25 + ky * 5 + kx], s[kx]);
+        for (int c = 0; c < 4; ++c) {
+          const int q = cbase + c;
+          const int am = S.a1[im][q];
+          const uint16_t g = S.dr1[im][q];
+          a[2 * c] = am == ty ? g : 0;
+          a[2 * c + 1] = am == ty + 1 ? g : 0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint16_t* src = S.x[im] + nb[u] + y * H0 + x0;
+        u16x8 b;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = nv[u] ? src[j] : 0;
+        acc[u] = mfma(a, b, acc[u]);
+      }
+    }
+    __syncthreads();  // w2f is dead after P2: reuse it for the per-wave partials
+    f32x4* part = reinterpret_cast<f32x4*>(&S.w2f[0][0][0]);
+    part[(wid * 2 + 0) * 64 + lane] = acc[0];
+    part[(wid * 2 + 1) * 64 + lane] = acc[1];
+    __syncthreads();
+    if (t < W1N) {
+      const int c = t / 25, kidx = t - c * 25, u = kidx >> 4;
+      const int l = (c >> 2) * 16 + (kidx & 15), r = c & 3;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s += part[(w * 2 + u) * 64 + l][r];
+      slab[O_W1 + t] = s;
+    } else if (t >= 256 && t < 256 + C1) {
+      const int c = t - 256;
+      float s = 0.f;
+      for (int im = 0; im < NI; ++im)
+        for (int q = 0; q < NC1; ++q) s += bf2f(S.dr1[im][c * NC1 + q]);
+      slab[O_B1 + c] = s;
+    }
   }
-  if (t >= 448 && t < 448 + NI * C1) {
-    const int u = t - 448, im = u / C1, co = u - im * C1;
-    float s = 0.f;
-    for (int c = 0; c < 144; ++c) s += S.dr1[im][co * 144 + c];
-    atomicAdd(&S.gb1[co], s);
-  }
-  __syncthreads();
   PDE_STAMP(11);
 
-  // ---- conv1 gradients to the slab; loss partial -----------------------------------------------------
-  for (int i = t; i < W1N + C1; i += T) slab[O_W1 + i] = (&S.gw1[0])[i];
-  // loss: threads 0..NI-1 of wave 0 hold it
+  // loss partial: threads 0..NI-1 of wave 0 hold it
   if (wid == 0) {
     const float l = wave_sum(loss_acc);
     if (lane == 0) loss_part[blockIdx.x] = l;
   }
 }
 
-// grads[i] (+)= gscale * sum_wg slabs[wg][i].  4 waves split the slabs, fixed order, LDS combine.
-__global__ __launch_bounds__(256) void k_cnn_reduce(const float* __restrict__ slabs, int nwg, const float* __restrict__ gscale,
-                                                    float* __restrict__ grads, int accumulate) {
-  __shared__ float part[4][64];
-  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int w = threadIdx.x >> 6;
-  float s0 = 0.f, s1 = 0.f;
-  if (i < NPARAM) {
-    int b = w;
-    for (; b + 4 < nwg; b += 8) {
-      s0 += slabs[static_cast<long>(b) * NPARAM + i];
-      s1 += slabs[static_cast<long>(b + 4) * NPARAM + i];
-    }
-    if (b < nwg) s0 += slabs[static_cast<long>(b) * NPARAM + i];
-  }
-  part[w][threadIdx.x & 63] = s0 + s1;
-  __syncthreads();
-  if (w == 0 && i < NPARAM) {
-    const float v = (part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x]) *
-                    (gscale ? gscale[0] : 1.f);
-    grads[i] = accumulate ? grads[i] + v : v;
-  }
-}
+// grads (+)= gscale * sum_wg slabs[wg] in a fixed order (deterministic).  Block = 8 waves over 16 float4
+// columns (64 parameters); lane = column + 16 x slab-lane, so one load instruction of a wave reads 4 slabs
+// x 256 B and each thread keeps nwg/32 independent float4 loads in flight.  Block 0 also reduces the
+// per-workgroup loss partials and advances the dropout RNG counter for the next step.
+constexpr int RED_T = 512, RED_COLS = 16, RED_LANES = RED_T / RED_COLS;  // 32 slab lanes
+constexpr int NPARAM4 = NPARAM / 4;
+static_assert(NPARAM % 4 == 0, "float4 columns");
 
-__global__ void k_cnn_loss(const float* __restrict__ part, int nwg, int B, float* __restrict__ loss,
-                           unsigned long long* __restrict__ rng) {
-  float s = 0.f;
-  for (int b = threadIdx.x; b < nwg; b += 64) s += part[b];
-  s = wave_sum(s);
-  if (threadIdx.x == 0) {
-    loss[0] = s / static_cast<float>(B);
-    rng[0] += 1;  // advance the dropout stream for the next step
+__global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ slabs, int nwg,
+                                                      const float* __restrict__ gscale, float* __restrict__ grads,
+                                                      int accumulate, const float* __restrict__ loss_part, int B,
+                                                      float* __restrict__ loss, unsigned long long* __restrict__ rng) {
+  __shared__ f32x4 part[RED_LANES][RED_COLS];
+  const int col = threadIdx.x % RED_COLS, sl = threadIdx.x / RED_COLS;
+  const int c4 = blockIdx.x * RED_COLS + col;
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(slabs);
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+  if (c4 < NPARAM4) {
+    int b = sl;
+    for (; b + 3 * RED_LANES < nwg; b += 4 * RED_LANES) {
+      a0 += s4[static_cast<long>(b) * NPARAM4 + c4];
+      a1 += s4[static_cast<long>(b + RED_LANES) * NPARAM4 + c4];
+      a2 += s4[static_cast<long>(b + 2 * RED_LANES) * NPARAM4 + c4];
+      a3 += s4[static_cast<long>(b + 3 * RED_LANES) * NPARAM4 + c4];
+    }
+    for (; b < nwg; b += RED_LANES) a0 += s4[static_cast<long>(b) * NPARAM4 + c4];
+  }
+  part[sl][col] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (sl == 0 && c4 < NPARAM4) {
+    f32x4 v = part[0][col];
+#pragma unroll 8
+    for (int k = 1; k < RED_LANES; ++k) v += part[k][col];
+    v *= gscale ? gscale[0] : 1.f;
+    f32x4* g4 = reinterpret_cast<f32x4*>(grads) + c4;
+    *g4 = accumulate ? *g4 + v : v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x >= RED_T - 64) {  // last wave: loss
+    const int lane = threadIdx.x - (RED_T - 64);
+    float s = 0.f;
+    for (int b = lane; b < nwg; b += 64) s += loss_part[b];
+    s = wave_sum(s);
+    if (lane == 0) {
+      loss[0] = s / static_cast<float>(B);
+      rng[0] += 1;  // advance the dropout stream for the next step
+    }
   }
 }
 
@@ -420,8 +598,9 @@ int cnn_images_per_workgroup() { return NI; }
 
 hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, const float* params,
                            unsigned long long* rng, float p_drop2, float p_drop1, int training, float* slabs,
-                           float* loss_part, int nwg, float* loss, hipStream_t s,
-                           unsigned long long* stamps) {
+                           float* loss_part, int nwg, float* loss, float* grads, const float* gscale,
+                           int accumulate, hipStream_t s, unsigned long long* stamps) {
+  if (reinterpret_cast<uintptr_t>(grads) & 15) return hipErrorInvalidValue;  // float4 gradient stores
   const size_t sm = sizeof(CnnSmem);
   static bool attr = false;
   if (!attr) {
@@ -431,14 +610,8 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, const
   }
   hipLaunchKernelGGL(k_cnn_train, dim3(nwg), dim3(T), sm, s, images, tgt, B, params, rng, p_drop2, p_drop1, training,
                      slabs, loss_part, stamps);
-  hipLaunchKernelGGL(k_cnn_loss, dim3(1), dim3(64), 0, s, loss_part, nwg, B, loss, rng);
-  return hipGetLastError();
-}
-
-hipError_t cnn_reduce_grads(const float* slabs, int nwg, const float* gscale, float* grads, int accumulate,
-                            hipStream_t s) {
-  hipLaunchKernelGGL(k_cnn_reduce, dim3(ceil_div(NPARAM, 64)), dim3(256), 0, s, slabs, nwg, gscale, grads,
-                     accumulate);
+  hipLaunchKernelGGL(k_cnn_reduce, dim3(ceil_div(NPARAM4, RED_COLS)), dim3(RED_T), 0, s, slabs, nwg, gscale, grads,
+                     accumulate, loss_part, B, loss, rng);
   return hipGetLastError();
 }
 

@@ -69,8 +69,7 @@ class FusedCNN:
         x = x.float().contiguous()
         y = y.long().contiguous()
         training = self.net.training
-        loss, slabs = C.cnn_train(x, y, self.flat, OF._rng_counter(x.device), p_drop2, p_drop1, training,
-                                  self._nwg(y.numel()), self.stamps)
-        C.cnn_reduce(slabs, None, grad_out, accumulate)
+        loss = C.cnn_train(x, y, self.flat, OF._rng_counter(x.device), p_drop2, p_drop1, training, grad_out,
+                           accumulate, None, self.stamps)
         OF.bump_weight_generation()
         return loss

@@ -37,11 +37,8 @@ class _FusedBase(torch.optim.Optimizer):
         if st is None:
             st = {"sig": None, "hp_key": None,
                   "hp": torch.zeros(8, dtype=torch.float32, device=dev),
-                  "step": torch.zeros(1, dtype=torch.int32, device=dev)}
-            # resume a step count restored from a state_dict
-            s0 = self.state[params[0]].get("step") if params else None
-            if s0 is not None:
-                st["step"].fill_(int(s0))
+                  # {steps taken, arrival counter of the update kernel}
+                  "step": torch.zeros(2, dtype=torch.int32, device=dev)}
             self._dev[gi] = st
         need_avg = self.KIND in ("adam", "adamw") or group["momentum"] != 0.0
         for p in params:
@@ -62,6 +59,9 @@ class _FusedBase(torch.optim.Optimizer):
         sig = tuple((p.data_ptr(), g.data_ptr(), g.is_contiguous()) for p, g in zip(params, grads)) + \
             tuple(t.data_ptr() for t in m) + tuple(t.data_ptr() for t in v)
         if st["sig"] != sig:
+            # (re)build: also re-sync the device step with the host state (new optimizer, load_state_dict)
+            s0 = self.state[params[0]].get("step") if params else None
+            st["step"][0].fill_(int(s0) if s0 is not None else 0)
             grads_c = [g if g.is_contiguous() else g.contiguous() for g in grads]
             table, total = C.optim_table([p.data for p in params], grads_c, m, v, [])
             st.update(sig=sig, table=table, total=total, n=len(params), grads_keep=grads_c)

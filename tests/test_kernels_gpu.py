@@ -232,3 +232,37 @@ def test_fused_optimizers(gpu, kind):
         o2.step()
     for a, b in zip(mine, ref):
         assert rel_err(a, b) < 1e-5
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adam", "adamw"])
+def test_fused_optimizers_views_and_device_step(gpu, kind):
+    """Parameters that are unaligned views of one flat buffer (scalar path next to the vector path) and
+    gradients updated in place, so the device-side step counter (not the host) drives bias correction."""
+    from pytorch_distributed_examples_amd.ops import optim as O
+
+    torch.manual_seed(7)
+    sizes = [10, 5000, 7, 20, 3, 16000]
+    flat = torch.randn(sum(sizes), device=gpu)
+    mine = [t.view(-1) for t in flat.split(sizes)]
+    for t in mine:
+        t.requires_grad_()
+    ref = [t.detach().clone().requires_grad_() for t in mine]
+    gflat = torch.zeros_like(flat)
+    for t, g in zip(mine, gflat.split(sizes)):
+        t.grad = g
+    if kind == "sgd":
+        o1, o2 = O.FusedSGD(mine, lr=0.05, momentum=0.9), torch.optim.SGD(ref, lr=0.05, momentum=0.9)
+    elif kind == "adam":
+        o1, o2 = O.FusedAdam(mine, lr=1e-3), torch.optim.Adam(ref, lr=1e-3)
+    else:
+        o1, o2 = O.FusedAdamW(mine, lr=1e-2), torch.optim.AdamW(ref, lr=1e-2)
+    for _ in range(4):
+        gs = torch.randn_like(flat)
+        gflat.copy_(gs)
+        for p, g in zip(ref, gs.split(sizes)):
+            p.grad = g.clone()
+        o1.step()
+        o2.step()
+    for a, b in zip(mine, ref):
+        assert rel_err(a, b) < 1e-5
+    assert int(o1._dev[0]["step"][0].item()) == 4 and int(o1._dev[0]["step"][1].item()) == 0

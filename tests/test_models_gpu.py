@@ -65,8 +65,9 @@ def test_resnet_shards_match_cpu(gpu):
     with OF.emulate_bf16_on_cpu():
         OF.mse_loss(out_cpu, t).backward()
     OF.mse_loss(out_gpu, t.to(gpu)).backward()
-    for (n, p1), p2 in zip(list(s1.named_parameters())[:6] + list(s2.named_parameters())[-4:],
-                           list(g1.parameters())[:6] + list(g2.parameters())[-4:]):
+    # gradients near the loss only: deeper ones go through up to 50 batch-4 BatchNorm backwards, where bf16
+    # noise is amplified chaotically (test_resnet_blocks_backward_match_cpu checks every block on its own)
+    for (n, p1), p2 in zip(list(s2.named_parameters())[-4:], list(g2.parameters())[-4:]):
         assert rel_err(p2.grad.cpu(), p1.grad) < 0.15, n
 
 
@@ -85,6 +86,30 @@ def test_resnet_blocks_match_cpu(gpu):
         out = out.float().permute(0, 3, 1, 2).cpu()
         assert out.shape == ref.shape
         assert rel_err(out, ref) < 3e-2, (c, hw, rel_err(out, ref))
+
+
+def test_resnet_blocks_backward_match_cpu(gpu):
+    """Backward of each bottleneck from the same upstream gradient: input grad and every conv / BN
+    parameter grad, GPU NHWC kernels vs the bf16-emulating CPU reference."""
+    torch.manual_seed(0)
+    s1, s2 = ResNetShard1(), ResNetShard2()
+    blocks = [s1.seq[4][0], s1.seq[5][0], s1.seq[5][1], s2.seq[0][0], s2.seq[1][0], s2.seq[1][2]]
+    shapes = [(64, 32), (256, 32), (512, 16), (512, 16), (1024, 8), (2048, 4)]
+    for blk, (c, hw) in zip(blocks, shapes):
+        x = torch.randn(8, c, hw, hw).to(torch.bfloat16).float().requires_grad_()
+        g = copy.deepcopy(blk).to(gpu)
+        with OF.emulate_bf16_on_cpu():
+            ref = blk(x)
+        up = torch.randn_like(ref).to(torch.bfloat16).float()
+        ref.backward(up)
+        xg = x.detach().permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(gpu).requires_grad_()
+        out = g(xg)
+        (out.float() * up.permute(0, 2, 3, 1).to(gpu)).sum().backward()
+        errs = {"x": rel_err(xg.grad.float().permute(0, 3, 1, 2).cpu(), x.grad)}
+        for (n, p1), p2 in zip(blk.named_parameters(), g.parameters()):
+            errs[n] = rel_err(p2.grad.cpu(), p1.grad)
+        bad = {k: v for k, v in errs.items() if v > 5e-2}
+        assert not bad, (c, hw, errs)
 
 
 def test_cnn_trains(gpu):
@@ -106,8 +131,26 @@ def test_cnn_trains(gpu):
     assert sum(losses[-5:]) / 5 < losses[0] * 0.7, losses
 
 
+def _mixed_reference_loss(m, x, y):
+    import torch.nn.functional as F
+
+    def st(t):  # bf16-rounded value, identity gradient
+        return t + (t.detach().to(torch.bfloat16).float() - t.detach())
+
+    c1 = F.conv2d(st(x), st(m.conv1.weight), m.conv1.bias)
+    r1 = st(F.relu(F.max_pool2d(c1, 2)))
+    c2 = F.conv2d(r1, st(m.conv2.weight), m.conv2.bias)
+    r2 = F.relu(F.max_pool2d(c2, 2)).flatten(1)
+    h = F.relu(F.linear(r2, m.fc1.weight, m.fc1.bias))
+    return F.nll_loss(F.log_softmax(F.linear(h, m.fc2.weight, m.fc2.bias), 1), y)
+
+
 def test_fused_cnn_matches_reference(gpu):
-    """Fused whole-network kernel (fp32) vs the fp32 CPU reference, dropout off (eval)."""
+    """Fused whole-network kernel (bf16 MFMA convs, fp32 accumulate / head) vs a CPU fp32 reference that
+    rounds the same operands to bf16 (straight-through, so gradients stay fp32), dropout off (eval).
+    With identical conv inputs the max-pool argmax decisions agree; against the plain fp32 model ~1% of
+    pooling windows pick another tap, which moves whole gradient contributions (~10% relative error on
+    the conv1 weight gradient, as measured)."""
     from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
 
     torch.manual_seed(0)
@@ -116,16 +159,17 @@ def test_fused_cnn_matches_reference(gpu):
     fused = FusedCNN(m_gpu)
     x = torch.randn(300, 1, 28, 28)
     y = torch.randint(0, 10, (300,))
-    l_cpu = OF.nll_loss(m_cpu(x), y)
+    l_cpu = _mixed_reference_loss(m_cpu, x, y)
     l_cpu.backward()
     g = torch.zeros(fused.flat.numel(), device=gpu)
     loss = fused.forward_backward(x.to(gpu), y.to(gpu), grad_out=g)
-    assert abs(loss.item() - l_cpu.item()) < 1e-4
-    off = 0
+    assert abs(loss.item() - l_cpu.item()) < 1e-2
+    off, errs = 0, {}
     for n, p in m_cpu.named_parameters():
         k = p.numel()
-        assert rel_err(g[off:off + k].cpu().view_as(p), p.grad) < 1e-3, n
+        errs[n] = rel_err(g[off:off + k].cpu().view_as(p), p.grad)
         off += k
+    assert all(v < 3e-2 for v in errs.values()), errs
 
 
 def test_fused_cnn_trains_with_dropout(gpu):
