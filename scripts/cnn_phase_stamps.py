@@ -1,8 +1,13 @@
 """Diagnostic: per-phase time of the fused CNN kernel from in-kernel wall_clock64 stamps (100 MHz)."""
-import torch
+import os
+import sys
 
-from pytorch_distributed_examples_amd.models.cnn import Net
-from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from pytorch_distributed_examples_amd.models.cnn import Net  # noqa: E402
+from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN  # noqa: E402
 
 dev = torch.device("cuda")
 net = Net().to(dev).train()
