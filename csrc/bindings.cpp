@@ -59,6 +59,20 @@ pde::Operand gather(const Tensor& t, int kind, int N, int H, int W, int C, int R
   return o;
 }
 
+// A 1x1 / stride-1 / pad-0 convolution is a plain GEMM over the NHWC activation: its operands are
+// described densely, which skips the implicit-GEMM gather arithmetic entirely.
+inline bool is_pointwise(int R, int S, int stride, int pad) { return R == 1 && S == 1 && stride == 1 && pad == 0; }
+
+// Optional fp32 gradient sink: the op's weight gradient is written (or added) straight into it.
+Tensor grad_sink(const optional<Tensor>& out, at::IntArrayRef shape, const Tensor& like) {
+  if (out.has_value() && out->defined()) {
+    CHECK_IN(*out); CHECK_F32(*out);
+    TORCH_CHECK(out->sizes() == shape, "gradient sink has the wrong shape");
+    return *out;
+  }
+  return at::empty(shape, like.options().dtype(at::kFloat));
+}
+
 // Split-K cap for a GEMM with reduction length K: at most 512 slabs, each >= 256 long, and the fp32
 // slab workspace bounded to 128 MiB (the kernel picks the actual split from the tile count).
 int split_cap(const pde::GemmArgs& a) {
@@ -119,18 +133,19 @@ Tensor linear_dgrad(const Tensor& dy, const Tensor& w, const optional<Tensor>& a
   return dx;
 }
 
-// dW[N,K] = dy[M,N]^T . x[M,K]   (fp32, split-K over the batch when the tile grid is small)
-Tensor linear_wgrad(const Tensor& dy, const Tensor& x) {
+// dW[N,K] = dy[M,N]^T . x[M,K]   (fp32, split-K over the batch when the tile grid is small); with ``out``
+// the result is written (accumulate: added) into that tensor, e.g. the parameter's .grad.
+Tensor linear_wgrad(const Tensor& dy, const Tensor& x, const optional<Tensor>& out, bool accumulate) {
   CHECK_IN(dy); CHECK_IN(x); CHECK_BF16(dy); CHECK_BF16(x);
   const int M = dy.size(0), N = dy.size(1), K = x.size(1);
   TORCH_CHECK(x.size(0) == M, "linear_wgrad: shape mismatch");
-  Tensor dw = at::empty({N, K}, dy.options().dtype(at::kFloat));
+  Tensor dw = grad_sink(out, {N, K}, dy);
   pde::GemmArgs a{};
   a.M = N; a.N = K; a.K = M;
   a.a = dense(dy, 1, N);
   a.b = dense(x, 1, K);
   a.out = dw.data_ptr(); a.ldo = K;
-  a.epi = pde::EPI_OUT_F32;
+  a.epi = pde::EPI_OUT_F32 | (accumulate ? pde::EPI_ACCUM : 0);
   run_gemm(a, dy, -1);
   return dw;
 }
@@ -149,7 +164,7 @@ Tensor conv_fwd(const Tensor& x, const Tensor& wf, const optional<Tensor>& bias,
   Tensor y = at::empty({N, Ho, Wo, Co}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
   pde::GemmArgs a{};
   a.M = N * Ho * Wo; a.N = Co; a.K = R * S * C;
-  a.a = gather(x, 1, N, H, W, C, R, S, stride, pad, Ho, Wo);
+  a.a = is_pointwise(R, S, stride, pad) ? dense(x, C, 1) : gather(x, 1, N, H, W, C, R, S, stride, pad, Ho, Wo);
   a.b = dense(wf, a.K, 1);
   a.out = y.data_ptr(); a.ldo = Co;
   a.bias = cf32(bias);
@@ -170,7 +185,7 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wd, int H, int W, int R, int S
   Tensor dx = at::empty({N, H, W, Ci}, dy.options());
   pde::GemmArgs a{};
   a.M = N * H * W; a.N = Ci; a.K = R * S * Co;
-  a.a = gather(dy, 3, N, Ho, Wo, Co, R, S, stride, pad, H, W);
+  a.a = is_pointwise(R, S, stride, pad) ? dense(dy, Co, 1) : gather(dy, 3, N, Ho, Wo, Co, R, S, stride, pad, H, W);
   a.b = dense(wd, a.K, 1);
   a.out = dx.data_ptr(); a.ldo = Ci;
   a.aux = cu16(aux); a.ldaux = Ci;
@@ -179,19 +194,24 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wd, int H, int W, int R, int S
   return dx;
 }
 
-// dW[Co, R*S*C] fp32 from dy[N,Ho,Wo,Co] and x[N,H,W,C]
-Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int R, int S, int stride, int pad) {
+// dW[Co, Ci, R, S] fp32 (the parameter's layout) from dy[N,Ho,Wo,Cop] and x[N,H,W,Cp]: the GEMM
+// dW[co][(r,s,c)] = sum_pixels dy[pixel][co] * x-gather[pixel][(r,s,c)] stores through the OIHW epilogue
+// remap, so no layout kernel runs; with ``out`` (accumulate: +=) it lands directly in the .grad tensor.
+Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int R, int S, int stride, int pad, int Co, int Ci,
+                  const optional<Tensor>& out, bool accumulate) {
   CHECK_IN(dy); CHECK_IN(x); CHECK_BF16(dy); CHECK_BF16(x);
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
-  const int Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
+  const int Ho = dy.size(1), Wo = dy.size(2), Cop = dy.size(3);
   TORCH_CHECK(C % 8 == 0, "conv_wgrad: input channels must be a multiple of 8");
-  Tensor dw = at::empty({Co, R * S * C}, dy.options().dtype(at::kFloat));
+  TORCH_CHECK(Co <= Cop && Ci <= C, "conv_wgrad: real channels exceed the padded activations");
+  Tensor dw = grad_sink(out, {Co, Ci, R, S}, dy);
   pde::GemmArgs a{};
   a.M = Co; a.N = R * S * C; a.K = N * Ho * Wo;
-  a.a = dense(dy, 1, Co);
-  a.b = gather(x, 2, N, H, W, C, R, S, stride, pad, Ho, Wo);
+  a.a = dense(dy, 1, Cop);
+  a.b = is_pointwise(R, S, stride, pad) ? dense(x, 1, C) : gather(x, 2, N, H, W, C, R, S, stride, pad, Ho, Wo);
   a.out = dw.data_ptr(); a.ldo = a.N;
-  a.epi = pde::EPI_OUT_F32;
+  a.epi = pde::EPI_OUT_F32 | pde::EPI_OIHW | (accumulate ? pde::EPI_ACCUM : 0);
+  a.oihw_ci = Ci; a.oihw_rs = R * S; a.oihw_cp = C;
   run_gemm(a, dy, -1);
   return dw;
 }
@@ -253,13 +273,37 @@ Tensor conv_wgrad_oihw(const Tensor& g, int Co, int Ci, int R, int S) {
         "conv_wgrad_oihw");
   return y;
 }
-Tensor colsum(const Tensor& x) {
+// Column sums (bias gradient) of the first ``ncols`` columns (-1: all); ``out``/accumulate as linear_wgrad.
+Tensor colsum(const Tensor& x, int64_t ncols, const optional<Tensor>& out, bool accumulate) {
   CHECK_IN(x); CHECK_BF16(x);
   const int N = x.size(-1);
   const int M = x.numel() / N;
-  Tensor y = at::empty({N}, x.options().dtype(at::kFloat));
+  const int nc = ncols < 0 ? N : static_cast<int>(ncols);
+  TORCH_CHECK(nc <= N, "colsum: ncols");
   const int ws_blocks = 512;
   Tensor ws = at::empty({static_cast<long>(ws_blocks) * N}, x.options().dtype(at::kFloat));
+  if (nc == N && out.has_value() && out->defined()) {  // straight into the sink (bias .grad)
+    Tensor o = *out;
+    CHECK_IN(o); CHECK_F32(o);
+    TORCH_CHECK(o.numel() == N, "colsum: out");
+    check(pde::colsum_bf16_ws(u16(x), o.data_ptr<float>(), M, N, accumulate ? 1 : 0, ws.data_ptr<float>(),
+                              ws_blocks, cur_stream()),
+          "colsum");
+    return o;
+  }
+  if (nc != N) {
+    // padded channels: full sums into a scratch row, then copy / add the real columns
+    Tensor full = colsum(x, -1, c10::nullopt, false);
+    Tensor res = full.narrow(0, 0, nc);
+    if (out.has_value() && out->defined()) {
+      Tensor o = *out;
+      TORCH_CHECK(o.numel() == nc && o.scalar_type() == at::kFloat, "colsum: out");
+      if (accumulate) o.add_(res.view(o.sizes())); else o.copy_(res.view(o.sizes()));
+      return o;
+    }
+    return res.contiguous();
+  }
+  Tensor y = at::empty({N}, x.options().dtype(at::kFloat));
   check(pde::colsum_bf16_ws(u16(x), y.data_ptr<float>(), M, N, 0, ws.data_ptr<float>(), ws_blocks, cur_stream()),
         "colsum");
   return y;
@@ -406,21 +450,26 @@ Tensor bn_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, const
         "bn_apply");
   return y;
 }
-// Returns dx, dgamma, dbeta, dres (dres undefined unless want_dres)
+// Returns dx, dgamma, dbeta, dres (dres undefined unless want_dres).  With dg_out / db_out (both, [C] fp32)
+// the parameter gradients are ADDED into those tensors (direct accumulation into .grad).
 std::vector<Tensor> bn_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const Tensor& mean,
-                           const Tensor& invstd, const optional<Tensor>& gamma, bool relu, bool want_dres) {
+                           const Tensor& invstd, const optional<Tensor>& gamma, bool relu, bool want_dres,
+                           const optional<Tensor>& dg_out, const optional<Tensor>& db_out) {
   CHECK_IN(dy); CHECK_IN(x); CHECK_IN(y); CHECK_BF16(dy);
   const int C = x.size(-1);
   const int P = x.numel() / C;
   auto fo = x.options().dtype(at::kFloat);
   Tensor dx = at::empty_like(x);
-  Tensor dg = at::empty({C}, fo), db = at::empty({C}, fo), coef = at::empty({3 * C}, fo);
+  const bool direct = dg_out.has_value() && dg_out->defined() && db_out.has_value() && db_out->defined();
+  Tensor dg = direct ? grad_sink(dg_out, {C}, x) : at::empty({C}, fo);
+  Tensor db = direct ? grad_sink(db_out, {C}, x) : at::empty({C}, fo);
+  Tensor coef = at::empty({3 * C}, fo);
   Tensor ws = at::empty({static_cast<long>(pde::bn_workspace_blocks(P, C)) * 2 * C}, fo);
   Tensor dres;
   if (want_dres) dres = at::empty_like(x);
   check(pde::bn_bwd(u16(dy), u16(x), u16(y), mean.data_ptr<float>(), invstd.data_ptr<float>(), cf32(gamma), P, C,
-                    relu, dg.data_ptr<float>(), db.data_ptr<float>(), ws.data_ptr<float>(), coef.data_ptr<float>(),
-                    u16(dx), want_dres ? u16(dres) : nullptr, cur_stream()),
+                    relu, dg.data_ptr<float>(), db.data_ptr<float>(), direct ? 1 : 0, ws.data_ptr<float>(),
+                    coef.data_ptr<float>(), u16(dx), want_dres ? u16(dres) : nullptr, cur_stream()),
         "bn_bwd");
   return {dx, dg, db, dres};
 }
@@ -549,10 +598,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) native kernels for pytorch_distributed_examples_amd";
   m.def("linear_fwd", &linear_fwd);
   m.def("linear_dgrad", &linear_dgrad);
-  m.def("linear_wgrad", &linear_wgrad);
+  m.def("linear_wgrad", &linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("out") = py::none(),
+        py::arg("accumulate") = false);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad);
-  m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),
+        py::arg("pad"), py::arg("Co"), py::arg("Ci"), py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("cast_bf16", &cast_bf16);
   m.def("cast_bf16_into", &cast_bf16_into);
   m.def("cast_f32", &cast_f32);
@@ -560,7 +611,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_w_fwd", &conv_w_fwd);
   m.def("conv_w_dgrad", &conv_w_dgrad);
   m.def("conv_wgrad_oihw", &conv_wgrad_oihw);
-  m.def("colsum", &colsum);
+  m.def("colsum", &colsum, py::arg("x"), py::arg("ncols") = -1, py::arg("out") = py::none(),
+        py::arg("accumulate") = false);
   m.def("relu_bwd", &relu_bwd);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
@@ -572,7 +624,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("optim_step", &optim_step);
   m.def("bn_fwd", &bn_fwd);
   m.def("bn_apply", &bn_apply);
-  m.def("bn_bwd", &bn_bwd);
+  m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("mean"), py::arg("invstd"),
+        py::arg("gamma"), py::arg("relu"), py::arg("want_dres"), py::arg("dg_out") = py::none(),
+        py::arg("db_out") = py::none());
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);

@@ -20,6 +20,8 @@ enum EpiFlags : int {
   EPI_DRELU = 4,      // * (aux[m, n] > 0)   aux: bf16 [M, ldaux] (saved post-ReLU activation)
   EPI_OUT_F32 = 8,    // output fp32 (else bf16)
   EPI_ACCUM = 16,     // out += result (fp32 output only)
+  EPI_OIHW = 32,      // conv weight gradient: m = co, n = (r*S + s)*Cp + ci written to out[co][ci][r][s]
+                      // (ci >= oihw_ci skipped; fp32 output)
 };
 
 // Operand description.  The GEMM computes  C[m, n] = sum_k A[m, k] * B[n, k].
@@ -55,6 +57,7 @@ struct GemmArgs {
   int epi;
   int splitk;                      // >1: fp32 partial slabs in workspace, then reduce + epilogue
   float* workspace;                // splitk * M * N fp32
+  int oihw_ci, oihw_rs, oihw_cp;   // EPI_OIHW: real Cin, R*S, padded Cin of the gathered activation
 };
 
 hipError_t gemm_bf16(const GemmArgs& args, hipStream_t stream);
@@ -125,9 +128,10 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
                         uint16_t* y, hipStream_t s);
 hipError_t bn_apply(const uint16_t* x, int P, int C, const float* scale, const float* shift, const uint16_t* res,
                     int relu, uint16_t* y, hipStream_t s);
+// dgamma / dbeta are written, or added to when accum_params != 0 (direct accumulation into .grad).
 hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
-                  const float* gamma, int P, int C, int relu, float* dgamma, float* dbeta, float* ws, float* coef,
-                  uint16_t* dx, uint16_t* dres, hipStream_t s);
+                  const float* gamma, int P, int C, int relu, float* dgamma, float* dbeta, int accum_params, float* ws,
+                  float* coef, uint16_t* dx, uint16_t* dres, hipStream_t s);
 hipError_t maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
                        int k, int st, int p, int relu, hipStream_t s);
 hipError_t maxpool_bwd(const uint16_t* dy, const uint16_t* y, const uint8_t* idx, uint16_t* dx, int N, int H, int W,

@@ -15,10 +15,18 @@
 //   * LDS images are K-contiguous rows padded by 16 B so MFMA fragments are single ds_read_b128.
 //     Operands that are contiguous along the row (M/N) dimension -- the transposed operands of
 //     dgrad / wgrad -- are loaded 16 B along the row and scattered into the K-contiguous image.
+//   * Implicit-GEMM gathers keep per-slot state: a row's (image, output-pixel) decomposition is done
+//     once per block, and the slot's (kh, kw, c) -- or, for the weight-gradient operand, its output
+//     pixel -- is advanced incrementally by BK per K-tile, so the K loop has no integer division.
 //   * Tiles are mapped XCD-aware (T1): consecutive tile ids go to the same XCD group so tiles
 //     sharing A rows / B columns hit the same L2.
-//   * Split-K writes fp32 partial slabs, reduced by gemm_splitk_reduce (which applies the fused
-//     epilogue), so wgrad GEMMs with a huge reduction (N*H*W) still fill 256 CUs.
+//   * Split-K writes fp32 partial slabs, reduced by a vectorised slab reduction (several slab lanes per
+//     float4 column, fixed order: deterministic) that applies the fused epilogue, so wgrad GEMMs with a
+//     huge reduction (N*H*W) still fill 256 CUs.
+//   * Epilogue options: bias, ReLU, ReLU-mask (backward), fp32 / bf16 output, accumulate, and an OIHW
+//     remap that writes a conv weight gradient straight into the parameter's [Co][Ci][R][S] fp32 grad.
+#include <type_traits>
+
 #include "common.cuh"
 #include "pde_kernels.h"
 
@@ -28,112 +36,132 @@ namespace {
 
 constexpr int kThreads = 256;
 
-// Load 8 consecutive K elements of row r (K-contiguous operand).
-__device__ __forceinline__ u16x8 load_kc(const Operand& op, int rows, int K, int r, int k0,
-                                         bool vec_ok) {
-  u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+__device__ __forceinline__ u16x8 zero8() { return u16x8{0, 0, 0, 0, 0, 0, 0, 0}; }
+
+// Dense K-contiguous / row-contiguous element loads (operand kind 0).
+__device__ __forceinline__ u16x8 load_dense_kc(const Operand& op, int rows, int K, int r, int k0, bool vec_ok) {
+  u16x8 v = zero8();
   if (r >= rows || k0 >= K) return v;
   const uint16_t* p = static_cast<const uint16_t*>(op.ptr);
-  if (op.kind == 0) {
-    const long base = static_cast<long>(r) * op.ld_r;
-    if (vec_ok && k0 + 8 <= K) {
-      v = *reinterpret_cast<const u16x8*>(p + base + k0);
-    } else {
+  const long base = static_cast<long>(r) * op.ld_r;
+  if (vec_ok && k0 + 8 <= K) {
+    v = *reinterpret_cast<const u16x8*>(p + base + k0);
+  } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (k0 + i < K) v[i] = p[base + static_cast<long>(k0 + i) * op.ld_k];
-    }
-    return v;
+    for (int i = 0; i < 8; ++i)
+      if (k0 + i < K) v[i] = p[base + static_cast<long>(k0 + i) * op.ld_k];
   }
-  const ConvGeom& g = op.g;
-  // k0 -> (kh, kw, c0); C % 8 == 0 so the 8 elements share (kh, kw)
-  const int c0 = k0 % g.C;
-  const int rs = k0 / g.C;
-  const int kw = rs % g.S;
-  const int kh = rs / g.S;
-  const int HWo = g.Ho * g.Wo;
-  const int n = r / HWo;
-  const int rem = r - n * HWo;
-  const int oy = rem / g.Wo;
-  const int ox = rem - oy * g.Wo;
-  int iy, ix;
-  if (op.kind == 1) {
-    iy = oy * g.stride - g.pad + kh;
-    ix = ox * g.stride - g.pad + kw;
-  } else {  // kind 3: transposed-conv gather (dgrad). (oy, ox) are dx coords, dy has dims H x W.
-    int ty = oy + g.pad - kh;
-    int tx = ox + g.pad - kw;
-    if (ty < 0 || tx < 0) return v;
-    if (g.stride > 1) {
-      if ((ty % g.stride) != 0 || (tx % g.stride) != 0) return v;
-      ty /= g.stride;
-      tx /= g.stride;
-    }
-    iy = ty;
-    ix = tx;
-  }
-  if (iy < 0 || iy >= g.H || ix < 0 || ix >= g.W) return v;
-  v = *reinterpret_cast<const u16x8*>(p + ((static_cast<long>(n) * g.H + iy) * g.W + ix) * g.C + c0);
   return v;
 }
 
-// Load 8 consecutive ROW elements r0..r0+7 at reduction index k (row-contiguous operand).
-__device__ __forceinline__ u16x8 load_rc(const Operand& op, int rows, int K, int r0, int k,
-                                         bool vec_ok) {
-  u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+__device__ __forceinline__ u16x8 load_dense_rc(const Operand& op, int rows, int K, int r0, int k, bool vec_ok) {
+  u16x8 v = zero8();
   if (r0 >= rows || k >= K) return v;
   const uint16_t* p = static_cast<const uint16_t*>(op.ptr);
-  if (op.kind == 0) {
-    const long base = static_cast<long>(k) * op.ld_k;
-    if (vec_ok && r0 + 8 <= rows) {
-      v = *reinterpret_cast<const u16x8*>(p + base + r0);
-    } else {
+  const long base = static_cast<long>(k) * op.ld_k;
+  if (vec_ok && r0 + 8 <= rows) {
+    v = *reinterpret_cast<const u16x8*>(p + base + r0);
+  } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (r0 + i < rows) v[i] = p[base + static_cast<long>(r0 + i) * op.ld_r];
-    }
-    return v;
+    for (int i = 0; i < 8; ++i)
+      if (r0 + i < rows) v[i] = p[base + static_cast<long>(r0 + i) * op.ld_r];
   }
-  // kind 2: rows are (kh, kw, c) of the conv, k is the output pixel (n, oy, ox)
-  const ConvGeom& g = op.g;
-  const int c0 = r0 % g.C;
-  const int rs = r0 / g.C;
-  const int kw = rs % g.S;
-  const int kh = rs / g.S;
-  const int HWo = g.Ho * g.Wo;
-  const int n = k / HWo;
-  const int rem = k - n * HWo;
-  const int oy = rem / g.Wo;
-  const int ox = rem - oy * g.Wo;
-  const int iy = oy * g.stride - g.pad + kh;
-  const int ix = ox * g.stride - g.pad + kw;
-  if (iy < 0 || iy >= g.H || ix < 0 || ix >= g.W) return v;
-  v = *reinterpret_cast<const u16x8*>(p + ((static_cast<long>(n) * g.H + iy) * g.W + ix) * g.C + c0);
   return v;
 }
 
-template <int BROWS, int BK, bool KC>
-struct TileLoader {
+// K-contiguous operand (kinds 0, 1, 3): each slot loads 8 consecutive K elements of one row.
+template <int BROWS, int BK>
+struct KcLoader {
   static constexpr int kVecs = BROWS * BK / 8;
   static constexpr int kPer = (kVecs + kThreads - 1) / kThreads;
   u16x8 regs[kPer];
+  int k0[kPer];                 // the slot's current reduction index
+  int c[kPer], kw[kPer], kh[kPer];
+  int by[kPer], bx[kPer];       // kind 1: oy*s - pad, ox*s - pad;  kind 3: h + pad, w + pad
+  long nb[kPer];                // image base offset in elements; -1: row out of range
 
-  __device__ __forceinline__ void load(const Operand& op, int rows, int K, int row0, int k0,
-                                       bool vec_ok) {
+  __device__ __forceinline__ void init(const Operand& op, int rows, int row0, int kbeg) {
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int v = threadIdx.x + i * kThreads;
-      if (v < kVecs) {
-        if constexpr (KC) {
-          const int row = v / (BK / 8);
-          const int kv = v - row * (BK / 8);
-          regs[i] = load_kc(op, rows, K, row0 + row, k0 + kv * 8, vec_ok);
-        } else {
-          const int kk = v / (BROWS / 8);
-          const int rv = v - kk * (BROWS / 8);
-          regs[i] = load_rc(op, rows, K, row0 + rv * 8, k0 + kk, vec_ok);
+      const int row = v / (BK / 8), kv = v - row * (BK / 8);
+      k0[i] = kbeg + kv * 8;
+      nb[i] = -1;
+      c[i] = kw[i] = kh[i] = by[i] = bx[i] = 0;
+      if (op.kind == 0 || v >= kVecs) continue;
+      const ConvGeom& g = op.g;
+      c[i] = k0[i] % g.C;  // C % 8 == 0: the slot's 8 elements share (kh, kw)
+      const int rs = k0[i] / g.C;
+      kw[i] = rs % g.S;
+      kh[i] = rs / g.S;
+      const int r = row0 + row;
+      if (r < rows) {
+        const int HWo = g.Ho * g.Wo;
+        const int n = r / HWo, rem = r - n * HWo, oy = rem / g.Wo, ox = rem - oy * g.Wo;
+        nb[i] = static_cast<long>(n) * g.H * g.W * g.C;
+        if (op.kind == 1) {
+          by[i] = oy * g.stride - g.pad;
+          bx[i] = ox * g.stride - g.pad;
+        } else {  // kind 3: (oy, ox) are dx coordinates; dy has dims H x W
+          by[i] = oy + g.pad;
+          bx[i] = ox + g.pad;
         }
       }
+    }
+  }
+
+  __device__ __forceinline__ void advance(const Operand& op) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      k0[i] += BK;
+      if (op.kind != 0) {
+        c[i] += BK;
+        while (c[i] >= op.g.C) {
+          c[i] -= op.g.C;
+          if (++kw[i] == op.g.S) {
+            kw[i] = 0;
+            ++kh[i];
+          }
+        }
+      }
+    }
+  }
+
+  __device__ __forceinline__ void load(const Operand& op, int rows, int K, int row0, bool vec_ok) {
+    const uint16_t* p = static_cast<const uint16_t*>(op.ptr);
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      u16x8 val = zero8();
+      if (v < kVecs && k0[i] < K) {
+        if (op.kind == 0) {
+          val = load_dense_kc(op, rows, K, row0 + v / (BK / 8), k0[i], vec_ok);
+        } else if (nb[i] >= 0) {
+          const ConvGeom& g = op.g;
+          int iy, ix;
+          bool ok = true;
+          if (op.kind == 1) {
+            iy = by[i] + kh[i];
+            ix = bx[i] + kw[i];
+          } else {
+            iy = by[i] - kh[i];
+            ix = bx[i] - kw[i];
+            ok = iy >= 0 && ix >= 0;
+            if (g.stride == 2) {
+              ok = ok && ((iy | ix) & 1) == 0;
+              iy >>= 1;
+              ix >>= 1;
+            } else if (g.stride > 2) {
+              ok = ok && (iy % g.stride) == 0 && (ix % g.stride) == 0;
+              iy /= g.stride;
+              ix /= g.stride;
+            }
+          }
+          if (ok && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W)
+            val = *reinterpret_cast<const u16x8*>(p + nb[i] + (static_cast<long>(iy) * g.W + ix) * g.C + c[i]);
+        }
+      }
+      regs[i] = val;
     }
   }
 
@@ -142,20 +170,105 @@ struct TileLoader {
     for (int i = 0; i < kPer; ++i) {
       const int v = threadIdx.x + i * kThreads;
       if (v < kVecs) {
-        if constexpr (KC) {
-          const int row = v / (BK / 8);
-          const int kv = v - row * (BK / 8);
-          *reinterpret_cast<u16x8*>(lds + row * (BK + 8) + kv * 8) = regs[i];
-        } else {
-          const int kk = v / (BROWS / 8);
-          const int rv = v - kk * (BROWS / 8);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) lds[(rv * 8 + j) * (BK + 8) + kk] = regs[i][j];
-        }
+        const int row = v / (BK / 8);
+        const int kv = v - row * (BK / 8);
+        *reinterpret_cast<u16x8*>(lds + row * (BK + 8) + kv * 8) = regs[i];
       }
     }
   }
 };
+
+// Row-contiguous operand (kinds 0 and 2): each slot loads 8 consecutive ROW elements at one k.
+// Kind 2 (weight-gradient B operand): rows are (kh, kw, c) of the conv (fixed per slot), k is the output
+// pixel (n, oy, ox), advanced incrementally.
+template <int BROWS, int BK>
+struct RcLoader {
+  static constexpr int kVecs = BROWS * BK / 8;
+  static constexpr int kPer = (kVecs + kThreads - 1) / kThreads;
+  u16x8 regs[kPer];
+  int k[kPer];
+  int c0[kPer], kw[kPer], kh[kPer];
+  int n[kPer], oy[kPer], ox[kPer];
+  bool rok[kPer];
+
+  __device__ __forceinline__ void init(const Operand& op, int rows, int row0, int kbeg) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      const int kk = v / (BROWS / 8), rv = v - kk * (BROWS / 8);
+      const int r0 = row0 + rv * 8;
+      k[i] = kbeg + kk;
+      rok[i] = v < kVecs && r0 < rows;
+      c0[i] = kw[i] = kh[i] = n[i] = oy[i] = ox[i] = 0;
+      if (op.kind != 2 || !rok[i]) continue;
+      const ConvGeom& g = op.g;
+      c0[i] = r0 % g.C;
+      const int rs = r0 / g.C;
+      kw[i] = rs % g.S;
+      kh[i] = rs / g.S;
+      const int HWo = g.Ho * g.Wo;
+      n[i] = k[i] / HWo;
+      const int rem = k[i] - n[i] * HWo;
+      oy[i] = rem / g.Wo;
+      ox[i] = rem - oy[i] * g.Wo;
+    }
+  }
+
+  __device__ __forceinline__ void advance(const Operand& op) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      k[i] += BK;
+      if (op.kind == 2) {
+        ox[i] += BK;
+        while (ox[i] >= op.g.Wo) {
+          ox[i] -= op.g.Wo;
+          if (++oy[i] == op.g.Ho) {
+            oy[i] = 0;
+            ++n[i];
+          }
+        }
+      }
+    }
+  }
+
+  __device__ __forceinline__ void load(const Operand& op, int rows, int K, int row0, bool vec_ok) {
+    const uint16_t* p = static_cast<const uint16_t*>(op.ptr);
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      u16x8 val = zero8();
+      if (v < kVecs && k[i] < K) {
+        if (op.kind == 0) {
+          val = load_dense_rc(op, rows, K, row0 + (v % (BROWS / 8)) * 8, k[i], vec_ok);
+        } else if (rok[i]) {
+          const ConvGeom& g = op.g;
+          const int iy = oy[i] * g.stride - g.pad + kh[i];
+          const int ix = ox[i] * g.stride - g.pad + kw[i];
+          if (iy >= 0 && iy < g.H && ix >= 0 && ix < g.W)
+            val = *reinterpret_cast<const u16x8*>(
+                p + ((static_cast<long>(n[i]) * g.H + iy) * g.W + ix) * g.C + c0[i]);
+        }
+      }
+      regs[i] = val;
+    }
+  }
+
+  __device__ __forceinline__ void store(uint16_t* lds) {  // lds: [BROWS][BK + 8], transposing scatter
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      if (v < kVecs) {
+        const int kk = v / (BROWS / 8);
+        const int rv = v - kk * (BROWS / 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) lds[(rv * 8 + j) * (BK + 8) + kk] = regs[i][j];
+      }
+    }
+  }
+};
+
+template <int BROWS, int BK, bool KC>
+using Loader = typename std::conditional<KC, KcLoader<BROWS, BK>, RcLoader<BROWS, BK>>::type;
 
 __device__ __forceinline__ float apply_epi(float v, int epi, int m, int n, const GemmArgs& a) {
   if ((epi & EPI_BIAS) && n < a.nbias) v += a.bias[n];
@@ -165,7 +278,14 @@ __device__ __forceinline__ float apply_epi(float v, int epi, int m, int n, const
 }
 
 __device__ __forceinline__ void store_out(float v, int epi, int m, int n, const GemmArgs& a) {
-  const long off = static_cast<long>(m) * a.ldo + n;
+  long off;
+  if (epi & EPI_OIHW) {  // m = co, n = (r*S + s)*Cp + ci  ->  [co][ci][r][s]
+    const int rs = n / a.oihw_cp, ci = n - rs * a.oihw_cp;
+    if (ci >= a.oihw_ci) return;
+    off = (static_cast<long>(m) * a.oihw_ci + ci) * a.oihw_rs + rs;
+  } else {
+    off = static_cast<long>(m) * a.ldo + n;
+  }
   if (epi & EPI_OUT_F32) {
     float* o = static_cast<float*>(a.out);
     if (epi & EPI_ACCUM) v += o[off];
@@ -217,13 +337,15 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  TileLoader<BM, BK, AKC> la;
-  TileLoader<BN, BK, BKC> lb;
+  Loader<BM, BK, AKC> la;
+  Loader<BN, BK, BKC> lb;
   const bool avec = a_vec != 0, bvec = b_vec != 0;
+  la.init(args.a, args.M, m0, kbeg);
+  lb.init(args.b, args.N, n0, kbeg);
   // Reduction bound for the loaders is kend (zero fill past the split's end).
   if (nk > 0) {
-    la.load(args.a, args.M, kend, m0, kbeg, avec);
-    lb.load(args.b, args.N, kend, n0, kbeg, bvec);
+    la.load(args.a, args.M, kend, m0, avec);
+    lb.load(args.b, args.N, kend, n0, bvec);
     la.store(smem);
     lb.store(smem + LDS_A);
   }
@@ -233,8 +355,10 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) {
-      la.load(args.a, args.M, kend, m0, kbeg + (kt + 1) * BK, avec);
-      lb.load(args.b, args.N, kend, n0, kbeg + (kt + 1) * BK, bvec);
+      la.advance(args.a);
+      lb.advance(args.b);
+      la.load(args.a, args.M, kend, m0, avec);
+      lb.load(args.b, args.N, kend, n0, bvec);
     }
     const uint16_t* As = smem + cur * (LDS_A + LDS_B);
     const uint16_t* Bs = As + LDS_A;
@@ -288,6 +412,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles
   }
 }
 
+// Split-K slab reduction, scalar form (N % 4 != 0).
 __global__ void gemm_splitk_reduce(GemmArgs args, int splits) {
   const long total = static_cast<long>(args.M) * args.N;
   for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
@@ -301,6 +426,43 @@ __global__ void gemm_splitk_reduce(GemmArgs args, int splits) {
   }
 }
 
+// Split-K slab reduction, vector form (N % 4 == 0): a block covers COLS float4 columns of the [M][N]
+// output with LANES slab-lanes each (thread = column + COLS x lane); partials meet in LDS in a fixed
+// order (deterministic), then the epilogue runs on the 4 outputs of each column.
+template <int LANES>
+__global__ __launch_bounds__(256) void gemm_splitk_reduce4(GemmArgs args, int splits) {
+  constexpr int COLS = 256 / LANES;
+  __shared__ f32x4 part[LANES][COLS];
+  const int total4 = args.M * (args.N / 4);
+  const int col = threadIdx.x % COLS, sl = threadIdx.x / COLS;
+  const int c4 = blockIdx.x * COLS + col;
+  const f32x4* w4 = reinterpret_cast<const f32x4*>(args.workspace);
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+  if (c4 < total4) {
+    int z = sl;
+    for (; z + LANES < splits; z += 2 * LANES) {
+      a0 += w4[static_cast<long>(z) * total4 + c4];
+      a1 += w4[static_cast<long>(z + LANES) * total4 + c4];
+    }
+    for (; z < splits; z += LANES) a0 += w4[static_cast<long>(z) * total4 + c4];
+  }
+  f32x4 v = a0 + a1;
+  if constexpr (LANES > 1) {
+    part[sl][col] = v;
+    __syncthreads();
+    if (sl == 0) {
+#pragma unroll
+      for (int k = 1; k < LANES; ++k) v += part[k][col];
+    }
+  }
+  if (sl == 0 && c4 < total4) {
+    const int q = args.N / 4;
+    const int m = c4 / q, n = (c4 - m * q) * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) store_out(apply_epi(v[j], args.epi, m, n + j, args), args.epi, m, n + j, args);
+  }
+}
+
 template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC>
 hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
   const int tm = ceil_div(a.M, BM), tn = ceil_div(a.N, BN);
@@ -309,18 +471,28 @@ hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
   splitk = ceil_div(a.K, kps);
   // Vector (16 B) loads are legal when the contiguous dimension and the other stride keep
   // every 8-element group 16-byte aligned.
-  auto vec_ok = [](const Operand& o, bool kc, int rows, int K) {
+  auto vec_ok = [](const Operand& o, bool kc) {
     if (o.kind != 0) return 1;
     if (kc) return (o.ld_k == 1 && o.ld_r % 8 == 0 && (reinterpret_cast<uintptr_t>(o.ptr) & 15) == 0) ? 1 : 0;
     return (o.ld_r == 1 && o.ld_k % 8 == 0 && (reinterpret_cast<uintptr_t>(o.ptr) & 15) == 0) ? 1 : 0;
   };
-  const int av = vec_ok(a.a, AKC, a.M, a.K), bv = vec_ok(a.b, BKC, a.N, a.K);
+  const int av = vec_ok(a.a, AKC), bv = vec_ok(a.b, BKC);
   dim3 grid(tm * tn, 1, splitk);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AKC, BKC>), grid, dim3(kThreads), 0, s, a, tm, tn,
                      kps, av, bv);
   if (splitk > 1) {
     const long total = static_cast<long>(a.M) * a.N;
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(stream_grid(total, 256)), dim3(256), 0, s, a, splitk);
+    if (a.N % 4 == 0 && total / 4 < (1L << 30) && (reinterpret_cast<uintptr_t>(a.workspace) & 15) == 0) {
+      const long t4 = total / 4;
+      if (splitk <= 2)
+        hipLaunchKernelGGL(gemm_splitk_reduce4<1>, dim3(ceil_div(t4, 256)), dim3(256), 0, s, a, splitk);
+      else if (splitk <= 16)
+        hipLaunchKernelGGL(gemm_splitk_reduce4<4>, dim3(ceil_div(t4, 64)), dim3(256), 0, s, a, splitk);
+      else
+        hipLaunchKernelGGL(gemm_splitk_reduce4<16>, dim3(ceil_div(t4, 16)), dim3(256), 0, s, a, splitk);
+    } else {
+      hipLaunchKernelGGL(gemm_splitk_reduce, dim3(stream_grid(total, 256)), dim3(256), 0, s, a, splitk);
+    }
   }
   return hipGetLastError();
 }
@@ -329,12 +501,12 @@ template <bool AKC, bool BKC>
 hipError_t dispatch_tiles(const GemmArgs& a, hipStream_t s) {
   const long t128 = static_cast<long>(ceil_div(a.M, 128)) * ceil_div(a.N, 128);
   const long t64 = static_cast<long>(ceil_div(a.M, 64)) * ceil_div(a.N, 64);
-  // Split-K only where a workspace was provided and the tile grid cannot fill the chip.
+  // Split-K only where a workspace was provided and the tile grid cannot fill the chip: aim for ~2
+  // blocks per CU while every split keeps >= 8 K-tiles of work (bounded slab traffic).
   auto pick_split = [&](long tiles, int bk) {
     if (a.workspace == nullptr || a.splitk <= 1) return 1;
     int sk = 1;
-    // target >= 4 blocks per CU (1024) while every split keeps >= 8 K-tiles of work
-    while (sk < a.splitk && tiles * sk < 1024 && a.K / (sk * 2) >= 4 * bk) sk *= 2;
+    while (sk < a.splitk && tiles * sk < 512 && a.K / (sk * 2) >= 8 * bk) sk *= 2;
     return sk;
   };
   if (a.N <= 32) {

@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const uint16_t* __restric
 // Per channel: dgamma, dbeta (written / accumulated) and the dx coefficients.
 __global__ void k_bn_bwd_finalize(const float* __restrict__ ws, int nblk, int P, int C, const float* __restrict__ gamma,
                                   const float* __restrict__ invstd, float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                  float* __restrict__ coef) {
+                                  int accum, float* __restrict__ coef) {
   const int c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (c >= C) return;
@@ -199,8 +199,8 @@ __global__ void k_bn_bwd_finalize(const float* __restrict__ ws, int nblk, int P,
   }
   const float s1 = wave_sum(p1), s2 = wave_sum(p2);
   if (lane != 0) return;
-  if (dgamma) dgamma[c] = s2;
-  if (dbeta) dbeta[c] = s1;
+  if (dgamma) dgamma[c] = accum ? dgamma[c] + s2 : s2;
+  if (dbeta) dbeta[c] = accum ? dbeta[c] + s1 : s1;
   const float a = (gamma ? gamma[c] : 1.f) * invstd[c];
   coef[c] = a;                                   // a
   coef[C + c] = a * s1 / static_cast<float>(P);  // b
@@ -462,13 +462,13 @@ hipError_t bn_apply(const uint16_t* x, int P, int C, const float* scale, const f
 }
 
 hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
-                  const float* gamma, int P, int C, int relu, float* dgamma, float* dbeta, float* ws, float* coef,
-                  uint16_t* dx, uint16_t* dres, hipStream_t s) {
+                  const float* gamma, int P, int C, int relu, float* dgamma, float* dbeta, int accum_params, float* ws,
+                  float* coef, uint16_t* dx, uint16_t* dres, hipStream_t s) {
   int rpb;
   const int nblk = bn_blocks(P, C, rpb);
   hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(nblk), dim3(256), 0, s, dy, x, y, mean, invstd, P, C, rpb, relu, ws);
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(ceil_div(C, 4)), dim3(256), 0, s, ws, nblk, P, C, gamma, invstd,
-                     dgamma, dbeta, coef);
+                     dgamma, dbeta, accum_params, coef);
   const long nvec = static_cast<long>(P) * C / 8;
   hipLaunchKernelGGL(k_bn_bwd_apply, dim3(stream_grid(nvec, 256)), dim3(256), 0, s, dy, x, y, mean, invstd, coef,
                      nvec, C, relu, dx, dres);

@@ -90,6 +90,42 @@ def _C():
     return _native.C()
 
 
+# ---------------------------------------------------------------------------------------------
+# direct gradient accumulation
+# ---------------------------------------------------------------------------------------------
+_DIRECT_GRAD = [True]
+
+
+class direct_grad_accumulation:
+    """Context manager toggling direct accumulation (default on): weight-gradient kernels add into an
+    existing ``param.grad`` themselves instead of returning a fresh tensor that autograd then adds --
+    one gradient tensor and one add kernel less per parameter and step.  The backward then returns
+    ``None`` for that parameter; autograd still runs the parameter's AccumulateGrad node, so
+    post-accumulate-grad hooks (DDP / Horovod overlap) fire exactly as before, after the kernel that
+    accumulated the gradient has been enqueued (tests/test_kernels_gpu.py::test_direct_grad_accumulation)."""
+
+    def __init__(self, enabled: bool = True):
+        self.enabled = enabled
+
+    def __enter__(self):
+        self._old = _DIRECT_GRAD[0]
+        _DIRECT_GRAD[0] = self.enabled
+
+    def __exit__(self, *exc):
+        _DIRECT_GRAD[0] = self._old
+
+
+def _grad_sink(p):
+    """``p.grad`` when a kernel may accumulate straight into it, else None (return the grad to autograd)."""
+    if p is None or not _DIRECT_GRAD[0]:
+        return None
+    g = p.grad
+    if (g is None or g.dtype != torch.float32 or g.device != p.device or g.shape != p.shape
+            or not g.is_contiguous() or g.requires_grad):
+        return None
+    return g
+
+
 def _bf16_weight(w: torch.Tensor) -> torch.Tensor:
     return _cached(w, "bf16", lambda: _C().cast_bf16(w.detach().contiguous()))
 
@@ -105,6 +141,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.relu = relu and not consumer_masks
         ctx.mask_input_grad = mask_input_grad
         ctx.has_bias = bias is not None
+        ctx.params = (weight, bias)
         ctx.save_for_backward(x, wb, y if ctx.relu else None)
         return y
 
@@ -119,10 +156,17 @@ class _LinearFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = _C().linear_dgrad(dy, wb, x if ctx.mask_input_grad else None)
+        weight, bias = ctx.params
         if ctx.needs_input_grad[1]:
-            dw = _C().linear_wgrad(dy, x)
+            sink = _grad_sink(weight)
+            dw = _C().linear_wgrad(dy, x, sink, sink is not None)
+            if sink is not None:
+                dw = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = _C().colsum(dy)
+            sink = _grad_sink(bias)
+            db = _C().colsum(dy, -1, sink, sink is not None)
+            if sink is not None:
+                db = None
         return dx, dw, db, None, None, None, None
 
 
@@ -156,6 +200,7 @@ class _Conv2dFn(torch.autograd.Function):
         ctx.geom = (co, ci, r, s, stride, pad, cp, cop, x.shape[1], x.shape[2])
         ctx.relu = relu
         ctx.has_bias = bias is not None
+        ctx.bias = bias
         ctx.save_for_backward(x, weight, y if relu else None)
         return y
 
@@ -172,10 +217,16 @@ class _Conv2dFn(torch.autograd.Function):
                          lambda: _C().conv_w_dgrad(weight.detach().contiguous(), cp, cop))
             dx = _C().conv_dgrad(dy, wd, h, w, r, s, stride, pad, None)
         if ctx.needs_input_grad[1]:
-            g = _C().conv_wgrad(dy, x, r, s, stride, pad)
-            dw = _C().conv_wgrad_oihw(g, co, ci, r, s)
+            # OIHW epilogue: the GEMM writes the parameter's layout (and adds into .grad when it exists)
+            sink = _grad_sink(weight)
+            dw = _C().conv_wgrad(dy, x, r, s, stride, pad, co, ci, sink, sink is not None)
+            if sink is not None:
+                dw = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = _C().colsum(dy)[:co]
+            sink = _grad_sink(ctx.bias)
+            db = _C().colsum(dy, co, sink, sink is not None)
+            if sink is not None:
+                db = None
         return dx, dw, db, None, None, None
 
 
@@ -206,14 +257,21 @@ class _BatchNormFn(torch.autograd.Function):
                                       eps, momentum, residual, relu)
         ctx.relu = relu
         ctx.has_res = residual is not None
+        ctx.beta = beta
         ctx.save_for_backward(x, y, mean, invstd, gamma)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, y, mean, invstd, gamma = ctx.saved_tensors
+        beta = ctx.beta
+        dg_sink, db_sink = _grad_sink(gamma), _grad_sink(beta)
+        direct = dg_sink is not None and db_sink is not None
         dx, dg, db, dres = _C().bn_bwd(dy.contiguous(), x, y, mean, invstd,
-                                       gamma.detach() if gamma is not None else None, ctx.relu, ctx.has_res)
+                                       gamma.detach() if gamma is not None else None, ctx.relu, ctx.has_res,
+                                       dg_sink if direct else None, db_sink if direct else None)
+        if direct:  # dgamma / dbeta were added into .grad by the finalize kernel
+            dg = db = None
         return dx, dg, db, None, None, (dres if ctx.has_res else None), None, None, None
 
 

@@ -266,3 +266,43 @@ def test_fused_optimizers_views_and_device_step(gpu, kind):
     for a, b in zip(mine, ref):
         assert rel_err(a, b) < 1e-5
     assert int(o1._dev[0]["step"][0].item()) == 4 and int(o1._dev[0]["step"][1].item()) == 0
+
+
+def test_direct_grad_accumulation(gpu):
+    """Weight-gradient kernels add into an existing .grad (conv OIHW epilogue, linear wgrad, bias colsum,
+    BN finalize); post-accumulate-grad hooks still fire once per backward; results equal autograd's own
+    accumulation."""
+    from pytorch_distributed_examples_amd.ops import layers as L
+
+    torch.manual_seed(3)
+    conv = L.Conv2d(16, 24, 3, stride=2, padding=1).to(gpu)
+    bn = L.BatchNorm2d(24).to(gpu)
+    fc = L.Linear(24, 10).to(gpu)
+    x = OF.to_native_image(torch.randn(4, 16, 12, 12, device=gpu))
+
+    def loss():
+        h = bn(conv(x), relu=True)
+        return OF.mse_loss(fc(OF.global_avg_pool_flat(h), out_f32=True), torch.ones(4, 10, device=gpu))
+
+    params = list(conv.parameters()) + list(bn.parameters()) + list(fc.parameters())
+    with OF.direct_grad_accumulation(False):
+        loss().backward()
+        loss().backward()
+    ref = [p.grad.clone() for p in params]
+    for p in params:
+        p.grad = torch.zeros_like(p)
+    fired = []
+    handles = [p.register_post_accumulate_grad_hook(lambda q: fired.append(q)) for p in params]
+    loss().backward()
+    loss().backward()
+    for h in handles:
+        h.remove()
+    assert len(fired) == 2 * len(params)
+    for p, r in zip(params, ref):
+        assert rel_err(p.grad, r) < 1e-5
+
+
+@pytest.mark.parametrize("cfg", [(4, 64, 16, 64, 1, 1, 0), (2, 24, 8, 40, 1, 1, 0)])
+def test_pointwise_conv_dense_path(gpu, cfg):
+    """1x1 / stride-1 convs take the dense-operand GEMM path (no gather): fwd, dgrad, wgrad."""
+    test_conv_fwd_bwd(gpu, cfg)
