@@ -7,6 +7,8 @@
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPGuard.h>
 
+#include <algorithm>
+#include <cstring>
 #include <vector>
 
 #include "pde_kernels.h"
@@ -174,19 +176,27 @@ Tensor conv_fwd(const Tensor& x, const Tensor& wf, const optional<Tensor>& bias,
   return y;
 }
 
-// dx[N,H,W,Ci] from dy[N,Ho,Wo,Co] and wd = [Ci, R*S*Co]
+// dx[N,H,W,Ci] from dy[N,Ho,Wo,Co] and wd = [Ci, R*S*Co]; or, for a 1x1 / stride-1 conv with
+// w_fwd_layout, from the forward copy wd = [Co, Ci] read transposed (no separate dgrad layout).
 Tensor conv_dgrad(const Tensor& dy, const Tensor& wd, int H, int W, int R, int S, int stride, int pad,
-                  const optional<Tensor>& aux) {
+                  const optional<Tensor>& aux, bool w_fwd_layout) {
   CHECK_IN(dy); CHECK_IN(wd); CHECK_BF16(dy); CHECK_BF16(wd);
   const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
   TORCH_CHECK(Co % 8 == 0, "conv_dgrad: Cout must be a multiple of 8");
-  const int Ci = wd.size(0);
-  TORCH_CHECK(wd.size(1) == R * S * Co, "conv_dgrad: weight must be [Ci, R*S*Co]");
+  int Ci;
+  if (w_fwd_layout) {
+    TORCH_CHECK(is_pointwise(R, S, stride, pad), "conv_dgrad: the forward-layout weight needs a 1x1/s1 conv");
+    TORCH_CHECK(wd.dim() == 2 && wd.size(0) == Co && wd.size(1) % 8 == 0, "conv_dgrad: weight must be [Co, Ci]");
+    Ci = wd.size(1);
+  } else {
+    Ci = wd.size(0);
+    TORCH_CHECK(wd.size(1) == R * S * Co, "conv_dgrad: weight must be [Ci, R*S*Co]");
+  }
   Tensor dx = at::empty({N, H, W, Ci}, dy.options());
   pde::GemmArgs a{};
   a.M = N * H * W; a.N = Ci; a.K = R * S * Co;
   a.a = is_pointwise(R, S, stride, pad) ? dense(dy, Co, 1) : gather(dy, 3, N, Ho, Wo, Co, R, S, stride, pad, H, W);
-  a.b = dense(wd, a.K, 1);
+  a.b = w_fwd_layout ? dense(wd, 1, Ci) : dense(wd, a.K, 1);
   a.out = dx.data_ptr(); a.ldo = Ci;
   a.aux = cu16(aux); a.ldaux = Ci;
   a.epi = a.aux ? pde::EPI_DRELU : 0;
@@ -245,20 +255,24 @@ Tensor nchw_to_nhwc(const Tensor& x, int Cp) {
   return y;
 }
 // [Co, Ci, R, S] fp32 -> [Cop, R*S*Cp] bf16 (zero padded channels)
-Tensor conv_w_fwd(const Tensor& w, int Cp, int Cop) {
+Tensor conv_w_fwd(const Tensor& w, int Cp, int Cop, const optional<Tensor>& out) {
   CHECK_IN(w); CHECK_F32(w);
   const int Co = w.size(0), Ci = w.size(1), R = w.size(2), S = w.size(3);
   TORCH_CHECK(Cp >= Ci && Cop >= Co, "conv_w_fwd: padding smaller than channels");
-  Tensor y = at::empty({Cop, R * S * Cp}, w.options().dtype(at::kBFloat16));
+  Tensor y = out.has_value() && out->defined() ? *out : at::empty({Cop, R * S * Cp}, w.options().dtype(at::kBFloat16));
+  CHECK_IN(y); CHECK_BF16(y);
+  TORCH_CHECK(y.numel() == static_cast<long>(Cop) * R * S * Cp, "conv_w_fwd: out size");
   check(pde::conv_weight_fwd_layout(w.data_ptr<float>(), u16(y), Co, Ci, R, S, Cp, Cop, cur_stream()), "conv_w_fwd");
   return y;
 }
 // [Co, Ci, R, S] fp32 -> [Cip, R*S*Cop] bf16
-Tensor conv_w_dgrad(const Tensor& w, int Cip, int Cop) {
+Tensor conv_w_dgrad(const Tensor& w, int Cip, int Cop, const optional<Tensor>& out) {
   CHECK_IN(w); CHECK_F32(w);
   const int Co = w.size(0), Ci = w.size(1), R = w.size(2), S = w.size(3);
   TORCH_CHECK(Cip >= Ci && Cop >= Co, "conv_w_dgrad: padding smaller than channels");
-  Tensor y = at::empty({Cip, R * S * Cop}, w.options().dtype(at::kBFloat16));
+  Tensor y = out.has_value() && out->defined() ? *out : at::empty({Cip, R * S * Cop}, w.options().dtype(at::kBFloat16));
+  CHECK_IN(y); CHECK_BF16(y);
+  TORCH_CHECK(y.numel() == static_cast<long>(Cip) * R * S * Cop, "conv_w_dgrad: out size");
   check(pde::conv_weight_dgrad_layout(w.data_ptr<float>(), u16(y), Co, Ci, R, S, Cip, Cop, cur_stream()),
         "conv_w_dgrad");
   return y;
@@ -377,43 +391,72 @@ Tensor mse_bwd(const Tensor& p, const Tensor& t, const Tensor& gout, bool dx_f32
 // ------------------------------------------------------------------------------------------------
 // Fused multi-tensor optimiser
 // ------------------------------------------------------------------------------------------------
-// Build the device table for a parameter set; returns (table bytes tensor on device, total elems).
-std::tuple<Tensor, int64_t> optim_table(const std::vector<Tensor>& params, const std::vector<Tensor>& grads,
-                                        const std::vector<Tensor>& exp_avg, const std::vector<Tensor>& exp_avg_sq,
-                                        const std::vector<Tensor>& bf16_copies) {
+// Build the device tables for a parameter set: per-tensor entries and the chunk list (tensors cut into
+// chunks of optim_chunk_elems(), a chunk never straddles two tensors).  Returns (table, chunks, nchunks).
+// bf16_copies: compute copies refreshed by the update (an empty tensor in any optional list = none).
+Tensor to_device_bytes(const void* src, long bytes, const at::TensorOptions& dev_opts) {
+  Tensor host = at::empty({bytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  std::memcpy(host.data_ptr(), src, bytes);
+  Tensor dev = at::empty({bytes}, dev_opts.dtype(at::kByte));
+  dev.copy_(host, /*non_blocking=*/true);
+  return dev;
+}
+
+inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+std::tuple<Tensor, Tensor, int64_t> optim_table(const std::vector<Tensor>& params, const std::vector<Tensor>& grads,
+                                                const std::vector<Tensor>& exp_avg,
+                                                const std::vector<Tensor>& exp_avg_sq,
+                                                const std::vector<Tensor>& bf16_copies) {
   const size_t n = params.size();
+  TORCH_CHECK(n > 0, "optim_table: no parameters");
   TORCH_CHECK(grads.size() == n, "optim_table: grads size");
   std::vector<pde::OptimEntry> tab(n);
-  long off = 0;
+  std::vector<pde::OptimChunk> chunks;
+  const int chunk = pde::optim_chunk_elems();
+  auto get = [&](const std::vector<Tensor>& v, size_t i) -> const Tensor* {
+    return i < v.size() && v[i].defined() && v[i].numel() > 0 ? &v[i] : nullptr;  // empty tensor = none
+  };
   for (size_t i = 0; i < n; ++i) {
     const Tensor& p = params[i];
     CHECK_IN(p); CHECK_F32(p);
-    pde::OptimEntry& e = tab[i];
+    TORCH_CHECK(p.numel() < (1L << 31), "optim_table: tensor too large");
+    pde::OptimEntry e{};
     e.param = p.data_ptr<float>();
-    e.grad = grads[i].defined() ? grads[i].data_ptr<float>() : nullptr;
-    if (grads[i].defined()) { CHECK_CONTIG(grads[i]); TORCH_CHECK(grads[i].numel() == p.numel(), "grad size"); }
-    e.exp_avg = i < exp_avg.size() && exp_avg[i].defined() ? exp_avg[i].data_ptr<float>() : nullptr;
-    e.exp_avg_sq = i < exp_avg_sq.size() && exp_avg_sq[i].defined() ? exp_avg_sq[i].data_ptr<float>() : nullptr;
-    e.bf16_copy = i < bf16_copies.size() && bf16_copies[i].defined() ? u16(bf16_copies[i]) : nullptr;
-    e.offset = off;
+    if (grads[i].defined()) {
+      CHECK_CONTIG(grads[i]); TORCH_CHECK(grads[i].numel() == p.numel(), "grad size");
+      e.grad = grads[i].data_ptr<float>();
+    }
+    if (auto t = get(exp_avg, i)) e.exp_avg = t->data_ptr<float>();
+    if (auto t = get(exp_avg_sq, i)) e.exp_avg_sq = t->data_ptr<float>();
+    if (auto t = get(bf16_copies, i)) {
+      CHECK_IN(*t);
+      TORCH_CHECK(t->numel() == p.numel() && t->scalar_type() == at::kBFloat16, "bf16 copy");
+      e.bf16_copy = u16(*t);
+    }
     e.size = p.numel();
-    off += (p.numel() + 3) / 4 * 4;  // groups of 4 elements never straddle two tensors
+    e.vec = al16(e.param) && (!e.grad || al16(e.grad)) && (!e.exp_avg || al16(e.exp_avg)) &&
+            (!e.exp_avg_sq || al16(e.exp_avg_sq)) && (!e.bf16_copy || (reinterpret_cast<uintptr_t>(e.bf16_copy) & 7) == 0);
+    tab[i] = e;
+    for (long s0 = 0; s0 < e.size; s0 += chunk)
+      chunks.push_back(pde::OptimChunk{static_cast<int>(i), static_cast<int>(s0),
+                                       static_cast<int>(std::min<long>(chunk, e.size - s0)), 0});
   }
-  const long bytes = static_cast<long>(n * sizeof(pde::OptimEntry));
-  Tensor host = at::empty({bytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
-  std::memcpy(host.data_ptr(), tab.data(), bytes);
-  Tensor dev = at::empty({bytes}, params.empty() ? at::TensorOptions().dtype(at::kByte)
-                                                 : params[0].options().dtype(at::kByte));
-  dev.copy_(host, /*non_blocking=*/true);
-  return {dev, off};
+  auto opts = params[0].options();
+  Tensor dtab = to_device_bytes(tab.data(), static_cast<long>(n * sizeof(pde::OptimEntry)), opts);
+  Tensor dchunks = to_device_bytes(chunks.data(), static_cast<long>(chunks.size() * sizeof(pde::OptimChunk)), opts);
+  return {dtab, dchunks, static_cast<int64_t>(chunks.size())};
 }
 
-void optim_step(const Tensor& table, int ntensors, int64_t total, int mode, const Tensor& hparams, Tensor& step) {
-  CHECK_IN(table); CHECK_IN(hparams); CHECK_IN(step);
+void optim_step(const Tensor& table, const Tensor& chunks, int64_t nchunks, int mode, const Tensor& hparams,
+                Tensor& step) {
+  CHECK_IN(table); CHECK_IN(chunks); CHECK_IN(hparams); CHECK_IN(step);
   TORCH_CHECK(hparams.numel() >= pde::HP_COUNT, "hparams size");
   TORCH_CHECK(step.scalar_type() == at::kInt && step.numel() >= 2, "step must be int32[2]");
-  check(pde::multi_tensor_optim(mode, reinterpret_cast<const pde::OptimEntry*>(table.data_ptr()), ntensors, total,
-                                hparams.data_ptr<float>(), step.data_ptr<int>(), cur_stream()),
+  check(pde::multi_tensor_optim(mode, reinterpret_cast<const pde::OptimEntry*>(table.data_ptr()),
+                                reinterpret_cast<const pde::OptimChunk*>(chunks.data_ptr()),
+                                static_cast<int>(nchunks), hparams.data_ptr<float>(), step.data_ptr<int>(),
+                                cur_stream()),
         "optim_step");
 }
 
@@ -601,15 +644,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_wgrad", &linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("out") = py::none(),
         py::arg("accumulate") = false);
   m.def("conv_fwd", &conv_fwd);
-  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wd"), py::arg("H"), py::arg("W"), py::arg("R"),
+        py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("aux") = py::none(), py::arg("w_fwd_layout") = false);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),
         py::arg("pad"), py::arg("Co"), py::arg("Ci"), py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("cast_bf16", &cast_bf16);
   m.def("cast_bf16_into", &cast_bf16_into);
   m.def("cast_f32", &cast_f32);
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
-  m.def("conv_w_fwd", &conv_w_fwd);
-  m.def("conv_w_dgrad", &conv_w_dgrad);
+  m.def("conv_w_fwd", &conv_w_fwd, py::arg("w"), py::arg("Cp"), py::arg("Cop"), py::arg("out") = py::none());
+  m.def("conv_w_dgrad", &conv_w_dgrad, py::arg("w"), py::arg("Cip"), py::arg("Cop"), py::arg("out") = py::none());
   m.def("conv_wgrad_oihw", &conv_wgrad_oihw);
   m.def("colsum", &colsum, py::arg("x"), py::arg("ncols") = -1, py::arg("out") = py::none(),
         py::arg("accumulate") = false);

@@ -107,15 +107,19 @@ struct OptimEntry {
   const float* grad;     // fp32 gradient (nullptr: treated as zero)
   float* exp_avg;        // Adam/AdamW m, SGD momentum buffer
   float* exp_avg_sq;     // Adam/AdamW v
-  uint16_t* bf16_copy;   // optional bf16 compute copy written after the update
-  long offset;           // prefix offset in the concatenated element space
+  uint16_t* bf16_copy;   // optional bf16 compute copy (same element order) written after the update
   long size;
+  int vec;               // every pointer 16-byte aligned: 16-byte loads / stores
+  int pad;
+};
+struct OptimChunk {      // elements [start, start + count) of tensor `tensor`
+  int tensor, start, count, pad;
 };
 enum HParam { HP_LR = 0, HP_BETA1, HP_BETA2, HP_EPS, HP_WD, HP_MOMENTUM, HP_GRAD_SCALE, HP_COUNT };
+int optim_chunk_elems();  // chunk size the host must cut tensors into
 // mode 0 SGD, 1 Adam, 2 AdamW.  dev_hparams: float[HP_COUNT]; dev_step: int[2] = {steps taken so far,
 // arrival counter (0 between launches)}; the step is advanced on device by the update itself.
-// Table offsets must be multiples of 4 (optim_table pads them).
-hipError_t multi_tensor_optim(int mode, const OptimEntry* dev_table, int ntensors, long total_elems,
+hipError_t multi_tensor_optim(int mode, const OptimEntry* dev_table, const OptimChunk* dev_chunks, int nchunks,
                               const float* dev_hparams, int* dev_step, hipStream_t s);
 
 // ---------------------------------------------------------------------------------------------

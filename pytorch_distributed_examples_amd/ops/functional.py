@@ -126,7 +126,51 @@ def _grad_sink(p):
     return g
 
 
+# ---------------------------------------------------------------------------------------------
+# optimizer-maintained compute copies
+# ---------------------------------------------------------------------------------------------
+def maintain_compute_copies(p: torch.Tensor):
+    """Allocate the bf16 compute copy of a GPU weight that the fused optimizer keeps in sync from now on
+    (it writes it in the same launch as the update, contiguous stores).  Covered: linear weights
+    (``_pde_linear``) and 1x1 conv weights (``_pde_conv``) with channel counts that need no padding --
+    for those the implicit-GEMM forward layout [Co, Ci] IS the OIHW order, and the dgrad GEMM reads the
+    same copy transposed.  Returns the copy dict (or None).  The copy is tied to the weight's version
+    counter: an in-place write outside the optimizer (load_state_dict, a broadcast, an elastic restore) is
+    detected by :func:`_maintained` and the copy is re-derived in place."""
+    if not p.is_cuda or p.dtype != torch.float32:
+        return None
+    d = {}
+    if getattr(p, "_pde_conv", False) and p.dim() == 4:
+        co, ci, r, s = p.shape
+        if r * s != 1 or ci % 8 or co % 8:
+            return None
+        d["bf16"] = torch.empty(p.shape, dtype=torch.bfloat16, device=p.device)
+        d["conv_fwd"] = d["bf16"].view(co, ci)
+    elif getattr(p, "_pde_linear", False) and p.dim() == 2:
+        d["bf16"] = torch.empty(p.shape, dtype=torch.bfloat16, device=p.device)
+    else:
+        return None
+    _C().cast_bf16_into(p.detach().contiguous(), d["bf16"])
+    d["version"] = p._version
+    p.__dict__["_pde_maint"] = d
+    return d
+
+
+def _maintained(p: torch.Tensor, kind: str):
+    """The optimizer-maintained copy ``kind`` of ``p`` (None if the optimizer does not maintain one)."""
+    d = p.__dict__.get("_pde_maint")
+    if d is None or kind not in d:
+        return None
+    if d["version"] != p._version:  # written outside the optimizer: re-derive in place
+        _C().cast_bf16_into(p.detach().contiguous(), d["bf16"])
+        d["version"] = p._version
+    return d[kind]
+
+
 def _bf16_weight(w: torch.Tensor) -> torch.Tensor:
+    m = _maintained(w, "bf16")
+    if m is not None:
+        return m
     return _cached(w, "bf16", lambda: _C().cast_bf16(w.detach().contiguous()))
 
 
@@ -195,7 +239,9 @@ class _Conv2dFn(torch.autograd.Function):
         co, ci, r, s = weight.shape
         cp = x.shape[3]
         cop = pad8(co)
-        wf = _cached(weight, ("conv_fwd", cp, cop), lambda: _C().conv_w_fwd(weight.detach().contiguous(), cp, cop))
+        wf = _maintained(weight, "conv_fwd") if cp == pad8(ci) else None
+        if wf is None:
+            wf = _cached(weight, ("conv_fwd", cp, cop), lambda: _C().conv_w_fwd(weight.detach().contiguous(), cp, cop))
         y = _C().conv_fwd(x, wf, bias.detach() if bias is not None else None, r, s, stride, pad, relu, False)
         ctx.geom = (co, ci, r, s, stride, pad, cp, cop, x.shape[1], x.shape[2])
         ctx.relu = relu
@@ -213,9 +259,13 @@ class _Conv2dFn(torch.autograd.Function):
             dy = _C().relu_bwd(dy, y)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            wd = _cached(weight, ("conv_dgrad", cp, cop),
-                         lambda: _C().conv_w_dgrad(weight.detach().contiguous(), cp, cop))
-            dx = _C().conv_dgrad(dy, wd, h, w, r, s, stride, pad, None)
+            wf = _maintained(weight, "conv_fwd") if (r == 1 and s == 1 and stride == 1 and pad == 0) else None
+            if wf is not None:  # 1x1: the dgrad GEMM reads the forward copy [Co, Ci] transposed
+                dx = _C().conv_dgrad(dy, wf, h, w, r, s, stride, pad, None, True)
+            else:
+                wd = _cached(weight, ("conv_dgrad", cp, cop),
+                             lambda: _C().conv_w_dgrad(weight.detach().contiguous(), cp, cop))
+                dx = _C().conv_dgrad(dy, wd, h, w, r, s, stride, pad, None)
         if ctx.needs_input_grad[1]:
             # OIHW epilogue: the GEMM writes the parameter's layout (and adds into .grad when it exists)
             sink = _grad_sink(weight)

@@ -22,6 +22,7 @@ class Linear(nn.Module):
         super().__init__()
         self.in_features, self.out_features, self.relu = in_features, out_features, relu
         self.weight = nn.Parameter(torch.empty(out_features, in_features))
+        self.weight._pde_linear = True  # the fused optimizer maintains its bf16 compute copy
         self.bias = nn.Parameter(torch.empty(out_features)) if bias else None
         self.reset_parameters()
 
@@ -46,6 +47,7 @@ class Conv2d(nn.Module):
         self.in_channels, self.out_channels = in_channels, out_channels
         self.kernel_size, self.stride, self.padding, self.relu = kernel_size, stride, padding, relu
         self.weight = nn.Parameter(torch.empty(out_channels, in_channels, kernel_size, kernel_size))
+        self.weight._pde_conv = True  # the fused optimizer maintains its implicit-GEMM compute copies
         self.bias = nn.Parameter(torch.empty(out_channels)) if bias else None
         self.reset_parameters()
 

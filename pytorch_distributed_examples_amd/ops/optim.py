@@ -3,7 +3,10 @@
 GPU parameters are updated by ONE ``multi_tensor_optim`` launch per param group (csrc/kernels/optim.hip)
 whose hyper-parameters and step counter live in device memory, so the update is hipGraph-capturable
 and an LR change between replays (Horovod-elastic ``on_state_reset``, horovod_mnist_elastic.py:80-82)
-is honoured.  CPU parameters use the same math in plain torch (the reference's CPU configuration).
+is honoured.  The same launch refreshes the bf16 compute copies of the weights it updates (linear and
+1x1-conv weights, whose compute layout is a plain cast), so those layers never re-derive them per step
+(:func:`.functional.maintain_compute_copies`).  CPU parameters use the same math in plain torch (the
+reference's CPU configuration).
 
 The per-parameter state uses torch's key names (``step``, ``exp_avg``, ``exp_avg_sq``,
 ``momentum_buffer``) so ``state_dict()`` round-trips with ``torch.optim`` and with the elastic
@@ -63,8 +66,11 @@ class _FusedBase(torch.optim.Optimizer):
             s0 = self.state[params[0]].get("step") if params else None
             st["step"][0].fill_(int(s0) if s0 is not None else 0)
             grads_c = [g if g.is_contiguous() else g.contiguous() for g in grads]
-            table, total = C.optim_table([p.data for p in params], grads_c, m, v, [])
-            st.update(sig=sig, table=table, total=total, n=len(params), grads_keep=grads_c)
+            copies = [OF.maintain_compute_copies(p) or {} for p in params]
+            none = torch.empty(0, device=params[0].device)
+            bf = [c.get("bf16", none) for c in copies]
+            table, chunks, nchunks = C.optim_table([p.data for p in params], grads_c, m, v, bf)
+            st.update(sig=sig, table=table, chunks=chunks, nchunks=nchunks, grads_keep=grads_c)
         b1, b2 = group["betas"]
         hp_key = (group["lr"], b1, b2, group["eps"], group["weight_decay"], group["momentum"], group["grad_scale"])
         if st["hp_key"] != hp_key:
@@ -86,7 +92,7 @@ class _FusedBase(torch.optim.Optimizer):
             if params[0].is_cuda:
                 C = C or _native.C()
                 st = self._group_dev(gi, group, params)
-                C.optim_step(st["table"], st["n"], st["total"], _MODES[self.KIND], st["hp"], st["step"])
+                C.optim_step(st["table"], st["chunks"], st["nchunks"], _MODES[self.KIND], st["hp"], st["step"])
                 for p in params:
                     self.state[p]["step"] = self.state[p].get("step", 0) + 1
             else:
