@@ -5,7 +5,10 @@
 //
 // Why: the network is 21,840 parameters and ~1 MFLOP/image forward; at the reference batch (1024 per
 // worker) the layer-by-layer path is ~40 kernels of a few microseconds each, every one far below the
-// chip's roofline.  Here ONE workgroup (8 wave64s) trains NI=4 images end to end:
+// chip's roofline.  Here ONE workgroup (16 wave64s, one per CU: the LDS image is
+// ~122 KB) trains NI=4 images end to end.  Every phase is a short dependent chain (LDS gathers feeding a
+// few MFMAs, L2 weight loads feeding a dot product), so the kernel is latency-bound: 16 waves (4 per
+// SIMD, <= 128 VGPRs) hide twice the latency of 8 and cut each phase's per-wave trip count in half:
 //   * the five convolution GEMMs -- conv1 fwd, conv2 fwd, conv2 dgrad, conv2 wgrad, conv1 wgrad -- run
 //     on the matrix cores (v_mfma_f32_16x16x32_bf16, fp32 accumulate) as implicit GEMMs whose operand
 //     fragments are gathered straight from the LDS-resident bf16 activations (im2col never exists);
@@ -22,6 +25,8 @@
 // Dropout masks come from a counter-based hash keyed by a device-resident counter that k_cnn_reduce
 // advances, so hipGraph replays draw fresh masks.  Precision: bf16 MFMA operands (images, conv weights,
 // conv activations and their gradients), fp32 accumulation, fp32 fc layers / loss / gradients.
+#include <cstddef>
+
 #include "common.cuh"
 #include "pde_kernels.h"
 
@@ -29,14 +34,18 @@ namespace pde {
 
 namespace {
 
-constexpr int T = 512;            // 8 waves
+constexpr int T = 1024;           // 16 waves
 constexpr int NW = T / 64;
 constexpr int NI = 4;             // images per workgroup
 constexpr int C1 = 10, C2 = 20, KS = 5, H0 = 28, O1 = 24, P1 = 12, O2 = 8, P2 = 4, F1 = 50, F2 = 10;
 constexpr int NX = H0 * H0, NC1 = P1 * P1, NR1 = C1 * NC1, NC2 = P2 * P2, NIN = C2 * NC2;  // 784 144 1440 16 320
 constexpr int W1N = C1 * KS * KS, W2N = C2 * C1 * KS * KS, FC1N = F1 * NIN, FC2N = F2 * F1;
-constexpr int K2 = C1 * KS * KS;       // 250: conv2 fwd reduction (ci,ky,kx)
-constexpr int KS2 = 8;                 // conv2 fwd k-steps of 32
+constexpr int K2 = C1 * KS * KS;       // 250: conv2 reduction (ci,ky,kx) in the weight's own order
+// conv2 fwd: K ordered (tap, ci) with ci padded to 16 over a channel-last copy of r1, so a lane's 8
+// k-values are ONE 16-byte LDS read: k = 32 ks + 8 lg + j -> tap 2 ks + lg/2, ci 8 (lg & 1) + j
+constexpr int C1P = 16;
+constexpr int KS2 = (KS * KS * C1P + 31) / 32;  // 13 k-steps (the last one half padding)
+constexpr int KSW2 = NI * 8 * 8 / 32;           // 8 conv2-wgrad k-steps: K = (image, y, x)
 // conv2 dgrad: one k-step per filter tap (ky,kx) with K = co (20 -> 32): the gradient is kept channel-last
 // (d2n[pos][co]) so a lane's 8 k-values are one 16-byte LDS read
 constexpr int KSD = KS * KS;           // 25 k-steps
@@ -66,6 +75,7 @@ struct CnnSmem {
   alignas(16) u16x8 w2f[KS2][2][64];   // conv2 fwd B fragments [kstep][ntile][lane]; P9 partials later
   alignas(16) u16x8 w2d[KSD][64];      // conv2 dgrad B fragments [tap][lane]: B[k=co][n=ci]
   alignas(16) u16x8 w1f[64];           // conv1 B fragment
+  alignas(16) uint16_t r1n[NI][NC1][C1P];  // relu(maxpool(conv1)) channel-last, ci padded with zeros
   // conv2-output gradient (non-zero only at the argmax taps), twice: channel-last for the dgrad A
   // fragments (co padded to 32 with zeros) and as 8x8 planes for the wgrad A fragments
   alignas(16) uint16_t d2n[NI][O2 * O2][C2P];
@@ -86,7 +96,12 @@ struct CnnSmem {
   unsigned char a2[NI][NIN];
 };
 static_assert(sizeof(CnnSmem) <= 160 * 1024, "LDS budget");
-static_assert(sizeof(u16x8) * KS2 * 2 * 64 >= NW * 2 * 64 * sizeof(f32x4), "P9 partials alias w2f");
+static_assert(sizeof(u16x8) * (KS2 * 2 * 64 + KSD * 64) >= NW * 2 * 64 * sizeof(f32x4),
+              "P9 partials alias w2f + w2d");
+static_assert(offsetof(CnnSmem, w2d) == offsetof(CnnSmem, w2f) + sizeof(u16x8) * KS2 * 2 * 64, "w2f, w2d adjacent");
+constexpr int NT2 = 16 / NW;  // conv2-wgrad N-tiles (250 -> 16 x 16) per wave
+constexpr int FC1R = (F1 + NW - 1) / NW;  // fc1 rows per wave
+static_assert(NT2 * NW == 16, "conv2 wgrad tiling");
 
 __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ images, const int64_t* __restrict__ tgt,
                                                  int B, const float* __restrict__ params,
@@ -119,11 +134,12 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   }
   for (int e = t; e < KS2 * 2 * 64 + KSD * 64 + 64; e += T) {
     u16x8 f;
-    if (e < KS2 * 2 * 64) {  // conv2 fwd: B[k=(ci,ky,kx)][n=co] = w2[co][k]
+    if (e < KS2 * 2 * 64) {  // conv2 fwd: B[k=(tap, ci16)][n=co] = w2[co][ci][tap]
       const int ks = e >> 7, nt = (e >> 6) & 1, l = e & 63;
-      const int co = nt * 16 + (l & 15), k0 = ks * 32 + (l >> 4) * 8;
+      const int co = nt * 16 + (l & 15), g = l >> 4, tap = 2 * ks + (g >> 1), c8 = (g & 1) * 8;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = (co < C2 && k0 + j < K2) ? f2bf(gW2[co * K2 + k0 + j]) : 0;
+      for (int j = 0; j < 8; ++j)
+        f[j] = (co < C2 && tap < KS * KS && c8 + j < C1) ? f2bf(gW2[co * K2 + (c8 + j) * KS * KS + tap]) : 0;
       S.w2f[ks][nt][l] = f;
     } else if (e < KS2 * 2 * 64 + KSD * 64) {  // conv2 dgrad, tap (ky,kx): B[k=co][n=ci] = w2[co][ci][ky][kx]
       const int e2 = e - KS2 * 2 * 64, tap = e2 >> 6, l = e2 & 63;
@@ -162,6 +178,14 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     S.valid[t - 384] = (n0 + t - 384) < B ? 1.f : 0.f;
   }
   float* slab = slabs + static_cast<long>(blockIdx.x) * NPARAM;
+  // fc1 rows of this wave (P3), fetched from L2 now so the loads complete under the conv phases
+  float fw[FC1R][NIN / 64];
+#pragma unroll
+  for (int i = 0; i < FC1R; ++i) {
+    const int j = wid + i * NW;
+#pragma unroll
+    for (int k = 0; k < NIN / 64; ++k) fw[i][k] = j < F1 ? gFC1W[j * NIN + lane + k * 64] : 0.f;
+  }
   __syncthreads();
   PDE_STAMP(1);
 
@@ -183,84 +207,72 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
 #pragma unroll
       for (int j = 0; j < 8; ++j) a[j] = koff[j] >= 0 ? xb[koff[j]] : 0;
       const f32x4 acc = mfma(a, bw, f32x4{0.f, 0.f, 0.f, 0.f});
-      const int co = lr;
-      if (co < C1) {  // rows (lg*4 + r) = taps r of cell c0 + lg
+      const int co = lr;  // rows (lg*4 + r) = taps r of cell c0 + lg
+      if (co < C1) {
         int am = 0;
         float m = acc[0];
         if (acc[1] > m) { m = acc[1]; am = 1; }
         if (acc[2] > m) { m = acc[2]; am = 2; }
         if (acc[3] > m) { m = acc[3]; am = 3; }
         const int q = co * NC1 + c0 + lg;
-        S.r1[im][q] = f2bf(fmaxf(m + S.b1[co], 0.f));
+        const uint16_t r = f2bf(fmaxf(m + S.b1[co], 0.f));
+        S.r1[im][q] = r;
+        S.r1n[im][c0 + lg][co] = r;
         S.a1[im][q] = static_cast<unsigned char>(am);
+      } else {
+        S.r1n[im][c0 + lg][co] = 0;  // ci padding 10..15
       }
     }
   }
   __syncthreads();
   PDE_STAMP(2);
 
-  // ---- P2: conv2 (MFMA, M = (cell, tap) 64/image, K = (ci,ky,kx) 250 -> 256, N = co 20 -> 32)
-  //          + dropout2d + maxpool2 + relu.  Wave w: image w/2, M-tiles 2(w&1), 2(w&1)+1, both N-tiles.
-  {
-    const int im = wid >> 1;
+  // ---- P2: conv2 (MFMA, M = (cell, tap) 64/image = 4 M-tiles, K = (ci,ky,kx) 250 -> 256, N = co 20 -> 32)
+  //          + dropout2d + maxpool2 + relu.  One (image, M-tile) per wave iteration, both N-tiles.
+  for (int mtile = wid; mtile < NI * 4; mtile += NW) {
+    const int im = mtile >> 2, mt = mtile & 3;
     const int tap = lr & 3, dy = tap >> 1, dx = tap & 1;
-    int rb[2];
+    const int cell = mt * 4 + (lr >> 2), py = cell >> 2, px = cell & 3;
+    const int rb = (2 * py + dy) * P1 + 2 * px + dx;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    const uint16_t* r1n = &S.r1n[im][0][(lg & 1) * 8];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int cell = ((wid & 1) * 2 + u) * 4 + (lr >> 2), py = cell >> 2, px = cell & 3;
-      rb[u] = (2 * py + dy) * P1 + 2 * px + dx;
-    }
-    f32x4 acc[2][2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) acc[u][0] = acc[u][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const uint16_t* r1 = S.r1[im];
     for (int ks = 0; ks < KS2; ++ks) {
-      int koff[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = ks * 32 + lg * 8 + j, ci = k / 25, r = k - ci * 25, ky = r / 5, kx = r - ky * 5;
-        koff[j] = k < K2 ? ci * NC1 + ky * P1 + kx : -1;
-      }
-      const u16x8 b0 = S.w2f[ks][0][lane], b1 = S.w2f[ks][1][lane];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        u16x8 a;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = koff[j] >= 0 ? r1[rb[u] + koff[j]] : 0;
-        acc[u][0] = mfma(a, b0, acc[u][0]);
-        acc[u][1] = mfma(a, b1, acc[u][1]);
-      }
+      const int tp = 2 * ks + (lg >> 1), ky = tp / KS, kx = tp - ky * KS;
+      const u16x8 a = tp < KS * KS ? *reinterpret_cast<const u16x8*>(r1n + (rb + ky * P1 + kx) * C1P)
+                                   : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      acc0 = mfma(a, S.w2f[ks][0][lane], acc0);
+      acc1 = mfma(a, S.w2f[ks][1][lane], acc1);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int co = nt * 16 + lr;
-        if (co < C2) {
-          const f32x4 v = acc[u][nt];
-          int am = 0;
-          float m = v[0];
-          if (v[1] > m) { m = v[1]; am = 1; }
-          if (v[2] > m) { m = v[2]; am = 2; }
-          if (v[3] > m) { m = v[3]; am = 3; }
-          const int q = co * NC2 + ((wid & 1) * 2 + u) * 4 + lg;
-          S.r2[im][q] = fmaxf((m + S.b2[co]) * S.mc2[im][co], 0.f);
-          S.a2[im][q] = static_cast<unsigned char>(am);
-        }
+    for (int nt = 0; nt < 2; ++nt) {
+      const int co = nt * 16 + lr;
+      if (co < C2) {
+        const f32x4 v = nt == 0 ? acc0 : acc1;
+        int am = 0;
+        float m = v[0];
+        if (v[1] > m) { m = v[1]; am = 1; }
+        if (v[2] > m) { m = v[2]; am = 2; }
+        if (v[3] > m) { m = v[3]; am = 3; }
+        const int q = co * NC2 + mt * 4 + lg;
+        S.r2[im][q] = fmaxf((m + S.b2[co]) * S.mc2[im][co], 0.f);
+        S.a2[im][q] = static_cast<unsigned char>(am);
       }
     }
   }
   __syncthreads();
   PDE_STAMP(3);
 
-  // ---- P3: fc1 + relu + dropout: wave per output row, lanes over inputs, 4 images per load ------
-  for (int j = wid; j < F1; j += NW) {
-    const float* wr = gFC1W + j * NIN;
+  // ---- P3: fc1 + relu + dropout: wave per output row (weights prefetched in P0), lanes over inputs ---
+#pragma unroll
+  for (int ii = 0; ii < FC1R; ++ii) {
+    const int j = wid + ii * NW;
+    if (j >= F1) break;
     float s[NI] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < NIN / 64; ++k) {
       const int i = lane + k * 64;
-      const float w = wr[i];
+      const float w = fw[ii][k];
 #pragma unroll
       for (int im = 0; im < NI; ++im) s[im] += w * S.r2[im][i];
     }
@@ -379,21 +391,21 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   PDE_STAMP(8);
 
   // ---- P7a: conv2 wgrad (MFMA): dW2[co][(ci,ky,kx)] = sum_(im,y,x) d2[co][y][x] * r1[ci][y+ky][x+kx].
-  // M = co (2 tiles), N = 250 -> 16 tiles (2 per wave), K = (im, y, x) 256 = 8 k-steps.  An A fragment
+  // M = co (2 tiles), N = 250 -> 16 tiles (NT2 per wave), K = (im, y, x) 256 = 8 k-steps.  An A fragment
   // is one 16-byte row of the d2 plane.
   {
-    int nb[2];
-    bool nv[2];
+    int nb[NT2];
+    bool nv[NT2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int kidx = (wid * 2 + u) * 16 + lr, ci = kidx / 25, r = kidx - ci * 25, ky = r / 5, kx = r - ky * 5;
+    for (int u = 0; u < NT2; ++u) {
+      const int kidx = (wid * NT2 + u) * 16 + lr, ci = kidx / 25, r = kidx - ci * 25, ky = r / 5, kx = r - ky * 5;
       nv[u] = kidx < K2;
       nb[u] = nv[u] ? ci * NC1 + ky * P1 + kx : 0;
     }
-    f32x4 acc[2][2];
+    f32x4 acc[2][NT2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) acc[0][u] = acc[1][u] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int ks = 0; ks < KS2; ++ks) {
+    for (int u = 0; u < NT2; ++u) acc[0][u] = acc[1][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < KSW2; ++ks) {
       const int im = ks >> 1, y = (ks & 1) * 4 + lg;  // this lane's 8 positions: row y, x = 0..7
       u16x8 a[2];
 #pragma unroll
@@ -402,7 +414,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
         a[mt] = co < C2 ? *reinterpret_cast<const u16x8*>(&S.d2[im][co][y * O2]) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < NT2; ++u) {
         const uint16_t* src = S.r1[im] + nb[u] + y * P1;
         u16x8 b;
 #pragma unroll
@@ -414,8 +426,8 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int kidx = (wid * 2 + u) * 16 + lr;
+      for (int u = 0; u < NT2; ++u) {
+        const int kidx = (wid * NT2 + u) * 16 + lr;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int co = mt * 16 + lg * 4 + r;
@@ -430,7 +442,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   // one k-step per filter tap with K = co: a lane's A fragment is the 16-byte co-block (lane >> 4) of
   // channel-last position (Y-ky, X-kx), or zero when that position is outside the 8x8 conv2 output.
   {
-    constexpr int MAXT = (NI * MTD + NW - 1) / NW;  // 5
+    constexpr int MAXT = (NI * MTD + NW - 1) / NW;  // 3
     f32x4 acc[MAXT];
     int ty[MAXT], tx[MAXT], tb[MAXT];
 #pragma unroll
@@ -475,7 +487,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
 
   // ---- P9: conv1 wgrad (MFMA): dW1[co][(ky,kx)] = sum_(im,y,x) dconv1[co][y][x] * x[y+ky][x+kx], with
   // dconv1 = dr1 at the argmax tap of each pooling window.  M = co, N = 25 -> 2 tiles, K = (im,y,x)
-  // 2304 = 72 k-steps split over the 8 waves (9 each); partials combined in LDS in a fixed order.
+  // 2304 = 72 k-steps split over the waves; partials combined in LDS in a fixed order.
   {
     int nb[2];
     bool nv[2];
@@ -512,7 +524,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
         acc[u] = mfma(a, b, acc[u]);
       }
     }
-    __syncthreads();  // w2f is dead after P2: reuse it for the per-wave partials
+    __syncthreads();  // w2f / w2d are dead after P7b: reuse them for the per-wave partials
     f32x4* part = reinterpret_cast<f32x4*>(&S.w2f[0][0][0]);
     part[(wid * 2 + 0) * 64 + lane] = acc[0];
     part[(wid * 2 + 1) * 64 + lane] = acc[1];
