@@ -620,7 +620,9 @@ Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, 
   Tensor slabs = at::empty({static_cast<long>(n) * pde::cnn_num_params()}, fo);
   Tensor part = at::empty({n}, fo);
   Tensor loss = at::empty({}, fo);
+  Tensor frag = at::empty({static_cast<long>(pde::cnn_frag_bytes())}, fo.dtype(at::kByte));
   check(pde::cnn_train_fused(images.data_ptr<float>(), tgt.data_ptr<int64_t>(), B, params.data_ptr<float>(),
+                             frag.data_ptr(),
                              reinterpret_cast<unsigned long long*>(rng.data_ptr()), static_cast<float>(p_drop2),
                              static_cast<float>(p_drop1), training ? 1 : 0, slabs.data_ptr<float>(),
                              part.data_ptr<float>(), n, loss.data_ptr<float>(), grads.data_ptr<float>(), cf32(gscale),

@@ -155,10 +155,11 @@ hipError_t embbag_fwd(const float* w, const int64_t* idx, const int64_t* off, in
 int cnn_num_params();
 size_t cnn_smem_bytes();
 int cnn_images_per_workgroup();
-// Two launches: the fused training kernel (per-workgroup gradient slabs + loss partials), then the
-// deterministic slab reduction into `grads` (16-B aligned; (+)= gscale * sum) which also finalises the
-// loss and advances the dropout counter.
-hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, const float* params,
+// Three launches: the weight-fragment prep, the fused training kernel (per-workgroup gradient slabs +
+// loss partials), then the deterministic slab reduction into `grads` (16-B aligned; (+)= gscale * sum)
+// which also finalises the loss and advances the dropout counter.
+size_t cnn_frag_bytes();  // workspace for the per-step bf16 weight-fragment image (16-B aligned)
+hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, const float* params, void* frag,
                            unsigned long long* rng, float p_drop2, float p_drop1, int training, float* slabs,
                            float* loss_part, int nwg, float* loss, float* grads, const float* gscale,
                            int accumulate, hipStream_t s, unsigned long long* stamps = nullptr);

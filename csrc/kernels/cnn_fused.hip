@@ -49,7 +49,7 @@ constexpr int KSW2 = NI * 8 * 8 / 32;           // 8 conv2-wgrad k-steps: K = (i
 // conv2 dgrad: one k-step per filter tap (ky,kx) with K = co (20 -> 32): the gradient is kept channel-last
 // (d2n[pos][co]) so a lane's 8 k-values are one 16-byte LDS read
 constexpr int KSD = KS * KS;           // 25 k-steps
-constexpr int C2P = 32;
+constexpr int C2P = 40;  // 80-byte rows: a ds_read_b128 lane octet spans all 64 banks (conflict-free)
 constexpr int MT1 = O1 * O1 / 16;      // 36 conv1 M-tiles per image (4 cells x 4 taps each)
 constexpr int MTD = NC1 * 1 / 16;      // 9 conv2-dgrad M-tiles per image (144 r1 positions)
 constexpr int KSW1 = O1 * O1 / 32;     // 18 conv1-wgrad k-steps per image
@@ -100,11 +100,21 @@ static_assert(sizeof(u16x8) * (KS2 * 2 * 64 + KSD * 64) >= NW * 2 * 64 * sizeof(
               "P9 partials alias w2f + w2d");
 static_assert(offsetof(CnnSmem, w2d) == offsetof(CnnSmem, w2f) + sizeof(u16x8) * KS2 * 2 * 64, "w2f, w2d adjacent");
 constexpr int NT2 = 16 / NW;  // conv2-wgrad N-tiles (250 -> 16 x 16) per wave
-constexpr int FC1R = (F1 + NW - 1) / NW;  // fc1 rows per wave
+constexpr int NFRAG = KS2 * 2 * 64 + KSD * 64 + 64;  // bf16 MFMA weight fragments (w2f, w2d, w1f)
+static_assert(offsetof(CnnSmem, w1f) == offsetof(CnnSmem, w2d) + sizeof(u16x8) * KSD * 64, "w2d, w1f adjacent");
+// fc1 forward: thread = (output j, 32-wide input chunk) over all images; fc1 backward dp2: thread = (input i,
+// chunk of fc1 outputs).  Their partial sums live in the w2f region (dead after P2), combined in a fixed
+// order (deterministic).
+constexpr int FC1_KC = NIN / 32;        // 10 input chunks
+constexpr int DP2_JC = 3;               // fc1-output chunks for dp2 (17, 17, 16 rows)
+static_assert(F1 * FC1_KC <= T && NIN * DP2_JC <= T, "fc1 work split");
+static_assert(sizeof(float) * NI * F1 * FC1_KC <= sizeof(u16x8) * KS2 * 2 * 64, "fc1 partials alias w2f");
+static_assert(sizeof(float) * NI * NIN * DP2_JC <= sizeof(u16x8) * KS2 * 2 * 64, "dp2 partials alias w2f");
 static_assert(NT2 * NW == 16, "conv2 wgrad tiling");
 
 __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ images, const int64_t* __restrict__ tgt,
                                                  int B, const float* __restrict__ params,
+                                                 const u16x8* __restrict__ frag,
                                                  const unsigned long long* __restrict__ rng, float p_drop2,
                                                  float p_drop1, int training, float* __restrict__ slabs,
                                                  float* __restrict__ loss_part,
@@ -132,32 +142,13 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     uint16_t* dst = &S.x[im][off];
     dst[0] = f2bf(v[0]); dst[1] = f2bf(v[1]); dst[2] = f2bf(v[2]); dst[3] = f2bf(v[3]);
   }
-  for (int e = t; e < KS2 * 2 * 64 + KSD * 64 + 64; e += T) {
-    u16x8 f;
-    if (e < KS2 * 2 * 64) {  // conv2 fwd: B[k=(tap, ci16)][n=co] = w2[co][ci][tap]
-      const int ks = e >> 7, nt = (e >> 6) & 1, l = e & 63;
-      const int co = nt * 16 + (l & 15), g = l >> 4, tap = 2 * ks + (g >> 1), c8 = (g & 1) * 8;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        f[j] = (co < C2 && tap < KS * KS && c8 + j < C1) ? f2bf(gW2[co * K2 + (c8 + j) * KS * KS + tap]) : 0;
-      S.w2f[ks][nt][l] = f;
-    } else if (e < KS2 * 2 * 64 + KSD * 64) {  // conv2 dgrad, tap (ky,kx): B[k=co][n=ci] = w2[co][ci][ky][kx]
-      const int e2 = e - KS2 * 2 * 64, tap = e2 >> 6, l = e2 & 63;
-      const int ci = l & 15, c0 = (l >> 4) * 8;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        f[j] = (ci < C1 && c0 + j < C2) ? f2bf(gW2[(c0 + j) * K2 + ci * 25 + tap]) : 0;
-      S.w2d[tap][l] = f;
-    } else {  // conv1: B[k=(ky,kx)][n=co] = w1[co][k]
-      const int l = e - KS2 * 2 * 64 - KSD * 64;
-      const int co = l & 15, k0 = (l >> 4) * 8;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = (co < C1 && k0 + j < 25) ? f2bf(gW1[co * 25 + k0 + j]) : 0;
-      S.w1f[l] = f;
-    }
+  {  // weight fragments, pre-laid-out in bf16 MFMA order by k_cnn_prep: straight 16-byte copies
+    u16x8* dst = &S.w2f[0][0][0];
+    for (int e = t; e < NFRAG; e += T) dst[e] = frag[e];
   }
-  for (int i = t; i < NI * O2 * O2 * (C2P - 16) / 8; i += T) {  // zero the co padding (20..31) once
-    const int pos = i >> 1, h = i & 1;
+  constexpr int PADG = (C2P - 16) / 8;  // co padding groups of 8 (co 16..C2P-1; 16..19 rewritten per step)
+  for (int i = t; i < NI * O2 * O2 * PADG; i += T) {
+    const int pos = i / PADG, h = i - pos * PADG;
     *reinterpret_cast<u16x8*>(&S.d2n[0][pos][16 + 8 * h]) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
   for (int i = t; i < C1; i += T) S.b1[i] = params[O_B1 + i];
@@ -178,14 +169,6 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     S.valid[t - 384] = (n0 + t - 384) < B ? 1.f : 0.f;
   }
   float* slab = slabs + static_cast<long>(blockIdx.x) * NPARAM;
-  // fc1 rows of this wave (P3), fetched from L2 now so the loads complete under the conv phases
-  float fw[FC1R][NIN / 64];
-#pragma unroll
-  for (int i = 0; i < FC1R; ++i) {
-    const int j = wid + i * NW;
-#pragma unroll
-    for (int k = 0; k < NIN / 64; ++k) fw[i][k] = j < F1 ? gFC1W[j * NIN + lane + k * 64] : 0.f;
-  }
   __syncthreads();
   PDE_STAMP(1);
 
@@ -263,25 +246,36 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   __syncthreads();
   PDE_STAMP(3);
 
-  // ---- P3: fc1 + relu + dropout: wave per output row (weights prefetched in P0), lanes over inputs ---
+  // ---- P3: fc1 + relu + dropout.  Thread (j, kc): the 32 weights W[j][32kc..] (8 x 16-B L2 loads, all
+  // in flight together) against the 4 images' inputs; partials [kc][im][j] summed in kc order. -------
+  {
+    float* part = reinterpret_cast<float*>(&S.w2f[0][0][0]);
+    if (t < F1 * FC1_KC) {
+      const int j = t / FC1_KC, kc = t - j * FC1_KC;
+      const f32x4* w4 = reinterpret_cast<const f32x4*>(gFC1W + j * NIN + kc * 32);
+      f32x4 w[8];
 #pragma unroll
-  for (int ii = 0; ii < FC1R; ++ii) {
-    const int j = wid + ii * NW;
-    if (j >= F1) break;
-    float s[NI] = {0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < 8; ++q) w[q] = w4[q];
+      float s4[NI] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < NIN / 64; ++k) {
-      const int i = lane + k * 64;
-      const float w = fw[ii][k];
+      for (int q = 0; q < 8; ++q)
 #pragma unroll
-      for (int im = 0; im < NI; ++im) s[im] += w * S.r2[im][i];
+        for (int im = 0; im < NI; ++im) {
+          const f32x4 x = *reinterpret_cast<const f32x4*>(&S.r2[im][kc * 32 + q * 4]);
+          s4[im] += w[q][0] * x[0] + w[q][1] * x[1] + w[q][2] * x[2] + w[q][3] * x[3];
+        }
+#pragma unroll
+      for (int im = 0; im < NI; ++im) part[(kc * NI + im) * F1 + j] = s4[im];
     }
+    __syncthreads();
+    if (t < NI * F1) {
+      const int im = t / F1, j = t - im * F1;
+      float s1 = gFC1B[j];
 #pragma unroll
-    for (int im = 0; im < NI; ++im) s[im] = wave_sum(s[im]);
-    if (lane < NI) {
-      const float h = fmaxf(s[lane] + gFC1B[j], 0.f);
-      S.h1[lane][j] = h;
-      S.h1d[lane][j] = h * S.m1[lane][j];
+      for (int kc = 0; kc < FC1_KC; ++kc) s1 += part[(kc * NI + im) * F1 + j];
+      const float h = fmaxf(s1, 0.f);
+      S.h1[im][j] = h;
+      S.h1d[im][j] = h * S.m1[im][j];
     }
   }
   __syncthreads();
@@ -352,17 +346,30 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     for (int im = 0; im < NI; ++im) s += S.dh[im][t];
     slab[O_FC1B + t] = s;
   }
-  if (t < NIN) {
-    const int i = t, co = i / NC2;
-    float s[NI] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 10
-    for (int j = 0; j < F1; ++j) {
-      const float w = gFC1W[j * NIN + i];
+  float* dpart = reinterpret_cast<float*>(&S.w2f[0][0][0]);  // [jc][im][i]
+  if (t < NIN * DP2_JC) {  // thread (i, jc): sum over fc1 outputs j in chunk jc (column loads coalesced)
+    const int jc = t / NIN, i = t - jc * NIN;
+    constexpr int JPER = (F1 + DP2_JC - 1) / DP2_JC;
+    const int j0 = jc * JPER, j1 = min(F1, j0 + JPER);
+    float w[JPER];
 #pragma unroll
-      for (int im = 0; im < NI; ++im) s[im] += w * S.dh[im][j];
-    }
+    for (int u = 0; u < JPER; ++u) w[u] = j0 + u < j1 ? gFC1W[(j0 + u) * NIN + i] : 0.f;
+    float s4[NI] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int im = 0; im < NI; ++im) S.dp2[im][i] = (S.r2[im][i] > 0.f) ? s[im] * S.mc2[im][co] : 0.f;
+    for (int u = 0; u < JPER; ++u)
+      if (j0 + u < j1)
+#pragma unroll
+        for (int im = 0; im < NI; ++im) s4[im] += w[u] * S.dh[im][j0 + u];
+#pragma unroll
+    for (int im = 0; im < NI; ++im) dpart[(jc * NI + im) * NIN + i] = s4[im];
+  }
+  __syncthreads();
+  for (int it = t; it < NI * NIN; it += T) {
+    const int im = it / NIN, i = it - im * NIN, co = i / NC2;
+    float s1 = 0.f;
+#pragma unroll
+    for (int jc = 0; jc < DP2_JC; ++jc) s1 += dpart[(jc * NI + im) * NIN + i];
+    S.dp2[im][i] = (S.r2[im][i] > 0.f) ? s1 * S.mc2[im][co] : 0.f;
   }
   __syncthreads();
   // scatter dp2 to the argmax taps (both layouts; every tap of every window is written); conv2 bias
@@ -553,6 +560,34 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   }
 }
 
+// The conv weights in bf16 MFMA B-fragment order (conv2 fwd [ks][ntile][lane], conv2 dgrad [tap][lane],
+// conv1 [lane]), written once per step so every training workgroup loads them with 16-byte copies.
+__global__ __launch_bounds__(256) void k_cnn_prep(const float* __restrict__ params, u16x8* __restrict__ frag) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= NFRAG) return;
+  const float* gW1 = params + O_W1;
+  const float* gW2 = params + O_W2;
+  u16x8 f;
+  if (e < KS2 * 2 * 64) {  // conv2 fwd: B[k=(tap, ci16)][n=co] = w2[co][ci][tap]
+    const int ks = e >> 7, nt = (e >> 6) & 1, l = e & 63;
+    const int co = nt * 16 + (l & 15), g = l >> 4, tap = 2 * ks + (g >> 1), c8 = (g & 1) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      f[j] = (co < C2 && tap < KS * KS && c8 + j < C1) ? f2bf(gW2[co * K2 + (c8 + j) * KS * KS + tap]) : 0;
+  } else if (e < KS2 * 2 * 64 + KSD * 64) {  // conv2 dgrad, tap (ky,kx): B[k=co][n=ci] = w2[co][ci][ky][kx]
+    const int e2 = e - KS2 * 2 * 64, tap = e2 >> 6, l = e2 & 63;
+    const int ci = l & 15, c0 = (l >> 4) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (ci < C1 && c0 + j < C2) ? f2bf(gW2[(c0 + j) * K2 + ci * 25 + tap]) : 0;
+  } else {  // conv1: B[k=(ky,kx)][n=co] = w1[co][k]
+    const int l = e - KS2 * 2 * 64 - KSD * 64;
+    const int co = l & 15, k0 = (l >> 4) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (co < C1 && k0 + j < 25) ? f2bf(gW1[co * 25 + k0 + j]) : 0;
+  }
+  frag[e] = f;
+}
+
 // grads (+)= gscale * sum_wg slabs[wg] in a fixed order (deterministic).  Block = 8 waves over 16 float4
 // columns (64 parameters); lane = column + 16 x slab-lane, so one load instruction of a wave reads 4 slabs
 // x 256 B and each thread keeps nwg/32 independent float4 loads in flight.  Block 0 also reduces the
@@ -605,10 +640,11 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
 }  // namespace
 
 int cnn_num_params() { return NPARAM; }
+size_t cnn_frag_bytes() { return sizeof(u16x8) * NFRAG; }
 size_t cnn_smem_bytes() { return sizeof(CnnSmem); }
 int cnn_images_per_workgroup() { return NI; }
 
-hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, const float* params,
+hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, const float* params, void* frag,
                            unsigned long long* rng, float p_drop2, float p_drop1, int training, float* slabs,
                            float* loss_part, int nwg, float* loss, float* grads, const float* gscale,
                            int accumulate, hipStream_t s, unsigned long long* stamps) {
@@ -620,8 +656,10 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, const
                               static_cast<int>(sm));
     attr = true;
   }
-  hipLaunchKernelGGL(k_cnn_train, dim3(nwg), dim3(T), sm, s, images, tgt, B, params, rng, p_drop2, p_drop1, training,
-                     slabs, loss_part, stamps);
+  if (reinterpret_cast<uintptr_t>(frag) & 15) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_cnn_prep, dim3(ceil_div(NFRAG, 256)), dim3(256), 0, s, params, static_cast<u16x8*>(frag));
+  hipLaunchKernelGGL(k_cnn_train, dim3(nwg), dim3(T), sm, s, images, tgt, B, params,
+                     static_cast<const u16x8*>(frag), rng, p_drop2, p_drop1, training, slabs, loss_part, stamps);
   hipLaunchKernelGGL(k_cnn_reduce, dim3(ceil_div(NPARAM4, RED_COLS)), dim3(RED_T), 0, s, slabs, nwg, gscale, grads,
                      accumulate, loss_part, B, loss, rng);
   return hipGetLastError();
