@@ -90,6 +90,8 @@ def main():
     ap.add_argument("--model", default="cnn", choices=["cnn", "mlp", "resnet50"])
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch")
     ap.add_argument("--no-graph", action="store_true", help="run the step eagerly (no hipGraph capture)")
+    ap.add_argument("--graph-steps", type=int, default=10,
+                    help="consecutive training steps recorded into one hipGraph (each reads its own batch)")
     ap.add_argument("--generic", action="store_true", help="CNN: layer-by-layer kernels instead of the fused step")
     ap.add_argument("--device", default="auto", choices=["auto", "cpu"], help="cpu: contract/plumbing check only")
     args = ap.parse_args()
@@ -132,28 +134,45 @@ def main():
         return loss
 
     graphed = None
+    group = None
     if use_graph:
-        from pytorch_distributed_examples_amd.utils.graph import CapturedStep
+        from pytorch_distributed_examples_amd.utils.graph import CapturedStep, CapturedSteps
 
         try:
             graphed = CapturedStep(train_step, batch_fn(0), warmup=3).capture()
+            if args.graph_steps > 1:
+                # G complete steps per replay, step j of the group reading dataset batch j in place:
+                # one host launch per G steps instead of one per step (the MNIST step is ~50 us of GPU work)
+                group = CapturedSteps(train_step, [batch_fn(j) for j in range(args.graph_steps)],
+                                      warmup=1).capture()
         except Exception as exc:  # capture unsupported (e.g. collective in capture): run eagerly
             if ctx.rank == 0:
                 print(f"[bench] hipGraph capture failed, running eagerly: {exc}", file=sys.stderr)
             use_graph = False
+            graphed = group = None
             ddp = DistributedDataParallel(model, overlap=True)
 
     def step(i):
         x, y = batch_fn(i)
         return graphed(x, y) if graphed is not None else train_step(x, y)
 
-    for i in range(args.warmup):
-        step(i)
+    def run(first, n):
+        """n full training steps starting at step index ``first``; returns the last loss."""
+        loss = None
+        i = 0
+        while group is not None and n - i >= group.steps:
+            loss = group.replay()
+            i += group.steps
+        while i < n:
+            loss = step(first + i)
+            i += 1
+        return loss
+
+    run(0, args.warmup)
     pdist.barrier(ctx)
     sync()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = step(args.warmup + i)
+    loss = run(args.warmup, args.steps)
     pdist.barrier(ctx)
     sync()
     dt = time.perf_counter() - t0
@@ -181,7 +200,8 @@ def main():
                        "global_batch": batch * ctx.world_size, "seq_len": None,
                        "image": "1x28x28" if args.model != "resnet50" else "3x128x128",
                        "parallelism": f"dp{ctx.world_size}", "final_loss": round(final_loss, 4),
-                       "hipgraph": graphed is not None, "fused_step": fused is not None},
+                       "hipgraph": graphed is not None, "fused_step": fused is not None,
+                       "steps_per_graph": group.steps if group is not None else (1 if graphed is not None else 0)},
         }), flush=True)
     pdist.shutdown()
 
