@@ -111,7 +111,8 @@ def main():
     fused = None
     if args.model == "cnn" and not args.generic and ctx.device.type == "cuda":
         # whole-network fused kernel (csrc/kernels/cnn_fused.hip): gradients land directly in the
-        # DDP flat buffer (forward layout), then one RCCL all-reduce and one fused SGD launch.
+        # DDP flat buffer (forward layout), then one RCCL all-reduce and one fused SGD launch that also
+        # refreshes the kernel's bf16 weight fragments (world 1: the SGD runs inside the slab reduction).
         from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
 
         fused = FusedCNN(model)
@@ -121,9 +122,11 @@ def main():
 
     def train_step(x, y):
         if fused is not None:
+            if ctx.world_size == 1:  # SGD + weight-fragment refresh inside the slab reduction
+                return fused.forward_backward(x, y, grad_out=ddp.flat_grad, sgd=opt)
             loss = fused.forward_backward(x, y, grad_out=ddp.flat_grad)
             ddp.sync_gradients()
-            opt.step()
+            fused.sgd_step(opt, ddp.flat_grad)  # SGD + weight-fragment refresh, one launch
             return loss
         ddp.zero_grad()
         loss = loss_fn(ddp(x), y)

@@ -602,7 +602,8 @@ Tensor embbag_bwd(const Tensor& dy, const Tensor& idx, const Tensor& off, int64_
 // the slabs into a gradient buffer with cnn_reduce (possibly the DDP flat gradient).
 Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, Tensor& rng, double p_drop2,
                  double p_drop1, bool training, Tensor& grads, bool accumulate, const optional<Tensor>& gscale,
-                 const optional<Tensor>& stamps) {
+                 const optional<Tensor>& stamps, const optional<Tensor>& frag_buf, bool prep,
+                 const optional<Tensor>& sgd_hp) {
   CHECK_IN(images); CHECK_IN(tgt); CHECK_IN(params); CHECK_IN(rng); CHECK_IN(grads);
   CHECK_F32(images); CHECK_F32(params); CHECK_F32(grads);
   TORCH_CHECK(params.numel() == pde::cnn_num_params(), "cnn_train: params must be the flat Net parameters");
@@ -620,7 +621,20 @@ Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, 
   Tensor slabs = at::empty({static_cast<long>(n) * pde::cnn_num_params()}, fo);
   Tensor part = at::empty({n}, fo);
   Tensor loss = at::empty({}, fo);
-  Tensor frag = at::empty({static_cast<long>(pde::cnn_frag_bytes())}, fo.dtype(at::kByte));
+  Tensor frag;
+  if (frag_buf.has_value() && frag_buf->defined()) {
+    frag = *frag_buf;
+    CHECK_IN(frag);
+    TORCH_CHECK(frag.nbytes() >= pde::cnn_frag_bytes() && reinterpret_cast<uintptr_t>(frag.data_ptr()) % 16 == 0,
+                "cnn_train: frag must be a 16-B aligned buffer of cnn_frag_bytes()");
+  } else {
+    TORCH_CHECK(prep, "cnn_train: prep=False needs a persistent frag buffer");
+    frag = at::empty({static_cast<long>(pde::cnn_frag_bytes())}, fo.dtype(at::kByte));
+  }
+  if (sgd_hp.has_value() && sgd_hp->defined()) {
+    CHECK_IN(*sgd_hp); CHECK_F32(*sgd_hp);
+    TORCH_CHECK(sgd_hp->numel() >= pde::HP_COUNT, "cnn_train: sgd_hp must hold the optimiser hyper-parameters");
+  }
   check(pde::cnn_train_fused(images.data_ptr<float>(), tgt.data_ptr<int64_t>(), B, params.data_ptr<float>(),
                              frag.data_ptr(),
                              reinterpret_cast<unsigned long long*>(rng.data_ptr()), static_cast<float>(p_drop2),
@@ -629,15 +643,33 @@ Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, 
                              accumulate ? 1 : 0, cur_stream(),
                              stamps.has_value() && stamps->defined()
                                  ? reinterpret_cast<unsigned long long*>(stamps->data_ptr())
-                                 : nullptr),
+                                 : nullptr,
+                             prep ? 1 : 0, sgd_hp.has_value() && sgd_hp->defined() ? sgd_hp->data_ptr<float>() : nullptr),
         "cnn_train");
   return loss;
+}
+
+// Plain SGD on the flat CNN parameters + fragment-image refresh (after the gradient all-reduce).
+void cnn_sgd(Tensor& params, const Tensor& grads, const Tensor& hp, Tensor& frag) {
+  CHECK_IN(params); CHECK_IN(grads); CHECK_IN(hp); CHECK_IN(frag);
+  CHECK_F32(params); CHECK_F32(grads); CHECK_F32(hp);
+  TORCH_CHECK(params.numel() == pde::cnn_num_params() && grads.numel() == pde::cnn_num_params(), "cnn_sgd: sizes");
+  TORCH_CHECK(hp.numel() >= pde::HP_COUNT, "cnn_sgd: hp");
+  TORCH_CHECK(frag.nbytes() >= pde::cnn_frag_bytes(), "cnn_sgd: frag size");
+  check(pde::cnn_sgd_fused(params.data_ptr<float>(), grads.data_ptr<float>(), hp.data_ptr<float>(), frag.data_ptr(),
+                           cur_stream()),
+        "cnn_sgd");
 }
 
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
-  m.def("cnn_train", &cnn_train);
+  m.def("cnn_train", &cnn_train, py::arg("images"), py::arg("tgt"), py::arg("params"), py::arg("rng"),
+        py::arg("p_drop2"), py::arg("p_drop1"), py::arg("training"), py::arg("grads"), py::arg("accumulate"),
+        py::arg("gscale") = py::none(), py::arg("stamps") = py::none(), py::arg("frag") = py::none(),
+        py::arg("prep") = true, py::arg("sgd_hp") = py::none());
+  m.def("cnn_sgd", &cnn_sgd);
+  m.def("cnn_frag_bytes", &pde::cnn_frag_bytes);
   m.def("cnn_num_params", &pde::cnn_num_params);
   m.def("cnn_smem_bytes", &pde::cnn_smem_bytes);
   m.doc() = "MI355X (gfx950) native kernels for pytorch_distributed_examples_amd";

@@ -159,10 +159,17 @@ int cnn_images_per_workgroup();
 // loss partials), then the deterministic slab reduction into `grads` (16-B aligned; (+)= gscale * sum)
 // which also finalises the loss and advances the dropout counter.
 size_t cnn_frag_bytes();  // workspace for the per-step bf16 weight-fragment image (16-B aligned)
-hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, const float* params, void* frag,
+// prep = 0 skips the fragment prep (the image is already current: the previous step's fused SGD wrote it).
+// sgd_hp != nullptr fuses plain SGD (lr = sgd_hp[HP_LR], grad scale sgd_hp[HP_GRAD_SCALE]) and the
+// fragment refresh into the slab reduction (single process: no all-reduce between reduce and update).
+hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float* params, void* frag,
                            unsigned long long* rng, float p_drop2, float p_drop1, int training, float* slabs,
                            float* loss_part, int nwg, float* loss, float* grads, const float* gscale,
-                           int accumulate, hipStream_t s, unsigned long long* stamps = nullptr);
+                           int accumulate, hipStream_t s, unsigned long long* stamps = nullptr, int prep = 1,
+                           const float* sgd_hp = nullptr);
+// params -= lr * gscale * grads (plain SGD) and the matching fragment-image refresh, one launch (used
+// after the gradient all-reduce when world > 1).
+hipError_t cnn_sgd_fused(float* params, const float* grads, const float* hp, void* frag, hipStream_t s);
 
 hipError_t embbag_bwd(const float* dy, const int64_t* idx, const int64_t* off, int B, long L, int D, float* dw,
                       hipStream_t s);

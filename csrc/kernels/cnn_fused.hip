@@ -588,6 +588,37 @@ __global__ __launch_bounds__(256) void k_cnn_prep(const float* __restrict__ para
   frag[e] = f;
 }
 
+// Single-element inverse of k_cnn_prep: parameter p (flat index) with new value w -> its bf16 slot(s) in
+// the fragment image (conv2 weights appear twice: forward and dgrad layouts; conv1 once; everything else
+// is not staged).  Padding slots are never touched, so the image stays valid once k_cnn_prep wrote it.
+__device__ __forceinline__ void write_frag(uint16_t* __restrict__ f, int p, float w) {
+  const uint16_t b = f2bf(w);
+  if (p >= O_W2 && p < O_W2 + W2N) {
+    const int q = p - O_W2, co = q / K2, r = q - co * K2, ci = r / (KS * KS), tap = r - ci * (KS * KS);
+    const int g = ((tap & 1) << 1) | (ci >> 3);
+    const int e = ((tap >> 1) << 7) | ((co >> 4) << 6) | (g << 4) | (co & 15);  // conv2 fwd [ks][ntile][lane]
+    f[e * 8 + (ci & 7)] = b;
+    const int e2 = KS2 * 2 * 64 + tap * 64 + (((co >> 3) << 4) | ci);          // conv2 dgrad [tap][lane]
+    f[e2 * 8 + (co & 7)] = b;
+  } else if (p >= O_W1 && p < O_W1 + W1N) {
+    const int co = p / (KS * KS), k = p - co * (KS * KS);
+    const int e = KS2 * 2 * 64 + KSD * 64 + (((k >> 3) << 4) | co);             // conv1 [lane]
+    f[e * 8 + (k & 7)] = b;
+  }
+}
+
+// Plain SGD (torch.optim.SGD, momentum 0, no weight decay: mnist_horovod.py:50) on the flat parameters
+// with the fragment image refreshed in the same pass, so the next step needs no k_cnn_prep.
+// hp: the fused optimiser's device hyper-parameters (HP_LR, HP_GRAD_SCALE).
+__global__ __launch_bounds__(256) void k_cnn_sgd(float* __restrict__ params, const float* __restrict__ grads,
+                                                 const float* __restrict__ hp, uint16_t* __restrict__ frag) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= NPARAM) return;
+  const float w = params[p] - hp[HP_LR] * (grads[p] * hp[HP_GRAD_SCALE]);
+  params[p] = w;
+  write_frag(frag, p, w);
+}
+
 // grads (+)= gscale * sum_wg slabs[wg] in a fixed order (deterministic).  Block = 8 waves over 16 float4
 // columns (64 parameters); lane = column + 16 x slab-lane, so one load instruction of a wave reads 4 slabs
 // x 256 B and each thread keeps nwg/32 independent float4 loads in flight.  Block 0 also reduces the
@@ -599,7 +630,9 @@ static_assert(NPARAM % 4 == 0, "float4 columns");
 __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ slabs, int nwg,
                                                       const float* __restrict__ gscale, float* __restrict__ grads,
                                                       int accumulate, const float* __restrict__ loss_part, int B,
-                                                      float* __restrict__ loss, unsigned long long* __restrict__ rng) {
+                                                      float* __restrict__ loss, unsigned long long* __restrict__ rng,
+                                                      float* __restrict__ params, const float* __restrict__ hp,
+                                                      uint16_t* __restrict__ frag) {
   __shared__ f32x4 part[RED_LANES][RED_COLS];
   const int col = threadIdx.x % RED_COLS, sl = threadIdx.x / RED_COLS;
   const int c4 = blockIdx.x * RED_COLS + col;
@@ -623,7 +656,19 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
     for (int k = 1; k < RED_LANES; ++k) v += part[k][col];
     v *= gscale ? gscale[0] : 1.f;
     f32x4* g4 = reinterpret_cast<f32x4*>(grads) + c4;
-    *g4 = accumulate ? *g4 + v : v;
+    if (accumulate) v += *g4;
+    *g4 = v;
+    if (hp) {  // single-process step: SGD + fragment refresh right here (no all-reduce in between)
+      const float lr = hp[HP_LR], gs = hp[HP_GRAD_SCALE];
+      f32x4* p4 = reinterpret_cast<f32x4*>(params) + c4;
+      f32x4 w = *p4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        w[j] -= lr * (v[j] * gs);
+        write_frag(frag, c4 * 4 + j, w[j]);
+      }
+      *p4 = w;
+    }
   }
   if (blockIdx.x == 0 && threadIdx.x >= RED_T - 64) {  // last wave: loss
     const int lane = threadIdx.x - (RED_T - 64);
@@ -644,10 +689,11 @@ size_t cnn_frag_bytes() { return sizeof(u16x8) * NFRAG; }
 size_t cnn_smem_bytes() { return sizeof(CnnSmem); }
 int cnn_images_per_workgroup() { return NI; }
 
-hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, const float* params, void* frag,
+hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float* params, void* frag,
                            unsigned long long* rng, float p_drop2, float p_drop1, int training, float* slabs,
                            float* loss_part, int nwg, float* loss, float* grads, const float* gscale,
-                           int accumulate, hipStream_t s, unsigned long long* stamps) {
+                           int accumulate, hipStream_t s, unsigned long long* stamps, int prep,
+                           const float* sgd_hp) {
   if (reinterpret_cast<uintptr_t>(grads) & 15) return hipErrorInvalidValue;  // float4 gradient stores
   const size_t sm = sizeof(CnnSmem);
   static bool attr = false;
@@ -657,11 +703,19 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, const
     attr = true;
   }
   if (reinterpret_cast<uintptr_t>(frag) & 15) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_cnn_prep, dim3(ceil_div(NFRAG, 256)), dim3(256), 0, s, params, static_cast<u16x8*>(frag));
+  if (prep)
+    hipLaunchKernelGGL(k_cnn_prep, dim3(ceil_div(NFRAG, 256)), dim3(256), 0, s, params, static_cast<u16x8*>(frag));
   hipLaunchKernelGGL(k_cnn_train, dim3(nwg), dim3(T), sm, s, images, tgt, B, params,
                      static_cast<const u16x8*>(frag), rng, p_drop2, p_drop1, training, slabs, loss_part, stamps);
   hipLaunchKernelGGL(k_cnn_reduce, dim3(ceil_div(NPARAM4, RED_COLS)), dim3(RED_T), 0, s, slabs, nwg, gscale, grads,
-                     accumulate, loss_part, B, loss, rng);
+                     accumulate, loss_part, B, loss, rng, params, sgd_hp, static_cast<uint16_t*>(frag));
+  return hipGetLastError();
+}
+
+hipError_t cnn_sgd_fused(float* params, const float* grads, const float* hp, void* frag, hipStream_t s) {
+  if (reinterpret_cast<uintptr_t>(frag) & 15) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_cnn_sgd, dim3(ceil_div(NPARAM, 256)), dim3(256), 0, s, params, grads, hp,
+                     static_cast<uint16_t*>(frag));
   return hipGetLastError();
 }
 

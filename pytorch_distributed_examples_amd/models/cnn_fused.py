@@ -13,6 +13,20 @@ straight into a flat gradient buffer -- the DDP wrapper's, when it is laid out i
 
 Semantics match ``nll_loss(net(x), y)`` + ``backward()`` in train mode, including Dropout2d(p=0.5) on
 conv2's output and dropout(p=0.5) on fc1's (fresh masks every call; dropout disabled in eval mode).
+
+Fused optimiser step (plain SGD, the reference's ``optim.SGD(lr=0.01)``, mnist_horovod.py:50): the training
+kernel reads the conv weights as a bf16 MFMA fragment image that a prep kernel writes from the fp32
+parameters.  With ``sgd=opt`` (single process) the slab reduction also applies the SGD update and rewrites
+the fragment slots of the weights it updates; with :meth:`sgd_step` (after the gradient all-reduce) one
+kernel does the same.  Either way the next step skips the prep launch::
+
+    loss = fused.forward_backward(x, y, grad_out=buf, sgd=opt)          # world 1: 2 launches per step
+    loss = fused.forward_backward(x, y, grad_out=ddp.flat_grad)         # world > 1
+    ddp.sync_gradients(); fused.sgd_step(opt, ddp.flat_grad)            #   3 launches + all-reduce
+
+The fragment image is re-derived (prep launch) whenever anything other than these fused updates may have
+written the weights: any other optimiser step bumps the weight generation (:func:`.functional.
+bump_weight_generation`); direct writes (``load_state_dict``, broadcasts) must call :meth:`invalidate`.
 """
 from __future__ import annotations
 
@@ -39,9 +53,40 @@ class FusedCNN:
                 p.data = flat[off:off + k].view_as(p)
                 off += k
         self.flat = flat
+        OF.bump_weight_generation()  # parameter storage moved: drop cached compute copies
         self.own_grad = None
         self.workgroups = workgroups
         self.stamps = None  # diagnostic: int64 [nwg, 16] tensor of per-phase wall-clock stamps
+        self.frag = torch.empty(C.cnn_frag_bytes(), dtype=torch.uint8, device=dev)
+        self._frag_gen = None  # weight generation at which the fragment image was last made current
+
+    def invalidate(self):
+        """The fp32 weights were written behind our back: rebuild the fragment image next step."""
+        self._frag_gen = None
+
+    @staticmethod
+    def _sgd_hp(opt):
+        """Device hyper-parameters of a FusedSGD that the fused update can apply (plain SGD only)."""
+        from ..ops.optim import FusedSGD
+
+        assert isinstance(opt, FusedSGD) and len(opt.param_groups) == 1, "fused update needs one FusedSGD group"
+        group = opt.param_groups[0]
+        assert group["momentum"] == 0.0 and group["weight_decay"] == 0.0, "fused update is plain SGD"
+        params = [p for p in group["params"] if p.grad is not None]
+        return opt._group_dev(0, group, params)["hp"], params
+
+    def _after_update(self, opt, params):
+        for p in params:
+            opt.state[p]["step"] = opt.state[p].get("step", 0) + 1
+        OF.bump_weight_generation()
+        self._frag_gen = OF.weight_generation()
+
+    @torch.no_grad()
+    def sgd_step(self, opt, grads: torch.Tensor):
+        """``opt.step()`` for the flat parameters (plain SGD) fused with the fragment-image refresh."""
+        hp, params = self._sgd_hp(opt)
+        _native.C().cnn_sgd(self.flat, grads, hp, self.frag)
+        self._after_update(opt, params)
 
     def _nwg(self, B: int) -> int:
         if self.workgroups:
@@ -61,15 +106,24 @@ class FusedCNN:
         return self.own_grad
 
     def forward_backward(self, x: torch.Tensor, y: torch.Tensor, grad_out: torch.Tensor | None = None,
-                         accumulate: bool = False, p_drop2: float = 0.5, p_drop1: float = 0.5) -> torch.Tensor:
-        """Loss (device scalar) of the batch; gradients of the mean loss written to ``grad_out``."""
+                         accumulate: bool = False, p_drop2: float = 0.5, p_drop1: float = 0.5,
+                         sgd=None) -> torch.Tensor:
+        """Loss (device scalar) of the batch; gradients of the mean loss written to ``grad_out``.
+
+        ``sgd``: a plain FusedSGD over these parameters -- also take the optimiser step (single process)."""
         C = _native.C()
         if grad_out is None:
             grad_out = self.grad_buffer()
         x = x.float().contiguous()
         y = y.long().contiguous()
         training = self.net.training
+        prep = self._frag_gen is None or self._frag_gen != OF.weight_generation()
+        hp, params = self._sgd_hp(sgd) if sgd is not None else (None, None)
         loss = C.cnn_train(x, y, self.flat, OF._rng_counter(x.device), p_drop2, p_drop1, training, grad_out,
-                           accumulate, None, self.stamps)
-        OF.bump_weight_generation()
+                           accumulate, None, self.stamps, self.frag, prep, hp)
+        if sgd is not None:
+            self._after_update(sgd, params)
+        else:
+            # the weights did not change: the image stays current until someone writes them
+            self._frag_gen = OF.weight_generation()
         return loss

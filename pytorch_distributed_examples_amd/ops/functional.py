@@ -36,6 +36,11 @@ def bump_weight_generation() -> None:
     _GEN[0] += 1
 
 
+def weight_generation() -> int:
+    """Current weight generation (changes whenever an optimiser step may have written the weights)."""
+    return _GEN[0]
+
+
 class recompute_weight_copies:
     """Context manager: never reuse cached copies (used while capturing a hipGraph so the layout
     kernels become part of the graph and see every replay's updated weights)."""

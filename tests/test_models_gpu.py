@@ -174,6 +174,49 @@ def test_fused_cnn_matches_reference(gpu):
     assert all(v < 3e-2 for v in errs.values()), errs
 
 
+@pytest.mark.parametrize("mode", ["reduce", "sgd_step"])
+def test_fused_cnn_sgd_matches_optimizer(gpu, mode):
+    """The fused SGD update (in the slab reduction, or the post-all-reduce cnn_sgd kernel) refreshes the
+    bf16 fragment image in place of the prep kernel: weights and losses must track the generic path
+    (prep every step + FusedSGD) bit for bit over several steps (eval mode: no dropout)."""
+    from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
+    from pytorch_distributed_examples_amd.ops.optim import FusedSGD
+
+    torch.manual_seed(0)
+    m_ref = Net().to(gpu).eval()
+    m_fus = copy.deepcopy(m_ref)
+    f_ref, f_fus = FusedCNN(m_ref), FusedCNN(m_fus)
+    g_ref, g_fus = f_ref.grad_buffer(), f_fus.grad_buffer()
+    o_ref, o_fus = FusedSGD(m_ref.parameters(), lr=0.05), FusedSGD(m_fus.parameters(), lr=0.05)
+    x = torch.randn(6, 256, 1, 28, 28, device=gpu)
+    y = torch.randint(0, 10, (6, 256), device=gpu)
+    # the reference runs first: its optimiser steps bump the (global) weight generation, which would
+    # otherwise make the fused model re-prep and hide the fragment-refresh path under test
+    l_ref = []
+    for i in range(6):
+        l_ref.append(f_ref.forward_backward(x[i], y[i], grad_out=g_ref).item())
+        o_ref.step()
+    for i in range(6):
+        if mode == "reduce":
+            l_fus = f_fus.forward_backward(x[i], y[i], grad_out=g_fus, sgd=o_fus)
+        else:
+            l_fus = f_fus.forward_backward(x[i], y[i], grad_out=g_fus)
+            f_fus.sgd_step(o_fus, g_fus)
+        assert i == 0 or f_fus._frag_gen is not None
+        assert l_ref[i] == l_fus.item(), (i, l_ref[i], l_fus.item())
+    torch.cuda.synchronize()
+    assert torch.equal(f_ref.flat, f_fus.flat)
+    # an external write must be picked up after invalidate()
+    with torch.no_grad():
+        m_fus.conv1.weight.mul_(0.5)
+        m_ref.conv1.weight.mul_(0.5)
+    f_fus.invalidate()
+    f_ref.invalidate()
+    l_ref = f_ref.forward_backward(x[0], y[0], grad_out=g_ref)
+    l_fus = f_fus.forward_backward(x[0], y[0], grad_out=g_fus)
+    assert l_ref.item() == l_fus.item()
+
+
 def test_fused_cnn_trains_with_dropout(gpu):
     from pytorch_distributed_examples_amd.data.synthetic import SyntheticMNIST
     from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
