@@ -46,7 +46,19 @@ __global__ __launch_bounds__(256) void k_bn_stats(const uint16_t* __restrict__ x
     const bool ok = mp.active && g < mp.G;
     if (ok) {
       load8(x + g * 8, piv);
-      for (int r = r0 + mp.r; r < r1; r += mp.rows_per_iter) {
+      const int st = mp.rows_per_iter;
+      int r = r0 + mp.r;
+      // 4 rows per trip, all loads issued before the math (4 x 16 B in flight per lane)
+      for (; r + 3 * st < r1; r += 4 * st) {
+        u16x8 u[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) u[q] = *reinterpret_cast<const u16x8*>(x + static_cast<long>(r + q * st) * C + g * 8);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { const float d = bf2f(u[q][j]) - piv[j]; s1[j] += d; s2[j] += d * d; }
+      }
+      for (; r < r1; r += st) {
         float v[8];
         load8(x + static_cast<long>(r) * C + g * 8, v);
 #pragma unroll
@@ -152,7 +164,29 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce(const uint16_t* __restric
       float mu[8], is[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) { mu[j] = mean[g * 8 + j]; is[j] = invstd[g * 8 + j]; }
-      for (int r = r0 + mp.r; r < r1; r += mp.rows_per_iter) {
+      const int st = mp.rows_per_iter;
+      int r = r0 + mp.r;
+      // 2 rows per trip with every load (dy, x, y of both rows) issued before the math
+      for (; r + st < r1; r += 2 * st) {
+        u16x8 ud[2], ux[2], uy[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const long off = static_cast<long>(r + q * st) * C + g * 8;
+          ud[q] = *reinterpret_cast<const u16x8*>(dy + off);
+          ux[q] = *reinterpret_cast<const u16x8*>(x + off);
+          if (relu) uy[q] = *reinterpret_cast<const u16x8*>(y + off);
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float d = bf2f(ud[q][j]);
+            if (relu && !(bf2f(uy[q][j]) > 0.f)) d = 0.f;
+            s1[j] += d;
+            s2[j] += d * (bf2f(ux[q][j]) - mu[j]) * is[j];
+          }
+      }
+      for (; r < r1; r += st) {
         const long off = static_cast<long>(r) * C + g * 8;
         float d[8], xv[8];
         load8(dy + off, d);
@@ -421,10 +455,13 @@ __global__ void k_embbag_bwd(const float* __restrict__ dy, const int64_t* __rest
 
 int bn_blocks(int P, int C, int& rows_per_block) {
   const int G = C / 8;
-  const int rpi = 256 / (G < 256 ? G : 256);
-  // aim for ~16 row-iterations per block, at most 512 blocks
-  int nblk = ceil_div(P, rpi * 16);
-  if (nblk > 512) nblk = 512;
+  // ~8 16-byte vectors per thread (enough loads in flight per lane with the unrolled loops), at most
+  // 1024 blocks (4 per CU); the fp32 partials stay <= C/4096 of the activation bytes
+  const long vecs = static_cast<long>(P) * G;
+  long nb = (vecs + 256L * 8 - 1) / (256L * 8);
+  if (nb > 1024) nb = 1024;
+  if (nb > P) nb = P;
+  int nblk = static_cast<int>(nb);
   if (nblk < 1) nblk = 1;
   rows_per_block = ceil_div(P, nblk);
   nblk = ceil_div(P, rows_per_block);
