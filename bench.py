@@ -107,7 +107,15 @@ def main():
     from pytorch_distributed_examples_amd.parallel.ddp import DistributedDataParallel
 
     model, opt, batch_fn, loss_fn = build(args.model, ctx.device, batch)
-    use_graph = not args.no_graph and on_gpu
+    # hipGraph capture needs capturable collectives: RCCL (or none at world 1), not gloo
+    use_graph = not args.no_graph and on_gpu and (ctx.world_size == 1 or ctx.backend == "nccl")
+    # GPU data plane for world > 1: our stream-ordered RCCL communicator (c10d's ProcessGroupNCCL aborts
+    # the process when its work is captured into a hipGraph on ROCm -- parallel/rccl.py)
+    comm = None
+    if on_gpu and ctx.world_size > 1 and ctx.backend == "nccl":
+        from pytorch_distributed_examples_amd.parallel.rccl import StreamComm
+
+        comm = StreamComm(ctx.device)
     fused = None
     if args.model == "cnn" and not args.generic and ctx.device.type == "cuda":
         # whole-network fused kernel (csrc/kernels/cnn_fused.hip): gradients land directly in the
@@ -116,9 +124,9 @@ def main():
         from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
 
         fused = FusedCNN(model)
-        ddp = DistributedDataParallel(model, overlap=False, param_order="forward")
+        ddp = DistributedDataParallel(model, overlap=False, param_order="forward", comm=comm)
     else:
-        ddp = DistributedDataParallel(model, overlap=not use_graph)
+        ddp = DistributedDataParallel(model, overlap=not use_graph, comm=comm)
 
     def train_step(x, y):
         if fused is not None:
@@ -151,9 +159,15 @@ def main():
         except Exception as exc:  # capture unsupported (e.g. collective in capture): run eagerly
             if ctx.rank == 0:
                 print(f"[bench] hipGraph capture failed, running eagerly: {exc}", file=sys.stderr)
+            from pytorch_distributed_examples_amd import _native
+
+            torch.cuda.synchronize()
+            _native.C().clear_last_error()  # the aborted capture leaves a sticky "last error" behind
             use_graph = False
             graphed = group = None
-            ddp = DistributedDataParallel(model, overlap=True)
+            if fused is None:  # the fused path keeps its forward-order, non-overlapped flat buffer
+                ddp.remove_hooks()
+                ddp = DistributedDataParallel(model, overlap=True, comm=comm)
 
     def step(i):
         x, y = batch_fn(i)

@@ -669,6 +669,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gscale") = py::none(), py::arg("stamps") = py::none(), py::arg("frag") = py::none(),
         py::arg("prep") = true, py::arg("sgd_hp") = py::none());
   m.def("cnn_sgd", &cnn_sgd);
+  m.def("clear_last_error", []() { return static_cast<int>(hipGetLastError()); },
+        "Read and reset the HIP last-error state (after an aborted stream capture).");
   m.def("cnn_frag_bytes", &pde::cnn_frag_bytes);
   m.def("cnn_num_params", &pde::cnn_num_params);
   m.def("cnn_smem_bytes", &pde::cnn_smem_bytes);

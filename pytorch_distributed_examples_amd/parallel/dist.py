@@ -55,7 +55,9 @@ def init_distributed(backend: str | None = None, device: str | None = None, time
     local_rank = env_int("LOCAL_RANK", rank)
     use_gpu = (device != "cpu") and torch.cuda.is_available()
     if backend is None:
-        backend = "nccl" if use_gpu else "gloo"
+        # PDE_BACKEND=gloo rehearses a multi-rank GPU job on ONE GPU (ranks share the card; gloo moves
+        # the CUDA tensors through the host) -- RCCL refuses two ranks on one device
+        backend = os.environ.get("PDE_BACKEND") or ("nccl" if use_gpu else "gloo")
     if use_gpu:
         ndev = torch.cuda.device_count()
         dev = torch.device("cuda", local_rank % max(1, ndev))

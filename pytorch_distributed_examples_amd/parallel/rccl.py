@@ -1,0 +1,72 @@
+"""Stream-ordered RCCL communicator for the DDP data plane (capturable into hipGraphs).
+
+c10d's ``ProcessGroupNCCL`` cannot be used inside a hipGraph on this ROCm build: its watchdog thread
+queries the work's completion event while the capturing stream is live and the process aborts with
+``hipErrorStreamCaptureUnsupported`` (measured on MI355X, ``tests/test_comm_gpu.py``).  The gradient
+all-reduce of a captured training step therefore goes through our own RCCL communicator
+(``csrc/comm/comm_manager.cpp``): ``ncclAllReduce`` enqueued on the caller's CURRENT stream, ordered
+after the kernels that produced the gradients and before the optimizer kernel -- no host
+synchronisation, no watchdog, nothing that breaks stream capture.  c10d (any backend) stays the control
+plane: it exchanges the RCCL unique id through the default store.
+
+Implements the communicator plug-in of :class:`.ddp.DistributedDataParallel` (``comm=``): ``size``,
+``rank``, ``supports_avg``, ``allreduce_async(t, avg) -> work`` and ``broadcast_(t, src)``.
+"""
+from __future__ import annotations
+
+import itertools
+
+import torch
+import torch.distributed as dist
+
+from .. import _native
+
+_SEQ = itertools.count()
+_RED_SUM, _RED_AVG = 0, 1
+
+
+class _StreamWork:
+    """The collective is stream-ordered: waiting is a no-op for stream consumers."""
+
+    def wait(self):
+        return True
+
+    def is_completed(self):
+        return True
+
+
+class StreamComm:
+    def __init__(self, device: torch.device, group=None):
+        assert device.type == "cuda", "StreamComm is the GPU data plane"
+        self.rank = dist.get_rank(group)
+        self.size = dist.get_world_size(group)
+        self.device = device
+        self.supports_avg = True
+        C = _native.comm()
+        # unique id through the default store; the key is unique per communicator and per group
+        store = dist.distributed_c10d._get_default_store()
+        seq = next(_SEQ)
+        ranks = dist.get_process_group_ranks(group) if group is not None else list(range(self.size))
+        key = f"pde_stream_comm/{seq}/{'-'.join(map(str, ranks))}"
+        if self.rank == 0:
+            store.set(key, C.rccl_unique_id())
+        uid = store.get(key)
+        self.rccl = C.RcclComm()
+        self.rccl.init(uid, self.rank, self.size, device.index, True)
+
+    def allreduce_async(self, t: torch.Tensor, avg: bool = False):
+        self.rccl.allreduce_(t, _RED_AVG if avg else _RED_SUM)
+        return _StreamWork()
+
+    def allreduce_(self, t: torch.Tensor, avg: bool = False) -> torch.Tensor:
+        self.rccl.allreduce_(t, _RED_AVG if avg else _RED_SUM)
+        return t
+
+    def broadcast_(self, t: torch.Tensor, src: int) -> torch.Tensor:
+        self.rccl.broadcast_(t, src)
+        return t
+
+    def destroy(self):
+        if self.rccl is not None:
+            self.rccl.destroy()
+            self.rccl = None
