@@ -36,6 +36,13 @@ namespace {
 
 constexpr int kThreads = 256;
 
+// LDS image swizzle: the 16-byte K-chunk c of image row r lives at chunk c ^ ((r >> 4) & 3).  The XOR is
+// constant over every 16-row MFMA fragment, so the fragment reads (16 rows x one chunk per 16-lane group)
+// keep the conflict-free 80-byte-pitch pattern, while the transposing scatter of the row-contiguous
+// loader (8 rows 8 apart per 16-B global load; 8 rows x 80 B = 0 mod 128 B) spreads its 2-byte writes
+// over 4x more banks.  Needs BK / 8 == 4 chunks per row.
+__device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row >> 4) & 3); }
+
 __device__ __forceinline__ u16x8 zero8() { return u16x8{0, 0, 0, 0, 0, 0, 0, 0}; }
 
 // Dense K-contiguous / row-contiguous element loads (operand kind 0).
@@ -172,7 +179,7 @@ struct KcLoader {
       if (v < kVecs) {
         const int row = v / (BK / 8);
         const int kv = v - row * (BK / 8);
-        *reinterpret_cast<u16x8*>(lds + row * (BK + 8) + kv * 8) = regs[i];
+        *reinterpret_cast<u16x8*>(lds + row * (BK + 8) + swz_chunk(row, kv) * 8) = regs[i];
       }
     }
   }
@@ -261,7 +268,10 @@ struct RcLoader {
         const int kk = v / (BROWS / 8);
         const int rv = v - kk * (BROWS / 8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) lds[(rv * 8 + j) * (BK + 8) + kk] = regs[i][j];
+        for (int j = 0; j < 8; ++j) {
+          const int row = rv * 8 + j;
+          lds[row * (BK + 8) + swz_chunk(row, kk >> 3) * 8 + (kk & 7)] = regs[i][j];
+        }
       }
     }
   }
@@ -299,6 +309,7 @@ template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles_m, int tiles_n,
                                                         int k_per_split, int a_vec, int b_vec) {
   static_assert(WM * WN == 4, "4 waves per block");
+  static_assert(BK == 32, "swz_chunk assumes 4 16-byte K-chunks per LDS row");
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int LDS_A = BM * (BK + 8), LDS_B = BN * (BK + 8);
@@ -366,13 +377,15 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles
     for (int kk = 0; kk < BK / 32; ++kk) {
       bf16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(
-            As + (wm * WTM + i * 16 + (lane & 15)) * (BK + 8) + kk * 32 + (lane >> 4) * 8);
+      for (int i = 0; i < FM; ++i) {
+        const int row = wm * WTM + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + row * (BK + 8) + swz_chunk(row, kk * 4 + (lane >> 4)) * 8);
+      }
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(
-            Bs + (wn * WTN + j * 16 + (lane & 15)) * (BK + 8) + kk * 32 + (lane >> 4) * 8);
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * WTN + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + row * (BK + 8) + swz_chunk(row, kk * 4 + (lane >> 4)) * 8);
+      }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
