@@ -94,10 +94,14 @@ def test_conv_fwd_bwd(gpu, cfg):
         assert xn.grad[..., ci:].abs().max().item() == 0.0
 
 
-@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
-def test_batchnorm(gpu, relu, res):
+# shapes: one 64-channel slice; C < 64 (partial slice, groups not dividing 256); C % 64 != 0 (ragged
+# last slice, several slices); many rows (256 row chunks per slice -> widest last-block combine)
+@pytest.mark.parametrize("relu,res,n,c,h", [(False, False, 8, 64, 16), (True, False, 8, 64, 16),
+                                            (True, True, 8, 64, 16), (True, False, 4, 24, 10),
+                                            (False, True, 2, 200, 9), (True, True, 32, 64, 64),
+                                            (False, False, 2, 2048, 4)])
+def test_batchnorm(gpu, relu, res, n, c, h):
     torch.manual_seed(2)
-    n, c, h = 8, 64, 16
     x = torch.randn(n, c, h, h, device=gpu) * 3 + 1
     gamma = (torch.rand(c, device=gpu) + 0.5).requires_grad_()
     beta = torch.randn(c, device=gpu).requires_grad_()
@@ -126,6 +130,13 @@ def test_batchnorm(gpu, relu, res):
     assert rel_err(beta.grad, b2.grad) < 2e-2
     if res:
         assert rel_err(rn.grad.permute(0, 3, 1, 2), rr.grad) < 2e-2
+    # the slice tickets are returned to 0 by each launch's last block: a second call is identical
+    gamma.grad = None
+    xn.grad = None
+    y2 = OF.batch_norm(xn, gamma, beta, rm, rv, True, 0.1, 1e-5, rn, relu)
+    assert torch.equal(y2, y)
+    y2.float().backward(gy.permute(0, 2, 3, 1))
+    assert rel_err(gamma.grad, g2.grad) < 2e-2
 
 
 @pytest.mark.parametrize("k,s,p,relu", [(3, 2, 1, False), (2, 2, 0, True)])
