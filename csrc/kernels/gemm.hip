@@ -25,6 +25,7 @@
 //     huge reduction (N*H*W) still fill 256 CUs.
 //   * Epilogue options: bias, ReLU, ReLU-mask (backward), fp32 / bf16 output, accumulate, and an OIHW
 //     remap that writes a conv weight gradient straight into the parameter's [Co][Ci][R][S] fp32 grad.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.cuh"
@@ -510,16 +511,44 @@ hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
   return hipGetLastError();
 }
 
+// Tile policy (measured on ResNet-50 128^2 b32 and the 5x1024 MLP, profiles/README.md r1h).  The K loop is
+// bound by global round trips (SQ_WAIT_ANY ~60% of wave cycles at 1 block per CU), so prefer the 64x64
+// tile (more blocks per CU) unless the 128x128 grid already has t128_min tiles.  Split-K until the grid
+// reaches split_target blocks, each split keeping >= split_min_kt K-tiles; outputs of at most
+// small_mn elements (cheap fp32 slabs: the MLP's linears) split further (small_* knobs).
+// PDE_GEMM_* environment variables override the knobs for tuning sweeps (read once).
+struct TilePolicy {
+  long t128_min = 2048, split_target = 512, small_mn = 262144, small_split_target = 1024;
+  int split_min_kt = 8, small_split_min_kt = 4;
+  TilePolicy() {
+    auto env_l = [](const char* n, long& v) { if (const char* e = std::getenv(n)) v = std::atol(e); };
+    auto env_i = [](const char* n, int& v) { if (const char* e = std::getenv(n)) v = std::atoi(e); };
+    env_l("PDE_GEMM_T128_MIN", t128_min);
+    env_l("PDE_GEMM_SPLIT_TARGET", split_target);
+    env_i("PDE_GEMM_SPLIT_MIN_KT", split_min_kt);
+    env_l("PDE_GEMM_SMALL_MN", small_mn);
+    env_l("PDE_GEMM_SMALL_SPLIT_TARGET", small_split_target);
+    env_i("PDE_GEMM_SMALL_SPLIT_MIN_KT", small_split_min_kt);
+  }
+};
+const TilePolicy& tile_policy() {
+  static const TilePolicy p;
+  return p;
+}
+
 template <bool AKC, bool BKC>
 hipError_t dispatch_tiles(const GemmArgs& a, hipStream_t s) {
+  const TilePolicy& tp = tile_policy();
   const long t128 = static_cast<long>(ceil_div(a.M, 128)) * ceil_div(a.N, 128);
   const long t64 = static_cast<long>(ceil_div(a.M, 64)) * ceil_div(a.N, 64);
-  // Split-K only where a workspace was provided and the tile grid cannot fill the chip: aim for ~2
-  // blocks per CU while every split keeps >= 8 K-tiles of work (bounded slab traffic).
+  const bool small = static_cast<long>(a.M) * a.N <= tp.small_mn;
+  const long target = small ? tp.small_split_target : tp.split_target;
+  const int min_kt = small ? tp.small_split_min_kt : tp.split_min_kt;
+  // Split-K only where a workspace was provided (a.splitk slabs: never exceeded).
   auto pick_split = [&](long tiles, int bk) {
     if (a.workspace == nullptr || a.splitk <= 1) return 1;
     int sk = 1;
-    while (sk < a.splitk && tiles * sk < 512 && a.K / (sk * 2) >= 8 * bk) sk *= 2;
+    while (sk * 2 <= a.splitk && tiles * sk < target && a.K / (sk * 2) >= min_kt * bk) sk *= 2;
     return sk;
   };
   if (a.N <= 32) {
@@ -530,7 +559,7 @@ hipError_t dispatch_tiles(const GemmArgs& a, hipStream_t s) {
     const long t = static_cast<long>(ceil_div(a.M, 32)) * ceil_div(a.N, 128);
     return launch_cfg<32, 128, 32, 1, 4, AKC, BKC>(a, s, pick_split(t, 32));
   }
-  if (t128 >= 256) return launch_cfg<128, 128, 32, 2, 2, AKC, BKC>(a, s, pick_split(t128, 32));
+  if (t128 >= tp.t128_min) return launch_cfg<128, 128, 32, 2, 2, AKC, BKC>(a, s, pick_split(t128, 32));
   return launch_cfg<64, 64, 32, 2, 2, AKC, BKC>(a, s, pick_split(t64, 32));
 }
 
