@@ -448,6 +448,42 @@ std::tuple<Tensor, Tensor, int64_t> optim_table(const std::vector<Tensor>& param
   return {dtab, dchunks, static_cast<int64_t>(chunks.size())};
 }
 
+// Device table for conv_layouts_step: weights w[i] [Co,Ci,R,S] fp32 with their bf16 forward ([Cop, R*S*Cp])
+// and dgrad ([Cp, R*S*Cop]) layout tensors.
+Tensor conv_layout_table(const std::vector<Tensor>& ws, const std::vector<Tensor>& fwds,
+                         const std::vector<Tensor>& dgrads, const std::vector<int64_t>& cps,
+                         const std::vector<int64_t>& cops) {
+  const size_t n = ws.size();
+  TORCH_CHECK(n > 0 && fwds.size() == n && dgrads.size() == n && cps.size() == n && cops.size() == n,
+              "conv_layout_table: list sizes");
+  std::vector<pde::ConvLayoutEntry> tab(n);
+  for (size_t i = 0; i < n; ++i) {
+    const Tensor& w = ws[i];
+    CHECK_IN(w); CHECK_F32(w); CHECK_IN(fwds[i]); CHECK_BF16(fwds[i]); CHECK_IN(dgrads[i]); CHECK_BF16(dgrads[i]);
+    TORCH_CHECK(w.dim() == 4, "conv_layout_table: 4-D weight");
+    pde::ConvLayoutEntry e{};
+    e.w = w.data_ptr<float>();
+    e.fwd = u16(fwds[i]);
+    e.dgrad = u16(dgrads[i]);
+    e.Co = w.size(0); e.Ci = w.size(1); e.R = w.size(2); e.S = w.size(3);
+    e.Cp = static_cast<int>(cps[i]); e.Cop = static_cast<int>(cops[i]);
+    TORCH_CHECK(e.Cp >= e.Ci && e.Cop >= e.Co, "conv_layout_table: padding smaller than channels");
+    const long total = static_cast<long>(e.Cop) * e.R * e.S * e.Cp;
+    TORCH_CHECK(fwds[i].numel() == total && dgrads[i].numel() == total, "conv_layout_table: layout sizes");
+    tab[i] = e;
+  }
+  return to_device_bytes(tab.data(), static_cast<long>(n * sizeof(pde::ConvLayoutEntry)), ws[0].options());
+}
+
+// blocks_x: x blocks per entry (size it for the largest weight; smaller entries' extra blocks exit).
+void conv_layouts_step(const Tensor& table, int64_t n, int64_t blocks_x) {
+  CHECK_IN(table);
+  TORCH_CHECK(table.numel() == static_cast<long>(n * sizeof(pde::ConvLayoutEntry)), "conv_layouts_step: table");
+  check(pde::conv_weight_layouts_multi(reinterpret_cast<const pde::ConvLayoutEntry*>(table.data_ptr()),
+                                       static_cast<int>(n), static_cast<int>(blocks_x), cur_stream()),
+        "conv_layouts_step");
+}
+
 void optim_step(const Tensor& table, const Tensor& chunks, int64_t nchunks, int mode, const Tensor& hparams,
                 Tensor& step) {
   CHECK_IN(table); CHECK_IN(chunks); CHECK_IN(hparams); CHECK_IN(step);
@@ -688,6 +724,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cast_bf16_into", &cast_bf16_into);
   m.def("cast_f32", &cast_f32);
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
+  m.def("conv_layout_table", &conv_layout_table, py::arg("ws"), py::arg("fwds"), py::arg("dgrads"),
+        py::arg("cps"), py::arg("cops"));
+  m.def("conv_layouts_step", &conv_layouts_step, py::arg("table"), py::arg("n"), py::arg("blocks_x"));
   m.def("conv_w_fwd", &conv_w_fwd, py::arg("w"), py::arg("Cp"), py::arg("Cop"), py::arg("out") = py::none());
   m.def("conv_w_dgrad", &conv_w_dgrad, py::arg("w"), py::arg("Cip"), py::arg("Cop"), py::arg("out") = py::none());
   m.def("conv_wgrad_oihw", &conv_wgrad_oihw);

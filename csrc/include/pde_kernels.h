@@ -76,6 +76,15 @@ hipError_t conv_weight_fwd_layout(const float* w, uint16_t* out, int Co, int Ci,
 // [Cout, Cin, R, S] fp32 -> [Cip, R, S, Cop] bf16 (dgrad B operand: n = ci, k = (r, s, co), zero padded)
 hipError_t conv_weight_dgrad_layout(const float* w, uint16_t* out, int Co, int Ci, int R, int S, int Cip, int Cop,
                                     hipStream_t s);
+// Both bf16 GEMM layouts of several KxK conv weights in one launch (run after the optimizer update: the
+// optimizer-maintained compute copies of the convs whose layout is not the parameter's own order).
+struct ConvLayoutEntry {
+  const float* w;    // [Co][Ci][R][S] fp32
+  uint16_t* fwd;     // [Cop][R][S][Cp]
+  uint16_t* dgrad;   // [Cp][R][S][Cop]
+  int Co, Ci, R, S, Cp, Cop;
+};
+hipError_t conv_weight_layouts_multi(const ConvLayoutEntry* dev_table, int n, int blocks_x, hipStream_t s);
 // dW gemm output [Cout, R*S*Cp] fp32 -> [Cout, Cin, R, S] fp32 (optionally accumulate)
 hipError_t conv_wgrad_to_oihw(const float* in, float* out, int Co, int Ci, int R, int S, int Cp, int accum,
                               hipStream_t s);

@@ -91,6 +91,53 @@ __global__ void k_conv_w_dgrad(const float* __restrict__ w, uint16_t* __restrict
   }
 }
 
+// Multi-tensor form of k_conv_w_fwd + k_conv_w_dgrad: blockIdx.y = table entry (block-uniform), the x
+// blocks grid-stride over (co, ci) pairs; each thread walks the pair's R*S taps (one contiguous run of
+// the OIHW source).  The forward pass puts ci on consecutive lanes, the dgrad pass co, so both passes store
+// 2-byte elements that are contiguous across the wave (the second pass re-reads the source from L2).
+// One (co, ci) pair: all RS taps loaded before any store (RS_T = 9: the 3x3 fast path, 0: runtime RS).
+template <int RS_T>
+__device__ __forceinline__ void conv_w_pair(const float* __restrict__ src, uint16_t* __restrict__ dst, long dstride,
+                                            int RS, bool ok) {
+  if constexpr (RS_T > 0) {
+    float v[RS_T];
+#pragma unroll
+    for (int t = 0; t < RS_T; ++t) v[t] = ok ? src[t] : 0.f;
+#pragma unroll
+    for (int t = 0; t < RS_T; ++t) dst[t * dstride] = f2bf(v[t]);
+  } else {
+    for (int t = 0; t < RS; ++t) dst[t * dstride] = ok ? f2bf(src[t]) : uint16_t(0);
+  }
+}
+
+template <int RS_T>
+__device__ __forceinline__ void conv_w_layouts_entry(const ConvLayoutEntry& e) {
+  const int RS = e.R * e.S;
+  const long pairs = static_cast<long>(e.Cop) * e.Cp;
+  const long start = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x;
+  const long stride = static_cast<long>(gridDim.x) * blockDim.x;
+  for (long i = start; i < pairs; i += stride) {  // fwd [co][r][s][ci]: ci fastest
+    const int ci = static_cast<int>(i % e.Cp), co = static_cast<int>(i / e.Cp);
+    const bool ok = ci < e.Ci && co < e.Co;
+    conv_w_pair<RS_T>(e.w + (static_cast<long>(co) * e.Ci + ci) * RS, e.fwd + static_cast<long>(co) * RS * e.Cp + ci,
+                      e.Cp, RS, ok);
+  }
+  for (long i = start; i < pairs; i += stride) {  // dgrad [ci][r][s][co]: co fastest
+    const int co = static_cast<int>(i % e.Cop), ci = static_cast<int>(i / e.Cop);
+    const bool ok = ci < e.Ci && co < e.Co;
+    conv_w_pair<RS_T>(e.w + (static_cast<long>(co) * e.Ci + ci) * RS,
+                      e.dgrad + static_cast<long>(ci) * RS * e.Cop + co, e.Cop, RS, ok);
+  }
+}
+
+__global__ void k_conv_w_layouts_multi(const ConvLayoutEntry* __restrict__ table) {
+  const ConvLayoutEntry e = table[blockIdx.y];
+  if (e.R * e.S == 9)
+    conv_w_layouts_entry<9>(e);
+  else
+    conv_w_layouts_entry<0>(e);
+}
+
 __global__ void k_wgrad_to_oihw(const float* __restrict__ in, float* __restrict__ out, int Co, int Ci,
                                 int R, int S, int Cp, int accum) {
   const long total = static_cast<long>(Co) * Ci * R * S;
@@ -218,6 +265,11 @@ hipError_t conv_weight_dgrad_layout(const float* w, uint16_t* out, int Co, int C
   const long total = static_cast<long>(Cop) * R * S * Cip;
   hipLaunchKernelGGL(k_conv_w_dgrad, dim3(stream_grid(total, 256)), dim3(256), 0, s, w, out, Co, Ci, R, S, Cip,
                      Cop);
+  return hipGetLastError();
+}
+hipError_t conv_weight_layouts_multi(const ConvLayoutEntry* dev_table, int n, int blocks_x, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_conv_w_layouts_multi, dim3(blocks_x < 1 ? 1 : blocks_x, n), dim3(256), 0, s, dev_table);
   return hipGetLastError();
 }
 hipError_t conv_wgrad_to_oihw(const float* in, float* out, int Co, int Ci, int R, int S, int Cp, int accum,

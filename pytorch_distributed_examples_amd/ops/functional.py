@@ -135,30 +135,47 @@ def _grad_sink(p):
 # optimizer-maintained compute copies
 # ---------------------------------------------------------------------------------------------
 def maintain_compute_copies(p: torch.Tensor):
-    """Allocate the bf16 compute copy of a GPU weight that the fused optimizer keeps in sync from now on
-    (it writes it in the same launch as the update, contiguous stores).  Covered: linear weights
-    (``_pde_linear``) and 1x1 conv weights (``_pde_conv``) with channel counts that need no padding --
-    for those the implicit-GEMM forward layout [Co, Ci] IS the OIHW order, and the dgrad GEMM reads the
-    same copy transposed.  Returns the copy dict (or None).  The copy is tied to the weight's version
-    counter: an in-place write outside the optimizer (load_state_dict, a broadcast, an elastic restore) is
-    detected by :func:`_maintained` and the copy is re-derived in place."""
+    """Allocate the bf16 compute copies of a GPU weight that the fused optimizer keeps in sync from now on.
+    Covered: linear weights (``_pde_linear``) and 1x1 conv weights (``_pde_conv``) with channel counts that
+    need no padding -- for those the implicit-GEMM forward layout [Co, Ci] IS the OIHW order, the optimizer
+    writes the copy in the same launch as the update (contiguous stores) and the dgrad GEMM reads it
+    transposed; and every other conv weight (3x3, 7x7, padded channels): its forward [Cop, R*S*Cp] and
+    dgrad [Cp, R*S*Cop] layouts (key ``"kxk"`` = (Cp, Cop)), refreshed for all such weights by ONE
+    multi-tensor launch after the update (``conv_layouts_step``) instead of two conversion kernels per
+    conv and step.  Returns the copy dict (or None).  The copies are tied to the weight's version counter:
+    an in-place write outside the optimizer (load_state_dict, a broadcast, an elastic restore) is detected
+    by :func:`_maintained` and the copies are re-derived in place."""
     if not p.is_cuda or p.dtype != torch.float32:
         return None
     d = {}
     if getattr(p, "_pde_conv", False) and p.dim() == 4:
         co, ci, r, s = p.shape
-        if r * s != 1 or ci % 8 or co % 8:
-            return None
-        d["bf16"] = torch.empty(p.shape, dtype=torch.bfloat16, device=p.device)
-        d["conv_fwd"] = d["bf16"].view(co, ci)
+        if r * s == 1 and ci % 8 == 0 and co % 8 == 0:
+            d["bf16"] = torch.empty(p.shape, dtype=torch.bfloat16, device=p.device)
+            d["conv_fwd"] = d["bf16"].view(co, ci)
+        else:
+            cp, cop = pad8(ci), pad8(co)
+            d["kxk"] = (cp, cop)
+            d["conv_fwd"] = torch.empty(cop, r * s * cp, dtype=torch.bfloat16, device=p.device)
+            d["conv_dgrad"] = torch.empty(cp, r * s * cop, dtype=torch.bfloat16, device=p.device)
     elif getattr(p, "_pde_linear", False) and p.dim() == 2:
         d["bf16"] = torch.empty(p.shape, dtype=torch.bfloat16, device=p.device)
     else:
         return None
-    _C().cast_bf16_into(p.detach().contiguous(), d["bf16"])
+    _derive_copies(p, d)
     d["version"] = p._version
     p.__dict__["_pde_maint"] = d
     return d
+
+
+def _derive_copies(p: torch.Tensor, d: dict):
+    w = p.detach().contiguous()
+    if "kxk" in d:
+        cp, cop = d["kxk"]
+        _C().conv_w_fwd(w, cp, cop, d["conv_fwd"])
+        _C().conv_w_dgrad(w, cp, cop, d["conv_dgrad"])
+    else:
+        _C().cast_bf16_into(w, d["bf16"])
 
 
 def _maintained(p: torch.Tensor, kind: str):
@@ -167,7 +184,7 @@ def _maintained(p: torch.Tensor, kind: str):
     if d is None or kind not in d:
         return None
     if d["version"] != p._version:  # written outside the optimizer: re-derive in place
-        _C().cast_bf16_into(p.detach().contiguous(), d["bf16"])
+        _derive_copies(p, d)
         d["version"] = p._version
     return d[kind]
 
@@ -265,11 +282,14 @@ class _Conv2dFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             wf = _maintained(weight, "conv_fwd") if (r == 1 and s == 1 and stride == 1 and pad == 0) else None
-            if wf is not None:  # 1x1: the dgrad GEMM reads the forward copy [Co, Ci] transposed
+            if wf is not None and weight.__dict__["_pde_maint"].get("kxk") is None:
+                # 1x1: the dgrad GEMM reads the forward copy [Co, Ci] transposed
                 dx = _C().conv_dgrad(dy, wf, h, w, r, s, stride, pad, None, True)
             else:
-                wd = _cached(weight, ("conv_dgrad", cp, cop),
-                             lambda: _C().conv_w_dgrad(weight.detach().contiguous(), cp, cop))
+                wd = _maintained(weight, "conv_dgrad") if cp == pad8(ci) else None
+                if wd is None:
+                    wd = _cached(weight, ("conv_dgrad", cp, cop),
+                                 lambda: _C().conv_w_dgrad(weight.detach().contiguous(), cp, cop))
                 dx = _C().conv_dgrad(dy, wd, h, w, r, s, stride, pad, None)
         if ctx.needs_input_grad[1]:
             # OIHW epilogue: the GEMM writes the parameter's layout (and adds into .grad when it exists)

@@ -71,6 +71,16 @@ class _FusedBase(torch.optim.Optimizer):
             bf = [c.get("bf16", none) for c in copies]
             table, chunks, nchunks = C.optim_table([p.data for p in params], grads_c, m, v, bf)
             st.update(sig=sig, table=table, chunks=chunks, nchunks=nchunks, grads_keep=grads_c)
+            # KxK conv weights: both bf16 GEMM layouts refreshed by one launch after the update
+            kxk = [(p, c) for p, c in zip(params, copies) if "kxk" in c]
+            st["conv_table"], st["nconv"], st["conv_blocks"] = None, 0, 0
+            if kxk:
+                st["conv_table"] = C.conv_layout_table([p.data for p, _ in kxk], [c["conv_fwd"] for _, c in kxk],
+                                                       [c["conv_dgrad"] for _, c in kxk],
+                                                       [c["kxk"][0] for _, c in kxk], [c["kxk"][1] for _, c in kxk])
+                st["nconv"] = len(kxk)
+                pairs = max(c["kxk"][0] * c["kxk"][1] for _, c in kxk)  # (co, ci) pairs of the largest
+                st["conv_blocks"] = max(1, min(1024, -(-pairs // 256)))
         b1, b2 = group["betas"]
         hp_key = (group["lr"], b1, b2, group["eps"], group["weight_decay"], group["momentum"], group["grad_scale"])
         if st["hp_key"] != hp_key:
@@ -93,6 +103,8 @@ class _FusedBase(torch.optim.Optimizer):
                 C = C or _native.C()
                 st = self._group_dev(gi, group, params)
                 C.optim_step(st["table"], st["chunks"], st["nchunks"], _MODES[self.KIND], st["hp"], st["step"])
+                if st["nconv"]:
+                    C.conv_layouts_step(st["conv_table"], st["nconv"], st["conv_blocks"])
                 for p in params:
                     self.state[p]["step"] = self.state[p].get("step", 0) + 1
             else:

@@ -322,7 +322,8 @@ def test_pointwise_conv_dense_path(gpu, cfg):
 @pytest.mark.parametrize("kind", ["sgd", "adam"])
 def test_optimizer_maintained_compute_copies(gpu, kind):
     """The fused optimizer writes the bf16 compute copies of linear and 1x1-conv weights in the same launch
-    as the update; they equal a fresh cast of the updated fp32 weights, an outside write (load_state_dict)
+    as the update, and both GEMM layouts of KxK conv weights in one batched launch after it; they equal a
+    fresh conversion of the updated fp32 weights, an outside write (load_state_dict)
     is picked up through the version counter, and a 1x1 conv's dgrad reading the forward copy transposed
     matches the dgrad-layout path."""
     from pytorch_distributed_examples_amd.ops import layers as L
@@ -330,7 +331,7 @@ def test_optimizer_maintained_compute_copies(gpu, kind):
 
     torch.manual_seed(4)
     conv = L.Conv2d(32, 48, 1, bias=False).to(gpu)
-    conv3 = L.Conv2d(3, 20, 3, padding=1).to(gpu)  # not maintained: per-step layout copies
+    conv3 = L.Conv2d(3, 20, 3, padding=1).to(gpu)  # KxK: layout copies refreshed after the update
     fc = L.Linear(40, 12).to(gpu)
     params = list(conv.parameters()) + list(conv3.parameters()) + list(fc.parameters())
     opt = (FusedSGD(params, lr=0.1, momentum=0.9) if kind == "sgd" else FusedAdam(params, lr=1e-2))
@@ -340,11 +341,17 @@ def test_optimizer_maintained_compute_copies(gpu, kind):
         opt.step()
     assert torch.equal(OF._maintained(conv.weight, "conv_fwd"), conv.weight.detach().view(48, 32).bfloat16())
     assert torch.equal(OF._maintained(fc.weight, "bf16"), fc.weight.detach().bfloat16())
-    assert OF._maintained(conv3.weight, "conv_fwd") is None
+    # KxK conv (3 -> 20 channels, padded to 8 / 24): both GEMM layouts refreshed by the one batched launch
+    C = OF._C()
+    w3 = conv3.weight.detach()
+    assert torch.equal(OF._maintained(conv3.weight, "conv_fwd"), C.conv_w_fwd(w3, 8, 24))
+    assert torch.equal(OF._maintained(conv3.weight, "conv_dgrad"), C.conv_w_dgrad(w3, 8, 24))
+    sd3 = {k: torch.randn_like(v) for k, v in conv3.state_dict().items()}
+    conv3.load_state_dict(sd3)
+    assert torch.equal(OF._maintained(conv3.weight, "conv_dgrad"), C.conv_w_dgrad(sd3["weight"], 8, 24))
     sd = {k: torch.randn_like(v) for k, v in conv.state_dict().items()}
     conv.load_state_dict(sd)
     assert torch.equal(OF._maintained(conv.weight, "conv_fwd"), sd["weight"].view(48, 32).bfloat16())
-    C = OF._C()
     dy = torch.randn(2, 5, 5, 48, device=gpu).bfloat16()
     wf = OF._maintained(conv.weight, "conv_fwd")
     a = C.conv_dgrad(dy, wf, 5, 5, 1, 1, 1, 0, None, True)
