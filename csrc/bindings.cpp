@@ -185,7 +185,8 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wd, int H, int W, int R, int S
   TORCH_CHECK(Co % 8 == 0, "conv_dgrad: Cout must be a multiple of 8");
   int Ci;
   if (w_fwd_layout) {
-    TORCH_CHECK(is_pointwise(R, S, stride, pad), "conv_dgrad: the forward-layout weight needs a 1x1/s1 conv");
+    // 1x1 (any stride): B[ci][co] = w[co][ci] is the forward copy read transposed; a strided conv gathers dy
+    TORCH_CHECK(R == 1 && S == 1 && pad == 0, "conv_dgrad: the forward-layout weight needs an unpadded 1x1 conv");
     TORCH_CHECK(wd.dim() == 2 && wd.size(0) == Co && wd.size(1) % 8 == 0, "conv_dgrad: weight must be [Co, Ci]");
     Ci = wd.size(1);
   } else {

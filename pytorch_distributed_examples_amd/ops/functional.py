@@ -281,9 +281,9 @@ class _Conv2dFn(torch.autograd.Function):
             dy = _C().relu_bwd(dy, y)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            wf = _maintained(weight, "conv_fwd") if (r == 1 and s == 1 and stride == 1 and pad == 0) else None
+            wf = _maintained(weight, "conv_fwd") if (r == 1 and s == 1 and pad == 0) else None
             if wf is not None and weight.__dict__["_pde_maint"].get("kxk") is None:
-                # 1x1: the dgrad GEMM reads the forward copy [Co, Ci] transposed
+                # 1x1 (stride 1 or 2): the dgrad GEMM reads the forward copy [Co, Ci] transposed
                 dx = _C().conv_dgrad(dy, wf, h, w, r, s, stride, pad, None, True)
             else:
                 wd = _maintained(weight, "conv_dgrad") if cp == pad8(ci) else None

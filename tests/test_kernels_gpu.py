@@ -357,3 +357,7 @@ def test_optimizer_maintained_compute_copies(gpu, kind):
     a = C.conv_dgrad(dy, wf, 5, 5, 1, 1, 1, 0, None, True)
     b = C.conv_dgrad(dy, C.conv_w_dgrad(conv.weight.detach(), 32, 48), 5, 5, 1, 1, 1, 0)
     assert rel_err(a, b) < 1e-3
+    # strided 1x1 (ResNet downsample): same transposed read, dy gathered at stride 2 (dx 10x10)
+    a2 = C.conv_dgrad(dy, wf, 10, 10, 1, 1, 2, 0, None, True)
+    b2 = C.conv_dgrad(dy, C.conv_w_dgrad(conv.weight.detach(), 32, 48), 10, 10, 1, 1, 2, 0)
+    assert rel_err(a2, b2) < 1e-3
