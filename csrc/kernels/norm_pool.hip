@@ -304,6 +304,93 @@ __global__ void k_maxpool_fwd(const uint16_t* __restrict__ x, uint16_t* __restri
   }
 }
 
+// 8-channel forms (C % 8 == 0, every ResNet pooling): one thread per (pixel, 8-channel group) with 16-byte
+// activation and 8-byte argmax accesses; same window order and tie rule as the scalar kernels.
+__global__ void k_maxpool_fwd8(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, uint8_t* __restrict__ idx,
+                               int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p, int relu) {
+  const int G = C / 8;
+  const long total = static_cast<long>(N) * Ho * Wo * G;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int g = static_cast<int>(i % G);
+    long t = i / G;
+    const int ox = static_cast<int>(t % Wo);
+    t /= Wo;
+    const int oy = static_cast<int>(t % Ho);
+    const int n = static_cast<int>(t / Ho);
+    float best[8];
+    int bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int ky = 0; ky < k; ++ky) {
+      const int iy = oy * s - p + ky;
+      if (iy < 0 || iy >= H) continue;
+      for (int kx = 0; kx < k; ++kx) {
+        const int ix = ox * s - p + kx;
+        if (ix < 0 || ix >= W) continue;
+        const u16x8 u = *reinterpret_cast<const u16x8*>(x + ((static_cast<long>(n) * H + iy) * W + ix) * C + g * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = bf2f(u[j]);
+          if (v > best[j]) { best[j] = v; bi[j] = ky * k + kx; }
+        }
+      }
+    }
+    u16x8 o;
+    unsigned long long packed = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = f2bf(relu ? fmaxf(best[j], 0.f) : best[j]);
+      packed |= static_cast<unsigned long long>(bi[j] & 0xff) << (8 * j);
+    }
+    reinterpret_cast<u16x8*>(y)[i] = o;
+    reinterpret_cast<unsigned long long*>(idx)[i] = packed;
+  }
+}
+
+__global__ void k_maxpool_bwd8(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+                               const uint8_t* __restrict__ idx, uint16_t* __restrict__ dx, int N, int H, int W, int C,
+                               int Ho, int Wo, int k, int s, int p, int relu) {
+  const int G = C / 8;
+  const long total = static_cast<long>(N) * H * W * G;
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int g = static_cast<int>(i % G);
+    long t = i / G;
+    const int ix = static_cast<int>(t % W);
+    t /= W;
+    const int iy = static_cast<int>(t % H);
+    const int n = static_cast<int>(t / H);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    const int oy_lo = max(0, (iy + p - k + s) / s), oy_hi = min(Ho - 1, (iy + p) / s);
+    const int ox_lo = max(0, (ix + p - k + s) / s), ox_hi = min(Wo - 1, (ix + p) / s);
+    for (int oy = oy_lo; oy <= oy_hi; ++oy) {
+      const int ky = iy + p - oy * s;
+      if (ky < 0 || ky >= k) continue;
+      for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+        const int kx = ix + p - ox * s;
+        if (kx < 0 || kx >= k) continue;
+        const long o8 = ((static_cast<long>(n) * Ho + oy) * Wo + ox) * G + g;  // 8-channel group index
+        const unsigned long long id = reinterpret_cast<const unsigned long long*>(idx)[o8];
+        const u16x8 d = reinterpret_cast<const u16x8*>(dy)[o8];
+        u16x8 yv;
+        if (relu) yv = reinterpret_cast<const u16x8*>(y)[o8];
+        const unsigned int tap = static_cast<unsigned int>(ky * k + kx);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (((id >> (8 * j)) & 0xff) == tap && (!relu || bf2f(yv[j]) > 0.f)) acc[j] += bf2f(d[j]);
+        }
+      }
+    }
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
+    reinterpret_cast<u16x8*>(dx)[i] = o;
+  }
+}
+
 // Gather form: each input element sums the grads of the outputs whose argmax it is (deterministic).
 __global__ void k_maxpool_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
                               const uint8_t* __restrict__ idx, uint16_t* __restrict__ dx, int N, int H, int W, int C,
@@ -515,6 +602,11 @@ hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, cons
 hipError_t maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
                        int k, int st, int p, int relu, hipStream_t s) {
   const long total = static_cast<long>(N) * Ho * Wo * C;
+  if (C % 8 == 0 && k * k <= 256) {
+    hipLaunchKernelGGL(k_maxpool_fwd8, dim3(stream_grid(total / 8, 256)), dim3(256), 0, s, x, y, idx, N, H, W, C, Ho,
+                       Wo, k, st, p, relu);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_maxpool_fwd, dim3(stream_grid(total, 256)), dim3(256), 0, s, x, y, idx, N, H, W, C, Ho, Wo,
                      k, st, p, relu);
   return hipGetLastError();
@@ -522,6 +614,11 @@ hipError_t maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int 
 hipError_t maxpool_bwd(const uint16_t* dy, const uint16_t* y, const uint8_t* idx, uint16_t* dx, int N, int H, int W,
                        int C, int Ho, int Wo, int k, int st, int p, int relu, hipStream_t s) {
   const long total = static_cast<long>(N) * H * W * C;
+  if (C % 8 == 0 && k * k <= 256) {
+    hipLaunchKernelGGL(k_maxpool_bwd8, dim3(stream_grid(total / 8, 256)), dim3(256), 0, s, dy, y, idx, dx, N, H, W,
+                       C, Ho, Wo, k, st, p, relu);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_maxpool_bwd, dim3(stream_grid(total, 256)), dim3(256), 0, s, dy, y, idx, dx, N, H, W, C, Ho,
                      Wo, k, st, p, relu);
   return hipGetLastError();

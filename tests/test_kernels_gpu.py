@@ -139,10 +139,12 @@ def test_batchnorm(gpu, relu, res, n, c, h):
     assert rel_err(gamma.grad, g2.grad) < 2e-2
 
 
-@pytest.mark.parametrize("k,s,p,relu", [(3, 2, 1, False), (2, 2, 0, True)])
-def test_maxpool(gpu, k, s, p, relu):
+# c = 16: 8-channel vector kernels; c = 10: scalar kernels (MNIST CNN channel counts)
+@pytest.mark.parametrize("k,s,p,relu,c", [(3, 2, 1, False, 16), (2, 2, 0, True, 16), (3, 2, 1, True, 64),
+                                          (2, 2, 0, True, 10), (3, 2, 1, False, 10)])
+def test_maxpool(gpu, k, s, p, relu, c):
     torch.manual_seed(3)
-    x = torch.randn(4, 16, 12, 12, device=gpu)
+    x = torch.randn(4, c, 12, 12, device=gpu)
     xn = bf(x).permute(0, 2, 3, 1).contiguous().bfloat16().requires_grad_()
     y = OF.max_pool2d(xn, k, s, p, relu)
     xr = bf(x).requires_grad_()
