@@ -12,7 +12,8 @@
 //   * A and B tiles are staged global -> registers -> LDS, double-buffered: the global loads of
 //     K-tile t+1 are issued before the MFMAs of tile t and written to the other LDS buffer after
 //     them (async-STAGE split, T14), one barrier per K-tile.
-//   * LDS images are K-contiguous rows padded by 16 B so MFMA fragments are single ds_read_b128.
+//   * LDS images are unpadded K-contiguous 64-B rows with an XOR chunk swizzle, so MFMA fragments are
+//     single conflict-free ds_read_b128 (see swz_chunk).
 //     Operands that are contiguous along the row (M/N) dimension -- the transposed operands of
 //     dgrad / wgrad -- are loaded 16 B along the row and scattered into the K-contiguous image.
 //   * Implicit-GEMM gathers keep per-slot state: a row's (image, output-pixel) decomposition is done
@@ -37,12 +38,20 @@ namespace {
 
 constexpr int kThreads = 256;
 
-// LDS image swizzle: the 16-byte K-chunk c of image row r lives at chunk c ^ ((r >> 4) & 3).  The XOR is
-// constant over every 16-row MFMA fragment, so the fragment reads (16 rows x one chunk per 16-lane group)
-// keep the conflict-free 80-byte-pitch pattern, while the transposing scatter of the row-contiguous
-// loader (8 rows 8 apart per 16-B global load; 8 rows x 80 B = 0 mod 128 B) spreads its 2-byte writes
-// over 4x more banks.  Needs BK / 8 == 4 chunks per row.
-__device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ ((row >> 4) & 3); }
+// LDS images are unpadded K-contiguous rows (BK = 32 -> 64 B, four 16-byte K-chunks) with an XOR swizzle
+// of the chunk index: chunk c of row r lives at c ^ H[(r >> 2) & 3] ^ ((r >> 4) & 3), H = {0, 3, 2, 1}.
+// gfx950 services ds_read_b128 in four NON-contiguous 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,
+// 28-31}, ...): an MFMA fragment read (lane -> row lane & 15, chunk lane >> 4) puts every row of the
+// fragment in each group, rows 0-3 / 12-15 at chunk c and rows 4-11 at chunk c+1.  With a 64-B pitch the
+// 16-B slot of (r, c) is 4 (r & 3) + chunk', and H makes the four rows sharing r & 3 land on four
+// different chunks in every group: conflict-free reads (an 80-B padded pitch, the previous layout, was
+// 2-way conflicted on exactly this grouping: SQ_LDS_BANK_CONFLICT = 50 % of SQ_LDS_IDX_ACTIVE in
+// profiles/r1h_resnet50_sq_counters.txt).  The (r >> 4) term is constant per 16-row fragment (reads stay
+// conflict-free) and spreads the row-contiguous loader's transposing 2-byte scatter (8 rows 8 apart) over
+// more banks; 16-B K-contiguous stores (8 contiguous lanes = 2 rows x 4 chunks) are conflict-free.
+__device__ __forceinline__ int swz_chunk(int row, int chunk) {
+  return chunk ^ ((-(row >> 2)) & 3) ^ ((row >> 4) & 3);
+}
 
 __device__ __forceinline__ u16x8 zero8() { return u16x8{0, 0, 0, 0, 0, 0, 0, 0}; }
 
@@ -173,14 +182,14 @@ struct KcLoader {
     }
   }
 
-  __device__ __forceinline__ void store(uint16_t* lds) {  // lds: [BROWS][BK + 8]
+  __device__ __forceinline__ void store(uint16_t* lds) {  // lds: [BROWS][BK]
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int v = threadIdx.x + i * kThreads;
       if (v < kVecs) {
         const int row = v / (BK / 8);
         const int kv = v - row * (BK / 8);
-        *reinterpret_cast<u16x8*>(lds + row * (BK + 8) + swz_chunk(row, kv) * 8) = regs[i];
+        *reinterpret_cast<u16x8*>(lds + row * BK + swz_chunk(row, kv) * 8) = regs[i];
       }
     }
   }
@@ -261,7 +270,7 @@ struct RcLoader {
     }
   }
 
-  __device__ __forceinline__ void store(uint16_t* lds) {  // lds: [BROWS][BK + 8], transposing scatter
+  __device__ __forceinline__ void store(uint16_t* lds) {  // lds: [BROWS][BK], transposing scatter
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int v = threadIdx.x + i * kThreads;
@@ -271,7 +280,7 @@ struct RcLoader {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int row = rv * 8 + j;
-          lds[row * (BK + 8) + swz_chunk(row, kk >> 3) * 8 + (kk & 7)] = regs[i][j];
+          lds[row * BK + swz_chunk(row, kk >> 3) * 8 + (kk & 7)] = regs[i][j];
         }
       }
     }
@@ -310,10 +319,10 @@ template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles_m, int tiles_n,
                                                         int k_per_split, int a_vec, int b_vec) {
   static_assert(WM * WN == 4, "4 waves per block");
-  static_assert(BK == 32, "swz_chunk assumes 4 16-byte K-chunks per LDS row");
+  static_assert(BK == 32, "swz_chunk assumes 4 16-byte K-chunks (64 B) per LDS row");
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
-  constexpr int LDS_A = BM * (BK + 8), LDS_B = BN * (BK + 8);
+  constexpr int LDS_A = BM * BK, LDS_B = BN * BK;
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (LDS_A + LDS_B)];
 
   // XCD-aware tile id remap (bijective; see cdna_hip_programming.md §5 "XCD swizzle").
@@ -380,12 +389,12 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int row = wm * WTM + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(As + row * (BK + 8) + swz_chunk(row, kk * 4 + (lane >> 4)) * 8);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + row * BK + swz_chunk(row, kk * 4 + (lane >> 4)) * 8);
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int row = wn * WTN + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + row * (BK + 8) + swz_chunk(row, kk * 4 + (lane >> 4)) * 8);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + swz_chunk(row, kk * 4 + (lane >> 4)) * 8);
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
