@@ -410,9 +410,66 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles
     __syncthreads();
   }
 
-  // Epilogue. C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + reg.
+  // Epilogue. C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + reg.  A lane's outputs are 4
+  // rows of one column, so direct stores are 2-byte (bf16) / 4-byte (slab) scatters.  Where the tile fits
+  // the (now idle) LDS, it is staged there and written back as 16-byte row vectors instead.
   const bool split = gridDim.z > 1;
   float* ws = args.workspace;
+  constexpr int SMEM_BYTES = static_cast<int>(sizeof(smem));
+  const bool vec_bf16 = !split && !(args.epi & (EPI_OIHW | EPI_OUT_F32)) && args.N % 8 == 0 && args.ldo % 8 == 0 &&
+                        (reinterpret_cast<uintptr_t>(args.out) & 15) == 0;
+  const bool vec_f32 = split && args.N % 4 == 0 && (reinterpret_cast<uintptr_t>(ws) & 15) == 0;
+  if constexpr (BM * BN * 2 <= SMEM_BYTES) {
+    if (vec_bf16) {
+      uint16_t* st = smem;  // [BM][BN] bf16 (the K loop ended with a barrier: LDS is free)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int nl = wn * WTN + j * 16 + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ml = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+            const int m = m0 + ml, n = n0 + nl;
+            float v = 0.f;
+            if (m < args.M && n < args.N) v = apply_epi(acc[i][j][r], args.epi, m, n, args);
+            st[ml * BN + nl] = f2bf(v);
+          }
+        }
+      __syncthreads();
+      uint16_t* out = static_cast<uint16_t*>(args.out);
+      for (int q = threadIdx.x; q < BM * BN / 8; q += kThreads) {
+        const int ml = q / (BN / 8), nl = (q % (BN / 8)) * 8;
+        const int m = m0 + ml, n = n0 + nl;
+        if (m < args.M && n < args.N)
+          *reinterpret_cast<u16x8*>(out + static_cast<long>(m) * args.ldo + n) =
+              *reinterpret_cast<const u16x8*>(st + ml * BN + nl);
+      }
+      return;
+    }
+  }
+  if constexpr (BM * BN * 4 <= SMEM_BYTES) {
+    if (vec_f32) {
+      float* st = reinterpret_cast<float*>(smem);  // [BM][BN] fp32 partials
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int nl = wn * WTN + j * 16 + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) st[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * BN + nl] = acc[i][j][r];
+        }
+      __syncthreads();
+      for (int q = threadIdx.x; q < BM * BN / 4; q += kThreads) {
+        const int ml = q / (BN / 4), nl = (q % (BN / 4)) * 4;
+        const int m = m0 + ml, n = n0 + nl;
+        if (m < args.M && n < args.N)
+          *reinterpret_cast<f32x4*>(ws + (static_cast<long>(kz) * args.M + m) * args.N + n) =
+              *reinterpret_cast<const f32x4*>(st + ml * BN + nl);
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
 #pragma unroll
