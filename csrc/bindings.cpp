@@ -178,8 +178,10 @@ Tensor conv_fwd(const Tensor& x, const Tensor& wf, const optional<Tensor>& bias,
 
 // dx[N,H,W,Ci] from dy[N,Ho,Wo,Co] and wd = [Ci, R*S*Co]; or, for a 1x1 / stride-1 conv with
 // w_fwd_layout, from the forward copy wd = [Co, Ci] read transposed (no separate dgrad layout).
+// aux: with add_aux, a bf16 [N*H*W, Ci] gradient added in the epilogue (the other branch of a residual
+// fork); otherwise the saved post-ReLU activation whose mask multiplies the result.
 Tensor conv_dgrad(const Tensor& dy, const Tensor& wd, int H, int W, int R, int S, int stride, int pad,
-                  const optional<Tensor>& aux, bool w_fwd_layout) {
+                  const optional<Tensor>& aux, bool w_fwd_layout, bool add_aux) {
   CHECK_IN(dy); CHECK_IN(wd); CHECK_BF16(dy); CHECK_BF16(wd);
   const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
   TORCH_CHECK(Co % 8 == 0, "conv_dgrad: Cout must be a multiple of 8");
@@ -200,7 +202,11 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wd, int H, int W, int R, int S
   a.b = w_fwd_layout ? dense(wd, 1, Ci) : dense(wd, a.K, 1);
   a.out = dx.data_ptr(); a.ldo = Ci;
   a.aux = cu16(aux); a.ldaux = Ci;
-  a.epi = a.aux ? pde::EPI_DRELU : 0;
+  if (a.aux) {
+    CHECK_IN(*aux); CHECK_BF16(*aux);
+    TORCH_CHECK(aux->numel() == dx.numel(), "conv_dgrad: aux must match dx");
+  }
+  a.epi = a.aux ? (add_aux ? pde::EPI_ADD_AUX : pde::EPI_DRELU) : 0;
   run_gemm(a, dy, -1);
   return dx;
 }
@@ -718,7 +724,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("accumulate") = false);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wd"), py::arg("H"), py::arg("W"), py::arg("R"),
-        py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("aux") = py::none(), py::arg("w_fwd_layout") = false);
+        py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("aux") = py::none(), py::arg("w_fwd_layout") = false,
+        py::arg("add_aux") = false);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),
         py::arg("pad"), py::arg("Co"), py::arg("Ci"), py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("cast_bf16", &cast_bf16);

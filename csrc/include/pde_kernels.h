@@ -21,6 +21,7 @@ enum EpiFlags : int {
   EPI_OUT_F32 = 8,    // output fp32 (else bf16)
   EPI_ACCUM = 16,     // out += result (fp32 output only)
   EPI_OIHW = 32,      // conv weight gradient: m = co, n = (r*S + s)*Cp + ci written to out[co][ci][r][s]
+  EPI_ADD_AUX = 64,   // + aux[m, n] (bf16): a second gradient branch summed in the epilogue
                       // (ci >= oihw_ci skipped; fp32 output)
 };
 
@@ -53,7 +54,7 @@ struct GemmArgs {
   void* out; long ldo;             // out[m * ldo + n]
   const float* bias;               // EPI_BIAS (bias[n] for n < nbias, 0 beyond: padded channels)
   int nbias;
-  const uint16_t* aux; long ldaux; // EPI_DRELU (bf16 bits)
+  const uint16_t* aux; long ldaux; // EPI_DRELU / EPI_ADD_AUX (bf16 bits)
   int epi;
   int splitk;                      // >1: fp32 partial slabs in workspace, then reduce + epilogue
   float* workspace;                // splitk * M * N fp32

@@ -293,6 +293,7 @@ using Loader = typename std::conditional<KC, KcLoader<BROWS, BK>, RcLoader<BROWS
 __device__ __forceinline__ float apply_epi(float v, int epi, int m, int n, const GemmArgs& a) {
   if ((epi & EPI_BIAS) && n < a.nbias) v += a.bias[n];
   if (epi & EPI_DRELU) v = (bf2f(a.aux[static_cast<long>(m) * a.ldaux + n]) > 0.f) ? v : 0.f;
+  if (epi & EPI_ADD_AUX) v += bf2f(a.aux[static_cast<long>(m) * a.ldaux + n]);
   if (epi & EPI_RELU) v = fmaxf(v, 0.f);
   return v;
 }

@@ -39,13 +39,16 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         identity = x
-        out = self.bn1(self.conv1(x), relu=True)
+        # identity shortcut on the GPU: x's two gradients (residual and conv1 branch) meet in conv1's dgrad
+        # epilogue instead of an autograd add (ops.functional.GradJoin)
+        join = OF.GradJoin() if (self.downsample is None and x.is_cuda and torch.is_grad_enabled()) else None
+        out = self.bn1(self.conv1(x, grad_join=join), relu=True)
         out = self.bn2(self.conv2(out), relu=True)
         if self.downsample is not None:
             conv, bn = self.downsample[0], self.downsample[1]
             identity = bn(conv(x))
         # relu(bn3(conv3(out)) + identity) in one fused kernel
-        return self.bn3(self.conv3(out), residual=identity, relu=True)
+        return self.bn3(self.conv3(out), residual=identity, relu=True, residual_grad_to=join)
 
 
 class _StemReLU(nn.Module):

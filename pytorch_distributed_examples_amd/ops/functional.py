@@ -257,7 +257,8 @@ def linear(x, weight, bias=None, relu=False, out_f32=False, consumer_masks=False
 # ---------------------------------------------------------------------------------------------
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, relu):
+    def forward(ctx, x, weight, bias, stride, pad, relu, join=None):
+        ctx.join = join
         co, ci, r, s = weight.shape
         cp = x.shape[3]
         cop = pad8(co)
@@ -281,16 +282,19 @@ class _Conv2dFn(torch.autograd.Function):
             dy = _C().relu_bwd(dy, y)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
+            # residual fork: the other branch's gradient (stored by the block's last BatchNorm) is added in the
+            # dgrad epilogue instead of by a separate autograd add
+            other = ctx.join.take() if ctx.join is not None else None
             wf = _maintained(weight, "conv_fwd") if (r == 1 and s == 1 and pad == 0) else None
             if wf is not None and weight.__dict__["_pde_maint"].get("kxk") is None:
                 # 1x1 (stride 1 or 2): the dgrad GEMM reads the forward copy [Co, Ci] transposed
-                dx = _C().conv_dgrad(dy, wf, h, w, r, s, stride, pad, None, True)
+                dx = _C().conv_dgrad(dy, wf, h, w, r, s, stride, pad, other, True, other is not None)
             else:
                 wd = _maintained(weight, "conv_dgrad") if cp == pad8(ci) else None
                 if wd is None:
                     wd = _cached(weight, ("conv_dgrad", cp, cop),
                                  lambda: _C().conv_w_dgrad(weight.detach().contiguous(), cp, cop))
-                dx = _C().conv_dgrad(dy, wd, h, w, r, s, stride, pad, None)
+                dx = _C().conv_dgrad(dy, wd, h, w, r, s, stride, pad, other, False, other is not None)
         if ctx.needs_input_grad[1]:
             # OIHW epilogue: the GEMM writes the parameter's layout (and adds into .grad when it exists)
             sink = _grad_sink(weight)
@@ -302,16 +306,40 @@ class _Conv2dFn(torch.autograd.Function):
             db = _C().colsum(dy, co, sink, sink is not None)
             if sink is not None:
                 db = None
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
-def conv2d(x, weight, bias=None, stride=1, padding=0, relu=False):
+class GradJoin:
+    """Hand-off of one gradient between the two consumers of a residual fork (GPU training).
+
+    In a bottleneck block without downsample, the block input feeds conv1 and the residual of the last
+    BatchNorm.  Passing the same ``GradJoin`` to ``batch_norm(..., residual_grad_to=j)`` and
+    ``conv2d(..., grad_join=j)`` makes the BatchNorm backward hand its residual gradient to the join
+    (instead of returning it to autograd), and conv1's dgrad GEMM adds it in its epilogue: one bf16 add kernel
+    and one gradient tensor fewer per block.  Autograd order is guaranteed by data dependence: conv1's
+    backward needs the gradient that flows back through the BatchNorm."""
+
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+    def put(self, g):
+        self.grad = g
+
+    def take(self):
+        g, self.grad = self.grad, None
+        return g
+
+
+def conv2d(x, weight, bias=None, stride=1, padding=0, relu=False, grad_join=None):
     """2-D convolution.  GPU: ``x`` is NHWC bf16 with C padded to a multiple of 8; output NHWC with
-    Cout padded to a multiple of 8 (padded channels are exactly zero).  CPU: NCHW fp32 F.conv2d."""
+    Cout padded to a multiple of 8 (padded channels are exactly zero).  CPU: NCHW fp32 F.conv2d.
+    ``grad_join``: see :class:`GradJoin` (GPU only; ignored on CPU)."""
     if not x.is_cuda:
         y = F.conv2d(_emu(x), _emu(weight), bias, stride=stride, padding=padding)
         return _emu(F.relu(y) if relu else y)
-    return _Conv2dFn.apply(x.contiguous(), weight, bias, int(stride), int(padding), relu)
+    return _Conv2dFn.apply(x.contiguous(), weight, bias, int(stride), int(padding), relu, grad_join)
 
 
 def to_native_image(x: torch.Tensor) -> torch.Tensor:
@@ -326,7 +354,8 @@ def to_native_image(x: torch.Tensor) -> torch.Tensor:
 # ---------------------------------------------------------------------------------------------
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, running_mean, running_var, residual, eps, momentum, relu):
+    def forward(ctx, x, gamma, beta, running_mean, running_var, residual, eps, momentum, relu, join=None):
+        ctx.join = join
         y, mean, invstd = _C().bn_fwd(x, gamma.detach() if gamma is not None else None,
                                       beta.detach() if beta is not None else None, running_mean, running_var,
                                       eps, momentum, residual, relu)
@@ -347,12 +376,16 @@ class _BatchNormFn(torch.autograd.Function):
                                        dg_sink if direct else None, db_sink if direct else None)
         if direct:  # dgamma / dbeta were added into .grad by the finalize kernel
             dg = db = None
-        return dx, dg, db, None, None, (dres if ctx.has_res else None), None, None, None
+        if ctx.has_res and ctx.join is not None:  # the residual fork's conv adds it in its dgrad epilogue
+            ctx.join.put(dres)
+            dres = None
+        return dx, dg, db, None, None, (dres if ctx.has_res else None), None, None, None, None
 
 
 def batch_norm(x, weight, bias, running_mean, running_var, training, momentum=0.1, eps=1e-5, residual=None,
-               relu=False):
-    """BatchNorm2d with optional fused residual add and ReLU:  relu?(bn(x) + residual)."""
+               relu=False, residual_grad_to=None):
+    """BatchNorm2d with optional fused residual add and ReLU:  relu?(bn(x) + residual).
+    ``residual_grad_to``: a :class:`GradJoin` that receives the residual's gradient (GPU training only)."""
     if not x.is_cuda:
         y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
         if residual is not None:
@@ -361,7 +394,8 @@ def batch_norm(x, weight, bias, running_mean, running_var, training, momentum=0.
     x = x.contiguous()
     if training:
         return _BatchNormFn.apply(x, weight, bias, running_mean, running_var,
-                                  residual.contiguous() if residual is not None else None, eps, momentum, relu)
+                                  residual.contiguous() if residual is not None else None, eps, momentum, relu,
+                                  residual_grad_to if residual is not None else None)
     invstd = torch.rsqrt(running_var + eps)
     scale = (weight * invstd if weight is not None else invstd).float().contiguous()
     shift = ((bias if bias is not None else 0) - running_mean * scale).float().contiguous()

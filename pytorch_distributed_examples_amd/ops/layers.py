@@ -58,8 +58,8 @@ class Conv2d(nn.Module):
             bound = 1 / math.sqrt(fan_in)
             nn.init.uniform_(self.bias, -bound, bound)
 
-    def forward(self, x):
-        return OF.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.relu)
+    def forward(self, x, grad_join=None):
+        return OF.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.relu, grad_join)
 
     def extra_repr(self):
         return (f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}, stride={self.stride}, "
@@ -90,14 +90,14 @@ class BatchNorm2d(nn.Module):
         self._flush_nbt()
         super()._save_to_state_dict(destination, prefix, keep_vars)
 
-    def forward(self, x, residual=None, relu=False):
+    def forward(self, x, residual=None, relu=False, residual_grad_to=None):
         if self.training:
             if x.is_cuda:
                 self._nbt_pending += 1
             else:
                 self.num_batches_tracked.add_(1)
         return OF.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
-                             self.momentum, self.eps, residual, relu)
+                             self.momentum, self.eps, residual, relu, residual_grad_to)
 
 
 class MaxPool2d(nn.Module):
