@@ -130,10 +130,44 @@ __device__ __forceinline__ void conv_w_layouts_entry(const ConvLayoutEntry& e) {
   }
 }
 
-__global__ void k_conv_w_layouts_multi(const ConvLayoutEntry* __restrict__ table) {
+// 3x3 fast path: a (32 co x 32 ci) tile of one weight is transposed through LDS.  The fp32 source rows
+// (ci, r, s contiguous per co) are read coalesced; both bf16 layouts are written as 64-byte runs
+// (fwd: ci contiguous, dgrad: co contiguous).  Padded channels come out as zeros.
+constexpr int kCwTile = 32;
+__device__ __forceinline__ void conv_w_layouts_tiled3x3(const ConvLayoutEntry& e) {
+  constexpr int RS = 9;
+  __shared__ float tile[RS][kCwTile][kCwTile + 1];
+  const int tco = (e.Cop + kCwTile - 1) / kCwTile, tci = (e.Cp + kCwTile - 1) / kCwTile;
+  for (int t = blockIdx.x; t < tco * tci; t += gridDim.x) {
+    const int co0 = (t / tci) * kCwTile, ci0 = (t % tci) * kCwTile;
+    for (int q = threadIdx.x; q < kCwTile * kCwTile * RS; q += blockDim.x) {
+      const int col = q / (kCwTile * RS), rem = q - col * (kCwTile * RS);
+      const int cil = rem / RS, tap = rem - cil * RS;
+      const int co = co0 + col, ci = ci0 + cil;
+      tile[tap][col][cil] = (co < e.Co && ci < e.Ci) ? e.w[(static_cast<long>(co) * e.Ci + ci) * RS + tap] : 0.f;
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < kCwTile * RS * kCwTile; q += blockDim.x) {  // fwd [co][tap][ci]
+      const int col = q / (RS * kCwTile), rem = q - col * (RS * kCwTile);
+      const int tap = rem / kCwTile, cil = rem - tap * kCwTile;
+      const int co = co0 + col, ci = ci0 + cil;
+      if (co < e.Cop && ci < e.Cp) e.fwd[(static_cast<long>(co) * RS + tap) * e.Cp + ci] = f2bf(tile[tap][col][cil]);
+    }
+    for (int q = threadIdx.x; q < kCwTile * RS * kCwTile; q += blockDim.x) {  // dgrad [ci][tap][co]
+      const int cil = q / (RS * kCwTile), rem = q - cil * (RS * kCwTile);
+      const int tap = rem / kCwTile, col = rem - tap * kCwTile;
+      const int co = co0 + col, ci = ci0 + cil;
+      if (co < e.Cop && ci < e.Cp)
+        e.dgrad[(static_cast<long>(ci) * RS + tap) * e.Cop + co] = f2bf(tile[tap][col][cil]);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_conv_w_layouts_multi(const ConvLayoutEntry* __restrict__ table) {
   const ConvLayoutEntry e = table[blockIdx.y];
   if (e.R * e.S == 9)
-    conv_w_layouts_entry<9>(e);
+    conv_w_layouts_tiled3x3(e);
   else
     conv_w_layouts_entry<0>(e);
 }

@@ -79,8 +79,9 @@ class _FusedBase(torch.optim.Optimizer):
                                                        [c["conv_dgrad"] for _, c in kxk],
                                                        [c["kxk"][0] for _, c in kxk], [c["kxk"][1] for _, c in kxk])
                 st["nconv"] = len(kxk)
-                pairs = max(c["kxk"][0] * c["kxk"][1] for _, c in kxk)  # (co, ci) pairs of the largest
-                st["conv_blocks"] = max(1, min(1024, -(-pairs // 256)))
+                # x blocks per entry: the largest weight's 32x32 (co, ci) tiles (3x3 path) / 256-pair chunks
+                tiles = max(-(-c["kxk"][0] // 32) * -(-c["kxk"][1] // 32) for _, c in kxk)
+                st["conv_blocks"] = max(1, min(1024, tiles))
         b1, b2 = group["betas"]
         hp_key = (group["lr"], b1, b2, group["eps"], group["weight_decay"], group["momentum"], group["grad_scale"])
         if st["hp_key"] != hp_key:
