@@ -246,6 +246,40 @@ __global__ __launch_bounds__(256) void k_colsum_vec(const uint16_t* __restrict__
 }
 
 // One wave per column: lanes stride the block partials, then a wave reduction.
+// Short inputs (M <= 1024 rows: the MLP's bias gradients at batch 128): one launch, no workspace.  A block
+// owns 64 columns (8 groups of 8); its 32 row-lanes per group each sum every 32nd row with 16-byte loads,
+// then lane 0 of the group adds the 32 partials in a fixed order (deterministic) and writes / accumulates.
+__global__ __launch_bounds__(256) void k_colsum_cols(const uint16_t* __restrict__ x, int M, int N,
+                                                     float* __restrict__ out, int accum) {
+  const int G = N / 8;
+  const int gl = threadIdx.x & 7, rl = threadIdx.x >> 3;  // 8 groups x 32 row-lanes
+  const int g = blockIdx.x * 8 + gl;
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  if (g < G) {
+    for (int r = rl; r < M; r += 32) {
+      const u16x8 u = *reinterpret_cast<const u16x8*>(x + static_cast<long>(r) * N + g * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += bf2f(u[j]);
+    }
+  }
+  __shared__ float part[32][8][9];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[rl][gl][j] = s[j];
+  __syncthreads();
+  if (threadIdx.x < 64) {  // (group, column) per thread
+    const int gq = threadIdx.x >> 3, j = threadIdx.x & 7;
+    const int gc = blockIdx.x * 8 + gq;
+    if (gc < G) {
+      float t = 0.f;
+      for (int k = 0; k < 32; ++k) t += part[k][gq][j];
+      const int col = gc * 8 + j;
+      out[col] = accum ? out[col] + t : t;
+    }
+  }
+}
+
 __global__ void k_colsum_final(const float* __restrict__ ws, int nblk, int N, float* __restrict__ out, int accum) {
   const int col = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -315,6 +349,10 @@ hipError_t conv_wgrad_to_oihw(const float* in, float* out, int Co, int Ci, int R
 }
 hipError_t colsum_bf16_ws(const uint16_t* x, float* out, int M, int N, int accum, float* ws, int ws_blocks,
                           hipStream_t s) {
+  if (N % 8 == 0 && M <= 1024) {
+    hipLaunchKernelGGL(k_colsum_cols, dim3(ceil_div(N / 8, 8)), dim3(256), 0, s, x, M, N, out, accum);
+    return hipGetLastError();
+  }
   if (N % 8 == 0 && ws != nullptr) {
     const int G = N / 8;
     const int rpi = 256 / (G < 256 ? G : 256);

@@ -94,6 +94,21 @@ def test_conv_fwd_bwd(gpu, cfg):
         assert xn.grad[..., ci:].abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("M,N", [(128, 1024), (37, 16), (1024, 264), (1025, 64), (5000, 1000), (64, 10)])
+def test_colsum(gpu, M, N):
+    """Bias-gradient column sums (single-launch short path for M <= 1024, two-level beyond, scalar for
+    N % 8 != 0), written and accumulated, against an fp32 torch sum."""
+    C = OF._C()
+    torch.manual_seed(5)
+    x = torch.randn(M, N, device=gpu).bfloat16()
+    ref = x.float().sum(0)
+    out = C.colsum(x, N, torch.zeros(N, device=gpu), False)
+    assert rel_err(out, ref) < 1e-4
+    base = torch.randn(N, device=gpu)
+    acc = C.colsum(x, N, base.clone(), True)
+    assert rel_err(acc, base + ref) < 1e-4
+
+
 # shapes: one 64-channel slice; C < 64 (partial slice, groups not dividing 256); C % 64 != 0 (ragged
 # last slice, several slices); many rows (256 row chunks per slice -> widest last-block combine)
 @pytest.mark.parametrize("relu,res,n,c,h", [(False, False, 8, 64, 16), (True, False, 8, 64, 16),
