@@ -41,5 +41,5 @@ def run_cmd(cmd, timeout=600, env=None):
 
 
 def torchrun(script_args, nproc=2, timeout=600, env=None):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--nproc-per-node", str(nproc)]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1", "--nproc-per-node", str(nproc)]
     return run_cmd(cmd + script_args, timeout, env)
