@@ -5,11 +5,13 @@
 
 #include "comm_manager.h"
 #include "fusion_engine.h"
+#include "xgmi_allreduce.h"
 
 namespace {
 
 using pde::FusionEngine;
 using pde::RcclComm;
+using pde::XgmiAllreduce;
 
 int code_of(const at::Tensor& t) {
   switch (t.scalar_type()) {
@@ -54,6 +56,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("size", &RcclComm::size)
       .def_property_readonly("device", &RcclComm::device)
       .def("async_error", &RcclComm::async_error)
+      .def("nranks", &RcclComm::nranks)
       // tensor-level collectives, enqueued on the caller's CURRENT torch stream (stream-ordered with
       // the producing kernels; no host synchronisation)
       .def("allreduce_",
@@ -109,11 +112,40 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("group_start", &RcclComm::group_start)
       .def("group_end", &RcclComm::group_end);
 
+  py::class_<XgmiAllreduce, std::shared_ptr<XgmiAllreduce>>(m, "XgmiAllreduce")
+      .def(py::init<int, int, int, int64_t, int, double>(), py::arg("rank"), py::arg("size"), py::arg("device"),
+           py::arg("max_bytes"), py::arg("blocks") = 64, py::arg("timeout_s") = 5.0)
+      .def("ipc_handle", [](XgmiAllreduce& x) { return py::bytes(x.ipc_handle()); })
+      .def("open",
+           [](XgmiAllreduce& x, const std::vector<py::bytes>& hs) {
+             std::vector<std::string> v;
+             for (const auto& h : hs) v.emplace_back(std::string(h));
+             x.open(v);
+           })
+      // in place (or src -> dst) on the caller's CURRENT stream; hipGraph-capturable
+      .def("allreduce_",
+           [](XgmiAllreduce& x, at::Tensor& t, double scale) {
+             check_gpu(t);
+             TORCH_CHECK(t.scalar_type() == at::kFloat, "xgmi allreduce: fp32 tensors");
+             x.allreduce(t.data_ptr<float>(), t.data_ptr<float>(), t.numel(), static_cast<float>(scale), cur(t));
+             return t;
+           },
+           py::arg("tensor"), py::arg("scale") = 1.0)
+      .def("error", [](XgmiAllreduce& x) { py::gil_scoped_release nogil; return x.error(); })
+      .def("close", [](XgmiAllreduce& x) { py::gil_scoped_release nogil; x.close(); })
+      .def_property_readonly("rank", &XgmiAllreduce::rank)
+      .def_property_readonly("size", &XgmiAllreduce::size)
+      .def_property_readonly("max_bytes", &XgmiAllreduce::max_bytes)
+      .def_property_readonly("calls", &XgmiAllreduce::calls);
+
   py::class_<FusionEngine, std::shared_ptr<FusionEngine>>(m, "FusionEngine")
-      .def(py::init<int, int, int64_t, const std::string&>(), py::arg("rank"), py::arg("size"),
-           py::arg("fusion_bytes"), py::arg("timeline_path") = "")
+      .def(py::init<int, int, int64_t, const std::string&, double>(), py::arg("rank"), py::arg("size"),
+           py::arg("fusion_bytes"), py::arg("timeline_path") = "", py::arg("cycle_ms") = 0.5)
       .def("set_rccl", &FusionEngine::set_rccl)
       .def("set_py_backend", &FusionEngine::set_py_backend)
+      .def("set_control", &FusionEngine::set_control, py::arg("process_group"))
+      .def("set_timeout", &FusionEngine::set_timeout)
+      .def("set_blocking_wait", &FusionEngine::set_blocking_wait)
       .def("allreduce", &FusionEngine::allreduce, py::arg("tensor"), py::arg("output"), py::arg("name"),
            py::arg("op"), py::arg("prescale") = 1.0, py::arg("postscale") = 1.0, py::arg("compress") = false)
       .def("broadcast", &FusionEngine::broadcast)
@@ -121,7 +153,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("flush", &FusionEngine::flush)
       .def("poll", &FusionEngine::poll)
       .def("wait", &FusionEngine::wait)
-      .def("shutdown", &FusionEngine::shutdown)
+      .def("shutdown", &FusionEngine::shutdown, py::arg("abort") = false)
+      .def("inject_error", &FusionEngine::inject_error)
+      .def_property_readonly("error", &FusionEngine::error)
       .def("stats", &FusionEngine::stats)
       .def_property("fusion_bytes", &FusionEngine::fusion_bytes, &FusionEngine::set_fusion_bytes);
 }

@@ -141,6 +141,13 @@ int RcclComm::async_error() const {
   return static_cast<int>(st);
 }
 
+int RcclComm::nranks() const {
+  if (comm_ == nullptr) return 0;
+  int n = 0;
+  check(ncclCommCount(comm_, &n), "ncclCommCount");
+  return n;
+}
+
 void RcclComm::allreduce(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t s) {
   check(ncclAllReduce(send, recv, count, to_nccl(dtype), to_nccl_op(op), comm_, s ? s : stream_), "allreduce");
 }

@@ -42,6 +42,8 @@ class RcclComm {
   ncclComm_t raw() const { return comm_; }
   // returns ncclSuccess / ncclInProgress / an async error
   int async_error() const;
+  // ncclCommCount: the number of ranks RCCL itself reports for this communicator
+  int nranks() const;
 
   // dtype codes: 0 f32, 1 bf16, 2 f16, 3 f64, 4 i32, 5 i64, 6 u8 ; op codes: 0 sum, 1 avg, 2 min, 3 max, 4 prod
   void allreduce(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t s);

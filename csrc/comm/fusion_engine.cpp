@@ -1,9 +1,11 @@
-// Horovod-style fusion engine: see fusion_engine.h.
+// Horovod-style fusion engine with negotiation: see fusion_engine.h.
 #include "fusion_engine.h"
 
 #include <c10/hip/HIPCachingAllocator.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
+#include <algorithm>
+#include <cstring>
 #include <sstream>
 
 #include "pack.h"
@@ -35,10 +37,26 @@ void record_on(const at::Tensor& t, hipStream_t s, int device) {
                                               c10::hip::getStreamFromExternal(s, device));
 }
 
+constexpr char kFieldSep = '\x1f';
+constexpr char kRecSep = '\x1e';
+const char* kTypeNames[] = {"allreduce", "broadcast", "allgather"};
+
 }  // namespace
 
-FusionEngine::FusionEngine(int rank, int size, int64_t fusion_bytes, const std::string& timeline_path)
-    : rank_(rank), size_(size), fusion_bytes_(fusion_bytes), t0_(std::chrono::steady_clock::now()) {
+std::string Request::signature() const {
+  std::ostringstream s;
+  s << kTypeNames[static_cast<int>(type)] << " dtype=" << c10::toString(tensor.scalar_type())
+    << " shape=" << tensor.sizes() << " device=" << (tensor.is_cuda() ? "gpu" : "cpu");
+  if (type == ReqType::ALLREDUCE)
+    s << " op=" << op << " prescale=" << prescale << " postscale=" << postscale << " compress=" << compress;
+  if (type == ReqType::BROADCAST) s << " root=" << root;
+  return s.str();
+}
+
+FusionEngine::FusionEngine(int rank, int size, int64_t fusion_bytes, const std::string& timeline_path,
+                           double cycle_ms)
+    : rank_(rank), size_(size), fusion_bytes_(fusion_bytes), cycle_ms_(cycle_ms),
+      t0_(std::chrono::steady_clock::now()) {
   if (!timeline_path.empty()) {
     trace_.open(timeline_path);
     trace_ << "[\n";
@@ -48,7 +66,7 @@ FusionEngine::FusionEngine(int rank, int size, int64_t fusion_bytes, const std::
 
 FusionEngine::~FusionEngine() {
   try {
-    shutdown();
+    shutdown(false);
   } catch (...) {
   }
 }
@@ -78,18 +96,52 @@ void FusionEngine::set_py_backend(py::object allreduce_fn, py::object broadcast_
   py_allgather_ = std::move(allgather_fn);
 }
 
-void FusionEngine::close_open_locked() {
-  if (!open_.reqs.empty()) {
-    closed_.push_back(std::move(open_));
-    open_ = Batch();
-    cv_.notify_one();
+void FusionEngine::set_control(c10::intrusive_ptr<c10d::ProcessGroup> pg) {
+  TORCH_CHECK(pg->getSize() == size_ && pg->getRank() == rank_, "fusion engine: control group rank/size mismatch");
+  control_ = std::move(pg);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// enqueue side (framework thread)
+// ---------------------------------------------------------------------------------------------------
+int64_t FusionEngine::enqueue(Request&& r) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!error_.empty()) {
+    if (r.ready) (void)hipEventDestroy(r.ready);
+    throw std::runtime_error("HorovodInternalError: " + error_);
   }
+  if (stop_requested_ || stopped_) {
+    if (r.ready) (void)hipEventDestroy(r.ready);
+    throw std::runtime_error("Horovod has been shut down");
+  }
+  const bool dup = announced_.count(r.name) > 0 ||
+                   std::any_of(unannounced_.begin(), unannounced_.end(),
+                               [&](const Request& q) { return q.name == r.name; });
+  if (dup) {
+    if (r.ready) (void)hipEventDestroy(r.ready);
+    TORCH_CHECK(false, "fusion engine: a request named '", r.name, "' is already outstanding on rank ", rank_);
+  }
+  r.handle = next_handle_++;
+  handles_[r.handle] = HandleState();
+  ++n_requests_;
+  const int64_t h = r.handle;
+  unannounced_.push_back(std::move(r));
+  cv_.notify_one();
+  return h;
+}
+
+static void record_ready(Request& r) {
+  if (!r.tensor.is_cuda()) return;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(r.tensor.device());
+  hip_ok(hipEventCreateWithFlags(&r.ready, hipEventDisableTiming), "event create");
+  hip_ok(hipEventRecord(r.ready, at::hip::getCurrentHIPStream(r.tensor.device().index()).stream()), "event record");
 }
 
 int64_t FusionEngine::allreduce(at::Tensor t, at::Tensor out, const std::string& name, int op, double prescale,
                                 double postscale, bool compress) {
   TORCH_CHECK(t.is_contiguous() && out.is_contiguous(), "fusion engine: tensors must be contiguous");
   TORCH_CHECK(t.numel() == out.numel(), "fusion engine: output size mismatch");
+  if (t.is_cuda()) TORCH_CHECK(gpu_backend_, "fusion engine: GPU tensor but no RCCL communicator");
   Request r;
   r.type = ReqType::ALLREDUCE;
   r.name = name;
@@ -100,35 +152,13 @@ int64_t FusionEngine::allreduce(at::Tensor t, at::Tensor out, const std::string&
   r.postscale = postscale;
   r.compress = compress && t.scalar_type() == at::kFloat;
   r.t_enqueue = now();
-  if (t.is_cuda()) {
-    TORCH_CHECK(gpu_backend_, "fusion engine: GPU tensor but no RCCL communicator");
-    c10::hip::HIPGuardMasqueradingAsCUDA guard(t.device());
-    hip_ok(hipEventCreateWithFlags(&r.ready, hipEventDisableTiming), "event create");
-    hip_ok(hipEventRecord(r.ready, at::hip::getCurrentHIPStream(t.device().index()).stream()), "event record");
-  }
-  const int64_t bytes = t.numel() * static_cast<int64_t>(r.compress ? 2 : t.element_size());
-  std::lock_guard<std::mutex> g(mu_);
-  r.handle = next_handle_++;
-  handles_[r.handle] = HandleState();
-  ++n_requests_;
-  // batch key: device, dtype, op, scales, compression -- a change closes the open batch
-  if (!open_.reqs.empty()) {
-    const Request& h = open_.reqs.front();
-    const bool same = h.tensor.device() == t.device() && h.tensor.scalar_type() == t.scalar_type() && h.op == op &&
-                      h.prescale == prescale && h.postscale == postscale && h.compress == r.compress;
-    if (!same || open_.bytes + bytes > fusion_bytes_.load() ||
-        static_cast<int>(open_.reqs.size()) >= kMaxPackSegs * 8)
-      close_open_locked();
-  }
-  const int64_t h = r.handle;
-  open_.reqs.push_back(std::move(r));
-  open_.bytes += bytes;
-  if (open_.bytes >= fusion_bytes_.load()) close_open_locked();
-  return h;
+  record_ready(r);
+  return enqueue(std::move(r));
 }
 
 int64_t FusionEngine::broadcast(at::Tensor t, int root, const std::string& name) {
   TORCH_CHECK(t.is_contiguous(), "fusion engine: tensor must be contiguous");
+  if (t.is_cuda()) TORCH_CHECK(gpu_backend_, "fusion engine: GPU tensor but no RCCL communicator");
   Request r;
   r.type = ReqType::BROADCAST;
   r.name = name;
@@ -136,28 +166,13 @@ int64_t FusionEngine::broadcast(at::Tensor t, int root, const std::string& name)
   r.output = t;
   r.root = root;
   r.t_enqueue = now();
-  if (t.is_cuda()) {
-    TORCH_CHECK(gpu_backend_, "fusion engine: GPU tensor but no RCCL communicator");
-    c10::hip::HIPGuardMasqueradingAsCUDA guard(t.device());
-    hip_ok(hipEventCreateWithFlags(&r.ready, hipEventDisableTiming), "event create");
-    hip_ok(hipEventRecord(r.ready, at::hip::getCurrentHIPStream(t.device().index()).stream()), "event record");
-  }
-  std::lock_guard<std::mutex> g(mu_);
-  r.handle = next_handle_++;
-  handles_[r.handle] = HandleState();
-  ++n_requests_;
-  close_open_locked();
-  Batch b;
-  b.bytes = t.numel() * t.element_size();
-  const int64_t h = r.handle;
-  b.reqs.push_back(std::move(r));
-  closed_.push_back(std::move(b));
-  cv_.notify_one();
-  return h;
+  record_ready(r);
+  return enqueue(std::move(r));
 }
 
 int64_t FusionEngine::allgather(at::Tensor t, const std::string& name) {
   TORCH_CHECK(t.is_contiguous(), "fusion engine: tensor must be contiguous");
+  if (t.is_cuda()) TORCH_CHECK(gpu_backend_, "fusion engine: GPU tensor but no RCCL communicator");
   Request r;
   r.type = ReqType::ALLGATHER;
   r.name = name;
@@ -167,29 +182,14 @@ int64_t FusionEngine::allgather(at::Tensor t, const std::string& name) {
   shape[0] *= size_;
   r.output = at::empty(shape, t.options());
   r.t_enqueue = now();
-  if (t.is_cuda()) {
-    TORCH_CHECK(gpu_backend_, "fusion engine: GPU tensor but no RCCL communicator");
-    c10::hip::HIPGuardMasqueradingAsCUDA guard(t.device());
-    hip_ok(hipEventCreateWithFlags(&r.ready, hipEventDisableTiming), "event create");
-    hip_ok(hipEventRecord(r.ready, at::hip::getCurrentHIPStream(t.device().index()).stream()), "event record");
-  }
-  std::lock_guard<std::mutex> g(mu_);
-  r.handle = next_handle_++;
-  handles_[r.handle] = HandleState();
-  ++n_requests_;
-  close_open_locked();
-  Batch b;
-  b.bytes = t.numel() * t.element_size();
-  const int64_t h = r.handle;
-  b.reqs.push_back(std::move(r));
-  closed_.push_back(std::move(b));
-  cv_.notify_one();
-  return h;
+  record_ready(r);
+  return enqueue(std::move(r));
 }
 
 void FusionEngine::flush() {
+  // negotiation cycles run on their own; kept for API compatibility (wakes the engine early)
   std::lock_guard<std::mutex> g(mu_);
-  close_open_locked();
+  cv_.notify_one();
 }
 
 bool FusionEngine::poll(int64_t h) {
@@ -206,47 +206,105 @@ at::Tensor FusionEngine::wait(int64_t h) {
   {
     py::gil_scoped_release nogil;
     std::unique_lock<std::mutex> lk(mu_);
-    // a handle still sitting in the open batch is flushed: every rank reaches this point in the same
-    // request order, so the cut stays deterministic
-    for (const auto& r : open_.reqs)
-      if (r.handle == h) {
-        close_open_locked();
-        break;
-      }
     auto it = handles_.find(h);
     TORCH_CHECK(it != handles_.end(), "fusion engine: unknown handle ", h);
-    done_cv_.wait(lk, [&] { return handles_[h].done || stop_; });
+    done_cv_.wait(lk, [&] { return handles_[h].done; });
     st = handles_[h];
     handles_.erase(h);
   }
-  if (!st.error.empty()) throw std::runtime_error("HorovodInternalError: " + st.error);
+  if (!st.error.empty()) {
+    if (st.finished) (void)hipEventDestroy(st.finished);
+    throw std::runtime_error("HorovodInternalError: " + st.error);
+  }
   if (st.finished != nullptr) {
-    // order the caller's stream after the collective; no host block
-    const int dev = st.output.device().index();
-    hipError_t e = hipStreamWaitEvent(at::hip::getCurrentHIPStream(dev).stream(), st.finished, 0);
+    if (blocking_wait_) {
+      // host-side completion poll with liveness checks: a failed peer surfaces HERE
+      py::gil_scoped_release nogil;
+      const auto t0 = std::chrono::steady_clock::now();
+      std::string err;
+      for (;;) {
+        hipError_t q = hipEventQuery(st.finished);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) {
+          err = std::string("GPU error while waiting: ") + hipGetErrorString(q);
+          break;
+        }
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          if (!error_.empty()) err = error_;
+        }
+        if (err.empty() && comm_) {
+          const int ae = comm_->async_error();
+          if (ae != ncclSuccess && ae != ncclInProgress) err = std::string("RCCL async error: ") +
+                                                                ncclGetErrorString(static_cast<ncclResult_t>(ae));
+        }
+        if (err.empty() && std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s_)
+          err = "collective did not complete within " + std::to_string(timeout_s_) + " s";
+        if (!err.empty()) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+      }
+      if (!err.empty()) {
+        set_error(err);
+        (void)hipEventDestroy(st.finished);
+        throw std::runtime_error("HorovodInternalError: " + err);
+      }
+    } else {
+      // order the caller's stream after the collective; no host block (the engine's watchdog aborts the
+      // communicator if the batch never completes)
+      const int dev = st.output.device().index();
+      hipError_t e = hipStreamWaitEvent(at::hip::getCurrentHIPStream(dev).stream(), st.finished, 0);
+      hip_ok(e, "stream wait");
+    }
     (void)hipEventDestroy(st.finished);
-    hip_ok(e, "stream wait");
   }
   return st.output;
 }
 
-void FusionEngine::shutdown() {
+void FusionEngine::inject_error(const std::string& why) { set_error(why); }
+
+void FusionEngine::shutdown(bool abort) {
   {
     std::lock_guard<std::mutex> g(mu_);
-    if (stop_) return;
-    close_open_locked();
-    stop_ = true;
+    if (stopped_ && !worker_.joinable()) return;
+    stop_requested_ = true;
     cv_.notify_all();
   }
+  if (abort) set_error("Horovod has been shut down (abort)");
   if (worker_.joinable()) {
+    auto join = [&] {
+      if (!abort) {
+        worker_.join();
+        return;
+      }
+      // an aborted engine may have its thread inside a control collective with a dead peer: bounded wait
+      for (int i = 0; i < 400; ++i) {
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          if (stopped_) break;
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(5));
+      }
+      bool done;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        done = stopped_;
+      }
+      if (done)
+        worker_.join();
+      else
+        worker_.detach();  // Python keeps this engine object alive (hvd.core._retired)
+    };
     if (PyGILState_Check()) {
       py::gil_scoped_release nogil;
-      worker_.join();
+      join();
     } else {
-      worker_.join();
+      join();
     }
   }
+  for (auto& f : inflight_) (void)hipEventDestroy(f.done);
+  inflight_.clear();
   if (trace_.is_open()) {
+    std::lock_guard<std::mutex> g(trace_mu_);
     trace_ << "\n]\n";
     trace_.close();
   }
@@ -259,42 +317,279 @@ py::dict FusionEngine::stats() {
   d["batches"] = n_batches_;
   d["fused_requests"] = n_fused_requests_;
   d["bytes"] = n_bytes_;
+  d["cycles"] = n_cycles_;
   d["fusion_bytes"] = fusion_bytes_.load();
   d["backend"] = gpu_backend_ ? "rccl" : "python";
+  d["negotiated"] = control_ ? true : false;
+  d["error"] = error_;
   return d;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// failure state
+// ---------------------------------------------------------------------------------------------------
+void FusionEngine::fail_all_locked(const std::string& err) {
+  for (auto& r : unannounced_)
+    if (r.ready) (void)hipEventDestroy(r.ready);
+  for (auto& kv : announced_)
+    if (kv.second.ready) (void)hipEventDestroy(kv.second.ready);
+  unannounced_.clear();
+  announced_.clear();
+  table_.clear();
+  for (auto& kv : handles_) {
+    if (!kv.second.done) {
+      kv.second.done = true;
+      kv.second.error = err;
+    }
+  }
+  done_cv_.notify_all();
+}
+
+void FusionEngine::set_error(const std::string& err) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (error_.empty()) error_ = err;
+    fail_all_locked(error_);
+  }
+  // release any collective hung on a dead peer (kernels spinning on a connection exit on abort)
+  if (comm_) comm_->abort();
+}
+
+void FusionEngine::check_inflight() {
+  if (inflight_.empty()) return;
+  std::string err;
+  size_t k = 0;
+  for (auto& f : inflight_) {
+    hipError_t q = hipEventQuery(f.done);
+    if (q == hipSuccess) {
+      (void)hipEventDestroy(f.done);
+      continue;
+    }
+    if (q != hipErrorNotReady && err.empty()) err = std::string("GPU error: ") + hipGetErrorString(q);
+    if (err.empty() && now() - f.t_start > timeout_s_ * 1e6)
+      err = "RCCL collective did not complete within " + std::to_string(timeout_s_) + " s";
+    inflight_[k++] = f;
+  }
+  inflight_.resize(k);
+  if (err.empty() && comm_ && !inflight_.empty()) {
+    const int ae = comm_->async_error();
+    if (ae != ncclSuccess && ae != ncclInProgress)
+      err = std::string("RCCL async error: ") + ncclGetErrorString(static_cast<ncclResult_t>(ae));
+  }
+  if (!err.empty()) set_error(err);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// background loop: cycle = (coalesce) -> negotiate -> fuse -> execute
+// ---------------------------------------------------------------------------------------------------
 void FusionEngine::loop() {
   for (;;) {
-    Batch b;
+    bool stop_local;
+    std::vector<Request> announce;
     {
       std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || !closed_.empty(); });
-      if (closed_.empty() && stop_) return;
-      b = std::move(closed_.front());
-      closed_.pop_front();
+      auto has_work = [&] { return stop_requested_ || !unannounced_.empty() || !announced_.empty(); };
+      if (!has_work()) {
+        if (inflight_.empty())
+          cv_.wait(lk, has_work);
+        else
+          cv_.wait_for(lk, std::chrono::milliseconds(5), has_work);
+      }
+      if (!has_work()) {
+        lk.unlock();
+        check_inflight();
+        continue;
+      }
+      if (!error_.empty()) {  // failed engine: nothing is negotiated any more
+        stopped_ = true;
+        done_cv_.notify_all();
+        return;
+      }
     }
-    execute(b);
+    // coalesce a burst of enqueues (backward hooks) into one cycle, as Horovod's cycle time does
+    if (cycle_ms_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(static_cast<int64_t>(cycle_ms_ * 1e3)));
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      while (!unannounced_.empty()) {
+        announce.push_back(std::move(unannounced_.front()));
+        unannounced_.pop_front();
+      }
+      stop_local = stop_requested_;
+    }
+    std::vector<Request> ready;
+    bool stop = stop_local;
+    const double tn = now();
+    if (size_ == 1 || !control_) {
+      ready = std::move(announce);
+    } else {
+      try {
+        negotiate(announce, ready, stop);
+      } catch (std::exception& e) {
+        set_error(std::string("control plane: ") + e.what());
+        std::lock_guard<std::mutex> g(mu_);
+        stopped_ = true;
+        done_cv_.notify_all();
+        return;
+      }
+    }
+    ++n_cycles_;
+    if (trace_.is_open() && !ready.empty()) trace("engine", "NEGOTIATE", tn, now(), 0);
+    std::vector<Batch> batches = make_batches(ready);
+    for (auto& b : batches) execute(b);
+    check_inflight();
+    if (stop) {
+      std::lock_guard<std::mutex> g(mu_);
+      stopped_ = true;
+      fail_all_locked("Horovod has been shut down");
+      return;
+    }
   }
 }
 
+void FusionEngine::negotiate(std::vector<Request>& announce, std::vector<Request>& ready, bool& stop) {
+  // 1. this rank's message: stop flag + (name, signature) records, in local enqueue order
+  std::string msg(1, stop ? 'S' : '-');
+  for (const auto& r : announce) {
+    msg += r.name;
+    msg += kFieldSep;
+    msg += r.signature();
+    msg += kRecSep;
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& r : announce) {
+      std::string name = r.name;
+      announced_.emplace(std::move(name), std::move(r));
+    }
+  }
+  announce.clear();
+  // 2. all-gather the lengths, then the padded payloads, over the gloo control group
+  auto i64 = at::TensorOptions().dtype(at::kLong);
+  std::vector<at::Tensor> len_in{at::full({1}, static_cast<int64_t>(msg.size()), i64)};
+  std::vector<std::vector<at::Tensor>> len_out(1);
+  for (int i = 0; i < size_; ++i) len_out[0].push_back(at::empty({1}, i64));
+  control_->allgather(len_out, len_in)->wait();
+  std::vector<int64_t> lens(size_);
+  int64_t L = 1;
+  for (int i = 0; i < size_; ++i) {
+    lens[i] = len_out[0][i].data_ptr<int64_t>()[0];
+    L = std::max(L, lens[i]);
+  }
+  auto u8 = at::TensorOptions().dtype(at::kByte);
+  at::Tensor payload = at::zeros({L}, u8);
+  std::memcpy(payload.data_ptr(), msg.data(), msg.size());
+  std::vector<at::Tensor> pay_in{payload};
+  std::vector<std::vector<at::Tensor>> pay_out(1);
+  for (int i = 0; i < size_; ++i) pay_out[0].push_back(at::empty({L}, u8));
+  control_->allgather(pay_out, pay_in)->wait();
+  // 3. the decentralised coordinator: every rank applies the same rule to the same table
+  bool any_stop = false;
+  for (int r = 0; r < size_; ++r) {
+    const char* p = reinterpret_cast<const char*>(pay_out[0][r].data_ptr());
+    std::string m(p, static_cast<size_t>(lens[r]));
+    if (m.empty()) continue;
+    any_stop |= m[0] == 'S';
+    size_t pos = 1;
+    while (pos < m.size()) {
+      size_t fs = m.find(kFieldSep, pos), rs = m.find(kRecSep, pos);
+      if (fs == std::string::npos || rs == std::string::npos || fs > rs) break;
+      std::string name = m.substr(pos, fs - pos), sig = m.substr(fs + 1, rs - fs - 1);
+      pos = rs + 1;
+      auto it = table_.find(name);
+      if (it == table_.end()) {
+        NegEntry e;
+        e.signature = sig;
+        e.count = 1;
+        e.order = order_seq_++;
+        table_.emplace(name, std::move(e));
+      } else {
+        if (it->second.signature != sig && it->second.error.empty())
+          it->second.error = "mismatched request for tensor '" + name + "': rank " + std::to_string(r) + " sent [" +
+                             sig + "] but another rank sent [" + it->second.signature + "]";
+        ++it->second.count;
+      }
+    }
+  }
+  std::vector<std::pair<int64_t, std::string>> complete;
+  for (const auto& kv : table_)
+    if (kv.second.count >= size_) complete.emplace_back(kv.second.order, kv.first);
+  std::sort(complete.begin(), complete.end());
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (const auto& c : complete) {
+      auto te = table_.find(c.second);
+      auto it = announced_.find(c.second);
+      if (it != announced_.end()) {
+        Request r = std::move(it->second);
+        r.error = te->second.error;
+        announced_.erase(it);
+        ready.push_back(std::move(r));
+      }
+      table_.erase(te);
+    }
+  }
+  stop = any_stop;
+}
+
+std::vector<Batch> FusionEngine::make_batches(std::vector<Request>& ready) {
+  std::vector<Batch> out;
+  Batch open;
+  auto close = [&] {
+    if (!open.reqs.empty()) {
+      out.push_back(std::move(open));
+      open = Batch();
+    }
+  };
+  for (auto& r : ready) {
+    const int64_t bytes = r.tensor.numel() * static_cast<int64_t>(r.compress ? 2 : r.tensor.element_size());
+    if (r.type != ReqType::ALLREDUCE || !r.error.empty()) {
+      close();
+      Batch b;
+      b.bytes = r.tensor.numel() * r.tensor.element_size();
+      b.reqs.push_back(std::move(r));
+      out.push_back(std::move(b));
+      continue;
+    }
+    if (!open.reqs.empty()) {
+      const Request& h = open.reqs.front();
+      const bool same = h.tensor.device() == r.tensor.device() && h.tensor.scalar_type() == r.tensor.scalar_type() &&
+                        h.op == r.op && h.prescale == r.prescale && h.postscale == r.postscale &&
+                        h.compress == r.compress;
+      if (!same || open.bytes + bytes > fusion_bytes_.load() ||
+          static_cast<int>(open.reqs.size()) >= kMaxPackSegs * 8)
+        close();
+    }
+    open.bytes += bytes;
+    open.reqs.push_back(std::move(r));
+    if (open.bytes >= fusion_bytes_.load()) close();
+  }
+  close();
+  return out;
+}
+
 void FusionEngine::finish(Batch& b, const std::string& err, bool gpu_done) {
+  hipEvent_t watch = nullptr;
+  if (gpu_done && hipEventCreateWithFlags(&watch, hipEventDisableTiming) == hipSuccess)
+    (void)hipEventRecord(watch, comm_->stream());
   std::lock_guard<std::mutex> g(mu_);
   ++n_batches_;
   n_bytes_ += b.bytes;
   if (b.reqs.size() > 1) n_fused_requests_ += static_cast<int64_t>(b.reqs.size());
   for (size_t i = 0; i < b.reqs.size(); ++i) {
     Request& r = b.reqs[i];
-    HandleState& st = handles_[r.handle];
-    st.done = true;
-    st.error = err;
-    st.output = r.output;
-    if (gpu_done) {
-      // each handle owns an event (the waiter destroys it)
-      hipEvent_t e2 = nullptr;
-      if (hipEventCreateWithFlags(&e2, hipEventDisableTiming) == hipSuccess) {
-        (void)hipEventRecord(e2, comm_->stream());
-        st.finished = e2;
+    auto hs = handles_.find(r.handle);
+    if (hs != handles_.end() && !hs->second.done) {
+      HandleState& st = hs->second;
+      st.done = true;
+      st.error = err;
+      st.output = r.output;
+      if (gpu_done) {
+        // each handle owns an event (the waiter destroys it)
+        hipEvent_t e2 = nullptr;
+        if (hipEventCreateWithFlags(&e2, hipEventDisableTiming) == hipSuccess) {
+          (void)hipEventRecord(e2, comm_->stream());
+          st.finished = e2;
+        }
       }
     }
     if (r.ready != nullptr) {
@@ -302,22 +597,29 @@ void FusionEngine::finish(Batch& b, const std::string& err, bool gpu_done) {
       r.ready = nullptr;
     }
   }
+  if (watch) inflight_.push_back({watch, now()});
   done_cv_.notify_all();
 }
 
 void FusionEngine::execute(Batch& b) {
+  const Request& r0 = b.reqs.front();
+  if (!r0.error.empty()) {
+    finish(b, r0.error, false);
+    return;
+  }
   std::string err;
-  const bool gpu = b.reqs.front().tensor.is_cuda();
+  const bool gpu = r0.tensor.is_cuda();
   const double t_start = now();
   try {
     if (gpu) {
+      TORCH_CHECK(comm_ && comm_->valid(), "RCCL communicator is not valid (aborted?)");
       hip_ok(hipSetDevice(comm_->device()), "set device");
-      if (b.reqs.front().type == ReqType::ALLREDUCE)
+      if (r0.type == ReqType::ALLREDUCE)
         run_allreduce_gpu(b);
       else
         run_single_gpu(b.reqs.front());
     } else {
-      if (b.reqs.front().type == ReqType::ALLREDUCE)
+      if (r0.type == ReqType::ALLREDUCE)
         run_allreduce_cpu(b);
       else
         run_single_cpu(b.reqs.front());
@@ -332,10 +634,11 @@ void FusionEngine::execute(Batch& b) {
   if (trace_.is_open()) {
     for (auto& r : b.reqs) {
       trace(r.name, "QUEUE", r.t_enqueue, t_start, 0);
-      trace(r.name, b.reqs.front().type == ReqType::ALLREDUCE ? "ALLREDUCE" : "COLLECTIVE", t_start, t_end, b.bytes);
+      trace(r.name, r0.type == ReqType::ALLREDUCE ? "ALLREDUCE" : "COLLECTIVE", t_start, t_end, b.bytes);
     }
   }
   finish(b, err, gpu && err.empty());
+  if (!err.empty() && gpu) set_error(err);  // a failed RCCL call leaves the communicator unusable
 }
 
 void FusionEngine::run_allreduce_gpu(Batch& b) {

@@ -1,26 +1,35 @@
 // Horovod-style tensor-fusion engine (the reference's Horovod core is C++:
-// background thread, ready queue, fusion buffer, timeline).  MI355X-native design:
+// background thread, coordinator negotiation, fusion buffer, timeline).  MI355X-native design:
 //
-//  * Requests (allreduce / broadcast / allgather on named tensors) are enqueued by the framework thread
+//  * Requests (allreduce / broadcast / allgather on NAMED tensors) are enqueued by the framework thread
 //    and return a handle immediately.  GPU requests record a HIP event on the producer's stream, so the
-//    engine never blocks the host on compute.
-//  * Allreduce requests are fused into batches of up to `fusion_bytes` (default sized for xGMI, see
-//    parallel/xgmi.py) with a DETERMINISTIC cut rule (cumulative bytes / op change / explicit flush at
-//    synchronize) instead of Horovod's coordinator negotiation: every rank issues the same request
-//    sequence (true for DistributedOptimizer's backward hooks), so every rank cuts identical batches
-//    without a control-plane round trip per cycle.
-//  * A background thread executes closed batches in order.  GPU backend: wait producer events on the
-//    engine's high-priority comm stream -> ONE pack kernel (pre-scale, optional fp32->bf16 wire
-//    compression) -> RCCL all-reduce (ncclAvg for Average) -> ONE unpack kernel (post-scale) ->
-//    completion event.  Single-tensor batches without scaling/compression reduce in place (no copies).
-//    CPU backend: the same batching, the collective delegated to a Python callable (gloo process group).
-//  * synchronize(handle) makes the caller's stream wait on the completion event (GPU) or blocks until
-//    done (CPU); failures surface as exceptions (-> hvd.HorovodInternalError in Python).
-//  * Optional Chrome-trace timeline (HOROVOD_TIMELINE-compatible env var handled in Python).
+//    engine never blocks the host on compute.  A name may be outstanding only once per rank.
+//  * Negotiation (Horovod's controller): the background thread runs a control CYCLE every
+//    `cycle_ms` while anything is outstanding.  Each cycle every rank all-gathers, over a CPU (gloo)
+//    control process group, the names + signatures (type, dtype, element count, op, root, scaling) of the
+//    requests it enqueued since the last cycle.  Every rank then applies the SAME deterministic rule to
+//    the same gathered table (a decentralised coordinator): a name is ready once all ranks announced it;
+//    ready names are executed in first-announcement order (rank-major), so ranks whose hooks fire in
+//    different orders still cut identical fusion batches.  A signature mismatch fails that request on
+//    every rank ("mismatched ...") instead of mis-reducing.  A shutdown request from any rank ends the
+//    engine on all ranks at the end of that cycle.  World size 1 skips the collective.
+//  * Ready allreduces are fused into batches of up to `fusion_bytes` (same dtype/op/scaling/compression).
+//    GPU backend: wait producer events on the engine's high-priority comm stream -> ONE pack kernel
+//    (pre-scale, optional fp32->bf16 wire compression) -> RCCL all-reduce (ncclAvg for Average) -> ONE
+//    unpack kernel (post-scale) -> completion event.  Single-tensor batches without scaling or
+//    compression reduce in place.  CPU backend: the collective is delegated to a Python callable (gloo).
+//  * Failure detection: a control-plane error (dead peer: gloo connection reset / timeout) or an RCCL
+//    failure puts the engine in an ERROR state: every outstanding and later request fails with an error
+//    that Python raises as hvd.HorovodInternalError.  In-flight GPU batches are watched: an RCCL async
+//    error or a batch older than `timeout_s` aborts the communicator (which releases hung kernels).
+//    `blocking_wait` makes synchronize() poll the batch's completion on the host (elastic mode), so a
+//    failure surfaces from the very synchronize() that waits on it.
+//  * Optional Chrome-trace timeline (HOROVOD_TIMELINE), with NEGOTIATE / QUEUE / ALLREDUCE phases.
 #pragma once
 
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 
 #include <atomic>
 #include <condition_variable>
@@ -37,7 +46,7 @@
 
 namespace pde {
 
-enum class ReqType { ALLREDUCE, BROADCAST, ALLGATHER };
+enum class ReqType { ALLREDUCE = 0, BROADCAST = 1, ALLGATHER = 2 };
 
 struct Request {
   int64_t handle = 0;
@@ -51,6 +60,8 @@ struct Request {
   bool compress = false;  // fp32 -> bf16 on the wire
   hipEvent_t ready = nullptr;
   double t_enqueue = 0.0;
+  std::string error;      // set when negotiation rejected it
+  std::string signature() const;
 };
 
 struct Batch {
@@ -65,13 +76,30 @@ struct HandleState {
   hipEvent_t finished = nullptr;  // GPU: recorded on the comm stream after the batch
 };
 
+// one in-flight GPU batch watched for completion / failure
+struct Inflight {
+  hipEvent_t done = nullptr;
+  double t_start = 0.0;
+};
+
+// negotiation table entry (identical on every rank)
+struct NegEntry {
+  std::string signature;
+  int count = 0;
+  int64_t order = 0;
+  std::string error;
+};
+
 class FusionEngine {
  public:
-  FusionEngine(int rank, int size, int64_t fusion_bytes, const std::string& timeline_path);
+  FusionEngine(int rank, int size, int64_t fusion_bytes, const std::string& timeline_path, double cycle_ms);
   ~FusionEngine();
 
   void set_rccl(std::shared_ptr<RcclComm> comm);
   void set_py_backend(py::object allreduce_fn, py::object broadcast_fn, py::object allgather_fn);
+  void set_control(c10::intrusive_ptr<c10d::ProcessGroup> pg);
+  void set_timeout(double seconds) { timeout_s_ = seconds; }
+  void set_blocking_wait(bool b) { blocking_wait_ = b; }
 
   int64_t allreduce(at::Tensor t, at::Tensor out, const std::string& name, int op, double prescale,
                     double postscale, bool compress);
@@ -80,41 +108,61 @@ class FusionEngine {
   void flush();
   bool poll(int64_t h);
   at::Tensor wait(int64_t h);
-  void shutdown();
+  void shutdown(bool abort);
   py::dict stats();
   int64_t fusion_bytes() const { return fusion_bytes_; }
   void set_fusion_bytes(int64_t b) { fusion_bytes_ = b; }
+  std::string error() {
+    std::lock_guard<std::mutex> g(mu_);
+    return error_;
+  }
+  // test hook: put the engine into the error state as a failed collective would
+  void inject_error(const std::string& why);
 
  private:
+  int64_t enqueue(Request&& r);
   void loop();
+  void negotiate(std::vector<Request>& announce, std::vector<Request>& ready, bool& stop);
   void execute(Batch& b);
   void run_allreduce_gpu(Batch& b);
   void run_allreduce_cpu(Batch& b);
   void run_single_gpu(Request& r);
   void run_single_cpu(Request& r);
   void finish(Batch& b, const std::string& err, bool gpu_done);
-  void close_open_locked();
+  void fail_all_locked(const std::string& err);
+  void set_error(const std::string& err);
+  void check_inflight();
+  std::vector<Batch> make_batches(std::vector<Request>& ready);
   double now() const;
   void trace(const std::string& name, const std::string& phase, double t0, double t1, int64_t bytes);
 
   int rank_, size_;
   std::atomic<int64_t> fusion_bytes_;
+  double cycle_ms_;
   std::shared_ptr<RcclComm> comm_;
+  c10::intrusive_ptr<c10d::ProcessGroup> control_;
   py::object py_allreduce_, py_broadcast_, py_allgather_;
   bool gpu_backend_ = false;
+  double timeout_s_ = 300.0;
+  bool blocking_wait_ = false;
 
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
-  Batch open_;
-  std::deque<Batch> closed_;
+  std::deque<Request> unannounced_;            // enqueued since the last cycle
+  std::map<std::string, Request> announced_;   // announced by this rank, not yet globally ready
+  std::map<std::string, NegEntry> table_;      // negotiation state (same on every rank)
+  int64_t order_seq_ = 0;
   std::map<int64_t, HandleState> handles_;
   int64_t next_handle_ = 1;
-  bool stop_ = false;
+  bool stop_requested_ = false;
+  bool stopped_ = false;
+  std::string error_;
   std::thread worker_;
   at::Tensor fused_;  // reusable fusion buffer (device or host)
+  std::vector<Inflight> inflight_;
 
   // stats
-  int64_t n_requests_ = 0, n_batches_ = 0, n_bytes_ = 0, n_fused_requests_ = 0;
+  int64_t n_requests_ = 0, n_batches_ = 0, n_bytes_ = 0, n_fused_requests_ = 0, n_cycles_ = 0;
 
   std::mutex trace_mu_;
   std::ofstream trace_;

@@ -1,0 +1,62 @@
+// One-shot peer all-reduce over xGMI for latency-bound buckets.
+//
+// An MI355X node is a full mesh: every GPU reaches each of its 7 peers over a direct xGMI link.  For a
+// small gradient bucket (the MNIST CNN's 87 KB, the hybrid fc's 544 B) a ring all-reduce is a chain of
+// 2(N-1) latency-bound hops; here each rank instead
+//   1. copies its bucket into its own IPC-exported, uncached staging slot,
+//   2. raises one flag per (workgroup, rank) in EVERY peer's flag array (system-scope release),
+//   3. waits for the N flags of its workgroup (one polling lane per peer, bounded spin),
+//   4. reads the same chunk from all N slots over xGMI (7 links in parallel) and sums them in rank order.
+// Every rank sums identical values in the same order, so the result is bit-identical on all ranks.
+//
+// Synchronisation is epoch based and needs no reset between calls: each workgroup keeps its own
+// monotonically increasing epoch in device memory (so the kernel is hipGraph-capturable and replays
+// advance it), flags are written with the epoch value, staging alternates between two slots (a peer can
+// be at most one call ahead: it cannot pass the next call's flag wait without this rank).  Spins are
+// bounded by s_memrealtime; a timeout sets an error word and the workgroup drains (never a hung grid).
+//
+// Memory: one hipExtMallocWithFlags(hipDeviceMallocUncached) allocation per rank = [flags | slot0 | slot1],
+// exported with hipIpcGetMemHandle; peers map it with hipIpcOpenMemHandle.  Uncached memory keeps the
+// staged bytes and flags coherent between GPUs (and between processes sharing one GPU in rehearsals).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace pde {
+
+constexpr int kXgmiMaxRanks = 8;
+
+class XgmiAllreduce {
+ public:
+  XgmiAllreduce(int rank, int size, int device, int64_t max_bytes, int blocks, double timeout_s);
+  ~XgmiAllreduce();
+  XgmiAllreduce(const XgmiAllreduce&) = delete;
+  XgmiAllreduce& operator=(const XgmiAllreduce&) = delete;
+
+  std::string ipc_handle() const;                   // this rank's exported allocation
+  void open(const std::vector<std::string>& handles);  // all ranks' handles, in rank order
+  // dst[i] = scale * sum_r src_r[i]; fp32; src may alias dst; n * 4 <= max_bytes; stream-ordered
+  void allreduce(const float* src, float* dst, int64_t n, float scale, hipStream_t s);
+  int error();   // 0, or 1 when some workgroup timed out waiting for a peer (synchronises the device)
+  void close();
+  int rank() const { return rank_; }
+  int size() const { return size_; }
+  int64_t max_bytes() const { return max_bytes_; }
+  int64_t calls() const { return calls_; }
+
+ private:
+  int rank_, size_, device_, blocks_;
+  int64_t max_bytes_, slot_bytes_, flag_bytes_;
+  uint64_t timeout_ticks_;
+  char* local_ = nullptr;       // my exported allocation
+  uint32_t* state_ = nullptr;   // [blocks] epochs + [1] error word (device-local)
+  std::vector<char*> peers_;    // mapped bases, peers_[rank_] == local_
+  bool opened_ = false;
+  int64_t calls_ = 0;
+};
+
+}  // namespace pde

@@ -32,7 +32,7 @@ EXTENSIONS = {
         ["bindings.cpp"],
     ),
     "_comm": (
-        ["comm/pack.hip"],
+        ["comm/pack.hip", "comm/xgmi_allreduce.hip"],
         ["comm/comm_manager.cpp", "comm/fusion_engine.cpp", "comm/comm_bindings.cpp"],
     ),
 }

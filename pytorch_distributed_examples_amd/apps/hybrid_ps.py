@@ -116,60 +116,106 @@ def run_worker(rank, world_size, epochs, ports, use_gpu):
 # ------------------------------------------------------------------------------------------------
 # ResNet-50 hybrid: pipeline stages x data parallel (SPMD under torchrun)
 # ------------------------------------------------------------------------------------------------
-def run_resnet_hybrid(stages: int, dp: int, steps: int, warmup: int, batch: int, split_size: int,
-                      schedule: str = "gpipe", quiet: bool = False):
-    from ..data.synthetic import resnet_batch
-    from ..models.resnet import ResNetShard1, ResNetShard2
-    from ..ops.optim import FusedSGD
-    from ..parallel import dist as pdist
-    from ..parallel.pipeline import PipelineEngine, hybrid_groups
+class ResNetPipelineDP:
+    """ResNet-50 in ``stages`` = 2 pipeline stages (one process / GPU each) x ``world / 2`` data-parallel
+    replicas of every stage (SPMD: every rank builds the same object).
 
-    ctx = pdist.init_distributed()
+    * pipelines are consecutive ranks (0,1), (2,3), ...; stage ``s``'s replicas {s, s+2, ...} form the
+      data-parallel group (``ncclCommSplit``-equivalent ``dist.new_group`` for control, and on GPUs a
+      stream-ordered RCCL communicator of our own for the gradient all-reduce, so the whole step --
+      micro-batch forwards/backwards, P2P sends/recvs, all-reduce, SGD -- records into ONE hipGraph);
+    * ``split_size`` is the micro-batch size (reference quirk Q2), BatchNorm statistics are per micro-batch
+      (Q17), each replica draws its own batch (seeded by pipeline index);
+    * ``step()`` runs one full training step and returns the loss on the last stage (a zero elsewhere).
+    """
+
+    def __init__(self, ctx, batch: int = 32, split_size: int = 8, image: int = 128, schedule: str = "gpipe",
+                 lr: float = 0.05, tag: str = "hybrid", seed: int = 1234):
+        from ..data.synthetic import resnet_batch
+        from ..models.resnet import ResNetShard1, ResNetShard2
+        from ..ops.optim import FusedSGD
+        from ..parallel.pipeline import PipelineEngine, hybrid_groups
+
+        self.stages = 2
+        world = ctx.world_size
+        if world % self.stages:
+            raise SystemExit(f"the ResNet-50 pipeline needs an even number of ranks (one per stage), got {world}")
+        if batch % split_size:
+            raise SystemExit(f"batch {batch} is not a multiple of the micro-batch size {split_size}")
+        self.ctx = ctx
+        self.dp = world // self.stages
+        self.batch, self.split_size = batch, split_size
+        _, dps = hybrid_groups(world, self.stages)
+        self.stage = ctx.rank % self.stages
+        self.last = self.stage == self.stages - 1
+        groups = [dist.new_group(g) for g in dps]  # every rank creates every group (c10d requirement)
+        self.dp_group = groups[self.stage]
+        dev = ctx.device
+        self.module = (ResNetShard1() if self.stage == 0 else ResNetShard2()).to(dev)
+        self.comm = None
+        if dev.type == "cuda" and self.dp > 1 and ctx.backend == "nccl":
+            from ..parallel.rccl import StreamComm
+
+            self.comm = StreamComm(dev, group=self.dp_group)
+        self.ddp = DistributedDataParallel(self.module, process_group=self.dp_group, overlap=False,
+                                           broadcast_buffers=False, comm=self.comm)
+        self.opt = FusedSGD(self.module.parameters(), lr=lr)
+        prev_rank = ctx.rank - 1 if self.stage > 0 else None
+        next_rank = ctx.rank + 1 if not self.last else None
+        self.engine = PipelineEngine(self.module, self.stage, self.stages, prev_rank, next_rank, dev,
+                                     loss_fn=OF.mse_loss, schedule=schedule, tag=tag)
+        g = torch.Generator().manual_seed(seed + ctx.rank // self.stages)
+        x, y = resnet_batch(batch, image, 1000, dev, g)
+        self.n_mb = batch // split_size
+        self.xs, self.ys = list(x.split(split_size)), list(y.split(split_size))
+        self._zero = torch.zeros((), device=dev)
+
+    @property
+    def images_per_step(self) -> int:
+        return self.batch * self.dp
+
+    def step(self):
+        self.ddp.zero_grad()
+        loss = self.engine.train_step(self.xs if self.stage == 0 else None, self.ys if self.last else None,
+                                      self.n_mb)
+        self.ddp.sync_gradients()
+        self.opt.step()
+        return loss if loss is not None else self._zero
+
+    def close(self):
+        self.engine.close()
+        if self.comm is not None:
+            self.comm.destroy()
+
+
+def run_resnet_hybrid(stages: int, dp: int, steps: int, warmup: int, batch: int, split_size: int,
+                      schedule: str = "gpipe", quiet: bool = False, image: int = 128, device: str | None = None):
+    from ..parallel import dist as pdist
+
+    ctx = pdist.init_distributed(device=device)
     world = ctx.world_size
     assert world == stages * dp, f"world {world} != stages {stages} x dp {dp}"
     assert stages == 2, "ResNet-50 is split at layer2|layer3 (2 stages)"
-    pipes, dps = hybrid_groups(world, stages)
-    stage = ctx.rank % stages
-    groups = [dist.new_group(g) for g in dps]  # every rank creates every group (c10d requirement)
-    my_dp = groups[stage]
-    module = (ResNetShard1() if stage == 0 else ResNetShard2()).to(ctx.device)
-    ddp = DistributedDataParallel(module, process_group=my_dp, overlap=False, broadcast_buffers=False)
-    opt = FusedSGD(module.parameters(), lr=0.05)
-    prev_rank = ctx.rank - 1 if stage > 0 else None
-    next_rank = ctx.rank + 1 if stage < stages - 1 else None
-    eng = PipelineEngine(module, stage, stages, prev_rank, next_rank, ctx.device, loss_fn=OF.mse_loss,
-                         schedule=schedule, tag="hybrid")
-    g = torch.Generator().manual_seed(1234 + ctx.rank // stages)
-    x, y = resnet_batch(batch, 128, 1000, ctx.device, g)
-    n_mb = batch // split_size
-    xs, ys = list(x.split(split_size)), list(y.split(split_size))
-
-    def step():
-        ddp.zero_grad()
-        loss = eng.train_step(xs if stage == 0 else None, ys if stage == stages - 1 else None, n_mb)
-        ddp.sync_gradients()
-        opt.step()
-        return loss
-
+    pipe = ResNetPipelineDP(ctx, batch, split_size, image, schedule)
     for _ in range(warmup):
-        step()
+        pipe.step()
     pdist.barrier(ctx)
     if ctx.device.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     loss = None
     for _ in range(steps):
-        loss = step()
+        loss = pipe.step()
     pdist.barrier(ctx)
     if ctx.device.type == "cuda":
         torch.cuda.synchronize()
     dt = pdist.max_over_ranks(time.perf_counter() - t0, ctx.device)
-    img_s = batch * dp * steps / dt
-    if not quiet and stage == stages - 1 and ctx.rank == stages - 1:
+    img_s = pipe.images_per_step * steps / dt
+    if not quiet and ctx.rank == stages - 1:
         print(f"resnet50 hybrid pp{stages} x dp{dp}: loss {loss.item():.4f} | {dt / steps * 1e3:.2f} ms/step | "
               f"{img_s:.1f} images/s (node)", flush=True)
-    eng.close()
-    return img_s, dt / steps
+    pipe.close()
+    return pipe, img_s, dt / steps
 
 
 def main(argv=None):
@@ -184,12 +230,13 @@ def main(argv=None):
     ap.add_argument("--batch-size", type=int, default=32)
     ap.add_argument("--split-size", type=int, default=8)
     ap.add_argument("--schedule", default="gpipe", choices=["gpipe", "1f1b"])
+    ap.add_argument("--image", type=int, default=128)
     args = ap.parse_args(argv)
     if args.model == "resnet50":
         world = int(os.environ.get("WORLD_SIZE", "1"))
         dp = args.dp or max(1, world // args.stages)
         run_resnet_hybrid(args.stages, dp, args.steps, args.warmup, args.batch_size, args.split_size,
-                          args.schedule)
+                          args.schedule, image=args.image, device="cpu" if args.device == "cpu" else None)
         dist.destroy_process_group()
         return
     use_gpu = torch.cuda.is_available() and args.device != "cpu"

@@ -1,0 +1,322 @@
+"""Images/sec benchmark harness behind the root ``bench.py`` (BASELINE.json metric).
+
+Workloads (``--model``), one process per GPU, synthetic data resident in HBM, random init:
+
+* ``cnn`` (default) -- BASELINE config 1: the reference's MNIST CNN ``Net`` (horovod/mnist_horovod.py:9-25)
+  at its per-worker batch 1024 (:44), SGD lr 0.01 (:50), NLL on log_softmax; data parallel over RCCL.  The
+  whole forward+loss+backward runs in one fused kernel (csrc/kernels/cnn_fused.hip).
+* ``mlp`` -- the elastic-DDP script's 5x1024 MLP (pytorch_elastic/mnist_ddp_elastic.py:133-173), batch 128,
+  Adam 1e-3, cross-entropy; data parallel.
+* ``resnet50`` -- ResNet-50 at 128x128, batch 32, MSE, SGD 0.05, pure data parallel.
+* ``resnet50_pp`` -- BASELINE configs 3 and 4: the 2-stage ResNet-50 of rpc/model_parallel_ResNet50.py
+  (stem+layer1+layer2 | layer3+layer4+fc, :85-139), batch 32 split into micro-batches of ``--split-size``
+  (the reference's ``split_size`` semantics, :171, quirk Q2), one stage per GPU, activations and their
+  gradients GPU->GPU over RCCL P2P (one direct xGMI link per stage pair), and ``world/2``-way data parallel
+  over each stage's replicas (world 2 = config 3, world 8 = pp2 x dp4 = config 4).
+
+Every timed step is a complete training step (forward, backward, gradient all-reduce, optimizer update);
+steps are recorded into hipGraphs (several steps per replay for the launch-bound MNIST nets).  W warmup steps
+run untimed; then K steps are timed between barrier + synchronize pairs and the MAX over ranks is taken.
+
+Multi-GPU runs verify themselves: the world size must equal ``--gpus``, and every rank all-reduces a
+checksum over the GPU data-plane communicator and reads back RCCL's own rank count (``rccl_nranks``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+from ..parallel import dist as pdist
+
+# BASELINE.json names one metric for the whole suite; ``config`` says which of its workloads this run measured.
+METRIC = "images/sec (whole node) MNIST DDP + ResNet50 RPC-MP at 1/2/4/8 MI355X"
+BASELINE_CONFIG = {"cnn": "1: MNIST CNN DDP bf16, RCCL allreduce over xGMI",
+                   "mlp": "0/1 workload of mnist_ddp_elastic.py (5x1024 MLP DDP)",
+                   "resnet50": "ResNet-50 128px data parallel (no BASELINE config; kernel reference point)",
+                   "resnet50_pp": "3 (world 2: ResNet50 model-parallel across 2 MI355X) / "
+                                  "4 (world 8: 2-stage pipeline x 4-way DDP)"}
+# The reference's own numbers, measured on CPU by the survey (no published figures exist).
+# Only same-workload, same-world comparisons are reported.
+REFERENCE_IMG_S = {("mlp", 1): 7452.0, ("mlp", 2): 2630.0, ("mlp", 4): 4620.0,
+                   ("resnet50_pp", 2): 18.0}
+DEFAULT_BATCH = {"cnn": 1024, "mlp": 128, "resnet50": 32, "resnet50_pp": 32}
+MODEL_NAMES = {"cnn": "mnist_cnn_Net", "mlp": "mnist_mlp_5x1024", "resnet50": "resnet50_128px",
+               "resnet50_pp": "resnet50_128px_2stage"}
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); bench.py launches them when run without torchrun")
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--model", default="cnn", choices=["cnn", "mlp", "resnet50", "resnet50_pp", "resnet50_hybrid"])
+    ap.add_argument("--batch", type=int, default=None, help="per-replica batch")
+    ap.add_argument("--split-size", type=int, default=8, help="resnet50_pp: micro-batch size (reference: 4 or 8)")
+    ap.add_argument("--schedule", default="gpipe", choices=["gpipe", "1f1b"], help="resnet50_pp schedule")
+    ap.add_argument("--image", type=int, default=None, help="override the image size (CPU plumbing tests)")
+    ap.add_argument("--no-graph", action="store_true", help="run the step eagerly (no hipGraph capture)")
+    ap.add_argument("--graph-steps", type=int, default=10,
+                    help="consecutive training steps recorded into one hipGraph (each reads its own batch)")
+    ap.add_argument("--generic", action="store_true", help="CNN: layer-by-layer kernels instead of the fused step")
+    ap.add_argument("--device", default="auto", choices=["auto", "cpu"], help="cpu: contract/plumbing check only")
+    args = ap.parse_args(argv)
+    if args.model == "resnet50_hybrid":
+        args.model = "resnet50_pp"
+    return args
+
+
+class Workload:
+    """What the timing loop needs: a step callable, an optional multi-step graph, the images per step."""
+
+    def __init__(self, step, images_per_step, parallelism, **info):
+        self.step = step              # step(i) -> loss (device tensor or None)
+        self.group = None             # CapturedSteps running several steps per replay
+        self.images_per_step = images_per_step
+        self.parallelism = parallelism
+        self.info = info
+        self.loss_rank = 0            # the rank whose loss is reported
+
+
+def _data_plane_check(ctx, comm) -> int:
+    """Checksum all-reduce over the data-plane communicator; returns the rank count it reports."""
+    n = ctx.world_size
+    if n == 1:
+        return 1
+    want = n * (n + 1) / 2
+    t = torch.full((16,), float(ctx.rank + 1), device=ctx.device)
+    if comm is not None:
+        comm.allreduce_(t)
+        nranks = comm.rccl.nranks()
+    else:
+        dist.all_reduce(t)
+        nranks = dist.get_world_size()
+    if not bool((t == want).all()):
+        raise RuntimeError(f"rank {ctx.rank}: data-plane checksum {t[0].item()} != {want}")
+    if nranks != n:
+        raise RuntimeError(f"rank {ctx.rank}: communicator reports {nranks} ranks, world is {n}")
+    return nranks
+
+
+def _capture(step_fn, batches, graph_steps, rank):
+    """(single-step graph, multi-step graph) or (None, None) when capture is not possible."""
+    from ..utils.graph import CapturedStep, CapturedSteps
+
+    try:
+        one = CapturedStep(step_fn, batches[0], warmup=3).capture()
+        group = None
+        if graph_steps > 1:
+            group = CapturedSteps(step_fn, [batches[j % len(batches)] for j in range(graph_steps)], warmup=1).capture()
+        return one, group
+    except Exception as exc:  # capture unsupported (e.g. a collective that cannot be captured): run eagerly
+        if rank == 0:
+            print(f"[bench] hipGraph capture failed, running eagerly: {exc}", file=sys.stderr)
+        from .. import _native
+
+        torch.cuda.synchronize()
+        _native.C().clear_last_error()  # the aborted capture leaves a sticky "last error" behind
+        return None, None
+
+
+def build_data_parallel(args, ctx, batch) -> Workload:
+    from ..ops import functional as OF
+    from ..ops.optim import FusedAdam, FusedSGD
+    from ..parallel.ddp import DistributedDataParallel
+
+    dev = ctx.device
+    on_gpu = dev.type == "cuda"
+    if args.model in ("cnn", "mlp"):
+        from ..data.synthetic import SyntheticMNIST
+
+        data = SyntheticMNIST(max(8 * batch, 16384), device=dev, seed=0)
+
+        def batch_fn(i):
+            return data.batch(i, batch)
+
+        if args.model == "cnn":
+            from ..models.cnn import Net
+
+            model = Net().to(dev)
+            opt = FusedSGD(model.parameters(), lr=0.01)
+            loss_fn = OF.nll_loss
+        else:
+            from ..models.mlp import reference_mlp
+
+            model = reference_mlp().to(dev)
+            opt = FusedAdam(model.parameters(), lr=1e-3)
+            loss_fn = OF.cross_entropy
+    else:
+        from ..data.synthetic import resnet_batch
+        from ..models.resnet import ResNet50
+
+        model = ResNet50().to(dev)
+        g = torch.Generator().manual_seed(0)
+        batches = [resnet_batch(batch, args.image or 128, 1000, dev, g) for _ in range(2)]
+        opt = FusedSGD(model.parameters(), lr=0.05)
+        loss_fn = OF.mse_loss
+
+        def batch_fn(i):
+            return batches[i % 2]
+
+    use_graph = not args.no_graph and on_gpu and (ctx.world_size == 1 or ctx.backend == "nccl")
+    # GPU data plane for world > 1: our stream-ordered RCCL communicator (c10d's ProcessGroupNCCL aborts the
+    # process when its work is captured into a hipGraph on ROCm -- parallel/rccl.py)
+    comm = None
+    if on_gpu and ctx.world_size > 1 and ctx.backend == "nccl":
+        from ..parallel.rccl import StreamComm
+
+        comm = StreamComm(dev)
+    nranks = _data_plane_check(ctx, comm)
+    if comm is not None and os.environ.get("PDE_XGMI", "1") != "0":
+        # latency-bound buckets (the CNN's single 87 KB bucket) take the one-shot xGMI peer all-reduce
+        from ..parallel.xgmi_allreduce import RoutedComm, XgmiAllreduce
+
+        comm = RoutedComm(comm, XgmiAllreduce(dev))
+    fused = None
+    if args.model == "cnn" and not args.generic and on_gpu:
+        # whole-network fused kernel: gradients land in the DDP flat buffer (forward layout), then one
+        # all-reduce and one fused SGD launch that also refreshes the kernel's bf16 weight fragments
+        # (world 1: the SGD runs inside the slab reduction)
+        from ..models.cnn_fused import FusedCNN
+
+        fused = FusedCNN(model)
+        ddp = DistributedDataParallel(model, overlap=False, param_order="forward", comm=comm)
+    else:
+        ddp = DistributedDataParallel(model, overlap=not use_graph, comm=comm)
+
+    def train_step(x, y):
+        if fused is not None:
+            if ctx.world_size == 1:
+                return fused.forward_backward(x, y, grad_out=ddp.flat_grad, sgd=opt)
+            loss = fused.forward_backward(x, y, grad_out=ddp.flat_grad)
+            ddp.sync_gradients()
+            fused.sgd_step(opt, ddp.flat_grad)
+            return loss
+        ddp.zero_grad()
+        loss = loss_fn(ddp(x), y)
+        loss.backward()
+        if not ddp.overlap:  # graph mode: buckets reduced after backward on the capturing stream
+            ddp.sync_gradients()
+        opt.step()
+        return loss
+
+    one = group = None
+    if use_graph:
+        one, group = _capture(train_step, [batch_fn(j) for j in range(max(1, args.graph_steps))],
+                              args.graph_steps, ctx.rank)
+        if one is None and fused is None:  # eager fallback: overlapped buckets (hooks) again
+            ddp.remove_hooks()
+            ddp = DistributedDataParallel(model, overlap=True, comm=comm)
+
+    def step(i):
+        x, y = batch_fn(i)
+        return one(x, y) if one is not None else train_step(x, y)
+
+    routed = getattr(comm, "routed", None)
+    w = Workload(step, batch * ctx.world_size, f"dp{ctx.world_size}", hipgraph=one is not None,
+                 fused_step=fused is not None, rccl_nranks=nranks,
+                 steps_per_graph=group.steps if group is not None else (1 if one is not None else 0),
+                 allreduce="xgmi-oneshot<=%dB+rccl" % comm.threshold if routed is not None else
+                 ("rccl" if comm is not None else ("gloo" if ctx.world_size > 1 else "none")))
+    w.group = group
+    if routed is not None:
+        w.check = comm.xgmi.check  # raises if any one-shot call timed out waiting for a peer
+    return w
+
+
+def build_pipeline(args, ctx, batch) -> Workload:
+    """ResNet-50 split in 2 stages (one GPU each) x world/2 data-parallel replicas of each stage
+    (:class:`..apps.hybrid_ps.ResNetPipelineDP`); the whole pipelined step is one hipGraph per rank."""
+    from ..apps.hybrid_ps import ResNetPipelineDP
+
+    on_gpu = ctx.device.type == "cuda"
+    nranks = _data_plane_check(ctx, None)
+    pipe = ResNetPipelineDP(ctx, batch, args.split_size, args.image or 128, args.schedule, tag="bench")
+    one = None
+    if not args.no_graph and on_gpu and ctx.backend == "nccl":
+        one, _ = _capture(pipe.step, [()], 1, ctx.rank)
+
+    def step(i):
+        return one() if one is not None else pipe.step()
+
+    w = Workload(step, pipe.images_per_step, f"pp{pipe.stages}xdp{pipe.dp}", hipgraph=one is not None,
+                 fused_step=False, rccl_nranks=nranks, steps_per_graph=1 if one is not None else 0,
+                 split_size=args.split_size, microbatches=pipe.n_mb, schedule=args.schedule)
+    w.loss_rank = pipe.stages - 1
+    w.close = pipe.close
+    return w
+
+
+def run_steps(work: Workload, first: int, n: int):
+    loss = None
+    i = 0
+    while work.group is not None and n - i >= work.group.steps:
+        loss = work.group.replay()
+        i += work.group.steps
+    while i < n:
+        loss = work.step(first + i)
+        i += 1
+    return loss
+
+
+def _report_loss(work, ctx, loss):
+    """The loss of the reporting rank (the last pipeline stage for resnet50_pp), as a float on rank 0."""
+    t = torch.zeros(1, dtype=torch.float32, device=ctx.device)
+    if loss is not None and ctx.rank == work.loss_rank:
+        t.copy_(loss.detach().float().reshape(-1)[:1])
+    if ctx.world_size > 1 and work.loss_rank != 0:
+        dist.broadcast(t, work.loss_rank)
+    return float(t.item())
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    batch = args.batch or DEFAULT_BATCH[args.model]
+    ctx = pdist.init_distributed(device="cpu" if args.device == "cpu" else None)
+    if args.gpus is not None and args.gpus != ctx.world_size:
+        raise SystemExit(f"--gpus {args.gpus} but the job has {ctx.world_size} ranks (WORLD_SIZE); "
+                         "run bench.py without torchrun to have it launch the ranks")
+    on_gpu = ctx.device.type == "cuda"
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
+    work = build_pipeline(args, ctx, batch) if args.model == "resnet50_pp" else build_data_parallel(args, ctx, batch)
+    run_steps(work, 0, args.warmup)
+    pdist.barrier(ctx)
+    sync()
+    t0 = time.perf_counter()
+    loss = run_steps(work, args.warmup, args.steps)
+    pdist.barrier(ctx)
+    sync()
+    dt = time.perf_counter() - t0
+    if hasattr(work, "check"):
+        work.check()
+    dt = pdist.max_over_ranks(dt, ctx.device)
+    final_loss = _report_loss(work, ctx, loss)
+    value = work.images_per_step * args.steps / dt
+    same_shape = args.image is None and batch == DEFAULT_BATCH[args.model]
+    ref = REFERENCE_IMG_S.get((args.model, ctx.world_size)) if same_shape else None
+    if ctx.rank == 0:
+        cfg = {"model": MODEL_NAMES[args.model], "baseline_config": BASELINE_CONFIG[args.model],
+               "global_batch": work.images_per_step, "seq_len": None,
+               "image": "1x28x28" if args.model in ("cnn", "mlp") else f"3x{args.image or 128}x{args.image or 128}",
+               "parallelism": work.parallelism, "final_loss": round(final_loss, 4)}
+        cfg.update(work.info)
+        print(json.dumps({
+            "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": ctx.world_size,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1000.0, 4),
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(value / ref, 2) if ref else None,
+            "dtype": "bf16" if on_gpu else "fp32", "data": "synthetic (random init)", "config": cfg,
+        }), flush=True)
+    if hasattr(work, "close"):
+        work.close()
+    pdist.shutdown()

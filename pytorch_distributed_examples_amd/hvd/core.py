@@ -1,23 +1,32 @@
 """Horovod-compatible core API on the MI355X runtime.
 
-``init()`` joins the job (torchrun env, the elastic driver's rendezvous, or a 1-process world), creates
-the c10d process group used for control messages and -- on GPUs -- an RCCL communicator of our own
-(:class:`_comm.RcclComm`, unique id exchanged through the c10d store) driving the C++ tensor-fusion
-engine (:class:`_comm.FusionEngine`).  On CPU the same engine batches tensors and calls the gloo group.
+``init()`` joins the job (torchrun env, the elastic driver's rendezvous, or a 1-process world).  Like
+Horovod (Gloo controller + NCCL data plane), the CONTROL plane is always CPU/gloo and the GPU DATA plane
+is RCCL:
+
+* the default process group is gloo (object broadcasts, barriers, elastic host-update checks), so a dead
+  peer surfaces as a connection error -- never as a hung or watchdog-aborted GPU collective;
+* the C++ tensor-fusion engine (:class:`_comm.FusionEngine`) gets a DEDICATED gloo group for its
+  negotiation cycles (and the CPU data plane), used only from the engine thread;
+* on GPUs the engine drives an RCCL communicator of our own (:class:`_comm.RcclComm`, unique id exchanged
+  through the c10d store) on a high-priority stream.
 
 Collectives return handles; ``synchronize(handle)`` orders the caller's stream after the collective (GPU)
-or blocks (CPU).  Environment knobs (Horovod names where one exists):
+or blocks (CPU); engine failures raise :class:`HorovodInternalError`.  Environment knobs (Horovod names
+where one exists):
 
     HOROVOD_FUSION_THRESHOLD   fusion buffer bytes (default: xGMI policy, 64 MiB cap)
+    HOROVOD_CYCLE_TIME         negotiation cycle in ms (default 0.5)
     HOROVOD_TIMELINE           Chrome-trace file written by the engine
-    PDE_HVD_TIMEOUT            seconds before a stuck collective is declared failed (GPU, default 300)
+    PDE_HVD_TIMEOUT            seconds before a stuck collective / control cycle is declared failed (300)
+    PDE_HVD_BLOCKING_WAIT      1: synchronize() polls GPU completion on the host with liveness checks
+                               (default on under the elastic driver, so failures raise from synchronize)
 """
 from __future__ import annotations
 
 import datetime
 import os
 import threading
-import time
 
 import torch
 import torch.distributed as dist
@@ -55,6 +64,8 @@ class _Ctx:
         self.engine = None
         self.comm = None
         self.group = None
+        self.engine_group = None
+        self.owns_pg = False
         self.rdzv = None
         self.generation = 0
         self.names: dict = {}
@@ -72,8 +83,13 @@ def _fusion_bytes(world: int) -> int:
     return max(xgmi.bucket_floor(max(world, 2)), min(xgmi.MAX_BUCKET_BYTES, 64 * 2 ** 20))
 
 
+# engines whose thread could not be joined after an abort (stuck in a control cycle with a dead peer):
+# kept alive so the detached thread never touches freed memory
+_retired: list = []
+
+
 def _py_allreduce(t, op):
-    group = _ctx.group
+    group = _ctx.engine_group
     if op == ReduceOp.Average:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
         t.div_(_ctx.size)
@@ -82,11 +98,11 @@ def _py_allreduce(t, op):
 
 
 def _py_broadcast(t, root):
-    dist.broadcast(t, root, group=_ctx.group)
+    dist.broadcast(t, root, group=_ctx.engine_group)
 
 
 def _py_allgather(t, out):
-    dist.all_gather_into_tensor(out, t, group=_ctx.group)
+    dist.all_gather_into_tensor(out, t, group=_ctx.engine_group)
 
 
 def init(comm=None, device: str | None = None):
@@ -94,7 +110,7 @@ def init(comm=None, device: str | None = None):
     if _ctx.initialized:
         return
     use_gpu = device != "cpu" and torch.cuda.is_available()
-    backend = "nccl" if use_gpu else "gloo"
+    backend = "gloo"  # control plane; the GPU data plane is the engine's own RCCL communicator
     timeout = datetime.timedelta(seconds=int(os.environ.get("PDE_HVD_TIMEOUT", "300")))
     if rendezvous.elastic_env():
         if _ctx.rdzv is None:
@@ -105,10 +121,12 @@ def init(comm=None, device: str | None = None):
             torch.cuda.set_device(local_rank % torch.cuda.device_count())
         store = _ctx.rdzv.pg_store()
         dist.init_process_group(backend, store=store, rank=rank, world_size=size, timeout=timeout)
+        _ctx.owns_pg = True
         _ctx.generation = rnd
     else:
         from ..parallel import dist as pdist
 
+        _ctx.owns_pg = not dist.is_initialized()
         ctx = pdist.init_distributed(backend=backend, device="cpu" if not use_gpu else None,
                                      timeout_s=int(timeout.total_seconds()))
         rank, size, local_rank = ctx.rank, ctx.world_size, ctx.local_rank
@@ -117,13 +135,23 @@ def init(comm=None, device: str | None = None):
     _ctx.local_rank = local_rank
     _ctx.local_size = int(os.environ.get("LOCAL_WORLD_SIZE", str(_ctx.size)))
     _ctx.device = torch.device("cuda", torch.cuda.current_device()) if use_gpu else torch.device("cpu")
-    _ctx.group = dist.group.WORLD
+    # control plane: the default group when it is gloo, else (an application that initialised RCCL/NCCL
+    # itself) a gloo group over the same ranks
+    _ctx.group = dist.group.WORLD if dist.get_backend() == "gloo" else dist.new_group(backend="gloo", timeout=timeout)
+    # the engine thread's own group: its negotiation collectives never interleave with the main thread's
+    _ctx.engine_group = dist.new_group(backend="gloo", timeout=timeout) if _ctx.size > 1 else _ctx.group
     C = _native.comm()
     tl = os.environ.get("HOROVOD_TIMELINE", "")
     if tl and _ctx.size > 1:
         tl = f"{tl}.rank{_ctx.rank}"
-    eng = C.FusionEngine(_ctx.rank, _ctx.size, _fusion_bytes(_ctx.size), tl)
+    cycle_ms = float(os.environ.get("HOROVOD_CYCLE_TIME", "0.5"))
+    eng = C.FusionEngine(_ctx.rank, _ctx.size, _fusion_bytes(_ctx.size), tl, cycle_ms)
     eng.set_py_backend(_py_allreduce, _py_broadcast, _py_allgather)
+    if _ctx.size > 1:
+        eng.set_control(_ctx.engine_group)
+    eng.set_timeout(float(timeout.total_seconds()))
+    blocking = os.environ.get("PDE_HVD_BLOCKING_WAIT")
+    eng.set_blocking_wait(blocking == "1" if blocking is not None else rendezvous.elastic_env())
     if use_gpu:
         key = f"pde/hvd/rccl_uid/{_ctx.generation}"
         if _ctx.rank == 0:
@@ -143,9 +171,11 @@ def shutdown(abort: bool = False):
     if not _ctx.initialized:
         return
     try:
-        _ctx.engine.shutdown()
+        _ctx.engine.shutdown(abort)
     except Exception:  # noqa: BLE001 - a failed peer may leave the engine in an error state
         pass
+    if abort:
+        _retired.append(_ctx.engine)
     if _ctx.comm is not None:
         if abort:
             _ctx.comm.abort()
@@ -156,11 +186,13 @@ def shutdown(abort: bool = False):
                 _ctx.comm.abort()
     _ctx.engine = None
     _ctx.comm = None
+    _ctx.engine_group = None
     try:
-        if dist.is_initialized():
+        if dist.is_initialized() and _ctx.owns_pg:
             dist.destroy_process_group()
     except Exception:  # noqa: BLE001
         pass
+    _ctx.owns_pg = False
     _ctx.initialized = False
 
 
@@ -322,25 +354,39 @@ def broadcast(tensor, root_rank, name=None):
 
 
 def alltoall(tensor, splits=None, name=None):
-    """All-to-all along dim 0 (direct c10d call; RCCL's all-to-all on GPU)."""
+    """All-to-all along dim 0.  GPU: RCCL (``ncclAllToAll`` for equal splits, grouped send/recv
+    otherwise); CPU: gloo.  Split sizes are exchanged over the gloo control plane."""
     _need()
+    t = tensor.contiguous()
+    rows = t.shape[0] if t.dim() else 1
     if splits is None:
-        out = torch.empty_like(tensor)
-        dist.all_to_all_single(out, tensor.contiguous(), group=_ctx.group)
-        return out
+        if rows % _ctx.size:
+            raise ValueError("alltoall without splits needs dim 0 divisible by the world size")
+        splits = [rows // _ctx.size] * _ctx.size
     splits = [int(s) for s in splits]
-    recv = torch.tensor(splits, dtype=torch.long)
-    all_splits = [torch.zeros_like(recv) for _ in range(_ctx.size)]
-    dist.all_gather(all_splits, recv, group=_ctx.group) if _ctx.device.type == "cpu" else None
-    if _ctx.device.type != "cpu":
-        g = recv.to(_ctx.device)
-        gathered = [torch.zeros_like(g) for _ in range(_ctx.size)]
-        dist.all_gather(gathered, g, group=_ctx.group)
-        all_splits = [x.cpu() for x in gathered]
-    in_splits = splits
+    if sum(splits) != rows:
+        raise ValueError("alltoall splits must sum to dim 0")
+    all_splits = allgather_object(splits)
     out_splits = [int(s[_ctx.rank]) for s in all_splits]
-    out = tensor.new_empty((sum(out_splits),) + tuple(tensor.shape[1:]))
-    dist.all_to_all_single(out, tensor.contiguous(), out_splits, in_splits, group=_ctx.group)
+    out = t.new_empty((sum(out_splits),) + tuple(t.shape[1:]))
+    if t.is_cuda:
+        row = max(1, t[0].numel()) if rows else 1
+        comm = _ctx.comm
+        if len(set(splits)) == 1 and len(set(out_splits)) == 1:
+            res = comm.alltoall(t.reshape(-1))
+            return res.view_as(out)
+        comm.group_start()
+        soff = roff = 0
+        for peer in range(_ctx.size):
+            if splits[peer]:
+                comm.send(t.reshape(-1)[soff * row:(soff + splits[peer]) * row], peer)
+            if out_splits[peer]:
+                comm.recv(out.reshape(-1)[roff * row:(roff + out_splits[peer]) * row], peer)
+            soff += splits[peer]
+            roff += out_splits[peer]
+        comm.group_end()
+        return out
+    dist.all_to_all_single(out, t, out_splits, splits, group=_ctx.group)
     return out
 
 
@@ -366,7 +412,7 @@ def poll(handle) -> bool:
 def join(device=-1) -> int:
     """Barrier; returns the last rank to join (Horovod semantics for uneven inputs, simplified)."""
     _need()
-    t = torch.tensor([_ctx.rank], dtype=torch.float32, device=_ctx.device)
+    t = torch.tensor([_ctx.rank], dtype=torch.float32)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=_ctx.group)
     return int(t.item())
 
@@ -382,8 +428,7 @@ def broadcast_object(obj, root_rank=0, name=None):
     if _ctx.size == 1:
         return obj
     lst = [obj if _ctx.rank == root_rank else None]
-    dist.broadcast_object_list(lst, src=root_rank, group=_ctx.group,
-                               device=_ctx.device if _ctx.device.type == "cuda" else None)
+    dist.broadcast_object_list(lst, src=root_rank, group=_ctx.group)
     return lst[0]
 
 
@@ -397,14 +442,3 @@ def allgather_object(obj, name=None):
 def engine_stats() -> dict:
     _need()
     return dict(_ctx.engine.stats())
-
-
-def _wait_with_timeout(h, timeout_s: float):
-    t0 = time.time()
-    while not poll(h):
-        if time.time() - t0 > timeout_s:
-            if _ctx.comm is not None:
-                _ctx.comm.abort()
-            raise HorovodInternalError(f"collective timed out after {timeout_s}s")
-        time.sleep(0.0005)
-    return synchronize(h)

@@ -57,9 +57,10 @@ class State:
             return
         updated = rd.hosts_updated()
         # every rank must agree (a rank that saw the flag late would otherwise keep training alone)
-        flag = torch.tensor([1.0 if updated else 0.0], device=core._ctx.device)
+        # gloo control plane (host tensor): a dead peer is a connection error here, not a hung GPU collective
+        flag = torch.tensor([1.0 if updated else 0.0])
         try:
-            torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX)
+            torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX, group=core._ctx.group)
         except Exception as exc:  # noqa: BLE001 - a dead peer surfaces here
             raise HorovodInternalError(str(exc)) from exc
         if flag.item() > 0:

@@ -87,9 +87,11 @@ class _DistributedOptimizerMixin:
     def _make_hook(self):
         def hook(p):
             if p in self._handles and self._handles[p] is not None:
-                if self._bpps <= 1:
-                    raise AssertionError("Gradients were computed more than backward_passes_per_step times "
-                                         "before call to step(). Increase backward_passes_per_step.")
+                # the gradient was already handed to the engine (in-place all-reduce in flight): another
+                # local pass would race with it and mix reduced and unreduced values
+                raise AssertionError("Gradients were computed more than backward_passes_per_step times "
+                                     "before call to step(). Increase backward_passes_per_step to "
+                                     "accumulate gradients locally.")
             self._counts[p] += 1
             if self._counts[p] >= self._bpps:
                 self._handles[p] = self._allreduce_grad(p)
@@ -122,6 +124,9 @@ class _DistributedOptimizerMixin:
             if p not in self._handles or self._handles[p] is None:
                 if p.grad is not None:
                     self._handles[p] = self._allreduce_grad(p)
+            # every parameter starts the next accumulation window from zero passes (Horovod resets the
+            # delay of every handled parameter), including those reduced early here
+            self._counts[p] = 0
         try:
             for p, h in list(self._handles.items()):
                 if h is not None:

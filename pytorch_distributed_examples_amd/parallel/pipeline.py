@@ -27,10 +27,20 @@ from .. import _native
 
 
 class P2PChannel:
-    """RCCL communicator between two neighbouring stage processes (ranks a < b of the default group).
+    """Point-to-point channel between two neighbouring stage processes (ranks lo < hi of the default group).
 
-    The unique id is published through the default process group's store.  ``send``/``recv`` enqueue
-    on the caller's current stream."""
+    GPU data plane: TWO 2-rank RCCL communicators, one per direction -- ``down`` carries lo -> hi
+    traffic (activations), ``up`` carries hi -> lo traffic (activation gradients).  RCCL executes the
+    operations of one communicator in issue order whatever stream they are enqueued on, so with a single
+    communicator the 1F1B steady state (stage 0: send a1, recv g0; stage 1: send g0, recv a1) would pair
+    a send with a send and deadlock.  With one communicator per direction every communicator only ever
+    sees send on one side and recv on the other, in the same order.  Unique ids go through the default
+    store; ``send``/``recv`` are stream-ordered (capturable into a hipGraph, no host synchronisation).
+
+    CPU configuration (and ``PDE_BACKEND=gloo`` rehearsals of a multi-rank GPU job on one card): gloo
+    ``isend``/``recv`` with one tag per direction; device tensors are staged through host memory."""
+
+    TAG_DOWN, TAG_UP = 11, 12
 
     def __init__(self, peer: int, tag: str, device: torch.device, store=None):
         me = dist.get_rank()
@@ -39,37 +49,59 @@ class P2PChannel:
         self.local_rank = 0 if me == self.lo else 1
         self.peer_local = 1 - self.local_rank
         self.device = device
-        self.comm = None
+        self.down = self.up = None
         self._meta = {}
         self._pending = []
+        self._inflight = []  # tensors sent on the side stream: kept alive until flush() joins the streams
         self._send_stream = None
-        if device.type != "cuda":
-            return  # CPU configuration: point-to-point over the default (gloo) process group
+        self.rccl = device.type == "cuda" and dist.get_backend() == "nccl"
+        if not self.rccl:
+            return
         store = store or dist.distributed_c10d._get_default_store()
         C = _native.comm()
-        key = f"pde/p2p/{tag}/{self.lo}-{self.hi}"
-        if self.local_rank == 0:
-            store.set(key, C.rccl_unique_id())
-        uid = store.get(key)
-        self.comm = C.RcclComm()
-        self.comm.init(uid, self.local_rank, 2, device.index, True)
+        comms = []
+        for direction in ("down", "up"):  # same creation order on both ranks
+            key = f"pde/p2p/{tag}/{self.lo}-{self.hi}/{direction}"
+            if self.local_rank == 0:
+                store.set(key, C.rccl_unique_id())
+            uid = store.get(key)
+            c = C.RcclComm()
+            c.init(uid, self.local_rank, 2, device.index, True)
+            comms.append(c)
+        self.down, self.up = comms
+
+    # direction of a send/recv from this rank's point of view
+    def _send_comm(self):
+        return self.down if self.local_rank == 0 else self.up
+
+    def _recv_comm(self):
+        return self.up if self.local_rank == 0 else self.down
+
+    def _tag(self, sending: bool) -> int:
+        lo_side = self.local_rank == 0
+        return self.TAG_DOWN if (lo_side == sending) else self.TAG_UP
 
     def send(self, t: torch.Tensor):
-        """Asynchronous send.  RCCL: enqueued on a dedicated send stream (after the producer's work),
-        so a later recv on the compute stream is never queued behind an unmatched send -- the 1F1B
-        steady state exchanges activations and gradients in opposite directions at the same time.
-        gloo: isend, completed in :meth:`flush`."""
+        """Asynchronous send.  RCCL: enqueued on a dedicated send stream (after the producer's work), so
+        the compute stream never waits for the peer to post its receive.  gloo: isend, completed in
+        :meth:`flush`."""
         t = t.contiguous()
-        if self.comm is None:
-            self._pending.append((dist.isend(t, self.peer), t))
+        if not self.rccl:
+            src = t.cpu() if t.is_cuda else t
+            self._pending.append((dist.isend(src, self.peer, tag=self._tag(True)), src))
             return
         if self._send_stream is None:
             self._send_stream = torch.cuda.Stream(device=self.device)
         cur = torch.cuda.current_stream(self.device)
         self._send_stream.wait_stream(cur)
         with torch.cuda.stream(self._send_stream):
-            self.comm.send(t, self.peer_local)
-        t.record_stream(self._send_stream)
+            self._send_comm().send(t, self.peer_local)
+        if torch.cuda.is_current_stream_capturing():
+            # inside a hipGraph capture: no allocator stream bookkeeping; the tensor stays referenced
+            # until flush() has joined the send stream back into the capturing stream
+            self._inflight.append(t)
+        else:
+            t.record_stream(self._send_stream)
 
     def flush(self):
         """Complete outstanding sends (gloo) / order the compute stream after them (RCCL)."""
@@ -78,13 +110,19 @@ class P2PChannel:
         self._pending = []
         if self._send_stream is not None:
             torch.cuda.current_stream(self.device).wait_stream(self._send_stream)
+        self._inflight = []
 
     def recv(self, shape, dtype) -> torch.Tensor:
         t = torch.empty(shape, dtype=dtype, device=self.device)
-        if self.comm is None:
-            dist.recv(t, self.peer)
+        if not self.rccl:
+            if t.is_cuda:
+                h = torch.empty(shape, dtype=dtype)
+                dist.recv(h, self.peer, tag=self._tag(False))
+                t.copy_(h)
+            else:
+                dist.recv(t, self.peer, tag=self._tag(False))
         else:
-            self.comm.recv(t, self.peer_local)
+            self._recv_comm().recv(t, self.peer_local)
         return t
 
     def send_meta(self, t: torch.Tensor):
@@ -102,8 +140,10 @@ class P2PChannel:
         return tuple(m[2:2 + m[0]]), dtype
 
     def close(self):
-        if self.comm is not None:
-            self.comm.destroy()
+        for c in (self.down, self.up):
+            if c is not None:
+                c.destroy()
+        self.down = self.up = None
 
 
 class PipelineEngine:

@@ -1,0 +1,105 @@
+"""One-shot xGMI peer all-reduce for latency-bound buckets, and the DDP communicator that routes buckets
+between it and RCCL (SURVEY.md §5.8 items 2-3, §7.1 ``xgmi_allreduce.hip``).
+
+Why: the MNIST CNN reduces one 87 KB gradient bucket per 50 us step (horovod/mnist_horovod.py:53 is a
+per-step all-reduce; rpc/server_model_data_parallel.py:41 a 544 B one).  A ring all-reduce of that size is
+2(N-1) dependent latency-bound hops; on a fully connected MI355X node every rank can instead read all 7
+peers' buckets directly over their 7 xGMI links and reduce locally: one kernel, one flag exchange
+(csrc/comm/xgmi_allreduce.hip).  Large buckets stay on RCCL, whose multi-channel rings/trees use the links'
+bandwidth better than 7 full copies per rank.
+
+    xa = XgmiAllreduce(device)            # collective: exchanges IPC handles through the c10d store
+    xa.allreduce_(grads, avg=True)        # stream-ordered, hipGraph-capturable, bit-identical on all ranks
+    comm = RoutedComm(StreamComm(device), xa, threshold_bytes=1 << 20)
+    ddp = DistributedDataParallel(model, comm=comm)
+
+On one GPU the same code runs with several processes sharing the card (the IPC mapping then points back
+at the same device), which is how the protocol is rehearsed on single-GPU boxes.
+"""
+from __future__ import annotations
+
+import itertools
+import os
+
+import torch
+import torch.distributed as dist
+
+from .. import _native
+
+_SEQ = itertools.count()
+DEFAULT_THRESHOLD = int(os.environ.get("PDE_XGMI_THRESHOLD", str(1 << 20)))
+
+
+class XgmiAllreduce:
+    def __init__(self, device: torch.device, group=None, max_bytes: int = 4 << 20, blocks: int = 64,
+                 timeout_s: float = 5.0):
+        assert device.type == "cuda", "the xGMI all-reduce is a GPU data plane"
+        self.device = device
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.size = dist.get_world_size(group) if dist.is_initialized() else 1
+        C = _native.comm()
+        self.impl = C.XgmiAllreduce(self.rank, self.size, device.index, int(max_bytes), int(blocks), float(timeout_s))
+        if self.size > 1:
+            store = dist.distributed_c10d._get_default_store()
+            ranks = dist.get_process_group_ranks(group) if group is not None else list(range(self.size))
+            key = f"pde/xgmi/{next(_SEQ)}/{'-'.join(map(str, ranks))}"
+            store.set(f"{key}/{self.rank}", self.impl.ipc_handle())
+            handles = [store.get(f"{key}/{r}") for r in range(self.size)]
+            self.impl.open(handles)
+
+    @property
+    def max_bytes(self) -> int:
+        return self.impl.max_bytes
+
+    def allreduce_(self, t: torch.Tensor, avg: bool = False) -> torch.Tensor:
+        self.impl.allreduce_(t, 1.0 / self.size if avg else 1.0)
+        return t
+
+    def check(self) -> None:
+        """Raise if any call timed out waiting for a peer (synchronises the device)."""
+        if self.impl.error():
+            raise RuntimeError("xGMI all-reduce: a workgroup timed out waiting for a peer's flag")
+
+    def close(self):
+        if self.impl is not None:
+            self.impl.close()
+            self.impl = None
+
+
+class _Done:
+    def wait(self):
+        return True
+
+    def is_completed(self):
+        return True
+
+
+class RoutedComm:
+    """DDP communicator plug-in (``size``, ``rank``, ``supports_avg``, ``allreduce_async``, ``broadcast_``):
+    fp32 buckets up to ``threshold_bytes`` take the one-shot xGMI path, the rest go to RCCL."""
+
+    def __init__(self, rccl, xgmi: XgmiAllreduce, threshold_bytes: int = DEFAULT_THRESHOLD):
+        self.rccl, self.xgmi = rccl, xgmi
+        self.size, self.rank = rccl.size, rccl.rank
+        self.supports_avg = True
+        self.threshold = min(int(threshold_bytes), xgmi.max_bytes)
+        self.routed = {"xgmi": 0, "rccl": 0}
+
+    def allreduce_async(self, t: torch.Tensor, avg: bool = False):
+        if t.dtype == torch.float32 and t.numel() * 4 <= self.threshold:
+            self.xgmi.allreduce_(t, avg)
+            self.routed["xgmi"] += 1
+            return _Done()
+        self.routed["rccl"] += 1
+        return self.rccl.allreduce_async(t, avg)
+
+    def allreduce_(self, t: torch.Tensor, avg: bool = False) -> torch.Tensor:
+        self.allreduce_async(t, avg)
+        return t
+
+    def broadcast_(self, t: torch.Tensor, src: int) -> torch.Tensor:
+        return self.rccl.broadcast_(t, src)
+
+    def destroy(self):
+        self.xgmi.close()
+        self.rccl.destroy()

@@ -30,8 +30,36 @@ def test_bench_cpu_single():
 def test_bench_cpu_torchrun_world2():
     rc, out = run_cmd(["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO, "bench.py"),
-                       "--gpus", "2", "--device", "cpu", "--steps", "2", "--warmup", "1", "--batch", "32",
+                       "--gpus", "2", "--device", "cpu", "--steps", "2", "--warmup", "1",
                        "--model", "mlp"], timeout=300)
     assert rc == 0, out
     rec = _parse(out)
-    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 64 and rec["vs_baseline"] is not None
+    # the reference's MLP DDP at world 2 (CPU) is the same workload: vs_baseline is reported
+    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 256 and rec["vs_baseline"] is not None
+
+
+def test_bench_launches_n_ranks_itself():
+    """``bench.py --gpus 2`` without torchrun launches 2 ranks (the driver's N-GPU contract)."""
+    rc, out = run_cmd(["python", os.path.join(REPO, "bench.py"), "--gpus", "2", "--device", "cpu", "--steps", "2",
+                       "--warmup", "1", "--batch", "16", "--model", "mlp"], timeout=300)
+    assert rc == 0, out
+    rec = _parse(out)
+    assert rec["n_gpus"] == 2 and rec["config"]["rccl_nranks"] == 2 and rec["config"]["parallelism"] == "dp2"
+
+
+def test_bench_world_mismatch_fails_fast():
+    rc, out = run_cmd(["python", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                       "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO, "bench.py"),
+                       "--gpus", "4", "--device", "cpu", "--steps", "1", "--warmup", "0"], timeout=300)
+    assert rc != 0 and "--gpus 4 but the job has 2 ranks" in out, out
+
+
+def test_bench_resnet_pipeline_world2():
+    """BASELINE config 3 plumbing: 2-stage ResNet-50 pipeline, one rank per stage (tiny images on CPU)."""
+    rc, out = run_cmd(["python", os.path.join(REPO, "bench.py"), "--gpus", "2", "--device", "cpu", "--steps", "2",
+                       "--warmup", "1", "--model", "resnet50_pp", "--batch", "4", "--split-size", "2",
+                       "--image", "32"], timeout=300)
+    assert rc == 0, out
+    rec = _parse(out)
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "pp2xdp1" and rec["config"]["microbatches"] == 2
+    assert rec["config"]["global_batch"] == 4 and rec["value"] > 0

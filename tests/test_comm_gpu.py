@@ -132,3 +132,28 @@ def test_stream_rccl_allreduce_inside_hipgraph(gpu):
     r = subprocess.run([sys.executable, "-c", _GRAPH_ALLREDUCE], env=env, capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0 and "GRAPH_ALLREDUCE_OK" in r.stdout, r.stderr[-3000:]
+
+
+def test_hvd_aborted_communicator_raises(gpu):
+    """A failed communicator surfaces as HorovodInternalError from synchronize() (what hvd.elastic.run
+    catches to restore the last commit), and the engine stays failed until reset."""
+    from pytorch_distributed_examples_amd import hvd
+    from pytorch_distributed_examples_amd.hvd import core
+
+    hvd.init()
+    try:
+        t = torch.ones(64, device=gpu)
+        hvd.synchronize(hvd.allreduce_async_(t, name="before", op=hvd.Sum))
+        core._ctx.comm.abort()  # what the watchdog does to a hung collective
+        with pytest.raises(hvd.HorovodInternalError):
+            hvd.synchronize(hvd.allreduce_async_(t, name="after", op=hvd.Sum))
+        with pytest.raises(hvd.HorovodInternalError):
+            hvd.allreduce_async_(t, name="later", op=hvd.Sum)
+    finally:
+        hvd.shutdown(abort=True)
+    hvd.init()  # a fresh engine + communicator (the elastic reset path)
+    try:
+        t = torch.full((8,), 2.0, device=gpu)
+        assert torch.equal(hvd.allreduce(t, op=hvd.Sum), t)
+    finally:
+        hvd.shutdown()

@@ -12,7 +12,7 @@ def test_fusion_engine_batches_deterministically(tmp_path):
 
     C = _native.comm()
     tl = str(tmp_path / "timeline.json")
-    eng = C.FusionEngine(0, 1, 1000, tl)
+    eng = C.FusionEngine(0, 1, 1000, tl, 50.0)  # 50 ms cycle: the 7 enqueues below land in one cycle
     calls = []
     eng.set_py_backend(lambda t, op: calls.append(t.numel()), lambda t, r: None, lambda t, o: o.copy_(t))
     ts = [torch.ones(100) for _ in range(7)]  # 400 B each -> batches of 2 (threshold 1000 B)
@@ -95,6 +95,79 @@ def test_hvd_api_world2():
     spawn(_hvd_worker, 2)
 
 
+def _negotiation_worker(rank, world):
+    """Ranks enqueue the same tensors in DIFFERENT orders (and in different cycles): negotiation still
+    fuses and reduces them correctly; a signature mismatch fails on every rank instead of mis-reducing."""
+    import time
+
+    from pytorch_distributed_examples_amd import hvd
+
+    hvd.init(device="cpu")
+    names = [f"g{i}" for i in range(6)]
+    ts = {n: torch.full((10 + i,), float(rank + 1) * (i + 1)) for i, n in enumerate(names)}
+    order = names if rank == 0 else list(reversed(names))
+    hs = {}
+    for k, n in enumerate(order):
+        hs[n] = hvd.allreduce_async_(ts[n], name=n, op=hvd.Sum)
+        if rank == 1 and k == 2:
+            time.sleep(0.05)  # rank 1's second half arrives several cycles later
+    for n in names:
+        hvd.synchronize(hs[n])
+    for i, n in enumerate(names):
+        assert torch.allclose(ts[n], torch.full((10 + i,), 3.0 * (i + 1))), (n, ts[n])
+    assert hvd.engine_stats()["negotiated"]
+    # same name, different shapes on the two ranks -> error everywhere
+    bad = torch.ones(4 if rank == 0 else 5)
+    with pytest.raises(hvd.HorovodInternalError, match="mismatched"):
+        hvd.synchronize(hvd.allreduce_async_(bad, name="bad", op=hvd.Sum))
+    # the engine keeps working after a rejected request
+    assert torch.allclose(hvd.allreduce(torch.ones(3), name="ok", op=hvd.Sum), torch.full((3,), 2.0))
+    # a duplicate outstanding name is refused locally
+    h = hvd.allreduce_async_(torch.ones(2), name="dup", op=hvd.Sum)
+    with pytest.raises(RuntimeError, match="already outstanding"):
+        hvd.allreduce_async_(torch.ones(2), name="dup", op=hvd.Sum)
+    hvd.synchronize(h)
+    hvd.shutdown()
+
+
+def test_hvd_negotiation_world2():
+    spawn(_negotiation_worker, 2)
+
+
+def _bpps_worker(rank, world):
+    """backward_passes_per_step=2 with a step() after ONE pass (end of an epoch): the early reduction resets
+    the pass counter, so the next window again accumulates 2 local passes before reducing."""
+    from pytorch_distributed_examples_amd import hvd
+
+    hvd.init(device="cpu")
+    torch.manual_seed(rank)
+    m = torch.nn.Linear(4, 2)
+    opt = hvd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1), named_parameters=m.named_parameters(),
+                                   backward_passes_per_step=2)
+    hvd.broadcast_parameters(m.state_dict(), root_rank=0)
+    g = torch.Generator().manual_seed(10 + rank)
+    for passes in (1, 2, 2):
+        opt.zero_grad()
+        for _ in range(passes):
+            m(torch.randn(3, 4, generator=g)).sum().backward()
+        opt.step()
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    both = hvd.allgather(flat.unsqueeze(0))
+    assert torch.equal(both[0], both[1]), both
+    # a third pass inside a window of 2 is an error (the all-reduce is already in flight)
+    opt.zero_grad()
+    for _ in range(2):
+        m(torch.randn(3, 4, generator=g)).sum().backward()
+    with pytest.raises(AssertionError, match="backward_passes_per_step"):
+        m(torch.randn(3, 4, generator=g)).sum().backward()
+    opt.synchronize()
+    hvd.shutdown()
+
+
+def test_hvd_backward_passes_per_step_world2():
+    spawn(_bpps_worker, 2)
+
+
 def _elastic_state_worker(rank, world):
     from pytorch_distributed_examples_amd import hvd
     from pytorch_distributed_examples_amd.models.cnn import Net
@@ -142,3 +215,21 @@ def test_hvd_scripts_and_elastic_recovery(tmp_path):
     assert "failed (exit 17)" in out and "round 1" in out
     accs = [line for line in out.splitlines() if line.startswith("Accuracy:")]
     assert len(accs) == 2 and accs[0] == accs[1], accs  # replicas identical after recovery
+
+
+def test_engine_error_state_cpu():
+    """An engine failure (dead peer on the control plane, RCCL error) fails outstanding handles and every
+    later request with an error that hvd.synchronize raises as HorovodInternalError."""
+    from pytorch_distributed_examples_amd import _native
+
+    C = _native.comm()
+    eng = C.FusionEngine(0, 1, 1 << 20, "", 20.0)
+    eng.set_py_backend(lambda t, op: None, lambda t, r: None, lambda t, o: o.copy_(t))
+    h = eng.allreduce(torch.ones(4), torch.ones(4), "x", 0, 1.0, 1.0, False)
+    eng.inject_error("peer 1 died")
+    with pytest.raises(RuntimeError, match="HorovodInternalError: peer 1 died"):
+        eng.wait(h)
+    with pytest.raises(RuntimeError, match="HorovodInternalError"):
+        eng.allreduce(torch.ones(4), torch.ones(4), "y", 0, 1.0, 1.0, False)
+    assert eng.error == "peer 1 died"
+    eng.shutdown(True)

@@ -1,0 +1,167 @@
+"""Multi-GPU data-plane tests at world N in {2, 4, 8}: one process per GPU over RCCL (xGMI on an MI355X
+node).  Each test skips when the box has fewer than N GPUs (the 1-GPU rehearsal boxes); the same code
+paths are exercised on gloo by the CPU suite and at world 1 by tests/test_comm_gpu.py.
+
+Checks, per world size:
+* the stream-ordered RCCL communicator (parallel/rccl.py) all-reduce against an fp32 sum of every
+  rank's data, plus the rank count RCCL reports;
+* the pipeline's per-direction P2P channel (parallel/pipeline.py) in both directions;
+* the Horovod engine (negotiated fusion over RCCL) against the same fp32 sum;
+* 2-stage pipeline gradients (gpipe and 1f1b, hipGraph-free) against a single-process reference;
+* the one-shot xGMI peer all-reduce (csrc/comm/xgmi_allreduce.hip) against RCCL.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_SCRIPT = r"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["REPO"])
+from pytorch_distributed_examples_amd.parallel import dist as pdist
+ctx = pdist.init_distributed()
+N, r, dev = ctx.world_size, ctx.rank, ctx.device
+
+def rank_data(k, n, seed):
+    g = torch.Generator().manual_seed(seed * 1000 + k)
+    return torch.randn(n, generator=g)
+
+# 1. stream-ordered RCCL all-reduce vs fp32 sum
+from pytorch_distributed_examples_amd.parallel.rccl import StreamComm
+comm = StreamComm(dev)
+assert comm.rccl.nranks() == N
+for n in (1, 1000, 21840, 1 << 20):
+    x = rank_data(r, n, n).to(dev)
+    comm.allreduce_(x)
+    ref = sum(rank_data(k, n, n) for k in range(N))
+    torch.cuda.synchronize()
+    assert torch.allclose(x.cpu(), ref, rtol=1e-5, atol=1e-5), n
+
+# 2. per-direction P2P channels between pipeline neighbours (2k, 2k+1)
+from pytorch_distributed_examples_amd.parallel.pipeline import P2PChannel
+peer = r + 1 if r % 2 == 0 else r - 1
+ch = P2PChannel(peer, "mgtest", dev)
+a = torch.full((4096,), float(r), device=dev, dtype=torch.bfloat16)
+for it in range(3):
+    if r % 2 == 0:
+        ch.send(a + it)
+        got = ch.recv((4096,), torch.bfloat16)   # the opposite direction at the same time
+    else:
+        got = ch.recv((4096,), torch.bfloat16)
+        ch.send(a + it)
+    ch.flush()
+    torch.cuda.synchronize()
+    assert torch.all(got.float() == float(peer + it)), (it, got[:4])
+ch.close()
+
+# 3. Horovod engine: negotiated, fused, RCCL
+from pytorch_distributed_examples_amd import hvd
+hvd.init()
+ts = [rank_data(r, n, 7 + i).to(dev) for i, n in enumerate((3, 1000, 17, 4096))]
+order = range(len(ts)) if r % 2 == 0 else reversed(range(len(ts)))
+hs = {i: hvd.allreduce_async_(ts[i], name=f"t{i}", op=hvd.Sum) for i in order}
+for i in range(len(ts)):
+    hvd.synchronize(hs[i])
+torch.cuda.synchronize()
+for i, n in enumerate((3, 1000, 17, 4096)):
+    ref = sum(rank_data(k, n, 7 + i) for k in range(N))
+    assert torch.allclose(ts[i].cpu(), ref, rtol=1e-5, atol=1e-5), i
+hvd.shutdown()
+
+# 4. one-shot xGMI peer all-reduce vs RCCL (small, latency-bound buckets)
+from pytorch_distributed_examples_amd.parallel.xgmi_allreduce import XgmiAllreduce
+xa = XgmiAllreduce(dev, max_bytes=4 << 20)
+for n in (1, 5, 21840, 262144):
+    x = rank_data(r, n, 99 + n).to(dev)
+    y = x.clone()
+    xa.allreduce_(x, avg=False)
+    comm.allreduce_(y)
+    torch.cuda.synchronize()
+    ref = sum(rank_data(k, n, 99 + n) for k in range(N))
+    assert torch.allclose(x.cpu(), ref, rtol=1e-5, atol=1e-5), n
+    # every rank sums in rank order: bit-identical results on every rank
+    gathered = [torch.empty_like(x) for _ in range(N)]
+    dist.all_gather(gathered, x)
+    for gth in gathered:
+        assert torch.equal(gth, x)
+xa.close()
+comm.destroy()
+dist.destroy_process_group()
+print("MULTIGPU_OK", r)
+"""
+
+_PIPE = r"""
+import os, sys, copy, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["REPO"])
+from torch import nn
+from pytorch_distributed_examples_amd.parallel import dist as pdist
+from pytorch_distributed_examples_amd.parallel.pipeline import PipelineEngine
+ctx = pdist.init_distributed()
+r, dev = ctx.rank, ctx.device
+torch.manual_seed(0)
+s0 = nn.Sequential(nn.Linear(64, 128), nn.ReLU()).to(dev)
+s1 = nn.Linear(128, 16).to(dev)
+full = nn.Sequential(copy.deepcopy(s0), copy.deepcopy(s1))
+stage = r % 2
+mod = s0 if stage == 0 else s1
+for sched in ("gpipe", "1f1b"):
+    for p in mod.parameters():
+        p.grad = None
+    eng = PipelineEngine(mod, stage, 2, r - 1 if stage else None, r + 1 if stage == 0 else None, dev,
+                         loss_fn=lambda a, b: ((a - b) ** 2).mean(), schedule=sched, tag="mg" + sched)
+    g = torch.Generator().manual_seed(5)
+    x, y = torch.randn(32, 64, generator=g).to(dev), torch.randn(32, 16, generator=g).to(dev)
+    loss = eng.train_step(list(x.split(8)) if stage == 0 else None, list(y.split(8)) if stage == 1 else None, 4)
+    for p in full.parameters():
+        p.grad = None
+    ref = ((full(x) - y) ** 2).mean()
+    ref.backward()
+    refmod = full[0] if stage == 0 else full[1]
+    for p, q in zip(mod.parameters(), refmod.parameters()):
+        assert torch.allclose(p.grad, q.grad, atol=1e-5, rtol=1e-4), sched
+    if stage == 1:
+        assert abs(loss.item() - ref.item()) < 1e-5
+    eng.close()
+dist.destroy_process_group()
+print("PIPE_OK", r)
+"""
+
+
+def _torchrun(script, n):
+    import tempfile
+
+    from pytorch_distributed_examples_amd.parallel.dist import free_port
+
+    env = dict(os.environ, REPO=REPO)
+    env.pop("PDE_BACKEND", None)
+    with tempfile.NamedTemporaryFile("w", suffix=".py", delete=False) as f:
+        f.write(script)
+        path = f.name
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), path]
+    try:
+        return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    finally:
+        os.unlink(path)
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_data_plane_world_n(gpu, n):
+    if torch.cuda.device_count() < n:
+        pytest.skip(f"needs {n} GPUs, box has {torch.cuda.device_count()}")
+    res = _torchrun(_SCRIPT, n)
+    assert res.returncode == 0 and res.stdout.count("MULTIGPU_OK") == n, (res.stdout[-3000:], res.stderr[-5000:])
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_pipeline_grads_world_n(gpu, n):
+    if torch.cuda.device_count() < n:
+        pytest.skip(f"needs {n} GPUs, box has {torch.cuda.device_count()}")
+    res = _torchrun(_PIPE, n)
+    assert res.returncode == 0 and res.stdout.count("PIPE_OK") == n, (res.stdout[-3000:], res.stderr[-5000:])
