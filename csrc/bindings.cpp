@@ -646,7 +646,7 @@ Tensor embbag_bwd(const Tensor& dy, const Tensor& idx, const Tensor& off, int64_
 Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, Tensor& rng, double p_drop2,
                  double p_drop1, bool training, Tensor& grads, bool accumulate, const optional<Tensor>& gscale,
                  const optional<Tensor>& stamps, const optional<Tensor>& frag_buf, bool prep,
-                 const optional<Tensor>& sgd_hp) {
+                 const optional<Tensor>& sgd_hp, int64_t stop_after) {
   CHECK_IN(images); CHECK_IN(tgt); CHECK_IN(params); CHECK_IN(rng); CHECK_IN(grads);
   CHECK_F32(images); CHECK_F32(params); CHECK_F32(grads);
   TORCH_CHECK(params.numel() == pde::cnn_num_params(), "cnn_train: params must be the flat Net parameters");
@@ -661,8 +661,9 @@ Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, 
     TORCH_CHECK(stamps->numel() >= static_cast<long>(n) * 16 && stamps->scalar_type() == at::kLong,
                 "cnn_train: stamps must be int64[nwg*16]");
   auto fo = images.options();
-  Tensor slabs = at::empty({static_cast<long>(n) * pde::cnn_num_params()}, fo);
+  Tensor slabs = at::empty({static_cast<long>(n) * pde::cnn_slab_floats()}, fo);
   Tensor part = at::empty({n}, fo);
+  Tensor acts = at::empty({static_cast<long>(pde::cnn_act_rows()) * n * ni}, fo);
   Tensor loss = at::empty({}, fo);
   Tensor frag;
   if (frag_buf.has_value() && frag_buf->defined()) {
@@ -682,12 +683,13 @@ Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, 
                              frag.data_ptr(),
                              reinterpret_cast<unsigned long long*>(rng.data_ptr()), static_cast<float>(p_drop2),
                              static_cast<float>(p_drop1), training ? 1 : 0, slabs.data_ptr<float>(),
-                             part.data_ptr<float>(), n, loss.data_ptr<float>(), grads.data_ptr<float>(), cf32(gscale),
+                             part.data_ptr<float>(), acts.data_ptr<float>(), n, loss.data_ptr<float>(), grads.data_ptr<float>(), cf32(gscale),
                              accumulate ? 1 : 0, cur_stream(),
                              stamps.has_value() && stamps->defined()
                                  ? reinterpret_cast<unsigned long long*>(stamps->data_ptr())
                                  : nullptr,
-                             prep ? 1 : 0, sgd_hp.has_value() && sgd_hp->defined() ? sgd_hp->data_ptr<float>() : nullptr),
+                             prep ? 1 : 0, sgd_hp.has_value() && sgd_hp->defined() ? sgd_hp->data_ptr<float>() : nullptr,
+                             static_cast<int>(stop_after)),
         "cnn_train");
   return loss;
 }
@@ -710,7 +712,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cnn_train", &cnn_train, py::arg("images"), py::arg("tgt"), py::arg("params"), py::arg("rng"),
         py::arg("p_drop2"), py::arg("p_drop1"), py::arg("training"), py::arg("grads"), py::arg("accumulate"),
         py::arg("gscale") = py::none(), py::arg("stamps") = py::none(), py::arg("frag") = py::none(),
-        py::arg("prep") = true, py::arg("sgd_hp") = py::none());
+        py::arg("prep") = true, py::arg("sgd_hp") = py::none(), py::arg("stop_after") = -1);
   m.def("cnn_sgd", &cnn_sgd);
   m.def("clear_last_error", []() { return static_cast<int>(hipGetLastError()); },
         "Read and reset the HIP last-error state (after an aborted stream capture).");

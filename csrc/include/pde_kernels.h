@@ -160,7 +160,7 @@ hipError_t embbag_fwd(const float* w, const int64_t* idx, const int64_t* off, in
 // ---------------------------------------------------------------------------------------------
 // Fused MNIST-CNN training step (cnn_fused.hip): forward + NLL + backward of horovod/mnist_horovod.py's
 // Net per image in LDS.  params: flat fp32 in torch parameter order (cnn_num_params() floats).
-// slabs: nwg * cnn_num_params() floats; loss_part: nwg floats.
+// slabs: nwg * cnn_slab_floats() floats; loss_part: nwg floats; acts: cnn_act_rows() x (nwg * 4) floats.
 // ---------------------------------------------------------------------------------------------
 int cnn_num_params();
 size_t cnn_smem_bytes();
@@ -172,11 +172,13 @@ size_t cnn_frag_bytes();  // workspace for the per-step bf16 weight-fragment ima
 // prep = 0 skips the fragment prep (the image is already current: the previous step's fused SGD wrote it).
 // sgd_hp != nullptr fuses plain SGD (lr = sgd_hp[HP_LR], grad scale sgd_hp[HP_GRAD_SCALE]) and the
 // fragment refresh into the slab reduction (single process: no all-reduce between reduce and update).
+int cnn_slab_floats();  // per-workgroup slab (every gradient except fc1's weight)
+int cnn_act_rows();     // rows of the per-batch activation image feeding the fc1 weight-gradient GEMM
 hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float* params, void* frag,
                            unsigned long long* rng, float p_drop2, float p_drop1, int training, float* slabs,
-                           float* loss_part, int nwg, float* loss, float* grads, const float* gscale,
+                           float* loss_part, float* acts, int nwg, float* loss, float* grads, const float* gscale,
                            int accumulate, hipStream_t s, unsigned long long* stamps = nullptr, int prep = 1,
-                           const float* sgd_hp = nullptr);
+                           const float* sgd_hp = nullptr, int stop_after = -1);
 // params -= lr * gscale * grads (plain SGD) and the matching fragment-image refresh, one launch (used
 // after the gradient all-reduce when world > 1).
 hipError_t cnn_sgd_fused(float* params, const float* grads, const float* hp, void* frag, hipStream_t s);

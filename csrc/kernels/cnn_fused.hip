@@ -46,16 +46,28 @@ constexpr int K2 = C1 * KS * KS;       // 250: conv2 reduction (ci,ky,kx) in the
 constexpr int C1P = 16;
 constexpr int KS2 = (KS * KS * C1P + 31) / 32;  // 13 k-steps (the last one half padding)
 constexpr int KSW2 = NI * 8 * 8 / 32;           // 8 conv2-wgrad k-steps: K = (image, y, x)
-// conv2 dgrad: one k-step per filter tap (ky,kx) with K = co (20 -> 32): the gradient is kept channel-last
-// (d2n[pos][co]) so a lane's 8 k-values are one 16-byte LDS read
-constexpr int KSD = KS * KS;           // 25 k-steps
+// conv2 dgrad: K = (tap, co) with co padded to 24 = 3 groups of 8, packed: k-step ks, lane group lg holds
+// group g = 4 ks + lg = (tap g / 3, channels 8 (g % 3) .. +7).  The gradient is kept channel-last
+// (d2n[pos][co], co 20..23 zero), so a lane's 8 k-values are ONE 16-byte LDS read of its own position.
+constexpr int CG = 3;                                // co groups of 8 per tap
+constexpr int NGD = KS * KS * CG;                    // 75 (tap, co-group) pairs
+constexpr int KSD = (NGD + 3) / 4;                   // 19 k-steps (25 with one k-step per tap)
 constexpr int C2P = 40;  // 80-byte rows: a ds_read_b128 lane octet spans all 64 banks (conflict-free)
+constexpr int D2R = O2 * O2 + 8;       // d2 plane row stride (u16): 144 B
 constexpr int MT1 = O1 * O1 / 16;      // 36 conv1 M-tiles per image (4 cells x 4 taps each)
 constexpr int MTD = NC1 * 1 / 16;      // 9 conv2-dgrad M-tiles per image (144 r1 positions)
 constexpr int KSW1 = O1 * O1 / 32;     // 18 conv1-wgrad k-steps per image
 // parameter offsets in the flat gradient (torch parameter order of Net)
 constexpr int O_W1 = 0, O_B1 = O_W1 + W1N, O_W2 = O_B1 + C1, O_B2 = O_W2 + W2N, O_FC1W = O_B2 + C2,
               O_FC1B = O_FC1W + FC1N, O_FC2W = O_FC1B + F1, O_FC2B = O_FC2W + FC2N, NPARAM = O_FC2B + F2;
+// Per-workgroup fp32 slabs hold every gradient EXCEPT fc1's weight (16,000 of the 21,840 parameters):
+// that one is a rank-B product dW = dH^T . R2 over the whole batch, so each workgroup writes its 4 images'
+// fc1 output gradients dH and inputs R2 (370 floats per image, K-contiguous) and k_cnn_reduce computes
+// it as one f32-MFMA GEMM -- 1.5 MB of activations instead of 16 MB of slabs written and read back.
+constexpr int NSLAB = NPARAM - FC1N;                     // 5,840 slab floats per workgroup
+constexpr int S_FC1B = O_FC1B - FC1N, S_FC2W = O_FC2W - FC1N, S_FC2B = O_FC2B - FC1N;
+constexpr int NACT = F1 + NIN;                           // activation rows: dH^T (50) then R2^T (320)
+static_assert(O_FC1W % 4 == 0 && FC1N % 4 == 0 && NSLAB % 4 == 0, "float4 slab columns");
 
 __device__ __forceinline__ float hash_u01(unsigned long long seed, unsigned long long id) {
   unsigned long long z = seed + 0x9E3779B97F4A7C15ULL * (id + 1);
@@ -73,20 +85,25 @@ __device__ __forceinline__ f32x4 mfma(const u16x8& a, const u16x8& b, const f32x
 struct CnnSmem {
   // bf16 MFMA operands
   alignas(16) u16x8 w2f[KS2][2][64];   // conv2 fwd B fragments [kstep][ntile][lane]; P9 partials later
-  alignas(16) u16x8 w2d[KSD][64];      // conv2 dgrad B fragments [tap][lane]: B[k=co][n=ci]
+  alignas(16) u16x8 w2d[KSD][64];      // conv2 dgrad B fragments [kstep][lane]: B[k=(tap,co)][n=ci]
   alignas(16) u16x8 w1f[64];           // conv1 B fragment
   alignas(16) uint16_t r1n[NI][NC1][C1P];  // relu(maxpool(conv1)) channel-last, ci padded with zeros
   // conv2-output gradient (non-zero only at the argmax taps), twice: channel-last for the dgrad A
   // fragments (co padded to 32 with zeros) and as 8x8 planes for the wgrad A fragments
   alignas(16) uint16_t d2n[NI][O2 * O2][C2P];
-  alignas(16) uint16_t d2[NI][C2][O2 * O2];
+  alignas(16) uint16_t d2[NI][C2][D2R];    // rows padded to 144 B: the 16 co rows of a wgrad A fragment hit
+                                           // 16 distinct 16-B bank groups (128-B rows: 4-8-way conflicts)
+  alignas(16) uint16_t zero16[8];      // 16 zero bytes: the target of every out-of-range operand read
   uint16_t x[NI][NX];                  // images
   uint16_t r1[NI][NR1];                // relu(maxpool(conv1)), [ci][cell]
   uint16_t dr1[NI][NR1];               // grad at r1 (relu'-masked) == conv1-output grad at argmax taps
   // fp32 head
-  float b1[C1], b2[C2];
-  float fc2w[FC2N], fc2b[F2];
-  float r2[NI][NIN];                   // fc1 input (NCHW flatten order)
+  alignas(16) float b1[C1];
+  alignas(16) float b2[C2];
+  alignas(16) float fc1b[F1];
+  alignas(16) float fc2w[FC2N];
+  alignas(16) float fc2b[F2];
+  alignas(16) float r2[NI][NIN];       // fc1 input (NCHW flatten order); read as float4 in P3
   alignas(16) float dp2[NI][NIN];      // grad at the pooled conv2 output (dropout2d applied)
   float h1[NI][F1], m1[NI][F1], h1d[NI][F1], dh[NI][F1];
   float mc2[NI][C2];
@@ -117,16 +134,19 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
                                                  const u16x8* __restrict__ frag,
                                                  const unsigned long long* __restrict__ rng, float p_drop2,
                                                  float p_drop1, int training, float* __restrict__ slabs,
-                                                 float* __restrict__ loss_part,
-                                                 unsigned long long* __restrict__ stamps) {
-  // optional phase timestamps (diagnostic only: stamps == nullptr in production launches)
-#define PDE_STAMP(k) \
-  if (stamps != nullptr && threadIdx.x == 0) stamps[blockIdx.x * 16 + (k)] = wall_clock64()
+                                                 float* __restrict__ loss_part, float* __restrict__ acts,
+                                                 unsigned long long* __restrict__ stamps, int stop_after) {
+  // optional phase timestamps (diagnostic only: stamps == nullptr in production launches); stop_after = k
+  // ends the kernel after phase stamp k (diagnostic: hardware counters of a kernel prefix)
+#define PDE_STAMP(k)                                                                      \
+  if (stamps != nullptr && threadIdx.x == 0) stamps[blockIdx.x * 16 + (k)] = wall_clock64(); \
+  if (stop_after == (k)) return
   PDE_STAMP(0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   CnnSmem& S = *reinterpret_cast<CnnSmem*>(smem_raw);
   const int t = threadIdx.x;
-  const int lane = t & 63, wid = t >> 6;
+  const int lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: scalar loop control / branches
   const int lr = lane & 15, lg = lane >> 4;  // fragment row/col (lane & 15) and k-group (lane >> 4)
   const float* gW1 = params + O_W1;
   const float* gW2 = params + O_W2;
@@ -151,8 +171,10 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     const int pos = i / PADG, h = i - pos * PADG;
     *reinterpret_cast<u16x8*>(&S.d2n[0][pos][16 + 8 * h]) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
+  if (t < 8) S.zero16[t] = 0;
   for (int i = t; i < C1; i += T) S.b1[i] = params[O_B1 + i];
   for (int i = t; i < C2; i += T) S.b2[i] = params[O_B2 + i];
+  for (int i = t; i < F1; i += T) S.fc1b[i] = gFC1B[i];
   for (int i = t; i < FC2N + F2; i += T) (&S.fc2w[0])[i] = params[O_FC2W + i];
   const unsigned long long seed = rng[0] * 0xD1B54A32D192ED03ULL;
   const float keep2 = training ? 1.f / (1.f - p_drop2) : 1.f;
@@ -168,27 +190,36 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   } else if (t >= 384 && t < 384 + NI) {
     S.valid[t - 384] = (n0 + t - 384) < B ? 1.f : 0.f;
   }
-  float* slab = slabs + static_cast<long>(blockIdx.x) * NPARAM;
+  float* slab = slabs + static_cast<long>(blockIdx.x) * NSLAB;
   __syncthreads();
   PDE_STAMP(1);
 
   // ---- P1: conv1 (MFMA, M = (cell, tap), K = 25 -> 32, N = co) + maxpool2 + relu -------------------
   {
-    int koff[8];
+    int koff[8];       // k = (ky,kx) offsets into the image; padding k (>= 25) reads offset 0, masked
+    uint16_t kmsk[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k = lg * 8 + j;
-      koff[j] = k < 25 ? (k / 5) * H0 + (k % 5) : -1;
+      koff[j] = k < 25 ? (k / 5) * H0 + (k % 5) : 0;
+      kmsk[j] = k < 25 ? 0xFFFFu : 0u;
     }
     const u16x8 bw = S.w1f[lane];
     const int tap = lr & 3, dy = tap >> 1, dx = tap & 1;
-    for (int tile = wid; tile < NI * MT1; tile += NW) {
+    auto gather = [&](int tile, u16x8& a) {
       const int im = tile / MT1, c0 = (tile - im * MT1) * 4;
       const int cell = c0 + (lr >> 2), py = cell / P1, px = cell - py * P1;
       const uint16_t* xb = S.x[im] + (2 * py + dy) * H0 + 2 * px + dx;
-      u16x8 a;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] = koff[j] >= 0 ? xb[koff[j]] : 0;
+      for (int j = 0; j < 8; ++j) a[j] = xb[koff[j]] & kmsk[j];
+    };
+    static_assert((NI * MT1) % NW == 0, "every wave runs the same number of conv1 tiles");
+    u16x8 an;
+    gather(wid, an);
+    for (int tile = wid; tile < NI * MT1; tile += NW) {
+      const u16x8 a = an;
+      if (tile + NW < NI * MT1) gather(tile + NW, an);  // next tile's gathers overlap this tile's MFMA + epilogue
+      const int im = tile / MT1, c0 = (tile - im * MT1) * 4;
       const f32x4 acc = mfma(a, bw, f32x4{0.f, 0.f, 0.f, 0.f});
       const int co = lr;  // rows (lg*4 + r) = taps r of cell c0 + lg
       if (co < C1) {
@@ -246,22 +277,24 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   __syncthreads();
   PDE_STAMP(3);
 
-  // ---- P3: fc1 + relu + dropout.  Thread (j, kc): the 32 weights W[j][32kc..] (8 x 16-B L2 loads, all
-  // in flight together) against the 4 images' inputs; partials [kc][im][j] summed in kc order. -------
+  // ---- P3: fc1 + relu + dropout.  Thread (j, kc): 32 weights of row j (8 x 16-B L2 loads, all in flight
+  // together) against the 4 images' inputs; partials [kc][im][j] summed in kc order. -------------------
   {
     float* part = reinterpret_cast<float*>(&S.w2f[0][0][0]);
     if (t < F1 * FC1_KC) {
       const int j = t / FC1_KC, kc = t - j * FC1_KC;
-      const f32x4* w4 = reinterpret_cast<const f32x4*>(gFC1W + j * NIN + kc * 32);
+      // chunk kc = inputs {40 q + 4 kc .. +3 : q = 0..7}: the 10 chunks of a wave read 10 consecutive
+      // float4s of r2 (conflict-free), and adjacent lanes load adjacent 16 B of the weight row
+      const f32x4* w4 = reinterpret_cast<const f32x4*>(gFC1W + j * NIN + kc * 4);
       f32x4 w[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) w[q] = w4[q];
+      for (int q = 0; q < 8; ++q) w[q] = w4[q * (FC1_KC)];
       float s4[NI] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int q = 0; q < 8; ++q)
 #pragma unroll
         for (int im = 0; im < NI; ++im) {
-          const f32x4 x = *reinterpret_cast<const f32x4*>(&S.r2[im][kc * 32 + q * 4]);
+          const f32x4 x = *reinterpret_cast<const f32x4*>(&S.r2[im][q * 4 * FC1_KC + kc * 4]);
           s4[im] += w[q][0] * x[0] + w[q][1] * x[1] + w[q][2] * x[2] + w[q][3] * x[3];
         }
 #pragma unroll
@@ -270,7 +303,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     __syncthreads();
     if (t < NI * F1) {
       const int im = t / F1, j = t - im * F1;
-      float s1 = gFC1B[j];
+      float s1 = S.fc1b[j];
 #pragma unroll
       for (int kc = 0; kc < FC1_KC; ++kc) s1 += part[(kc * NI + im) * F1 + j];
       const float h = fmaxf(s1, 0.f);
@@ -314,13 +347,13 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     float s = 0.f;
 #pragma unroll
     for (int im = 0; im < NI; ++im) s += S.dlog[im][v] * S.h1d[im][j];
-    slab[O_FC2W + i] = s;
+    slab[S_FC2W + i] = s;
   }
   if (t < F2) {
     float s = 0.f;
 #pragma unroll
     for (int im = 0; im < NI; ++im) s += S.dlog[im][t];
-    slab[O_FC2B + t] = s;
+    slab[S_FC2B + t] = s;
   }
   if (t >= 256 && t < 256 + NI * F1) {
     const int u = t - 256, im = u / F1, j = u - im * F1;
@@ -332,19 +365,23 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   __syncthreads();
   PDE_STAMP(7);
 
-  // ---- P6: fc1 backward: dW, db (straight to the slab), dp2 = grad at the pooled conv2 output -------
-  for (int idx = t; idx < FC1N; idx += T) {
-    const int j = idx / NIN, i = idx - j * NIN;
-    float s = 0.f;
+  // ---- P6: fc1 backward: dH / R2 columns for the batch-wide dW GEMM (k_cnn_reduce), db to the slab, and
+  // dp2 = grad at the pooled conv2 output.  Columns n0..n0+3 of the K-contiguous [row][Bk] image: one
+  // 16-byte store per row (rows 0..49 dH^T, 50..369 R2^T).
+  {
+    const int Bk = gridDim.x * NI;
+    for (int row = t; row < NACT; row += T) {
+      f32x4 v;
 #pragma unroll
-    for (int im = 0; im < NI; ++im) s += S.dh[im][j] * S.r2[im][i];
-    slab[O_FC1W + idx] = s;
+      for (int im = 0; im < NI; ++im) v[im] = row < F1 ? S.dh[im][row] : S.r2[im][row - F1];
+      *reinterpret_cast<f32x4*>(acts + static_cast<long>(row) * Bk + n0) = v;
+    }
   }
   if (t < F1) {
     float s = 0.f;
 #pragma unroll
     for (int im = 0; im < NI; ++im) s += S.dh[im][t];
-    slab[O_FC1B + t] = s;
+    slab[S_FC1B + t] = s;
   }
   float* dpart = reinterpret_cast<float*>(&S.w2f[0][0][0]);  // [jc][im][i]
   if (t < NIN * DP2_JC) {  // thread (i, jc): sum over fc1 outputs j in chunk jc (column loads coalesced)
@@ -401,6 +438,8 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   // M = co (2 tiles), N = 250 -> 16 tiles (NT2 per wave), K = (im, y, x) 256 = 8 k-steps.  An A fragment
   // is one 16-byte row of the d2 plane.
   {
+    // the B gathers stay CONDITIONAL u16 reads: unconditional ones are merged by the compiler into one
+    // 16-byte read at a 2-byte-aligned address, which LDS replays as an unaligned access (64 cycles)
     int nb[NT2];
     bool nv[NT2];
 #pragma unroll
@@ -417,12 +456,12 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       u16x8 a[2];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
-        const int co = mt * 16 + lr;
-        a[mt] = co < C2 ? *reinterpret_cast<const u16x8*>(&S.d2[im][co][y * O2]) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        const int co = mt * 16 + lr;  // rows 20..31 read the zero block
+        a[mt] = *reinterpret_cast<const u16x8*>(co < C2 ? &S.d2[im][co][y * O2] : &S.zero16[0]);
       }
 #pragma unroll
       for (int u = 0; u < NT2; ++u) {
-        const uint16_t* src = S.r1[im] + nb[u] + y * P1;
+        const uint16_t* src = S.r1[im] + nb[u] + y * P1;  // unmerged u16 reads (see P9)
         u16x8 b;
 #pragma unroll
         for (int j = 0; j < 8; ++j) b[j] = nv[u] ? src[j] : 0;
@@ -446,8 +485,9 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
 
   // ---- P7b: conv2 dgrad (MFMA): dr1[ci][Y][X] = sum_(ky,kx) sum_co d2[Y-ky][X-kx][co] * w2[co][ci][ky][kx],
   // then relu'(r1).  M = r1 positions (9 tiles per image, 36 total, round-robin over waves), N = ci,
-  // one k-step per filter tap with K = co: a lane's A fragment is the 16-byte co-block (lane >> 4) of
-  // channel-last position (Y-ky, X-kx), or zero when that position is outside the 8x8 conv2 output.
+  // K = (tap, co24) packed into 19 k-steps: a lane's A fragment is the 16-byte co-group of ITS tap's source
+  // position (Y-ky, X-kx), or the zero block when that position lies outside the 8x8 conv2 output -- every
+  // read is unconditional, so the k-loop pipelines its LDS reads ahead of the MFMAs.
   {
     constexpr int MAXT = (NI * MTD + NW - 1) / NW;  // 3
     f32x4 acc[MAXT];
@@ -455,25 +495,36 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
 #pragma unroll
     for (int u = 0; u < MAXT; ++u) {
       acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int tile = wid + u * NW;
+      const int tile = min(wid + u * NW, NI * MTD - 1);  // a 2-tile wave's third slot mirrors a real tile
       const int im = tile / MTD, pos = (tile % MTD) * 16 + lr;
       ty[u] = pos / P1;
       tx[u] = pos - ty[u] * P1;
-      tb[u] = ((im * O2 * O2) + ty[u] * O2 + tx[u]) * C2P + lg * 8;  // element offset at tap (0,0)
+      tb[u] = ((im * O2 * O2) + ty[u] * O2 + tx[u]) * C2P;  // element offset at tap (0,0), channel 0
     }
     const uint16_t* base = &S.d2n[0][0][0];
-    for (int tap = 0; tap < KSD; ++tap) {
-      const int ky = tap / KS, kx = tap - ky * KS;
-      const int tofs = -(ky * O2 + kx) * C2P;
-      const u16x8 b = S.w2d[tap][lane];
+    const int zoff = static_cast<int>(&S.zero16[0] - base);
+    const int ntile = wid < NI * MTD - 2 * NW ? 3 : 2;  // wave-uniform (36 tiles over 16 waves)
+    auto load = [&](int ks, u16x8 (&a)[MAXT], u16x8& b) {
+      const int g = ks * 4 + lg, tap = g / CG, cg = g - tap * CG, ky = tap / KS, kx = tap - ky * KS;
+      const int tofs = -(ky * O2 + kx) * C2P + cg * 8;
+      b = S.w2d[ks][lane];
 #pragma unroll
       for (int u = 0; u < MAXT; ++u) {
-        if (wid + u * NW < NI * MTD) {
-          const bool ok = static_cast<unsigned>(ty[u] - ky) < O2 && static_cast<unsigned>(tx[u] - kx) < O2;
-          const u16x8 a = ok ? *reinterpret_cast<const u16x8*>(base + tb[u] + tofs) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-          acc[u] = mfma(a, b, acc[u]);
-        }
+        const bool ok = g < NGD && static_cast<unsigned>(ty[u] - ky) < O2 && static_cast<unsigned>(tx[u] - kx) < O2;
+        a[u] = *reinterpret_cast<const u16x8*>(base + (ok ? tb[u] + tofs : zoff));
       }
+    };
+    u16x8 an[MAXT], bn;
+    load(0, an, bn);
+#pragma unroll
+    for (int ks = 0; ks < KSD; ++ks) {  // reads of k-step ks+1 are issued before the MFMAs of ks
+      u16x8 ac[MAXT], bc = bn;
+#pragma unroll
+      for (int u = 0; u < MAXT; ++u) ac[u] = an[u];
+      if (ks + 1 < KSD) load(ks + 1, an, bn);
+      acc[0] = mfma(ac[0], bc, acc[0]);
+      acc[1] = mfma(ac[1], bc, acc[1]);
+      if (ntile == 3) acc[2] = mfma(ac[2], bc, acc[2]);
     }
 #pragma unroll
     for (int u = 0; u < MAXT; ++u) {
@@ -524,6 +575,8 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
+        // 8 separate u16 reads (this file is built without unaligned-access mode, _build.HIP_FLAGS): merged
+        // into one 16-byte read at this 2-byte-aligned address the LDS would replay it as an unaligned access
         const uint16_t* src = S.x[im] + nb[u] + y * H0 + x0;
         u16x8 b;
 #pragma unroll
@@ -558,6 +611,11 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     const float l = wave_sum(loss_acc);
     if (lane == 0) loss_part[blockIdx.x] = l;
   }
+  if (stamps != nullptr) {  // diagnostic: every wave's stores drained, then the workgroup's last stamp
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    PDE_STAMP(12);
+  }
 }
 
 // The conv weights in bf16 MFMA B-fragment order (conv2 fwd [ks][ntile][lane], conv2 dgrad [tap][lane],
@@ -574,11 +632,12 @@ __global__ __launch_bounds__(256) void k_cnn_prep(const float* __restrict__ para
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       f[j] = (co < C2 && tap < KS * KS && c8 + j < C1) ? f2bf(gW2[co * K2 + (c8 + j) * KS * KS + tap]) : 0;
-  } else if (e < KS2 * 2 * 64 + KSD * 64) {  // conv2 dgrad, tap (ky,kx): B[k=co][n=ci] = w2[co][ci][ky][kx]
-    const int e2 = e - KS2 * 2 * 64, tap = e2 >> 6, l = e2 & 63;
-    const int ci = l & 15, c0 = (l >> 4) * 8;
+  } else if (e < KS2 * 2 * 64 + KSD * 64) {  // conv2 dgrad: B[k=(tap, co24)][n=ci] = w2[co][ci][tap]
+    const int e2 = e - KS2 * 2 * 64, ks = e2 >> 6, l = e2 & 63;
+    const int ci = l & 15, g = ks * 4 + (l >> 4), tap = g / CG, c0 = (g - tap * CG) * 8;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = (ci < C1 && c0 + j < C2) ? f2bf(gW2[(c0 + j) * K2 + ci * 25 + tap]) : 0;
+    for (int j = 0; j < 8; ++j)
+      f[j] = (g < NGD && ci < C1 && c0 + j < C2) ? f2bf(gW2[(c0 + j) * K2 + ci * 25 + tap]) : 0;
   } else {  // conv1: B[k=(ky,kx)][n=co] = w1[co][k]
     const int l = e - KS2 * 2 * 64 - KSD * 64;
     const int co = l & 15, k0 = (l >> 4) * 8;
@@ -598,7 +657,8 @@ __device__ __forceinline__ void write_frag(uint16_t* __restrict__ f, int p, floa
     const int g = ((tap & 1) << 1) | (ci >> 3);
     const int e = ((tap >> 1) << 7) | ((co >> 4) << 6) | (g << 4) | (co & 15);  // conv2 fwd [ks][ntile][lane]
     f[e * 8 + (ci & 7)] = b;
-    const int e2 = KS2 * 2 * 64 + tap * 64 + (((co >> 3) << 4) | ci);          // conv2 dgrad [tap][lane]
+    const int gd = tap * CG + (co >> 3);                                         // conv2 dgrad [kstep][lane]
+    const int e2 = KS2 * 2 * 64 + (gd >> 2) * 64 + (((gd & 3) << 4) | ci);
     f[e2 * 8 + (co & 7)] = b;
   } else if (p >= O_W1 && p < O_W1 + W1N) {
     const int co = p / (KS * KS), k = p - co * (KS * KS);
@@ -619,55 +679,123 @@ __global__ __launch_bounds__(256) void k_cnn_sgd(float* __restrict__ params, con
   write_frag(frag, p, w);
 }
 
-// grads (+)= gscale * sum_wg slabs[wg] in a fixed order (deterministic).  Block = 8 waves over 16 float4
-// columns (64 parameters); lane = column + 16 x slab-lane, so one load instruction of a wave reads 4 slabs
-// x 256 B and each thread keeps nwg/32 independent float4 loads in flight.  Block 0 also reduces the
-// per-workgroup loss partials and advances the dropout RNG counter for the next step.
+// grads (+)= gscale * (sum_wg slabs[wg] | dH^T . R2) in a fixed order (deterministic).
+//  * slab blocks (blockIdx < RED_SLAB_BLOCKS): 8 waves over 16 float4 slab columns; lane = column + 16 x
+//    slab-lane, so one load instruction of a wave reads 4 slabs x 256 B and each thread keeps nwg/32
+//    independent float4 loads in flight;
+//  * fc1 blocks: one 16 x 16 tile of dW_fc1[j][i] = sum_n dH[n][j] R2[n][i] on the f32 matrix cores
+//    (v_mfma_f32_16x16x4_f32, exact f32 products), the batch K split over the 8 waves, partials summed in
+//    wave order.  Lane (lr, lg) loads 16 B of row j (A) / row i (B) at k = kb + 4 lg: MFMA s of the chunk
+//    uses component s, the same k on both operands;
+//  * block 0 also reduces the per-workgroup loss partials and advances the dropout RNG counter.
+// With hp (single process, no all-reduce in between) every block also applies the SGD update to the
+// parameters it reduced and refreshes their bf16 fragment slots.
 constexpr int RED_T = 512, RED_COLS = 16, RED_LANES = RED_T / RED_COLS;  // 32 slab lanes
-constexpr int NPARAM4 = NPARAM / 4;
-static_assert(NPARAM % 4 == 0, "float4 columns");
+constexpr int NSLAB4 = NSLAB / 4;
+constexpr int RED_SLAB_BLOCKS = (NSLAB4 + RED_COLS - 1) / RED_COLS;
+constexpr int FC1_JT = (F1 + 15) / 16, FC1_IT = NIN / 16;   // 4 x 20 output tiles
+constexpr int RED_BLOCKS = RED_SLAB_BLOCKS + FC1_JT * FC1_IT;
+static_assert(NIN % 16 == 0, "fc1 input tiles");
+static_assert(NI == 4, "activation columns are written as one float4 per row");
+
+__device__ __forceinline__ void sgd_update(float* params, const float* hp, uint16_t* frag, int p, float g) {
+  const float w = params[p] - hp[HP_LR] * (g * hp[HP_GRAD_SCALE]);
+  params[p] = w;
+  write_frag(frag, p, w);
+}
 
 __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ slabs, int nwg,
+                                                      const float* __restrict__ acts,
                                                       const float* __restrict__ gscale, float* __restrict__ grads,
                                                       int accumulate, const float* __restrict__ loss_part, int B,
                                                       float* __restrict__ loss, unsigned long long* __restrict__ rng,
                                                       float* __restrict__ params, const float* __restrict__ hp,
                                                       uint16_t* __restrict__ frag) {
-  __shared__ f32x4 part[RED_LANES][RED_COLS];
-  const int col = threadIdx.x % RED_COLS, sl = threadIdx.x / RED_COLS;
-  const int c4 = blockIdx.x * RED_COLS + col;
-  const f32x4* s4 = reinterpret_cast<const f32x4*>(slabs);
-  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
-  if (c4 < NPARAM4) {
-    int b = sl;
-    for (; b + 3 * RED_LANES < nwg; b += 4 * RED_LANES) {
-      a0 += s4[static_cast<long>(b) * NPARAM4 + c4];
-      a1 += s4[static_cast<long>(b + RED_LANES) * NPARAM4 + c4];
-      a2 += s4[static_cast<long>(b + 2 * RED_LANES) * NPARAM4 + c4];
-      a3 += s4[static_cast<long>(b + 3 * RED_LANES) * NPARAM4 + c4];
-    }
-    for (; b < nwg; b += RED_LANES) a0 += s4[static_cast<long>(b) * NPARAM4 + c4];
-  }
-  part[sl][col] = (a0 + a1) + (a2 + a3);
-  __syncthreads();
-  if (sl == 0 && c4 < NPARAM4) {
-    f32x4 v = part[0][col];
-#pragma unroll 8
-    for (int k = 1; k < RED_LANES; ++k) v += part[k][col];
-    v *= gscale ? gscale[0] : 1.f;
-    f32x4* g4 = reinterpret_cast<f32x4*>(grads) + c4;
-    if (accumulate) v += *g4;
-    *g4 = v;
-    if (hp) {  // single-process step: SGD + fragment refresh right here (no all-reduce in between)
-      const float lr = hp[HP_LR], gs = hp[HP_GRAD_SCALE];
-      f32x4* p4 = reinterpret_cast<f32x4*>(params) + c4;
-      f32x4 w = *p4;
+  __shared__ f32x4 part[RED_LANES][RED_COLS];  // slab: [lane][column]; fc1: [wave][lane] (same 8 KB)
+  const float gs = gscale ? gscale[0] : 1.f;
+  if (blockIdx.x < RED_SLAB_BLOCKS) {
+    const int col = threadIdx.x % RED_COLS, sl = threadIdx.x / RED_COLS;
+    const int c4 = blockIdx.x * RED_COLS + col;
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(slabs);
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+    if (c4 < NSLAB4) {
+      int b = sl;
+      for (; b + 7 * RED_LANES < nwg; b += 8 * RED_LANES) {  // 8 independent loads in flight
+        f32x4 v[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        w[j] -= lr * (v[j] * gs);
-        write_frag(frag, c4 * 4 + j, w[j]);
+        for (int u = 0; u < 8; ++u) v[u] = s4[static_cast<long>(b + u * RED_LANES) * NSLAB4 + c4];
+        a0 += v[0] + v[4];
+        a1 += v[1] + v[5];
+        a2 += v[2] + v[6];
+        a3 += v[3] + v[7];
       }
-      *p4 = w;
+      for (; b < nwg; b += RED_LANES) a0 += s4[static_cast<long>(b) * NSLAB4 + c4];
+    }
+    part[sl][col] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (sl == 0 && c4 < NSLAB4) {
+      f32x4 v = part[0][col];
+#pragma unroll 8
+      for (int k = 1; k < RED_LANES; ++k) v += part[k][col];
+      v *= gs;
+      const int p4 = c4 < O_FC1W / 4 ? c4 : c4 + FC1N / 4;  // slab column -> parameter float4
+      f32x4* g4 = reinterpret_cast<f32x4*>(grads) + p4;
+      if (accumulate) v += *g4;
+      *g4 = v;
+      if (hp) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sgd_update(params, hp, frag, p4 * 4 + j, v[j]);
+      }
+    }
+  } else {
+    const int fb = blockIdx.x - RED_SLAB_BLOCKS;
+    const int j0 = (fb / FC1_IT) * 16, i0 = (fb % FC1_IT) * 16;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, lr = lane & 15, lg = lane >> 4;
+    const int Bk = nwg * NI;
+    const int kper = ((Bk + 8 * 16 - 1) / (8 * 16)) * 16;  // this wave's K slice, a multiple of 16
+    const int k0 = wid * kper, k1 = min(Bk, k0 + kper);
+    const bool jv = j0 + lr < F1;
+    const float* arow = acts + static_cast<long>(jv ? j0 + lr : 0) * Bk;
+    const float* brow = acts + static_cast<long>(F1 + i0 + lr) * Bk;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    constexpr int CH = 8;  // 16-deep chunks per pass: all 2 x CH loads in flight before the first MFMA
+    for (int kb = k0; kb < k1; kb += 16 * CH) {
+      f32x4 a[CH], b[CH];
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const int k = kb + 16 * c + 4 * lg;
+        const bool ok = k < k1;
+        a[c] = (ok && jv) ? *reinterpret_cast<const f32x4*>(arow + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+        b[c] = ok ? *reinterpret_cast<const f32x4*>(brow + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][0], b[c][0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][1], b[c][1], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][2], b[c][2], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][3], b[c][3], acc1, 0, 0, 0);
+      }
+    }
+    f32x4* wpart = &part[0][0];
+    wpart[wid * 64 + lane] = acc0 + acc1;
+    __syncthreads();
+    if (wid == 0) {
+      f32x4 v = wpart[lane];
+#pragma unroll
+      for (int w = 1; w < RED_T / 64; ++w) v += wpart[w * 64 + lane];
+      v *= gs;
+      const int i = i0 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = j0 + lg * 4 + r;
+        if (j < F1) {
+          const int p = O_FC1W + j * NIN + i;
+          float g = v[r];
+          if (accumulate) g += grads[p];
+          grads[p] = g;
+          if (hp) sgd_update(params, hp, frag, p, g);
+        }
+      }
     }
   }
   if (blockIdx.x == 0 && threadIdx.x >= RED_T - 64) {  // last wave: loss
@@ -689,11 +817,14 @@ size_t cnn_frag_bytes() { return sizeof(u16x8) * NFRAG; }
 size_t cnn_smem_bytes() { return sizeof(CnnSmem); }
 int cnn_images_per_workgroup() { return NI; }
 
+int cnn_slab_floats() { return NSLAB; }
+int cnn_act_rows() { return NACT; }
+
 hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float* params, void* frag,
                            unsigned long long* rng, float p_drop2, float p_drop1, int training, float* slabs,
-                           float* loss_part, int nwg, float* loss, float* grads, const float* gscale,
+                           float* loss_part, float* acts, int nwg, float* loss, float* grads, const float* gscale,
                            int accumulate, hipStream_t s, unsigned long long* stamps, int prep,
-                           const float* sgd_hp) {
+                           const float* sgd_hp, int stop_after) {
   if (reinterpret_cast<uintptr_t>(grads) & 15) return hipErrorInvalidValue;  // float4 gradient stores
   const size_t sm = sizeof(CnnSmem);
   static bool attr = false;
@@ -705,9 +836,11 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
   if (reinterpret_cast<uintptr_t>(frag) & 15) return hipErrorInvalidValue;
   if (prep)
     hipLaunchKernelGGL(k_cnn_prep, dim3(ceil_div(NFRAG, 256)), dim3(256), 0, s, params, static_cast<u16x8*>(frag));
+  if (reinterpret_cast<uintptr_t>(acts) & 15) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_cnn_train, dim3(nwg), dim3(T), sm, s, images, tgt, B, params,
-                     static_cast<const u16x8*>(frag), rng, p_drop2, p_drop1, training, slabs, loss_part, stamps);
-  hipLaunchKernelGGL(k_cnn_reduce, dim3(ceil_div(NPARAM4, RED_COLS)), dim3(RED_T), 0, s, slabs, nwg, gscale, grads,
+                     static_cast<const u16x8*>(frag), rng, p_drop2, p_drop1, training, slabs, loss_part, acts, stamps,
+                     stop_after);
+  hipLaunchKernelGGL(k_cnn_reduce, dim3(RED_BLOCKS), dim3(RED_T), 0, s, slabs, nwg, acts, gscale, grads,
                      accumulate, loss_part, B, loss, rng, params, sgd_hp, static_cast<uint16_t*>(frag));
   return hipGetLastError();
 }

@@ -38,6 +38,15 @@ EXTENSIONS = {
 }
 
 
+# Per-source device flags.  cnn_fused.hip gathers 8 consecutive bf16 values from 2-byte-aligned LDS
+# addresses: with gfx950's unaligned-access mode the compiler merges them into one 16-byte ds_read that the
+# LDS replays as an unaligned access (64 cycles; measured SQ_LDS_UNALIGNED_STALL), so that mode is off there.
+# (The host compiler ignores the device target feature with a warning.)
+HIP_FLAGS = {
+    "kernels/cnn_fused.hip": ["-Xclang", "-target-feature", "-Xclang", "-unaligned-access-mode"],
+}
+
+
 def _torch_paths():
     import torch  # noqa: WPS433
 
@@ -91,8 +100,8 @@ def build(verbose: bool = False, jobs: int | None = None) -> list[Path]:
             objs.append(obj)
             if _stale(obj, src, headers):
                 tasks.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", abi,
-                              "-munsafe-fp-atomics", *common_inc, *([f"-I{ROCM / 'include'}"]),
-                              "-c", str(src), "-o", str(obj)])
+                              "-munsafe-fp-atomics", *HIP_FLAGS.get(rel, []), *common_inc,
+                              *([f"-I{ROCM / 'include'}"]), "-c", str(src), "-o", str(obj)])
         for rel in cpp_srcs:
             src = CSRC / rel
             obj = BUILD / (rel.replace("/", "_") + ".o")

@@ -267,6 +267,17 @@ class _Handle:
         self.h, self.output, self.post = h, output, post
 
 
+def _enqueue(fn, *args):
+    """Engine enqueue; a failed engine (dead peer, aborted communicator) raises HorovodInternalError."""
+    try:
+        return fn(*args)
+    except RuntimeError as exc:
+        msg = str(exc)
+        if msg.startswith("HorovodInternalError") or "has been shut down" in msg:
+            raise HorovodInternalError(msg.split("\n")[0]) from exc
+        raise
+
+
 def _auto_name(prefix: str, name: str | None) -> str:
     if name is not None:
         return name
@@ -289,8 +300,8 @@ def allreduce_async_(tensor, average=None, name=None, op=None, prescale_factor=1
     _need()
     op = _resolve_op(average, op)
     t = tensor if tensor.is_contiguous() else tensor.contiguous()
-    h = _ctx.engine.allreduce(t, t, _auto_name("allreduce", name), op, float(prescale_factor),
-                              float(postscale_factor), compression_bf16)
+    h = _enqueue(_ctx.engine.allreduce, t, t, _auto_name("allreduce", name), op, float(prescale_factor),
+                 float(postscale_factor), compression_bf16)
     post = None if t is tensor else (lambda out, tensor=tensor: tensor.copy_(out))
     return _Handle(h, t, post)
 
@@ -300,8 +311,8 @@ def allreduce_async(tensor, average=None, name=None, op=None, prescale_factor=1.
     op = _resolve_op(average, op)
     t = tensor.contiguous()
     out = torch.empty_like(t)
-    h = _ctx.engine.allreduce(t, out, _auto_name("allreduce", name), op, float(prescale_factor),
-                              float(postscale_factor), False)
+    h = _enqueue(_ctx.engine.allreduce, t, out, _auto_name("allreduce", name), op, float(prescale_factor),
+                 float(postscale_factor), False)
     return _Handle(h, out)
 
 
@@ -325,7 +336,7 @@ def grouped_allreduce(tensors, average=None, name=None, op=None):
 
 def allgather_async(tensor, name=None):
     _need()
-    h = _ctx.engine.allgather(tensor.contiguous(), _auto_name("allgather", name))
+    h = _enqueue(_ctx.engine.allgather, tensor.contiguous(), _auto_name("allgather", name))
     return _Handle(h, None)
 
 
@@ -336,7 +347,7 @@ def allgather(tensor, name=None):
 def broadcast_async_(tensor, root_rank, name=None):
     _need()
     t = tensor if tensor.is_contiguous() else tensor.contiguous()
-    h = _ctx.engine.broadcast(t, int(root_rank), _auto_name("broadcast", name))
+    h = _enqueue(_ctx.engine.broadcast, t, int(root_rank), _auto_name("broadcast", name))
     post = None if t is tensor else (lambda out, tensor=tensor: tensor.copy_(out))
     return _Handle(h, t, post)
 
@@ -397,7 +408,7 @@ def synchronize(handle):
     try:
         out = _ctx.engine.wait(handle.h)
     except RuntimeError as exc:
-        raise HorovodInternalError(str(exc)) from exc
+        raise HorovodInternalError(str(exc).split("\n")[0]) from exc
     if handle.post is not None:
         handle.post(out)
         return handle.output if handle.output is not None else out

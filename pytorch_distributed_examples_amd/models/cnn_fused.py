@@ -57,6 +57,7 @@ class FusedCNN:
         self.own_grad = None
         self.workgroups = workgroups
         self.stamps = None  # diagnostic: int64 [nwg, 16] tensor of per-phase wall-clock stamps
+        self.stop_after = -1  # diagnostic: end the training kernel after phase stamp k (counter attribution)
         self.frag = torch.empty(C.cnn_frag_bytes(), dtype=torch.uint8, device=dev)
         self._frag_gen = None  # weight generation at which the fragment image was last made current
 
@@ -120,7 +121,7 @@ class FusedCNN:
         prep = self._frag_gen is None or self._frag_gen != OF.weight_generation()
         hp, params = self._sgd_hp(sgd) if sgd is not None else (None, None)
         loss = C.cnn_train(x, y, self.flat, OF._rng_counter(x.device), p_drop2, p_drop1, training, grad_out,
-                           accumulate, None, self.stamps, self.frag, prep, hp)
+                           accumulate, None, self.stamps, self.frag, prep, hp, self.stop_after)
         if sgd is not None:
             self._after_update(sgd, params)
         else:

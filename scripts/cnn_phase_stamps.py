@@ -29,3 +29,19 @@ for i, n in enumerate(names):
     print(f"{n:14s} median {d[:, i].median().item():7.2f} us  max {d[:, i].max().item():7.2f} us")
 print("total median", (st[:, 11] - st[:, 0]).median().item() / 100.0, "us")
 print("span (first start -> last stamp)", (st[:, 11].max() - st[:, 0].min()).item() / 100.0, "us")
+print("workgroup start spread (last - first stamp 0)", (st[:, 0].max() - st[:, 0].min()).item() / 100.0, "us")
+print("drain span (first start -> last workgroup end, stores drained)",
+      (st[:, 12].max() - st[:, 0].min()).item() / 100.0, "us")
+# the same launch timed from the host around a single stream-ordered call (includes dispatch + end of kernel)
+s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+f.stamps = None
+ts = []
+for _ in range(20):
+    torch.cuda.synchronize()
+    s_ev.record()
+    f.forward_backward(x, y)
+    e_ev.record()
+    torch.cuda.synchronize()
+    ts.append(s_ev.elapsed_time(e_ev) * 1000.0)
+ts.sort()
+print(f"host events around one forward_backward (train + reduce): median {ts[len(ts) // 2]:.1f} us  min {ts[0]:.1f} us")
