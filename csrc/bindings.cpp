@@ -646,7 +646,7 @@ Tensor embbag_bwd(const Tensor& dy, const Tensor& idx, const Tensor& off, int64_
 Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, Tensor& rng, double p_drop2,
                  double p_drop1, bool training, Tensor& grads, bool accumulate, const optional<Tensor>& gscale,
                  const optional<Tensor>& stamps, const optional<Tensor>& frag_buf, bool prep,
-                 const optional<Tensor>& sgd_hp, int64_t stop_after) {
+                 const optional<Tensor>& sgd_hp, int64_t stop_after, const optional<Tensor>& sgd_step) {
   CHECK_IN(images); CHECK_IN(tgt); CHECK_IN(params); CHECK_IN(rng); CHECK_IN(grads);
   CHECK_F32(images); CHECK_F32(params); CHECK_F32(grads);
   TORCH_CHECK(params.numel() == pde::cnn_num_params(), "cnn_train: params must be the flat Net parameters");
@@ -689,20 +689,23 @@ Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, 
                                  ? reinterpret_cast<unsigned long long*>(stamps->data_ptr())
                                  : nullptr,
                              prep ? 1 : 0, sgd_hp.has_value() && sgd_hp->defined() ? sgd_hp->data_ptr<float>() : nullptr,
-                             static_cast<int>(stop_after)),
+                             static_cast<int>(stop_after),
+                             sgd_step.has_value() && sgd_step->defined() ? sgd_step->data_ptr<int>() : nullptr),
         "cnn_train");
   return loss;
 }
 
 // Plain SGD on the flat CNN parameters + fragment-image refresh (after the gradient all-reduce).
-void cnn_sgd(Tensor& params, const Tensor& grads, const Tensor& hp, Tensor& frag) {
+void cnn_sgd(Tensor& params, const Tensor& grads, const Tensor& hp, Tensor& frag, const optional<Tensor>& step) {
   CHECK_IN(params); CHECK_IN(grads); CHECK_IN(hp); CHECK_IN(frag);
   CHECK_F32(params); CHECK_F32(grads); CHECK_F32(hp);
   TORCH_CHECK(params.numel() == pde::cnn_num_params() && grads.numel() == pde::cnn_num_params(), "cnn_sgd: sizes");
   TORCH_CHECK(hp.numel() >= pde::HP_COUNT, "cnn_sgd: hp");
   TORCH_CHECK(frag.nbytes() >= pde::cnn_frag_bytes(), "cnn_sgd: frag size");
+  if (step.has_value() && step->defined())
+    TORCH_CHECK(step->is_cuda() && step->scalar_type() == at::kInt, "cnn_sgd: step must be a device int32 tensor");
   check(pde::cnn_sgd_fused(params.data_ptr<float>(), grads.data_ptr<float>(), hp.data_ptr<float>(), frag.data_ptr(),
-                           cur_stream()),
+                           cur_stream(), step.has_value() && step->defined() ? step->data_ptr<int>() : nullptr),
         "cnn_sgd");
 }
 
@@ -712,8 +715,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cnn_train", &cnn_train, py::arg("images"), py::arg("tgt"), py::arg("params"), py::arg("rng"),
         py::arg("p_drop2"), py::arg("p_drop1"), py::arg("training"), py::arg("grads"), py::arg("accumulate"),
         py::arg("gscale") = py::none(), py::arg("stamps") = py::none(), py::arg("frag") = py::none(),
-        py::arg("prep") = true, py::arg("sgd_hp") = py::none(), py::arg("stop_after") = -1);
-  m.def("cnn_sgd", &cnn_sgd);
+        py::arg("prep") = true, py::arg("sgd_hp") = py::none(), py::arg("stop_after") = -1,
+        py::arg("sgd_step") = py::none());
+  m.def("cnn_sgd", &cnn_sgd, py::arg("params"), py::arg("grads"), py::arg("hp"), py::arg("frag"),
+        py::arg("step") = py::none());
   m.def("clear_last_error", []() { return static_cast<int>(hipGetLastError()); },
         "Read and reset the HIP last-error state (after an aborted stream capture).");
   m.def("cnn_frag_bytes", &pde::cnn_frag_bytes);

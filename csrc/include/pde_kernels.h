@@ -178,10 +178,11 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
                            unsigned long long* rng, float p_drop2, float p_drop1, int training, float* slabs,
                            float* loss_part, float* acts, int nwg, float* loss, float* grads, const float* gscale,
                            int accumulate, hipStream_t s, unsigned long long* stamps = nullptr, int prep = 1,
-                           const float* sgd_hp = nullptr, int stop_after = -1);
+                           const float* sgd_hp = nullptr, int stop_after = -1, int* sgd_step = nullptr);
 // params -= lr * gscale * grads (plain SGD) and the matching fragment-image refresh, one launch (used
 // after the gradient all-reduce when world > 1).
-hipError_t cnn_sgd_fused(float* params, const float* grads, const float* hp, void* frag, hipStream_t s);
+hipError_t cnn_sgd_fused(float* params, const float* grads, const float* hp, void* frag, hipStream_t s,
+                         int* step = nullptr);  // step: the optimiser's device step counter (+1 per call)
 
 hipError_t embbag_bwd(const float* dy, const int64_t* idx, const int64_t* off, int B, long L, int D, float* dw,
                       hipStream_t s);

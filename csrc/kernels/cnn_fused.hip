@@ -671,7 +671,9 @@ __device__ __forceinline__ void write_frag(uint16_t* __restrict__ f, int p, floa
 // with the fragment image refreshed in the same pass, so the next step needs no k_cnn_prep.
 // hp: the fused optimiser's device hyper-parameters (HP_LR, HP_GRAD_SCALE).
 __global__ __launch_bounds__(256) void k_cnn_sgd(float* __restrict__ params, const float* __restrict__ grads,
-                                                 const float* __restrict__ hp, uint16_t* __restrict__ frag) {
+                                                 const float* __restrict__ hp, uint16_t* __restrict__ frag,
+                                                 int* __restrict__ step) {
+  if (step != nullptr && blockIdx.x == 0 && threadIdx.x == 0) step[0] += 1;  // the optimiser's device step
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= NPARAM) return;
   const float w = params[p] - hp[HP_LR] * (grads[p] * hp[HP_GRAD_SCALE]);
@@ -710,7 +712,7 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
                                                       int accumulate, const float* __restrict__ loss_part, int B,
                                                       float* __restrict__ loss, unsigned long long* __restrict__ rng,
                                                       float* __restrict__ params, const float* __restrict__ hp,
-                                                      uint16_t* __restrict__ frag) {
+                                                      uint16_t* __restrict__ frag, int* __restrict__ step) {
   __shared__ f32x4 part[RED_LANES][RED_COLS];  // slab: [lane][column]; fc1: [wave][lane] (same 8 KB)
   const float gs = gscale ? gscale[0] : 1.f;
   if (blockIdx.x < RED_SLAB_BLOCKS) {
@@ -806,6 +808,7 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
     if (lane == 0) {
       loss[0] = s / static_cast<float>(B);
       rng[0] += 1;  // advance the dropout stream for the next step
+      if (hp != nullptr && step != nullptr) step[0] += 1;  // the fused SGD's device step counter
     }
   }
 }
@@ -824,7 +827,7 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
                            unsigned long long* rng, float p_drop2, float p_drop1, int training, float* slabs,
                            float* loss_part, float* acts, int nwg, float* loss, float* grads, const float* gscale,
                            int accumulate, hipStream_t s, unsigned long long* stamps, int prep,
-                           const float* sgd_hp, int stop_after) {
+                           const float* sgd_hp, int stop_after, int* sgd_step) {
   if (reinterpret_cast<uintptr_t>(grads) & 15) return hipErrorInvalidValue;  // float4 gradient stores
   const size_t sm = sizeof(CnnSmem);
   static bool attr = false;
@@ -841,14 +844,14 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
                      static_cast<const u16x8*>(frag), rng, p_drop2, p_drop1, training, slabs, loss_part, acts, stamps,
                      stop_after);
   hipLaunchKernelGGL(k_cnn_reduce, dim3(RED_BLOCKS), dim3(RED_T), 0, s, slabs, nwg, acts, gscale, grads,
-                     accumulate, loss_part, B, loss, rng, params, sgd_hp, static_cast<uint16_t*>(frag));
+                     accumulate, loss_part, B, loss, rng, params, sgd_hp, static_cast<uint16_t*>(frag), sgd_step);
   return hipGetLastError();
 }
 
-hipError_t cnn_sgd_fused(float* params, const float* grads, const float* hp, void* frag, hipStream_t s) {
+hipError_t cnn_sgd_fused(float* params, const float* grads, const float* hp, void* frag, hipStream_t s, int* step) {
   if (reinterpret_cast<uintptr_t>(frag) & 15) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_cnn_sgd, dim3(ceil_div(NPARAM, 256)), dim3(256), 0, s, params, grads, hp,
-                     static_cast<uint16_t*>(frag));
+                     static_cast<uint16_t*>(frag), step);
   return hipGetLastError();
 }
 

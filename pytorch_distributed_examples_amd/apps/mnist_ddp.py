@@ -14,8 +14,10 @@ lines, and ``Execution time``.
 
 MI355X-first differences: RCCL (``nccl``) over xGMI on GPUs -- gloo on CPU -- with the xGMI bucket
 policy; bf16 MFMA kernels; HBM-resident synthetic MNIST; atomic snapshot by global rank 0 only;
-``--model cnn`` runs BASELINE config 1's CNN through the same plumbing; ``--rewire`` keeps the worker
-alive across membership changes (in-process RCCL communicator re-wire, :mod:`..elastic.rewire`).
+``--model cnn`` runs BASELINE config 1's CNN through the same plumbing (``--fused``: the whole-network
+training kernel of csrc/kernels/cnn_fused.hip, gradients straight into the DDP flat buffer, one all-reduce
+on the GPU data plane of :mod:`..parallel.comm`, one fused SGD launch); ``--rewire`` keeps the worker alive
+across membership changes (in-process RCCL communicator re-wire, :mod:`..elastic.rewire`).
 """
 from __future__ import annotations
 
@@ -55,7 +57,7 @@ def load_train_objs(model_name: str, device, train_size: int, test_size: int):
 
 class Trainer:
     def __init__(self, ctx, model, train_data, test_data, make_opt, criterion, save_every, snapshot_path,
-                 log, metrics=None, save_optimizer=True):
+                 log, metrics=None, save_optimizer=True, fused=False):
         self.ctx = ctx
         self.global_rank = int(os.environ.get("RANK", ctx.rank))
         self.local_rank = int(os.environ.get("LOCAL_RANK", ctx.local_rank))
@@ -73,7 +75,17 @@ class Trainer:
         if os.path.exists(snapshot_path):
             log.print("Loading snapshot")
             self._load_snapshot(snapshot_path)
-        self.ddp = DistributedDataParallel(self.model)
+        self.fused = None
+        if fused:
+            from ..models.cnn_fused import FusedCNN
+            from ..parallel.comm import data_plane
+
+            if ctx.device.type != "cuda":
+                raise SystemExit("--fused runs the gfx950 training kernel: it needs a GPU")
+            self.fused = FusedCNN(self.model)
+            self.ddp = DistributedDataParallel(self.model, overlap=False, param_order="forward", comm=data_plane(ctx))
+        else:
+            self.ddp = DistributedDataParallel(self.model)
 
     def _load_snapshot(self, path):
         snap = load_snapshot(path)
@@ -84,6 +96,16 @@ class Trainer:
         self.log.print(f"Resuming training from snapshot at Epoch {self.epochs_run}")
 
     def _run_batch(self, source, targets):
+        if self.fused is not None:
+            if self.ddp.world == 1:  # SGD + fragment refresh inside the slab reduction
+                loss = self.fused.forward_backward(source, targets, grad_out=self.ddp.flat_grad, sgd=self.optimizer)
+            else:
+                loss = self.fused.forward_backward(source, targets, grad_out=self.ddp.flat_grad)
+                self.ddp.sync_gradients()
+                self.fused.sgd_step(self.optimizer, self.ddp.flat_grad)
+            fault.maybe_fault(self.global_step, self.global_rank)
+            self.global_step += 1
+            return loss
         self.ddp.zero_grad()
         output = self.ddp(source)
         loss = self.criterion(output, targets)
@@ -152,6 +174,7 @@ def main(argv=None):
     parser.add_argument("save_every", type=int, help="How often to save a snapshot")
     parser.add_argument("--batch_size", default=128, type=int, help="Input batch size on each device (default: 128)")
     parser.add_argument("--model", default="mlp", choices=["mlp", "cnn"])
+    parser.add_argument("--fused", action="store_true", help="cnn: whole-network fused training kernel (GPU)")
     parser.add_argument("--device", default="auto", choices=["auto", "cpu", "gpu"])
     parser.add_argument("--snapshot_path", default="snapshot.pt")
     parser.add_argument("--train_size", type=int, default=60000)
@@ -177,7 +200,7 @@ def main(argv=None):
         train_data = ShardedLoader(train_set, args.batch_size, ctx.world_size, ctx.rank, shuffle=True)
         test_data = ShardedLoader(test_set, args.batch_size, ctx.world_size, ctx.rank, shuffle=False)
         trainer = Trainer(ctx, model, train_data, test_data, make_opt, criterion, args.save_every,
-                          args.snapshot_path, log, metrics)
+                          args.snapshot_path, log, metrics, fused=args.fused and args.model == "cnn")
         trainer.train(args.total_epochs)
         pdist.shutdown()
     end = time.time()

@@ -167,17 +167,12 @@ def build_data_parallel(args, ctx, batch) -> Workload:
     use_graph = not args.no_graph and on_gpu and (ctx.world_size == 1 or ctx.backend == "nccl")
     # GPU data plane for world > 1: our stream-ordered RCCL communicator (c10d's ProcessGroupNCCL aborts the
     # process when its work is captured into a hipGraph on ROCm -- parallel/rccl.py)
-    comm = None
-    if on_gpu and ctx.world_size > 1 and ctx.backend == "nccl":
-        from ..parallel.rccl import StreamComm
+    # GPU data plane (parallel/comm.py): RCCL + the one-shot xGMI all-reduce for latency-bound buckets (the
+    # CNN's single 87 KB bucket)
+    from ..parallel.comm import data_plane
 
-        comm = StreamComm(dev)
-    nranks = _data_plane_check(ctx, comm)
-    if comm is not None and os.environ.get("PDE_XGMI", "1") != "0":
-        # latency-bound buckets (the CNN's single 87 KB bucket) take the one-shot xGMI peer all-reduce
-        from ..parallel.xgmi_allreduce import RoutedComm, XgmiAllreduce
-
-        comm = RoutedComm(comm, XgmiAllreduce(dev))
+    comm = data_plane(ctx)
+    nranks = _data_plane_check(ctx, getattr(comm, "rccl", comm))
     fused = None
     if args.model == "cnn" and not args.generic and on_gpu:
         # whole-network fused kernel: gradients land in the DDP flat buffer (forward layout), then one
@@ -253,6 +248,45 @@ def build_pipeline(args, ctx, batch) -> Workload:
     return w
 
 
+def _secondary_pipeline(ctx, timeout_s: float = 420.0):
+    """BASELINE configs 3/4 measured alongside the headline: after the CNN measurement, every rank launches
+    one child process running ``bench.py --model resnet50_pp`` on the same GPU (a fresh process group on a new
+    port; world 2 = the 2-stage pipeline, world 8 = pp2 x dp4).  Children are separate processes so a failure
+    or hang there can never cost the headline line: each parent kills its child at ``timeout_s``."""
+    import subprocess
+
+    store = dist.distributed_c10d._get_default_store()
+    if ctx.rank == 0:
+        store.set("pde/bench/secondary_port", str(pdist.free_port()))
+    port = store.get("pde/bench/secondary_port").decode()
+    bench_py = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "bench.py")
+    # a plain env:// job: drop torchrun's agent-store variables (TORCHELASTIC_USE_AGENT_STORE would make the
+    # child's rank 0 connect to a store server that does not exist on the new port)
+    env = {k: v for k, v in os.environ.items() if not k.startswith(("TORCHELASTIC_", "GROUP_", "ROLE_"))}
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port, RANK=str(ctx.rank), WORLD_SIZE=str(ctx.world_size),
+               LOCAL_RANK=str(ctx.local_rank), PDE_BENCH_CHILD="1")
+    cmd = [sys.executable, bench_py, "--model", "resnet50_pp", "--gpus", str(ctx.world_size), "--steps", "20",
+           "--warmup", "5"] + os.environ.get("PDE_BENCH_SECONDARY_ARGS", "").split()
+    result = {"model": MODEL_NAMES["resnet50_pp"], "baseline_config": BASELINE_CONFIG["resnet50_pp"]}
+    try:
+        res = subprocess.run(cmd, env=env, timeout=timeout_s, capture_output=True, text=True)
+        line = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+        if res.returncode != 0:
+            result["error"] = f"rc={res.returncode}: " + res.stderr.strip().splitlines()[-1][:300] if res.stderr.strip() \
+                else f"rc={res.returncode}"
+        elif line:
+            rec = json.loads(line[-1])
+            result.update(value=rec["value"], unit=rec["unit"], ms_per_step=rec["ms_per_step"], steps=rec["steps"],
+                          warmup=rec["warmup"], vs_baseline=rec["vs_baseline"],
+                          parallelism=rec["config"]["parallelism"], hipgraph=rec["config"]["hipgraph"],
+                          global_batch=rec["config"]["global_batch"], final_loss=rec["config"]["final_loss"])
+    except subprocess.TimeoutExpired:
+        result["error"] = f"timeout after {timeout_s:.0f} s"
+    except Exception as exc:  # noqa: BLE001 - never let the secondary measurement cost the headline
+        result["error"] = repr(exc)[:300]
+    return result
+
+
 def run_steps(work: Workload, first: int, n: int):
     loss = None
     i = 0
@@ -302,6 +336,11 @@ def main(argv=None):
     dt = pdist.max_over_ranks(dt, ctx.device)
     final_loss = _report_loss(work, ctx, loss)
     value = work.images_per_step * args.steps / dt
+    secondary = None
+    mode = os.environ.get("PDE_BENCH_SECONDARY", "1")  # 0: off; force: also on CPU/gloo (plumbing tests)
+    if (args.model == "cnn" and ctx.world_size >= 2 and ctx.world_size % 2 == 0 and mode != "0" and
+            "PDE_BENCH_CHILD" not in os.environ and (mode == "force" or (on_gpu and ctx.backend == "nccl"))):
+        secondary = _secondary_pipeline(ctx)
     same_shape = args.image is None and batch == DEFAULT_BATCH[args.model]
     ref = REFERENCE_IMG_S.get((args.model, ctx.world_size)) if same_shape else None
     if ctx.rank == 0:
@@ -310,6 +349,8 @@ def main(argv=None):
                "image": "1x28x28" if args.model in ("cnn", "mlp") else f"3x{args.image or 128}x{args.image or 128}",
                "parallelism": work.parallelism, "final_loss": round(final_loss, 4)}
         cfg.update(work.info)
+        if secondary is not None:
+            cfg["secondary"] = secondary
         print(json.dumps({
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": ctx.world_size,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1000.0, 4),

@@ -74,19 +74,20 @@ class FusedCNN:
         group = opt.param_groups[0]
         assert group["momentum"] == 0.0 and group["weight_decay"] == 0.0, "fused update is plain SGD"
         params = [p for p in group["params"] if p.grad is not None]
-        return opt._group_dev(0, group, params)["hp"], params
+        st = opt._group_dev(0, group, params)
+        return (st["hp"], st["step"]), params
 
     def _after_update(self, opt, params):
-        for p in params:
-            opt.state[p]["step"] = opt.state[p].get("step", 0) + 1
+        # the step count lives in the optimizer's device counter (advanced by the fused kernels, so hipGraph
+        # replays count too); FusedSGD.state_dict() reads it back
         OF.bump_weight_generation()
         self._frag_gen = OF.weight_generation()
 
     @torch.no_grad()
     def sgd_step(self, opt, grads: torch.Tensor):
         """``opt.step()`` for the flat parameters (plain SGD) fused with the fragment-image refresh."""
-        hp, params = self._sgd_hp(opt)
-        _native.C().cnn_sgd(self.flat, grads, hp, self.frag)
+        (hp, step), params = self._sgd_hp(opt)
+        _native.C().cnn_sgd(self.flat, grads, hp, self.frag, step)
         self._after_update(opt, params)
 
     def _nwg(self, B: int) -> int:
@@ -119,9 +120,9 @@ class FusedCNN:
         y = y.long().contiguous()
         training = self.net.training
         prep = self._frag_gen is None or self._frag_gen != OF.weight_generation()
-        hp, params = self._sgd_hp(sgd) if sgd is not None else (None, None)
+        (hp, step), params = self._sgd_hp(sgd) if sgd is not None else ((None, None), None)
         loss = C.cnn_train(x, y, self.flat, OF._rng_counter(x.device), p_drop2, p_drop1, training, grad_out,
-                           accumulate, None, self.stamps, self.frag, prep, hp, self.stop_after)
+                           accumulate, None, self.stamps, self.frag, prep, hp, self.stop_after, step)
         if sgd is not None:
             self._after_update(sgd, params)
         else:

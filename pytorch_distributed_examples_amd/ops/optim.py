@@ -42,6 +42,9 @@ class _FusedBase(torch.optim.Optimizer):
                   "hp": torch.zeros(8, dtype=torch.float32, device=dev),
                   # {steps taken, arrival counter of the update kernel}
                   "step": torch.zeros(2, dtype=torch.int32, device=dev)}
+            # a new group state (new optimizer, or after load_state_dict): the host step is authoritative once
+            s0 = self.state[params[0]].get("step") if params else None
+            st["step"][0].fill_(int(s0) if s0 is not None else 0)
             self._dev[gi] = st
         need_avg = self.KIND in ("adam", "adamw") or group["momentum"] != 0.0
         for p in params:
@@ -62,9 +65,7 @@ class _FusedBase(torch.optim.Optimizer):
         sig = tuple((p.data_ptr(), g.data_ptr(), g.is_contiguous()) for p, g in zip(params, grads)) + \
             tuple(t.data_ptr() for t in m) + tuple(t.data_ptr() for t in v)
         if st["sig"] != sig:
-            # (re)build: also re-sync the device step with the host state (new optimizer, load_state_dict)
-            s0 = self.state[params[0]].get("step") if params else None
-            st["step"][0].fill_(int(s0) if s0 is not None else 0)
+            # (re)build the tables; the device step counter carries on
             grads_c = [g if g.is_contiguous() else g.contiguous() for g in grads]
             copies = [OF.maintain_compute_copies(p) or {} for p in params]
             none = torch.empty(0, device=params[0].device)
@@ -106,8 +107,7 @@ class _FusedBase(torch.optim.Optimizer):
                 C.optim_step(st["table"], st["chunks"], st["nchunks"], _MODES[self.KIND], st["hp"], st["step"])
                 if st["nconv"]:
                     C.conv_layouts_step(st["conv_table"], st["nconv"], st["conv_blocks"])
-                for p in params:
-                    self.state[p]["step"] = self.state[p].get("step", 0) + 1
+                # host ``step`` is synchronised from the device counter by state_dict() (graph replays)
             else:
                 self._cpu_step(group, params)
         OF.bump_weight_generation()
@@ -149,6 +149,23 @@ class _FusedBase(torch.optim.Optimizer):
             bc2 = 1 - b2 ** t
             denom = (v.sqrt() / (bc2 ** 0.5)).add_(eps)
             p.addcdiv_(m, denom, value=-lr / bc1)
+
+    def sync_step_from_device(self):
+        """Copy each GPU group's device step counter into the per-parameter host ``step``.  The device counter
+        is authoritative: hipGraph replays of a captured training step (and the fused CNN update kernels)
+        advance it without running this Python code."""
+        for gi, group in enumerate(self.param_groups):
+            st = self._dev.get(gi)
+            if st is None:
+                continue
+            steps = int(st["step"][0].item())
+            for p in group["params"]:
+                if p in self.state:
+                    self.state[p]["step"] = steps
+
+    def state_dict(self):
+        self.sync_step_from_device()
+        return super().state_dict()
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)

@@ -63,3 +63,17 @@ def test_bench_resnet_pipeline_world2():
     rec = _parse(out)
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "pp2xdp1" and rec["config"]["microbatches"] == 2
     assert rec["config"]["global_batch"] == 4 and rec["value"] > 0
+
+
+def test_bench_secondary_pipeline_measurement():
+    """At N >= 2 the headline run also measures BASELINE config 3/4 (resnet50_pp) in child processes and
+    reports it under config.secondary (forced on CPU here, tiny images)."""
+    env = {"PDE_BENCH_SECONDARY": "force",
+           "PDE_BENCH_SECONDARY_ARGS": "--device cpu --batch 4 --split-size 2 --image 32 --steps 1 --warmup 1"}
+    rc, out = run_cmd(["python", os.path.join(REPO, "bench.py"), "--gpus", "2", "--device", "cpu", "--steps", "2",
+                       "--warmup", "1", "--batch", "16"], timeout=300, env=env)
+    assert rc == 0, out
+    rec = _parse(out)
+    sec = rec["config"]["secondary"]
+    assert "error" not in sec, sec
+    assert sec["parallelism"] == "pp2xdp1" and sec["value"] > 0 and sec["global_batch"] == 4

@@ -52,17 +52,24 @@ def test_linear_identity_asymmetric(gpu):
     assert torch.equal(y, B.float().t())
 
 
-CONV_CFGS = [
+# Every unique conv of the ResNet-50 shards at 128x128 (model_parallel_ResNet50.py:94-130):
+# (Cin, Cout, k, stride, pad, H_in), micro-batch 4; plus the two MNIST convs (mnist_horovod.py:9-25).
+RESNET_CONVS = [
+    # shard 1: stem + layer1 + layer2
+    (3, 64, 7, 2, 3, 128), (64, 64, 1, 1, 0, 32), (64, 64, 3, 1, 1, 32), (64, 256, 1, 1, 0, 32),
+    (256, 64, 1, 1, 0, 32), (256, 128, 1, 1, 0, 32), (128, 128, 3, 2, 1, 32), (256, 512, 1, 2, 0, 32),
+    (128, 512, 1, 1, 0, 16), (128, 128, 3, 1, 1, 16), (512, 128, 1, 1, 0, 16),
+    # shard 2: layer3 + layer4
+    (512, 256, 1, 1, 0, 16), (256, 256, 3, 2, 1, 16), (512, 1024, 1, 2, 0, 16), (256, 1024, 1, 1, 0, 8),
+    (256, 256, 3, 1, 1, 8), (1024, 256, 1, 1, 0, 8), (1024, 512, 1, 1, 0, 8), (512, 512, 3, 2, 1, 8),
+    (1024, 2048, 1, 2, 0, 8), (512, 2048, 1, 1, 0, 4), (512, 512, 3, 1, 1, 4), (2048, 512, 1, 1, 0, 4),
+]
+CONV_CFGS = [(4, ci, h, co, k, s, p) for ci, co, k, s, p, h in RESNET_CONVS] + [
     # N, Cin, H, Cout, k, stride, pad
-    (4, 3, 128, 64, 7, 2, 3),     # ResNet stem
-    (4, 64, 32, 64, 3, 1, 1),
-    (4, 64, 32, 256, 1, 1, 0),
-    (4, 128, 32, 128, 3, 2, 1),
-    (4, 256, 32, 512, 1, 2, 0),
-    (4, 512, 4, 2048, 1, 1, 0),
     (8, 1, 28, 10, 5, 1, 0),      # MNIST conv1
     (8, 10, 12, 20, 5, 1, 0),     # MNIST conv2
 ]
+assert len(CONV_CFGS) == 25
 
 
 @pytest.mark.parametrize("cfg", CONV_CFGS)

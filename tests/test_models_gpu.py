@@ -234,3 +234,50 @@ def test_fused_cnn_trains_with_dropout(gpu):
         losses.append(fused.forward_backward(x, y).item())
         opt.step()
     assert sum(losses[-5:]) / 5 < losses[0] * 0.7, losses
+
+
+def test_optimizer_step_survives_graph_replays(gpu, tmp_path):
+    """The optimizer's device step counter advances on every hipGraph replay (and in the fused CNN update);
+    state_dict() -- hence a snapshot's OPTIMIZER_STATE -- reports it, and a reload resumes from it."""
+    from pytorch_distributed_examples_amd.elastic.snapshot import load_snapshot, save_snapshot
+    from pytorch_distributed_examples_amd.models.cnn import Net
+    from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
+    from pytorch_distributed_examples_amd.ops.optim import FusedAdam, FusedSGD
+
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(16, 4).to(gpu)
+    opt = FusedAdam(lin.parameters(), lr=1e-3)
+    for p in lin.parameters():
+        p.grad = torch.ones_like(p)
+    opt.step()                                   # eager: step 1
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        opt.step()                               # warm-up on the side stream: step 2
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g):
+        opt.step()                               # captured (not executed)
+    for _ in range(5):
+        g.replay()                               # steps 3..7
+    torch.cuda.synchronize()
+    sd = opt.state_dict()
+    assert all(st["step"] == 7 for st in sd["state"].values()), sd["state"]
+    path = str(tmp_path / "snap.pt")
+    save_snapshot(path, lin.state_dict(), 3, sd)
+    opt2 = FusedAdam(lin.parameters(), lr=1e-3)
+    opt2.load_state_dict(load_snapshot(path)["OPTIMIZER_STATE"])
+    opt2.step()
+    assert all(st["step"] == 8 for st in opt2.state_dict()["state"].values())
+    # fused CNN update paths advance the same counter
+    net = Net().to(gpu).train()
+    sgd = FusedSGD(net.parameters(), lr=0.01)
+    f = FusedCNN(net)
+    x = torch.randn(64, 1, 28, 28, device=gpu)
+    y = torch.randint(0, 10, (64,), device=gpu)
+    buf = f.grad_buffer()
+    f.forward_backward(x, y, grad_out=buf, sgd=sgd)   # update inside the reduction
+    f.forward_backward(x, y, grad_out=buf)
+    f.sgd_step(sgd, buf)                               # separate update launch
+    torch.cuda.synchronize()
+    assert all(st["step"] == 2 for st in sgd.state_dict()["state"].values())
