@@ -75,6 +75,8 @@ class FusedCNN:
         assert group["momentum"] == 0.0 and group["weight_decay"] == 0.0, "fused update is plain SGD"
         params = [p for p in group["params"] if p.grad is not None]
         st = opt._group_dev(0, group, params)
+        for p in params:  # the fused update writes the fp32 weights only (plus its own fragment image)
+            OF.release_compute_copies(p)
         return (st["hp"], st["step"]), params
 
     def _after_update(self, opt, params):

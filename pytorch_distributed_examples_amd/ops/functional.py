@@ -178,6 +178,13 @@ def _derive_copies(p: torch.Tensor, d: dict):
         _C().cast_bf16_into(w, d["bf16"])
 
 
+def release_compute_copies(p: torch.Tensor) -> None:
+    """Stop treating ``p``'s bf16 compute copies as optimizer-maintained: an update path that writes the
+    fp32 weights without refreshing them (the fused CNN step keeps its own fragment image) must not leave
+    the layers reading stale copies; the layers fall back to generation-keyed cached copies."""
+    p.__dict__.pop("_pde_maint", None)
+
+
 def _maintained(p: torch.Tensor, kind: str):
     """The optimizer-maintained copy ``kind`` of ``p`` (None if the optimizer does not maintain one)."""
     d = p.__dict__.get("_pde_maint")

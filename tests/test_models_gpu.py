@@ -281,3 +281,31 @@ def test_optimizer_step_survives_graph_replays(gpu, tmp_path):
     f.sgd_step(sgd, buf)                               # separate update launch
     torch.cuda.synchronize()
     assert all(st["step"] == 2 for st in sgd.state_dict()["state"].values())
+
+
+def test_fused_cnn_training_is_visible_to_eval(gpu):
+    """After fused training steps (update inside the slab reduction), the layer-by-layer eval forward sees
+    the updated weights: it matches a forward through a fresh copy of the same state_dict."""
+    from pytorch_distributed_examples_amd.models.cnn import Net
+    from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
+    from pytorch_distributed_examples_amd.ops.optim import FusedSGD
+
+    torch.manual_seed(0)
+    net = Net().to(gpu).train()
+    sgd = FusedSGD(net.parameters(), lr=0.5)
+    f = FusedCNN(net)
+    x = torch.randn(256, 1, 28, 28, device=gpu)
+    y = torch.randint(0, 10, (256,), device=gpu)
+    net.eval()
+    before = net(x).float()
+    net.train()
+    buf = f.grad_buffer()
+    for _ in range(3):
+        f.forward_backward(x, y, grad_out=buf, sgd=sgd)
+    net.eval()
+    after = net(x).float()
+    fresh = Net().to(gpu).eval()
+    fresh.load_state_dict(net.state_dict())
+    ref = fresh(x).float()
+    assert (after - before).abs().max().item() > 1e-3  # the weights moved
+    assert torch.allclose(after, ref, atol=2e-2, rtol=2e-2)
