@@ -59,6 +59,7 @@ struct GemmArgs {
   int splitk;                      // >1: fp32 partial slabs in workspace, then reduce + epilogue
   float* workspace;                // splitk * M * N fp32
   int oihw_ci, oihw_rs, oihw_cp;   // EPI_OIHW: real Cin, R*S, padded Cin of the gathered activation
+  int* tickets;                    // set by gemm_bf16: per-tile arrival counters of the in-kernel split-K reduce
 };
 
 hipError_t gemm_bf16(const GemmArgs& args, hipStream_t stream);

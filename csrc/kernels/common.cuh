@@ -11,6 +11,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float bf2f(uint16_t b) {
   return __uint_as_float(static_cast<uint32_t>(b) << 16);

@@ -21,9 +21,11 @@
 //     pixel -- is advanced incrementally by BK per K-tile, so the K loop has no integer division.
 //   * Tiles are mapped XCD-aware (T1): consecutive tile ids go to the same XCD group so tiles
 //     sharing A rows / B columns hit the same L2.
-//   * Split-K writes fp32 partial slabs, reduced by a vectorised slab reduction (several slab lanes per
-//     float4 column, fixed order: deterministic) that applies the fused epilogue, so wgrad GEMMs with a
-//     huge reduction (N*H*W) still fill 256 CUs.
+//   * Split-K writes fp32 partial slabs; the LAST K-slice block of a tile to arrive (agent-scope release ->
+//     per-tile ticket -> acquire, cdna_hip_programming.md §5 "in-launch split-K reduction") sums the slabs in
+//     fixed z order (deterministic) and applies the fused epilogue: no separate reduce launch (the
+//     launch-boundary cost per split GEMM was ~5 us in a hipGraph).  A vectorised slab-reduction kernel
+//     remains as the fallback (first call inside a graph capture, before the ticket array exists).
 //   * Epilogue options: bias, ReLU, ReLU-mask (backward), fp32 / bf16 output, accumulate, and an OIHW
 //     remap that writes a conv weight gradient straight into the parameter's [Co][Ci][R][S] fp32 grad.
 #include <cstdlib>
@@ -316,6 +318,126 @@ __device__ __forceinline__ void store_out(float v, int epi, int m, int n, const 
   }
 }
 
+// Split-K with the reduction inside the launch: every K-slice block stores its fp32 partial tile to the
+// slab workspace, then the tile's LAST arriving block (per-tile ticket) reduces all slabs in z order and
+// runs the epilogue.  Publish / consume is the write-through form of cdna_hip_programming.md §6
+// Guideline 16 (counter row of MI355X_MICROARCH.md § visibility): slab bytes are stored sc1 (through to
+// memory, so no L2 write-back fence -- an agent-scope release here costs every K-slice block a write-back
+// of its XCD's dirty L2 and measured 2x slower end to end), every storing wave drains, the block meets,
+// one lane takes a relaxed agent-scope ticket; the reducer reads every slab with sc1 loads (L1 bypassed,
+// so no acquire).  The reducer resets the ticket (the array starts zeroed, so every launch finds 0).
+constexpr int kMaxInKernelSplits = 8;  // more slabs per tile: the serial combine loses to a reduce launch
+template <int BM, int BN>
+constexpr int SMEM_BYTES_OF() { return 2 * (BM + BN) * 32 * 2; }  // gemm_kernel's LDS (BK = 32, bf16)
+
+template <int BM, int BN, int FM, int FN, int WTM, int WTN>
+__device__ __forceinline__ void write_slab_and_reduce(const GemmArgs& args, const f32x4 (&acc)[FM][FN],
+                                                      uint16_t* smem, int m0, int n0, int kz, int wm, int wn,
+                                                      int lane) {
+  float* ws = args.workspace;
+  const long MN = static_cast<long>(args.M) * args.N;
+  const int splits = gridDim.z;
+  // one buffer descriptor over all slabs (host checks splits*M*N*4 < 2^31)
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(ws, 0, static_cast<int>(splits * MN * 4), 0x00020000);
+  constexpr int SC1 = 16;  // aux bit: write-through store / L1-bypassing load
+  const bool vec = args.N % 4 == 0 && (reinterpret_cast<uintptr_t>(ws) & 15) == 0;
+  if (vec && BM * BN * 4 <= SMEM_BYTES_OF<BM, BN>()) {
+    // stage the partial tile in the idle LDS, then 16-byte row stores
+    float* st = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int nl = wn * WTN + j * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * BN + nl] = acc[i][j][r];
+      }
+    __syncthreads();
+    for (int q = threadIdx.x; q < BM * BN / 4; q += kThreads) {
+      const int ml = q / (BN / 4), nl = (q % (BN / 4)) * 4;
+      const int m = m0 + ml, n = n0 + nl;
+      if (m < args.M && n < args.N) {
+        const int off = static_cast<int>((kz * MN + static_cast<long>(m) * args.N + n) * 4);
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(st + ml * BN + nl), rsrc, off, 0, SC1);
+      }
+    }
+  } else {
+    float* slab = ws + kz * MN;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * WTN + j * 16 + (lane & 15);
+        if (n >= args.N) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+          if (m < args.M)
+            __hip_atomic_store(slab + static_cast<long>(m) * args.N + n, acc[i][j][r], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slab stores
+  __syncthreads();
+  int* last = reinterpret_cast<int*>(smem);  // staging reads are behind the barrier: LDS is free
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(args.tickets + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last[0] = t == splits - 1;
+  }
+  __syncthreads();
+  if (!last[0]) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+  const bool out_vec = vec && !(args.epi & (EPI_OIHW | EPI_OUT_F32)) && args.ldo % 4 == 0 &&
+                       (reinterpret_cast<uintptr_t>(args.out) & 7) == 0;
+  if (vec) {
+    // all of a thread's slab loads in flight at once (splits <= kMaxInKernelSplits, host-checked)
+    constexpr int QI = BM * BN / 4 / kThreads;
+    f32x4 v[QI];
+#pragma unroll
+    for (int i = 0; i < QI; ++i) {
+      const int q = threadIdx.x + i * kThreads;
+      const int m = m0 + q / (BN / 4), n = n0 + (q % (BN / 4)) * 4;
+      const bool ok = m < args.M && n < args.N;
+      const int off = ok ? static_cast<int>((static_cast<long>(m) * args.N + n) * 4) : 0;
+      u32x4 u[kMaxInKernelSplits];
+#pragma unroll
+      for (int z = 0; z < kMaxInKernelSplits; ++z)
+        if (z < splits) u[z] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + static_cast<int>(z * MN * 4), 0, SC1);
+      v[i] = *reinterpret_cast<const f32x4*>(&u[0]);
+#pragma unroll
+      for (int z = 1; z < kMaxInKernelSplits; ++z)
+        if (z < splits) v[i] += *reinterpret_cast<const f32x4*>(&u[z]);
+    }
+#pragma unroll
+    for (int i = 0; i < QI; ++i) {
+      const int q = threadIdx.x + i * kThreads;
+      const int m = m0 + q / (BN / 4), n = n0 + (q % (BN / 4)) * 4;
+      if (m >= args.M || n >= args.N) continue;
+      if (out_vec) {
+        u16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = f2bf(apply_epi(v[i][j], args.epi, m, n + j, args));
+        *reinterpret_cast<u16x4*>(static_cast<uint16_t*>(args.out) + static_cast<long>(m) * args.ldo + n) = o;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) store_out(apply_epi(v[i][j], args.epi, m, n + j, args), args.epi, m, n + j, args);
+      }
+    }
+  } else {
+    for (int q = threadIdx.x; q < BM * BN; q += kThreads) {
+      const int ml = q / BN, nl = q % BN;
+      const int m = m0 + ml, n = n0 + nl;
+      if (m >= args.M || n >= args.N) continue;
+      const long off = static_cast<long>(m) * args.N + n;
+      float v = 0.f;
+      for (int z = 0; z < splits; ++z) v += __hip_atomic_load(ws + z * MN + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      store_out(apply_epi(v, args.epi, m, n, args), args.epi, m, n, args);
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(args.tickets + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles_m, int tiles_n,
                                                         int k_per_split, int a_vec, int b_vec) {
@@ -325,6 +447,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int LDS_A = BM * BK, LDS_B = BN * BK;
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (LDS_A + LDS_B)];
+  static_assert(sizeof(smem) == SMEM_BYTES_OF<BM, BN>(), "split-K staging size");
 
   // XCD-aware tile id remap (bijective; see cdna_hip_programming.md §5 "XCD swizzle").
   const int ntiles = tiles_m * tiles_n;
@@ -416,6 +539,10 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles
   // the (now idle) LDS, it is staged there and written back as 16-byte row vectors instead.
   const bool split = gridDim.z > 1;
   float* ws = args.workspace;
+  if (split && args.tickets != nullptr) {
+    write_slab_and_reduce<BM, BN, FM, FN, WTM, WTN>(args, acc, smem, m0, n0, kz, wm, wn, lane);
+    return;
+  }
   constexpr int SMEM_BYTES = static_cast<int>(sizeof(smem));
   const bool vec_bf16 = !split && !(args.epi & (EPI_OIHW | EPI_OUT_F32)) && args.N % 8 == 0 && args.ldo % 8 == 0 &&
                         (reinterpret_cast<uintptr_t>(args.out) & 15) == 0;
@@ -544,6 +671,40 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce4(GemmArgs args, int sp
   }
 }
 
+// Per-tile arrival counters for the in-kernel split-K reduction: one zeroed device array per GPU, handed
+// out in rolling windows (consecutive launches on one stream may share slots -- each launch leaves its
+// tickets at 0 -- and the window keeps launches on different streams apart).  Allocated on first use
+// outside a graph capture; until then (or if allocation fails) split GEMMs use the reduce kernel.
+// OPT-IN (PDE_GEMM_INKERNEL_SPLITK=1): measured on MI355X (scripts/gpu_gemm_ab.sh, profiles/README.md r2c)
+// the last-arriver combine is slower than the separate, chip-wide reduce launch on both the MLP
+// (0.39 vs 0.33 ms/step) and ResNet-50 (5.89 vs 5.80 ms/step): the tile's reducer is one workgroup reading
+// up to 8 slabs after the whole K range finished, a serial tail the 1.5-2 us launch boundary does not cost.
+constexpr int kTicketSlots = 1 << 22;
+int* split_tickets(int tiles, hipStream_t s) {
+  static int* base[64] = {};
+  static int next[64] = {};
+  static bool enabled = std::getenv("PDE_GEMM_INKERNEL_SPLITK") != nullptr &&
+                        std::getenv("PDE_GEMM_INKERNEL_SPLITK")[0] == '1';
+  if (!enabled || tiles > kTicketSlots) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (base[dev] == nullptr) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+    void* p = nullptr;
+    if (hipMalloc(&p, sizeof(int) * kTicketSlots) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, sizeof(int) * kTicketSlots) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(p);
+      return nullptr;
+    }
+    base[dev] = static_cast<int*>(p);
+  }
+  if (next[dev] + tiles > kTicketSlots) next[dev] = 0;
+  int* t = base[dev] + next[dev];
+  next[dev] += tiles;
+  return t;
+}
+
 template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC>
 hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
   const int tm = ceil_div(a.M, BM), tn = ceil_div(a.N, BN);
@@ -559,9 +720,13 @@ hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
   };
   const int av = vec_ok(a.a, AKC), bv = vec_ok(a.b, BKC);
   dim3 grid(tm * tn, 1, splitk);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AKC, BKC>), grid, dim3(kThreads), 0, s, a, tm, tn,
+  GemmArgs ka = a;
+  const bool in_kernel = splitk > 1 && splitk <= kMaxInKernelSplits &&
+                         static_cast<long>(splitk) * a.M * a.N * 4 < (1L << 31);  // buffer offsets
+  ka.tickets = in_kernel ? split_tickets(tm * tn, s) : nullptr;
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AKC, BKC>), grid, dim3(kThreads), 0, s, ka, tm, tn,
                      kps, av, bv);
-  if (splitk > 1) {
+  if (splitk > 1 && ka.tickets == nullptr) {
     const long total = static_cast<long>(a.M) * a.N;
     if (a.N % 4 == 0 && total / 4 < (1L << 30) && (reinterpret_cast<uintptr_t>(a.workspace) & 15) == 0) {
       const long t4 = total / 4;

@@ -385,3 +385,18 @@ def test_optimizer_maintained_compute_copies(gpu, kind):
     a2 = C.conv_dgrad(dy, wf, 10, 10, 1, 1, 2, 0, None, True)
     b2 = C.conv_dgrad(dy, C.conv_w_dgrad(conv.weight.detach(), 32, 48), 10, 10, 1, 1, 2, 0)
     assert rel_err(a2, b2) < 1e-3
+
+
+def test_inkernel_splitk_path(gpu):
+    """The opt-in in-launch split-K combine (gemm.hip write_slab_and_reduce, PDE_GEMM_INKERNEL_SPLITK=1)
+    is read once per process, so the linear and conv shape tests rerun in a child with it on."""
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.abspath(__file__)
+    env = dict(os.environ, PDE_GEMM_INKERNEL_SPLITK="1")
+    res = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "--timeout", "120",
+                          f"{here}::test_linear_fwd_bwd", f"{here}::test_conv_fwd_bwd"],
+                         env=env, capture_output=True, text=True, timeout=300, cwd=os.path.dirname(os.path.dirname(here)))
+    assert res.returncode == 0, res.stdout[-3000:] + res.stderr[-3000:]
