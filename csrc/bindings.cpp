@@ -646,8 +646,24 @@ Tensor embbag_bwd(const Tensor& dy, const Tensor& idx, const Tensor& off, int64_
 Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, Tensor& rng, double p_drop2,
                  double p_drop1, bool training, Tensor& grads, bool accumulate, const optional<Tensor>& gscale,
                  const optional<Tensor>& stamps, const optional<Tensor>& frag_buf, bool prep,
-                 const optional<Tensor>& sgd_hp, int64_t stop_after, const optional<Tensor>& sgd_step) {
+                 const optional<Tensor>& sgd_hp, int64_t stop_after, const optional<Tensor>& sgd_step,
+                 const optional<std::vector<int64_t>>& xgmi_view, double xscale) {
   CHECK_IN(images); CHECK_IN(tgt); CHECK_IN(params); CHECK_IN(rng); CHECK_IN(grads);
+  pde::XgmiView xv{};
+  const bool have_xv = xgmi_view.has_value();
+  if (have_xv) {  // XgmiAllreduce.view(): base[8], state, timeout_ticks, flag_bytes, slot_bytes, rank, size, blocks
+    const auto& w = *xgmi_view;
+    TORCH_CHECK(w.size() == pde::kXgmiMaxRanks + 7, "cnn_train: malformed xgmi view");
+    for (int r = 0; r < pde::kXgmiMaxRanks; ++r) xv.base[r] = reinterpret_cast<char*>(w[r]);
+    xv.state = reinterpret_cast<uint32_t*>(w[8]);
+    xv.timeout_ticks = static_cast<uint64_t>(w[9]);
+    xv.flag_bytes = w[10];
+    xv.slot_bytes = w[11];
+    xv.rank = static_cast<int>(w[12]);
+    xv.size = static_cast<int>(w[13]);
+    xv.blocks = static_cast<int>(w[14]);
+    TORCH_CHECK(!accumulate, "cnn_train: the xGMI gradient exchange replaces accumulation");
+  }
   CHECK_F32(images); CHECK_F32(params); CHECK_F32(grads);
   TORCH_CHECK(params.numel() == pde::cnn_num_params(), "cnn_train: params must be the flat Net parameters");
   TORCH_CHECK(grads.numel() == pde::cnn_num_params(), "cnn_train: grads size");
@@ -690,7 +706,8 @@ Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, 
                                  : nullptr,
                              prep ? 1 : 0, sgd_hp.has_value() && sgd_hp->defined() ? sgd_hp->data_ptr<float>() : nullptr,
                              static_cast<int>(stop_after),
-                             sgd_step.has_value() && sgd_step->defined() ? sgd_step->data_ptr<int>() : nullptr),
+                             sgd_step.has_value() && sgd_step->defined() ? sgd_step->data_ptr<int>() : nullptr,
+                             have_xv ? &xv : nullptr, static_cast<float>(xscale)),
         "cnn_train");
   return loss;
 }
@@ -716,7 +733,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("p_drop2"), py::arg("p_drop1"), py::arg("training"), py::arg("grads"), py::arg("accumulate"),
         py::arg("gscale") = py::none(), py::arg("stamps") = py::none(), py::arg("frag") = py::none(),
         py::arg("prep") = true, py::arg("sgd_hp") = py::none(), py::arg("stop_after") = -1,
-        py::arg("sgd_step") = py::none());
+        py::arg("sgd_step") = py::none(), py::arg("xgmi_view") = py::none(), py::arg("xscale") = 1.0);
   m.def("cnn_sgd", &cnn_sgd, py::arg("params"), py::arg("grads"), py::arg("hp"), py::arg("frag"),
         py::arg("step") = py::none());
   m.def("clear_last_error", []() { return static_cast<int>(hipGetLastError()); },

@@ -131,6 +131,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              return t;
            },
            py::arg("tensor"), py::arg("scale") = 1.0)
+      .def("view",
+           [](const XgmiAllreduce& x) {  // flat device view for kernels that fold the exchange in (xgmi_view.h)
+             const pde::XgmiView v = x.view();
+             std::vector<int64_t> w;
+             for (int r = 0; r < pde::kXgmiMaxRanks; ++r) w.push_back(reinterpret_cast<int64_t>(v.base[r]));
+             w.push_back(reinterpret_cast<int64_t>(v.state));
+             w.push_back(static_cast<int64_t>(v.timeout_ticks));
+             w.push_back(v.flag_bytes);
+             w.push_back(v.slot_bytes);
+             w.push_back(v.rank);
+             w.push_back(v.size);
+             w.push_back(v.blocks);
+             return w;
+           })
       .def("error", [](XgmiAllreduce& x) { py::gil_scoped_release nogil; return x.error(); })
       .def("close", [](XgmiAllreduce& x) { py::gil_scoped_release nogil; x.close(); })
       .def_property_readonly("rank", &XgmiAllreduce::rank)

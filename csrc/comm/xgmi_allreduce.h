@@ -26,9 +26,9 @@
 #include <string>
 #include <vector>
 
-namespace pde {
+#include "xgmi_view.h"
 
-constexpr int kXgmiMaxRanks = 8;
+namespace pde {
 
 class XgmiAllreduce {
  public:
@@ -41,6 +41,7 @@ class XgmiAllreduce {
   void open(const std::vector<std::string>& handles);  // all ranks' handles, in rank order
   // dst[i] = scale * sum_r src_r[i]; fp32; src may alias dst; n * 4 <= max_bytes; stream-ordered
   void allreduce(const float* src, float* dst, int64_t n, float scale, hipStream_t s);
+  XgmiView view() const;  // device view for kernels that fold the exchange in (xgmi_device.h)
   int error();   // 0, or 1 when some workgroup timed out waiting for a peer (synchronises the device)
   void close();
   int rank() const { return rank_; }

@@ -7,6 +7,7 @@
 #include <string>
 
 #include "xgmi_allreduce.h"
+#include "xgmi_device.h"
 
 namespace pde {
 
@@ -14,43 +15,23 @@ namespace {
 
 constexpr int kThreads = 256;
 
-struct Peers {
-  char* base[kXgmiMaxRanks];
-};
-
 void hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("xgmi allreduce: ") + what + ": " + hipGetErrorString(e));
 }
 
-__device__ __forceinline__ uint32_t load_flag(uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__device__ __forceinline__ void store_flag(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// grid = one workgroup per chunk of `chunk` elements (the same grid on every rank and every call: the
+// grid = one workgroup per chunk of `chunk` elements (the same grid on every rank for the same n: the
 // per-workgroup epochs must advance in step across ranks).
 template <int NR, bool VEC>
 __global__ __launch_bounds__(kThreads) void k_xgmi_oneshot(const float* src, float* dst, int64_t n, float scale,
-                                                            Peers peers, int rank, int64_t chunk,
-                                                            int64_t flag_bytes, int64_t slot_bytes,
-                                                            uint32_t* state, uint64_t timeout_ticks) {
+                                                            XgmiView xv, int64_t chunk) {
   __shared__ uint32_t s_epoch;
   __shared__ int s_fail;
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
-  if (tid == 0) {
-    s_epoch = state[b] + 1u;
-    s_fail = 0;
-  }
-  __syncthreads();
-  const uint32_t epoch = s_epoch;
-  const int64_t slot_off = flag_bytes + static_cast<int64_t>(epoch & 1u) * slot_bytes;
+  const uint32_t epoch = xgmi_epoch(xv, b, &s_epoch);
   const int64_t lo = static_cast<int64_t>(b) * chunk;
   const int64_t hi = lo + chunk < n ? lo + chunk : n;
-  float* mine = reinterpret_cast<float*>(peers.base[rank] + slot_off);
+  float* mine = xgmi_slot(xv, xv.rank, epoch);
 
   // 1. stage this workgroup's chunk into my exported slot
   if (VEC) {
@@ -59,43 +40,12 @@ __global__ __launch_bounds__(kThreads) void k_xgmi_oneshot(const float* src, flo
   } else {
     for (int64_t i = lo + tid; i < hi; i += kThreads) mine[i] = src[i];
   }
-  // 2. publish: every storing wave drains its stores, the workgroup meets, one lane releases at system
-  //    scope, then one lane per peer raises this workgroup's flag in that peer's flag array
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  if (tid < NR) {
-    uint32_t* f = reinterpret_cast<uint32_t*>(peers.base[tid]) + b * kXgmiMaxRanks + rank;
-    store_flag(f, epoch);
-  }
-  // 3. wait for every rank's flag of this workgroup: one polling lane per peer, bounded by wall clock
-  if (tid < NR) {
-    uint32_t* f = reinterpret_cast<uint32_t*>(peers.base[rank]) + b * kXgmiMaxRanks + tid;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (static_cast<int32_t>(load_flag(f) - epoch) < 0) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
-        s_fail = 1;
-        __hip_atomic_store(state + gridDim.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  // 4. sum the chunk over all ranks' slots in rank order (bit-identical on every rank)
-  if (!s_fail) {
+  // 2.-3. publish my chunk to every peer and wait for theirs
+  if (xgmi_publish_and_wait(xv, b, epoch, &s_fail)) {
+    // 4. sum the chunk over all ranks' slots in rank order (bit-identical on every rank)
     const float* slots[NR];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) slots[r] = reinterpret_cast<const float*>(peers.base[r] + slot_off);
+    for (int r = 0; r < NR; ++r) slots[r] = xgmi_slot(xv, r, epoch);
     if (VEC) {
       for (int64_t i = lo + 4 * tid; i < hi; i += 4 * kThreads) {
         float4 v[NR];
@@ -127,8 +77,8 @@ __global__ __launch_bounds__(kThreads) void k_xgmi_oneshot(const float* src, flo
       }
     }
   }
-  // 5. this workgroup's epoch advances (read again by the same workgroup index next call)
-  if (tid == 0) state[b] = epoch;
+  // 5. this workgroup's epoch advances
+  xgmi_finish(xv, b, epoch);
 }
 
 __global__ void k_scale(const float* src, float* dst, int64_t n, float scale) {
@@ -139,14 +89,11 @@ __global__ void k_scale(const float* src, float* dst, int64_t n, float scale) {
 
 template <int NR>
 void launch(bool vec, dim3 grid, hipStream_t s, const float* src, float* dst, int64_t n, float scale,
-            const Peers& p, int rank, int64_t chunk, int64_t flag_bytes, int64_t slot_bytes, uint32_t* state,
-            uint64_t ticks) {
+            const XgmiView& v, int64_t chunk) {
   if (vec)
-    hipLaunchKernelGGL((k_xgmi_oneshot<NR, true>), grid, dim3(kThreads), 0, s, src, dst, n, scale, p, rank, chunk,
-                       flag_bytes, slot_bytes, state, ticks);
+    hipLaunchKernelGGL((k_xgmi_oneshot<NR, true>), grid, dim3(kThreads), 0, s, src, dst, n, scale, v, chunk);
   else
-    hipLaunchKernelGGL((k_xgmi_oneshot<NR, false>), grid, dim3(kThreads), 0, s, src, dst, n, scale, p, rank, chunk,
-                       flag_bytes, slot_bytes, state, ticks);
+    hipLaunchKernelGGL((k_xgmi_oneshot<NR, false>), grid, dim3(kThreads), 0, s, src, dst, n, scale, v, chunk);
 }
 
 }  // namespace
@@ -211,25 +158,39 @@ void XgmiAllreduce::allreduce(const float* src, float* dst, int64_t n, float sca
     return;
   }
   if (!opened_) throw std::runtime_error("xgmi allreduce: peers not opened");
-  Peers p{};
-  for (int r = 0; r < size_; ++r) p.base[r] = peers_[r];
-  // chunk per workgroup, a multiple of 64 floats (256 B rows) so float4 lanes stay aligned
-  int64_t chunk = (n + blocks_ - 1) / blocks_;
+  const XgmiView v = view();
+  // chunk per workgroup: >= 1 KB (small buckets use few workgroups: each one pays a flag round trip), a
+  // multiple of 64 floats (256 B rows) so float4 lanes stay aligned; grid <= blocks_
+  int64_t chunk = std::max<int64_t>((n + blocks_ - 1) / blocks_, 256);
   chunk = ((chunk + 63) / 64) * 64;
   const bool vec = (n % 4 == 0) && (reinterpret_cast<uintptr_t>(src) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(dst) % 16 == 0);
-  const dim3 grid(blocks_);
+  const dim3 grid(static_cast<unsigned>((n + chunk - 1) / chunk));
   switch (size_) {
-    case 2: launch<2>(vec, grid, s, src, dst, n, scale, p, rank_, chunk, flag_bytes_, slot_bytes_, state_, timeout_ticks_); break;
-    case 3: launch<3>(vec, grid, s, src, dst, n, scale, p, rank_, chunk, flag_bytes_, slot_bytes_, state_, timeout_ticks_); break;
-    case 4: launch<4>(vec, grid, s, src, dst, n, scale, p, rank_, chunk, flag_bytes_, slot_bytes_, state_, timeout_ticks_); break;
-    case 5: launch<5>(vec, grid, s, src, dst, n, scale, p, rank_, chunk, flag_bytes_, slot_bytes_, state_, timeout_ticks_); break;
-    case 6: launch<6>(vec, grid, s, src, dst, n, scale, p, rank_, chunk, flag_bytes_, slot_bytes_, state_, timeout_ticks_); break;
-    case 7: launch<7>(vec, grid, s, src, dst, n, scale, p, rank_, chunk, flag_bytes_, slot_bytes_, state_, timeout_ticks_); break;
-    default: launch<8>(vec, grid, s, src, dst, n, scale, p, rank_, chunk, flag_bytes_, slot_bytes_, state_, timeout_ticks_); break;
+    case 2: launch<2>(vec, grid, s, src, dst, n, scale, v, chunk); break;
+    case 3: launch<3>(vec, grid, s, src, dst, n, scale, v, chunk); break;
+    case 4: launch<4>(vec, grid, s, src, dst, n, scale, v, chunk); break;
+    case 5: launch<5>(vec, grid, s, src, dst, n, scale, v, chunk); break;
+    case 6: launch<6>(vec, grid, s, src, dst, n, scale, v, chunk); break;
+    case 7: launch<7>(vec, grid, s, src, dst, n, scale, v, chunk); break;
+    default: launch<8>(vec, grid, s, src, dst, n, scale, v, chunk); break;
   }
   hip_check(hipGetLastError(), "oneshot launch");
   ++calls_;
+}
+
+XgmiView XgmiAllreduce::view() const {
+  if (size_ > 1 && !opened_) throw std::runtime_error("xgmi allreduce: peers not opened");
+  XgmiView v{};
+  for (int r = 0; r < size_; ++r) v.base[r] = peers_[r];
+  v.state = state_;
+  v.timeout_ticks = timeout_ticks_;
+  v.flag_bytes = flag_bytes_;
+  v.slot_bytes = slot_bytes_;
+  v.rank = rank_;
+  v.size = size_;
+  v.blocks = blocks_;
+  return v;
 }
 
 int XgmiAllreduce::error() {

@@ -1,0 +1,73 @@
+// Device side of the one-shot xGMI peer exchange (protocol: xgmi_allreduce.h), shared by the stand-alone
+// all-reduce kernel (xgmi_allreduce.hip) and kernels that fold the exchange into their own epilogue (the
+// fused CNN's gradient reduction, cnn_fused.hip): such a kernel stages its output chunk into its slot,
+// calls xgmi_publish_and_wait, and reads every rank's chunk back from the peers' slots in rank order.
+//
+// XgmiView (xgmi_view.h) is plain data filled by XgmiAllreduce::view(); a kernel takes it by value.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "xgmi_view.h"
+
+namespace pde {
+
+// Workgroup b's epoch for this call (block-collective: every thread gets it through LDS).
+__device__ __forceinline__ uint32_t xgmi_epoch(const XgmiView& v, int b, uint32_t* s_epoch) {
+  if (threadIdx.x == 0) *s_epoch = v.state[b] + 1u;
+  __syncthreads();
+  return *s_epoch;
+}
+
+// Rank r's staging slot for this epoch (two slots alternate: a peer is at most one call ahead).
+__device__ __forceinline__ float* xgmi_slot(const XgmiView& v, int r, uint32_t epoch) {
+  return reinterpret_cast<float*>(v.base[r] + v.flag_bytes + static_cast<int64_t>(epoch & 1u) * v.slot_bytes);
+}
+
+// Block-collective, after every thread issued its stores into xgmi_slot(v, v.rank, epoch):
+//   every storing wave drains, the workgroup meets, one lane releases at system scope, one lane per rank
+//   raises flag (b, my rank) in that rank's flag array; one lane per rank polls my flag (b, r) until it
+//   reaches the epoch (bounded by wall clock: a timeout sets the error word and the result is dropped),
+//   then one lane acquires at system scope and the workgroup meets again.
+// Returns true when every rank's chunk of workgroup b may be read.
+__device__ __forceinline__ bool xgmi_publish_and_wait(const XgmiView& v, int b, uint32_t epoch, int* s_fail) {
+  const int tid = threadIdx.x;
+  if (tid == 0) *s_fail = 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (tid < v.size) {
+    uint32_t* f = reinterpret_cast<uint32_t*>(v.base[tid]) + b * kXgmiMaxRanks + v.rank;
+    __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* mine = reinterpret_cast<uint32_t*>(v.base[v.rank]) + b * kXgmiMaxRanks + tid;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (static_cast<int32_t>(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks) {
+        *s_fail = 1;
+        __hip_atomic_store(v.state + v.blocks, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  return *s_fail == 0;
+}
+
+// Workgroup b's epoch advances (read again by the same workgroup index next call, on every rank).
+__device__ __forceinline__ void xgmi_finish(const XgmiView& v, int b, uint32_t epoch) {
+  if (threadIdx.x == 0) v.state[b] = epoch;
+}
+
+}  // namespace pde

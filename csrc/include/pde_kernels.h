@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "xgmi_view.h"
+
 namespace pde {
 
 // ---------------------------------------------------------------------------------------------
@@ -172,14 +174,17 @@ int cnn_images_per_workgroup();
 size_t cnn_frag_bytes();  // workspace for the per-step bf16 weight-fragment image (16-B aligned)
 // prep = 0 skips the fragment prep (the image is already current: the previous step's fused SGD wrote it).
 // sgd_hp != nullptr fuses plain SGD (lr = sgd_hp[HP_LR], grad scale sgd_hp[HP_GRAD_SCALE]) and the
-// fragment refresh into the slab reduction (single process: no all-reduce between reduce and update).
+// fragment refresh into the slab reduction.  xv (world > 1, an XgmiAllreduce's view): the reduction
+// first exchanges each workgroup's gradient chunk with every peer over xGMI and sums all ranks' chunks in
+// rank order (x xscale), so the update stays fused at any world size -- 2 launches per step.
 int cnn_slab_floats();  // per-workgroup slab (every gradient except fc1's weight)
 int cnn_act_rows();     // rows of the per-batch activation image feeding the fc1 weight-gradient GEMM
 hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float* params, void* frag,
                            unsigned long long* rng, float p_drop2, float p_drop1, int training, float* slabs,
                            float* loss_part, float* acts, int nwg, float* loss, float* grads, const float* gscale,
                            int accumulate, hipStream_t s, unsigned long long* stamps = nullptr, int prep = 1,
-                           const float* sgd_hp = nullptr, int stop_after = -1, int* sgd_step = nullptr);
+                           const float* sgd_hp = nullptr, int stop_after = -1, int* sgd_step = nullptr,
+                           const XgmiView* xv = nullptr, float xscale = 1.f);
 // params -= lr * gscale * grads (plain SGD) and the matching fragment-image refresh, one launch (used
 // after the gradient all-reduce when world > 1).
 hipError_t cnn_sgd_fused(float* params, const float* grads, const float* hp, void* frag, hipStream_t s,

@@ -29,6 +29,7 @@
 
 #include "common.cuh"
 #include "pde_kernels.h"
+#include "xgmi_device.h"
 
 namespace pde {
 
@@ -712,9 +713,17 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
                                                       int accumulate, const float* __restrict__ loss_part, int B,
                                                       float* __restrict__ loss, unsigned long long* __restrict__ rng,
                                                       float* __restrict__ params, const float* __restrict__ hp,
-                                                      uint16_t* __restrict__ frag, int* __restrict__ step) {
+                                                      uint16_t* __restrict__ frag, int* __restrict__ step,
+                                                      XgmiView xv, float xscale) {
   __shared__ f32x4 part[RED_LANES][RED_COLS];  // slab: [lane][column]; fc1: [wave][lane] (same 8 KB)
+  __shared__ uint32_t s_epoch;
+  __shared__ int s_fail;
   const float gs = gscale ? gscale[0] : 1.f;
+  // world > 1 with a peer view: this block's gradients go through the one-shot xGMI exchange (stage to my
+  // slot, flags, read all ranks' values in rank order, x xscale) before the store + SGD update
+  const bool xchg = xv.size > 1;
+  const uint32_t epoch = xchg ? xgmi_epoch(xv, blockIdx.x, &s_epoch) : 0u;
+  float* xmine = xchg ? xgmi_slot(xv, xv.rank, epoch) : nullptr;
   if (blockIdx.x < RED_SLAB_BLOCKS) {
     const int col = threadIdx.x % RED_COLS, sl = threadIdx.x / RED_COLS;
     const int c4 = blockIdx.x * RED_COLS + col;
@@ -735,12 +744,33 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
     }
     part[sl][col] = (a0 + a1) + (a2 + a3);
     __syncthreads();
-    if (sl == 0 && c4 < NSLAB4) {
-      f32x4 v = part[0][col];
+    const bool owner = sl == 0 && c4 < NSLAB4;
+    const int p4 = c4 < O_FC1W / 4 ? c4 : c4 + FC1N / 4;  // slab column -> parameter float4
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (owner) {
+      v = part[0][col];
 #pragma unroll 8
       for (int k = 1; k < RED_LANES; ++k) v += part[k][col];
       v *= gs;
-      const int p4 = c4 < O_FC1W / 4 ? c4 : c4 + FC1N / 4;  // slab column -> parameter float4
+      if (xchg) reinterpret_cast<f32x4*>(xmine)[p4] = v;
+    }
+    bool ok = true;
+    if (xchg) {
+      ok = xgmi_publish_and_wait(xv, blockIdx.x, epoch, &s_fail);
+      if (owner && ok) {
+        f32x4 r4[kXgmiMaxRanks];
+#pragma unroll
+        for (int r = 0; r < kXgmiMaxRanks; ++r)
+          if (r < xv.size) r4[r] = reinterpret_cast<const f32x4*>(xgmi_slot(xv, r, epoch))[p4];
+        v = r4[0];
+#pragma unroll
+        for (int r = 1; r < kXgmiMaxRanks; ++r)
+          if (r < xv.size) v += r4[r];
+        v *= xscale;
+      }
+      xgmi_finish(xv, blockIdx.x, epoch);
+    }
+    if (owner && ok) {
       f32x4* g4 = reinterpret_cast<f32x4*>(grads) + p4;
       if (accumulate) v += *g4;
       *g4 = v;
@@ -781,12 +811,43 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
     f32x4* wpart = &part[0][0];
     wpart[wid * 64 + lane] = acc0 + acc1;
     __syncthreads();
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    const int i = i0 + lr;
     if (wid == 0) {
-      f32x4 v = wpart[lane];
+      v = wpart[lane];
 #pragma unroll
       for (int w = 1; w < RED_T / 64; ++w) v += wpart[w * 64 + lane];
       v *= gs;
-      const int i = i0 + lr;
+      if (xchg) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = j0 + lg * 4 + r;
+          if (j < F1) xmine[O_FC1W + j * NIN + i] = v[r];
+        }
+      }
+    }
+    bool ok = true;
+    if (xchg) {
+      ok = xgmi_publish_and_wait(xv, blockIdx.x, epoch, &s_fail);
+      if (wid == 0 && ok) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = j0 + lg * 4 + r;
+          const int p = O_FC1W + (j < F1 ? j : 0) * NIN + i;
+          float a[kXgmiMaxRanks];
+#pragma unroll
+          for (int q = 0; q < kXgmiMaxRanks; ++q)
+            if (q < xv.size) a[q] = xgmi_slot(xv, q, epoch)[p];
+          float g = a[0];
+#pragma unroll
+          for (int q = 1; q < kXgmiMaxRanks; ++q)
+            if (q < xv.size) g += a[q];
+          v[r] = g * xscale;
+        }
+      }
+      xgmi_finish(xv, blockIdx.x, epoch);
+    }
+    if (wid == 0 && ok) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int j = j0 + lg * 4 + r;
@@ -827,8 +888,18 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
                            unsigned long long* rng, float p_drop2, float p_drop1, int training, float* slabs,
                            float* loss_part, float* acts, int nwg, float* loss, float* grads, const float* gscale,
                            int accumulate, hipStream_t s, unsigned long long* stamps, int prep,
-                           const float* sgd_hp, int stop_after, int* sgd_step) {
+                           const float* sgd_hp, int stop_after, int* sgd_step, const XgmiView* xv,
+                           float xscale) {
   if (reinterpret_cast<uintptr_t>(grads) & 15) return hipErrorInvalidValue;  // float4 gradient stores
+  XgmiView view{};
+  view.size = 1;
+  if (xv != nullptr && xv->size > 1) {
+    // the exchange replaces the all-reduce of the gradients: no local accumulation in between, one flag
+    // row and one staging float per parameter for each of this kernel's workgroups
+    if (accumulate || xv->blocks < RED_BLOCKS || xv->slot_bytes < static_cast<int64_t>(NPARAM) * 4)
+      return hipErrorInvalidValue;
+    view = *xv;
+  }
   const size_t sm = sizeof(CnnSmem);
   static bool attr = false;
   if (!attr) {
@@ -844,7 +915,8 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
                      static_cast<const u16x8*>(frag), rng, p_drop2, p_drop1, training, slabs, loss_part, acts, stamps,
                      stop_after);
   hipLaunchKernelGGL(k_cnn_reduce, dim3(RED_BLOCKS), dim3(RED_T), 0, s, slabs, nwg, acts, gscale, grads,
-                     accumulate, loss_part, B, loss, rng, params, sgd_hp, static_cast<uint16_t*>(frag), sgd_step);
+                     accumulate, loss_part, B, loss, rng, params, sgd_hp, static_cast<uint16_t*>(frag), sgd_step,
+                     view, xscale);
   return hipGetLastError();
 }
 

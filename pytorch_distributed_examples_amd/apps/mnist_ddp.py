@@ -15,8 +15,9 @@ lines, and ``Execution time``.
 MI355X-first differences: RCCL (``nccl``) over xGMI on GPUs -- gloo on CPU -- with the xGMI bucket
 policy; bf16 MFMA kernels; HBM-resident synthetic MNIST; atomic snapshot by global rank 0 only;
 ``--model cnn`` runs BASELINE config 1's CNN through the same plumbing (``--fused``: the whole-network
-training kernel of csrc/kernels/cnn_fused.hip, gradients straight into the DDP flat buffer, one all-reduce
-on the GPU data plane of :mod:`..parallel.comm`, one fused SGD launch); ``--rewire`` keeps the worker alive
+training kernel of csrc/kernels/cnn_fused.hip, gradients straight into the DDP flat buffer; on the xGMI data
+plane of :mod:`..parallel.comm` the all-reduce and the SGD update run inside the slab-reduction kernel, else
+one all-reduce and one fused SGD launch); ``--rewire`` keeps the worker alive
 across membership changes (in-process RCCL communicator re-wire, :mod:`..elastic.rewire`).
 """
 from __future__ import annotations
@@ -97,8 +98,12 @@ class Trainer:
 
     def _run_batch(self, source, targets):
         if self.fused is not None:
+            xgmi = getattr(self.ddp.comm, "xgmi", None)
             if self.ddp.world == 1:  # SGD + fragment refresh inside the slab reduction
                 loss = self.fused.forward_backward(source, targets, grad_out=self.ddp.flat_grad, sgd=self.optimizer)
+            elif xgmi is not None:  # + the gradient all-reduce, exchanged over xGMI inside that kernel
+                loss = self.fused.forward_backward(source, targets, grad_out=self.ddp.flat_grad, sgd=self.optimizer,
+                                                   xgmi=xgmi)
             else:
                 loss = self.fused.forward_backward(source, targets, grad_out=self.ddp.flat_grad)
                 self.ddp.sync_gradients()

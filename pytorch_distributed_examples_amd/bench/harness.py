@@ -184,11 +184,16 @@ def build_data_parallel(args, ctx, batch) -> Workload:
         ddp = DistributedDataParallel(model, overlap=False, param_order="forward", comm=comm)
     else:
         ddp = DistributedDataParallel(model, overlap=not use_graph, comm=comm)
+    # world > 1 on the xGMI data plane: the fused CNN exchanges its gradients inside the slab reduction
+    # (PDE_CNN_XCHG=0: all-reduce through the DDP communicator + a separate SGD launch instead)
+    xgmi = getattr(comm, "xgmi", None) if fused is not None and os.environ.get("PDE_CNN_XCHG", "1") != "0" else None
 
     def train_step(x, y):
         if fused is not None:
             if ctx.world_size == 1:
                 return fused.forward_backward(x, y, grad_out=ddp.flat_grad, sgd=opt)
+            if xgmi is not None:  # all-reduce folded into the slab reduction: still 2 launches per step
+                return fused.forward_backward(x, y, grad_out=ddp.flat_grad, sgd=opt, xgmi=xgmi)
             loss = fused.forward_backward(x, y, grad_out=ddp.flat_grad)
             ddp.sync_gradients()
             fused.sgd_step(opt, ddp.flat_grad)
@@ -217,7 +222,8 @@ def build_data_parallel(args, ctx, batch) -> Workload:
     w = Workload(step, batch * ctx.world_size, f"dp{ctx.world_size}", hipgraph=one is not None,
                  fused_step=fused is not None, rccl_nranks=nranks,
                  steps_per_graph=group.steps if group is not None else (1 if one is not None else 0),
-                 allreduce="xgmi-oneshot<=%dB+rccl" % comm.threshold if routed is not None else
+                 allreduce=("xgmi-in-reduce-kernel" if xgmi is not None else
+                            "xgmi-oneshot<=%dB+rccl" % comm.threshold) if routed is not None else
                  ("rccl" if comm is not None else ("gloo" if ctx.world_size > 1 else "none")))
     w.group = group
     if routed is not None:

@@ -21,8 +21,14 @@ the fragment slots of the weights it updates; with :meth:`sgd_step` (after the g
 kernel does the same.  Either way the next step skips the prep launch::
 
     loss = fused.forward_backward(x, y, grad_out=buf, sgd=opt)          # world 1: 2 launches per step
-    loss = fused.forward_backward(x, y, grad_out=ddp.flat_grad)         # world > 1
+    loss = fused.forward_backward(x, y, grad_out=g, sgd=opt, xgmi=xa)   # world > 1 on one node: 2 launches
+    loss = fused.forward_backward(x, y, grad_out=ddp.flat_grad)         # world > 1, any data plane:
     ddp.sync_gradients(); fused.sgd_step(opt, ddp.flat_grad)            #   3 launches + all-reduce
+
+With ``xgmi`` (a :class:`..parallel.xgmi_allreduce.XgmiAllreduce` over the data-parallel ranks) the slab
+reduction exchanges every workgroup's gradient chunk with all peers over xGMI inside the same kernel and
+sums the ranks' chunks in rank order (``avg``: x 1/world), so ``grad_out`` receives the all-reduced
+gradients, identical on every rank, and the SGD update stays fused -- the all-reduce costs no launch.
 
 The fragment image is re-derived (prep launch) whenever anything other than these fused updates may have
 written the weights: any other optimiser step bumps the weight generation (:func:`.functional.
@@ -111,10 +117,12 @@ class FusedCNN:
 
     def forward_backward(self, x: torch.Tensor, y: torch.Tensor, grad_out: torch.Tensor | None = None,
                          accumulate: bool = False, p_drop2: float = 0.5, p_drop1: float = 0.5,
-                         sgd=None) -> torch.Tensor:
-        """Loss (device scalar) of the batch; gradients of the mean loss written to ``grad_out``.
+                         sgd=None, xgmi=None, avg: bool = True) -> torch.Tensor:
+        """Loss (device scalar) of the local batch; gradients of the mean loss written to ``grad_out``.
 
-        ``sgd``: a plain FusedSGD over these parameters -- also take the optimiser step (single process)."""
+        ``sgd``: a plain FusedSGD over these parameters -- also take the optimiser step.
+        ``xgmi``: an XgmiAllreduce over the data-parallel ranks -- ``grad_out`` receives the all-reduced
+        gradients (``avg``: averaged), exchanged inside the reduction kernel."""
         C = _native.C()
         if grad_out is None:
             grad_out = self.grad_buffer()
@@ -123,8 +131,11 @@ class FusedCNN:
         training = self.net.training
         prep = self._frag_gen is None or self._frag_gen != OF.weight_generation()
         (hp, step), params = self._sgd_hp(sgd) if sgd is not None else ((None, None), None)
+        view, xscale = None, 1.0
+        if xgmi is not None and xgmi.size > 1:
+            view, xscale = xgmi.view(), (1.0 / xgmi.size if avg else 1.0)
         loss = C.cnn_train(x, y, self.flat, OF._rng_counter(x.device), p_drop2, p_drop1, training, grad_out,
-                           accumulate, None, self.stamps, self.frag, prep, hp, self.stop_after, step)
+                           accumulate, None, self.stamps, self.frag, prep, hp, self.stop_after, step, view, xscale)
         if sgd is not None:
             self._after_update(sgd, params)
         else:

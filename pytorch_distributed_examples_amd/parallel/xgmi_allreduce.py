@@ -10,6 +10,7 @@ bandwidth better than 7 full copies per rank.
 
     xa = XgmiAllreduce(device)            # collective: exchanges IPC handles through the c10d store
     xa.allreduce_(grads, avg=True)        # stream-ordered, hipGraph-capturable, bit-identical on all ranks
+    fused.forward_backward(x, y, sgd=opt, xgmi=xa)   # the CNN folds the exchange into its reduction kernel
     comm = RoutedComm(StreamComm(device), xa, threshold_bytes=1 << 20)
     ddp = DistributedDataParallel(model, comm=comm)
 
@@ -31,7 +32,7 @@ DEFAULT_THRESHOLD = int(os.environ.get("PDE_XGMI_THRESHOLD", str(1 << 20)))
 
 
 class XgmiAllreduce:
-    def __init__(self, device: torch.device, group=None, max_bytes: int = 4 << 20, blocks: int = 64,
+    def __init__(self, device: torch.device, group=None, max_bytes: int = 4 << 20, blocks: int = 256,
                  timeout_s: float = 5.0):
         assert device.type == "cuda", "the xGMI all-reduce is a GPU data plane"
         self.device = device
@@ -54,6 +55,11 @@ class XgmiAllreduce:
     def allreduce_(self, t: torch.Tensor, avg: bool = False) -> torch.Tensor:
         self.impl.allreduce_(t, 1.0 / self.size if avg else 1.0)
         return t
+
+    def view(self) -> list:
+        """Flat device view (csrc/comm/xgmi_view.h) for kernels that fold the exchange into their own
+        epilogue: the fused CNN's gradient reduction (``FusedCNN.forward_backward(..., xgmi=self)``)."""
+        return self.impl.view()
 
     def check(self) -> None:
         """Raise if any call timed out waiting for a peer (synchronises the device)."""

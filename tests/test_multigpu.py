@@ -8,7 +8,9 @@ Checks, per world size:
 * the pipeline's per-direction P2P channel (parallel/pipeline.py) in both directions;
 * the Horovod engine (negotiated fusion over RCCL) against the same fp32 sum;
 * 2-stage pipeline gradients (gpipe and 1f1b, hipGraph-free) against a single-process reference;
-* the one-shot xGMI peer all-reduce (csrc/comm/xgmi_allreduce.hip) against RCCL.
+* the one-shot xGMI peer all-reduce (csrc/comm/xgmi_allreduce.hip) against RCCL;
+* the fused CNN step with that exchange folded into its reduction kernel against local gradients +
+  RCCL all-reduce + the separate SGD launch (replicas bit-identical).
 """
 import os
 import subprocess
@@ -90,6 +92,33 @@ for n in (1, 5, 21840, 262144):
     dist.all_gather(gathered, x)
     for gth in gathered:
         assert torch.equal(gth, x)
+# 5. fused CNN with the exchange inside its reduction kernel vs local gradients + RCCL all-reduce + SGD launch
+from pytorch_distributed_examples_amd.models.cnn import Net
+from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
+from pytorch_distributed_examples_amd.ops.optim import FusedSGD
+torch.manual_seed(0)
+net_a, net_b = Net().to(dev), Net().to(dev)
+net_b.load_state_dict(net_a.state_dict())
+fa, fb = FusedCNN(net_a), FusedCNN(net_b)
+oa, ob = FusedSGD(net_a.parameters(), lr=0.05), FusedSGD(net_b.parameters(), lr=0.05)
+ga, gb = fa.grad_buffer(), fb.grad_buffer()
+gen = torch.Generator().manual_seed(100 + r)
+for it in range(3):
+    x = torch.randn(512, 1, 28, 28, generator=gen).to(dev)
+    y = torch.randint(0, 10, (512,), generator=gen).to(dev)
+    fa.forward_backward(x, y, grad_out=ga, sgd=oa, xgmi=xa, p_drop2=0.0, p_drop1=0.0)
+    fb.forward_backward(x, y, grad_out=gb, p_drop2=0.0, p_drop1=0.0)
+    comm.allreduce_(gb)
+    gb.mul_(1.0 / N)
+    fb.sgd_step(ob, gb)
+torch.cuda.synchronize()
+xa.check()
+assert torch.allclose(ga, gb, rtol=1e-4, atol=1e-6), (ga - gb).abs().max()
+assert torch.allclose(fa.flat, fb.flat, rtol=1e-4, atol=1e-6), (fa.flat - fb.flat).abs().max()
+gathered = [torch.empty_like(fa.flat) for _ in range(N)]
+dist.all_gather(gathered, fa.flat)
+for gth in gathered:
+    assert torch.equal(gth, fa.flat)  # bit-identical replicas
 xa.close()
 comm.destroy()
 dist.destroy_process_group()

@@ -1,8 +1,8 @@
 """One-shot peer all-reduce (csrc/comm/xgmi_allreduce.hip) rehearsed on ONE GPU: 2 and 4 processes share
 the card, each maps the others' IPC-exported staging buffers exactly as the ranks of an 8-GPU node map
 their peers' over xGMI.  Checks the result against an fp32 reference, bit-identity across ranks, the
-hipGraph-captured form (epochs advance on every replay), a late peer (bounded spin, no timeout), and the
-DDP routing communicator.  The N-GPU form against RCCL is in tests/test_multigpu.py."""
+hipGraph-captured form (epochs advance on every replay), a late peer (bounded spin, no timeout), the
+DDP routing communicator, and the fused CNN's reduction kernel with the exchange folded in.  The N-GPU form against RCCL is in tests/test_multigpu.py."""
 import os
 import subprocess
 import sys
@@ -93,6 +93,37 @@ torch.cuda.synchronize()
 assert torch.allclose(ddp.flat_grad, torch.full_like(ddp.flat_grad, (N - 1) / 2)), ddp.flat_grad[:4]
 assert comm.routed["xgmi"] >= 1
 xa.check()
+# fused CNN: the gradient exchange inside the slab-reduction kernel (+ fused SGD) against local gradients
+# all-reduced over gloo + the separate SGD launch; both replicas start from the same weights.
+# Rehearsed at 2 ranks only: with 3+ processes on ONE GPU the ranks that reached their reduction kernel
+# fill the CUs with spinning workgroups (8 waves each) and the last rank's 122 KB-LDS training kernel cannot
+# be placed until they time out -- on a node every rank owns its GPU and that cannot happen.
+if N > 2:
+    dist.barrier(); xa.close(); dist.destroy_process_group(); print("XGMI_OK", r); sys.exit(0)
+from pytorch_distributed_examples_amd.models.cnn import Net
+from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
+from pytorch_distributed_examples_amd.ops.optim import FusedSGD
+torch.manual_seed(0)
+net_a, net_b = Net().to(dev), Net().to(dev)
+net_b.load_state_dict(net_a.state_dict())
+fa, fb = FusedCNN(net_a), FusedCNN(net_b)
+oa, ob = FusedSGD(net_a.parameters(), lr=0.05), FusedSGD(net_b.parameters(), lr=0.05)
+ga, gb = fa.grad_buffer(), fb.grad_buffer()  # installs the p.grad views the optimisers step
+gen = torch.Generator().manual_seed(100 + r)
+for it in range(3):
+    x = torch.randn(200 + 56 * r, 1, 28, 28, generator=gen).to(dev)   # ranks may hold different batch sizes
+    y = torch.randint(0, 10, (x.shape[0],), generator=gen).to(dev)
+    fa.forward_backward(x, y, grad_out=ga, sgd=oa, xgmi=xa, p_drop2=0.0, p_drop1=0.0)
+    fb.forward_backward(x, y, grad_out=gb, p_drop2=0.0, p_drop1=0.0)
+    h = gb.cpu(); dist.all_reduce(h); gb.copy_(h / N)
+    fb.sgd_step(ob, gb)
+torch.cuda.synchronize()
+xa.check()
+assert torch.allclose(ga, gb, rtol=1e-5, atol=1e-7), (ga - gb).abs().max()
+assert torch.allclose(fa.flat, fb.flat, rtol=1e-5, atol=1e-7), (fa.flat - fb.flat).abs().max()
+ws = [torch.empty_like(fa.flat.cpu()) for _ in range(N)]
+dist.all_gather(ws, fa.flat.cpu())
+assert all(torch.equal(w, ws[0]) for w in ws)  # every replica holds bit-identical weights
 dist.barrier()
 xa.close()
 dist.destroy_process_group()
@@ -118,7 +149,12 @@ def _run(n):
 @pytest.mark.parametrize("n", [2, 4])
 def test_xgmi_oneshot_rehearsal_one_gpu(gpu, n):
     res = _run(n)
-    assert res.returncode == 0 and res.stdout.count("XGMI_OK") == n, (res.stdout[-3000:], res.stderr[-6000:])
+    ranks = "\n".join(l for l in res.stderr.splitlines() if l.startswith("[rank"))  # the ranks' tracebacks
+    if res.returncode != 0:  # full logs for the post-mortem (pytest truncates long assertion messages)
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(REPO, "gpurun_out", f"xgmi_rehearsal_{n}.err"), "w") as f:
+            f.write(res.stdout + "\n----\n" + res.stderr)
+    assert res.returncode == 0 and res.stdout.count("XGMI_OK") == n, (res.stdout[-2000:], ranks[-6000:])
 
 
 def test_xgmi_world1(gpu):
