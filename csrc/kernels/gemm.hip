@@ -12,20 +12,21 @@
 //   * A and B tiles are staged global -> registers -> LDS, double-buffered: the global loads of
 //     K-tile t+1 are issued before the MFMAs of tile t and written to the other LDS buffer after
 //     them (async-STAGE split, T14), one barrier per K-tile.
-//   * LDS images are unpadded K-contiguous 64-B rows with an XOR chunk swizzle, so MFMA fragments are
-//     single conflict-free ds_read_b128 (see swz_chunk).
-//     Operands that are contiguous along the row (M/N) dimension -- the transposed operands of
-//     dgrad / wgrad -- are loaded 16 B along the row and scattered into the K-contiguous image.
+//   * K-contiguous operands: LDS images are unpadded K-contiguous 64-B rows with an XOR chunk swizzle, so
+//     MFMA fragments are single conflict-free ds_read_b128 (see swz_chunk).
+//     Operands contiguous along the row (M/N) dimension -- the transposed operands of dgrad / wgrad -- are
+//     stored as loaded: [k][row] images written with 16-B stores, and the MFMA fragments are read with
+//     gfx950's transposing LDS read (ds_read_b64_tr_b16, two per fragment; see rc_swz / rc_frag), so no
+//     operand is ever scattered element-wise into LDS.
 //   * Implicit-GEMM gathers keep per-slot state: a row's (image, output-pixel) decomposition is done
 //     once per block, and the slot's (kh, kw, c) -- or, for the weight-gradient operand, its output
 //     pixel -- is advanced incrementally by BK per K-tile, so the K loop has no integer division.
 //   * Tiles are mapped XCD-aware (T1): consecutive tile ids go to the same XCD group so tiles
 //     sharing A rows / B columns hit the same L2.
-//   * Split-K writes fp32 partial slabs; the LAST K-slice block of a tile to arrive (agent-scope release ->
-//     per-tile ticket -> acquire, cdna_hip_programming.md §5 "in-launch split-K reduction") sums the slabs in
-//     fixed z order (deterministic) and applies the fused epilogue: no separate reduce launch (the
-//     launch-boundary cost per split GEMM was ~5 us in a hipGraph).  A vectorised slab-reduction kernel
-//     remains as the fallback (first call inside a graph capture, before the ticket array exists).
+//   * Split-K writes fp32 partial slabs, summed in fixed z order (deterministic) by a vectorised
+//     slab-reduction kernel that applies the fused epilogue.  Opt-in (PDE_GEMM_INKERNEL_SPLITK=1): the LAST
+//     K-slice block of a tile to arrive reduces in the same launch (write-through slabs -> per-tile ticket,
+//     cdna_hip_programming.md §5 "in-launch split-K reduction") -- measured slower here, see split_tickets.
 //   * Epilogue options: bias, ReLU, ReLU-mask (backward), fp32 / bf16 output, accumulate, and an OIHW
 //     remap that writes a conv weight gradient straight into the parameter's [Co][Ci][R][S] fp32 grad.
 #include <cstdlib>
@@ -56,6 +57,38 @@ __device__ __forceinline__ int swz_chunk(int row, int chunk) {
 }
 
 __device__ __forceinline__ u16x8 zero8() { return u16x8{0, 0, 0, 0, 0, 0, 0, 0}; }
+
+// Row-contiguous LDS image: [BK = 32][BROWS] -- row k holds BROWS consecutive row (M/N) elements, its
+// 16-B chunks XOR-swizzled by rc_swz(k).  A 16x16x32 fragment (lane l: row rb + (l & 15), k = 8 (l >> 4)
+// + j) is two ds_read_b64_tr_b16: the 16-lane group g reads the 4 x 16 blocks k = 8g..8g+3 and 8g+4..8g+7
+// (lane 4q + p addresses row k0 + q, columns rb + 4p..4p+3; lane i receives column i).  A 32-lane half
+// then touches rows {k0..k0+3, k0+8..k0+11} x 2 chunks each; the swizzle gives those 16 (row, chunk) pairs
+// distinct 4-bank slots (bank = (k * 2 BROWS + 16 chunk') / 4 mod 64), so the reads are conflict-free.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+template <int BROWS>
+__device__ __forceinline__ int rc_swz(int k) {
+  constexpr int CH = BROWS / 8;  // 16-B chunks per row
+  static_assert(CH == 4 || CH == 8 || CH == 16, "row-contiguous image widths 32 / 64 / 128");
+  if constexpr (CH == 4) return 2 * ((k >> 3) & 1);
+  else if constexpr (CH == 8) return 2 * ((k >> 1) & 1) + 4 * ((k >> 3) & 1);
+  else return 2 * (k & 3) + 8 * ((k >> 3) & 1);
+}
+
+template <int BROWS>
+__device__ __forceinline__ bf16x8 rc_frag(const uint16_t* lds, int rb, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int c = (rb >> 3) + (p >> 1);
+  const int k1 = 8 * g + q, k2 = k1 + 4;
+  const uint16_t* a1 = lds + k1 * BROWS + ((c ^ rc_swz<BROWS>(k1)) << 3) + 4 * (p & 1);
+  const uint16_t* a2 = lds + k2 * BROWS + ((c ^ rc_swz<BROWS>(k2)) << 3) + 4 * (p & 1);
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+  const s16x4 r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a2));
+  const s16x8 v = __builtin_shufflevector(r1, r2, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
 
 // Dense K-contiguous / row-contiguous element loads (operand kind 0).
 __device__ __forceinline__ u16x8 load_dense_kc(const Operand& op, int rows, int K, int r, int k0, bool vec_ok) {
@@ -272,18 +305,14 @@ struct RcLoader {
     }
   }
 
-  __device__ __forceinline__ void store(uint16_t* lds) {  // lds: [BROWS][BK], transposing scatter
+  __device__ __forceinline__ void store(uint16_t* lds) {  // lds: [BK][BROWS] (rc_swz), 16-B stores
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int v = threadIdx.x + i * kThreads;
       if (v < kVecs) {
         const int kk = v / (BROWS / 8);
         const int rv = v - kk * (BROWS / 8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int row = rv * 8 + j;
-          lds[row * BK + swz_chunk(row, kk >> 3) * 8 + (kk & 7)] = regs[i][j];
-        }
+        *reinterpret_cast<u16x8*>(lds + kk * BROWS + ((rv ^ rc_swz<BROWS>(kk)) << 3)) = regs[i];
       }
     }
   }
@@ -512,13 +541,21 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles
       bf16x8 af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const int row = wm * WTM + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(As + row * BK + swz_chunk(row, kk * 4 + (lane >> 4)) * 8);
+        if constexpr (AKC) {
+          const int row = wm * WTM + i * 16 + (lane & 15);
+          af[i] = *reinterpret_cast<const bf16x8*>(As + row * BK + swz_chunk(row, kk * 4 + (lane >> 4)) * 8);
+        } else {
+          af[i] = rc_frag<BM>(As, wm * WTM + i * 16, lane);
+        }
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int row = wn * WTN + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + swz_chunk(row, kk * 4 + (lane >> 4)) * 8);
+        if constexpr (BKC) {
+          const int row = wn * WTN + j * 16 + (lane & 15);
+          bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + swz_chunk(row, kk * 4 + (lane >> 4)) * 8);
+        } else {
+          bfr[j] = rc_frag<BN>(Bs, wn * WTN + j * 16, lane);
+        }
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
