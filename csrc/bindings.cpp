@@ -153,6 +153,91 @@ Tensor linear_wgrad(const Tensor& dy, const Tensor& x, const optional<Tensor>& o
 }
 
 // ------------------------------------------------------------------------------------------------
+// Linear ops on strided row views (the fused MLP step, models/mlp_fused.py): operands and outputs are 2-D
+// views whose rows may be padded (stride(0) = ld >= cols, stride(1) = 1), e.g. activations that carry a
+// trailing ones column for the bias gradient.
+// ------------------------------------------------------------------------------------------------
+#define CHECK_ROWS(x) \
+  CHECK_DEV(x);       \
+  TORCH_CHECK((x).dim() == 2 && (x).stride(1) == 1, #x " must be a 2-D row-major view")
+
+// out = relu?(x W^T + b)
+void linear_fwd_out(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, bool relu, Tensor& out) {
+  CHECK_ROWS(x); CHECK_IN(w); CHECK_ROWS(out); CHECK_BF16(x); CHECK_BF16(w);
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) == N, "linear_fwd_out: shape mismatch");
+  const bool f32 = out.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32 || out.scalar_type() == at::kBFloat16, "linear_fwd_out: out must be fp32 or bf16");
+  pde::GemmArgs a{};
+  a.M = M; a.N = N; a.K = K;
+  a.a = dense(x, x.stride(0), 1);
+  a.b = dense(w, K, 1);
+  a.out = out.data_ptr(); a.ldo = out.stride(0);
+  a.bias = cf32(bias);
+  a.nbias = a.bias ? static_cast<int>(bias->numel()) : 0;
+  a.epi = (a.bias ? pde::EPI_BIAS : 0) | (relu ? pde::EPI_RELU : 0) | (f32 ? pde::EPI_OUT_F32 : 0);
+  run_gemm(a, x, -1);
+}
+
+// out = (dy . W) * (aux > 0 when aux is given)
+void linear_dgrad_out(const Tensor& dy, const Tensor& w, const optional<Tensor>& aux, Tensor& out) {
+  CHECK_ROWS(dy); CHECK_IN(w); CHECK_ROWS(out); CHECK_BF16(dy); CHECK_BF16(w); CHECK_BF16(out);
+  const int M = dy.size(0), N = dy.size(1), K = w.size(1);
+  TORCH_CHECK(w.size(0) == N && out.size(0) == M && out.size(1) == K, "linear_dgrad_out: shape mismatch");
+  pde::GemmArgs a{};
+  a.M = M; a.N = K; a.K = N;
+  a.a = dense(dy, dy.stride(0), 1);
+  a.b = dense(w, 1, K);
+  a.out = out.data_ptr(); a.ldo = out.stride(0);
+  if (aux.has_value() && aux->defined()) {
+    CHECK_ROWS(*aux); CHECK_BF16(*aux);
+    TORCH_CHECK(aux->size(0) == M && aux->size(1) >= K, "linear_dgrad_out: aux shape");
+    a.aux = cu16(aux); a.ldaux = aux->stride(0);
+    a.epi = pde::EPI_DRELU;
+  }
+  run_gemm(a, dy, -1);
+}
+
+// out_w = dy^T . x_ext[:, :K],  out_b = dy^T . x_ext[:, K] (= column sums of dy: x_ext's last column is
+// all ones) -- weight and bias gradients of a linear layer in ONE GEMM (fp32, written or accumulated).
+void linear_wgrad_bias(const Tensor& dy, const Tensor& x_ext, Tensor& out_w, Tensor& out_b, bool accumulate) {
+  CHECK_ROWS(dy); CHECK_ROWS(x_ext); CHECK_IN(out_w); CHECK_IN(out_b); CHECK_BF16(dy); CHECK_BF16(x_ext);
+  CHECK_F32(out_w); CHECK_F32(out_b);
+  const int M = dy.size(0), N = dy.size(1), K = x_ext.size(1) - 1;
+  TORCH_CHECK(x_ext.size(0) == M && out_w.numel() == static_cast<long>(N) * K && out_b.numel() == N,
+              "linear_wgrad_bias: shape mismatch");
+  pde::GemmArgs a{};
+  a.M = N; a.N = K + 1; a.K = M;
+  a.a = dense(dy, 1, dy.stride(0));
+  a.b = dense(x_ext, 1, x_ext.stride(0));
+  a.out = out_w.data_ptr(); a.ldo = K;
+  a.bias_grad = out_b.data_ptr<float>(); a.bias_col = K;
+  a.epi = pde::EPI_OUT_F32 | (accumulate ? pde::EPI_ACCUM : 0);
+  run_gemm(a, dy, -1);
+}
+
+// x [B, K] fp32 -> out[:, :K] bf16 and out[:, K] = 1 (out: a [B, >= K + 1] row view)
+void cast_rows_ones(const Tensor& x, Tensor& out) {
+  CHECK_IN(x); CHECK_F32(x); CHECK_ROWS(out); CHECK_BF16(out);
+  const int B = x.size(0), K = x.numel() / std::max<int64_t>(1, x.size(0));
+  TORCH_CHECK(out.size(0) == B && out.size(1) >= K + 1, "cast_rows_ones: out must be [B, >= K + 1]");
+  check(pde::cast_rows_bf16(x.data_ptr<float>(), B, K, u16(out), out.stride(0), 1, cur_stream()), "cast_rows_ones");
+}
+
+// (mean cross-entropy loss, d loss / d logits as bf16) in one launch
+std::vector<Tensor> ce_fused(const Tensor& x, const Tensor& tgt) {
+  CHECK_IN(x); CHECK_IN(tgt);
+  TORCH_CHECK(tgt.scalar_type() == at::kLong, "targets must be int64");
+  const int B = x.size(0), V = x.size(1);
+  Tensor loss = at::empty({}, x.options().dtype(at::kFloat));
+  Tensor dx = at::empty({B, V}, x.options().dtype(at::kBFloat16));
+  check(pde::ce_fused(x.data_ptr(), x.scalar_type() == at::kFloat, tgt.data_ptr<int64_t>(), B, V,
+                      loss.data_ptr<float>(), u16(dx), cur_stream()),
+        "ce_fused");
+  return {loss, dx};
+}
+
+// ------------------------------------------------------------------------------------------------
 // NHWC implicit-GEMM convolution
 // ------------------------------------------------------------------------------------------------
 Tensor conv_fwd(const Tensor& x, const Tensor& wf, const optional<Tensor>& bias, int R, int S, int stride, int pad,
@@ -766,6 +851,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("accumulate") = false);
   m.def("relu_bwd", &relu_bwd);
   m.def("ce_fwd", &ce_fwd);
+  m.def("ce_fused", &ce_fused);
+  m.def("linear_fwd_out", &linear_fwd_out);
+  m.def("linear_dgrad_out", &linear_dgrad_out);
+  m.def("linear_wgrad_bias", &linear_wgrad_bias);
+  m.def("cast_rows_ones", &cast_rows_ones);
   m.def("ce_bwd", &ce_bwd);
   m.def("log_softmax_fwd", &log_softmax_fwd);
   m.def("log_softmax_bwd", &log_softmax_bwd);

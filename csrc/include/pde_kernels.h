@@ -62,6 +62,8 @@ struct GemmArgs {
   float* workspace;                // splitk * M * N fp32
   int oihw_ci, oihw_rs, oihw_cp;   // EPI_OIHW: real Cin, R*S, padded Cin of the gathered activation
   int* tickets;                    // set by gemm_bf16: per-tile arrival counters of the in-kernel split-K reduce
+  float* bias_grad;                // EPI_OUT_F32: output column bias_col goes to bias_grad[m] instead (the
+  int bias_col;                    //   "ones column" bias gradient of a linear wgrad), columns beyond are dropped
 };
 
 hipError_t gemm_bf16(const GemmArgs& args, hipStream_t stream);
@@ -70,6 +72,9 @@ hipError_t gemm_bf16(const GemmArgs& args, hipStream_t stream);
 // Elementwise / layout (elementwise.hip)
 // ---------------------------------------------------------------------------------------------
 hipError_t cast_f32_bf16(const float* in, uint16_t* out, long n, hipStream_t s);
+// in [rows][cols] fp32 -> out [rows][ldo] bf16, plus out[r][cols] = 1 when ones != 0 (the ones column a
+// linear wgrad GEMM turns into the bias gradient)
+hipError_t cast_rows_bf16(const float* in, int rows, int cols, uint16_t* out, int ldo, int ones, hipStream_t s);
 hipError_t cast_bf16_f32(const uint16_t* in, float* out, long n, hipStream_t s);
 // NCHW fp32 -> NHWC bf16 with channel padding to Cp (zero fill)
 hipError_t nchw_f32_to_nhwc_bf16(const float* in, uint16_t* out, int N, int C, int H, int W, int Cp,
@@ -106,6 +111,10 @@ hipError_t ce_fwd(const void* x, int x_f32, const int64_t* tgt, int B, int V, in
                   hipStream_t s);
 hipError_t ce_bwd(const void* x, int x_f32, const int64_t* tgt, const float* lse, const float* gout, int B, int V,
                   int mode, void* dx, int dx_f32, hipStream_t s);
+// Mean cross-entropy and its input gradient in one launch (mode 0 of ce_fwd/ce_bwd with d loss = 1):
+// loss[0] = mean_b (lse_b - x[b, t_b]),  dx[b, v] = (softmax(x_b)_v - [v == t_b]) / B  (bf16).
+hipError_t ce_fused(const void* x, int x_f32, const int64_t* tgt, int B, int V, float* loss, uint16_t* dx,
+                    hipStream_t s);
 hipError_t log_softmax_fwd(const void* x, int x_f32, int B, int V, float* y, hipStream_t s);
 hipError_t log_softmax_bwd(const float* dy, const float* y, int B, int V, void* dx, int dx_f32, hipStream_t s);
 hipError_t mse_fwd(const void* p, int p_f32, const float* t, long n, float* loss, hipStream_t s);

@@ -8,6 +8,18 @@ namespace pde {
 
 namespace {
 
+// Strided row cast with an optional trailing ones column (element (r, cols)).
+__global__ void k_cast_rows_bf16(const float* __restrict__ in, int rows, int cols, uint16_t* __restrict__ out,
+                                 int ldo, int ones) {
+  const long n = static_cast<long>(rows) * (cols + 1);
+  for (long i = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int r = static_cast<int>(i / (cols + 1)), c = static_cast<int>(i - static_cast<long>(r) * (cols + 1));
+    if (c < cols) out[static_cast<long>(r) * ldo + c] = f2bf(in[static_cast<long>(r) * cols + c]);
+    else if (ones) out[static_cast<long>(r) * ldo + c] = f2bf(1.f);
+  }
+}
+
 __global__ void k_cast_f32_bf16(const float* __restrict__ in, uint16_t* __restrict__ out, long n) {
   const long nv = n / 8;
   const long stride = static_cast<long>(gridDim.x) * blockDim.x;
@@ -307,6 +319,12 @@ __global__ void k_relu_bwd(const uint16_t* __restrict__ dy, const uint16_t* __re
 }
 
 }  // namespace
+
+hipError_t cast_rows_bf16(const float* in, int rows, int cols, uint16_t* out, int ldo, int ones, hipStream_t s) {
+  const long n = static_cast<long>(rows) * (cols + 1);
+  hipLaunchKernelGGL(k_cast_rows_bf16, dim3(stream_grid(n, 256)), dim3(256), 0, s, in, rows, cols, out, ldo, ones);
+  return hipGetLastError();
+}
 
 hipError_t cast_f32_bf16(const float* in, uint16_t* out, long n, hipStream_t s) {
   hipLaunchKernelGGL(k_cast_f32_bf16, dim3(stream_grid(n, 256, 8)), dim3(256), 0, s, in, out, n);

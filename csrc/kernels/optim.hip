@@ -51,32 +51,17 @@ __device__ __forceinline__ void update(const Hyper& h, float& p, float g, float&
   }
 }
 
+// One chunk's state for one thread: kGroups x 16 B of every state tensor, loaded before any math.
 template <int MODE>
-__global__ __launch_bounds__(kThreads) void k_optim(const OptimEntry* __restrict__ tab,
-                                                    const OptimChunk* __restrict__ chunks, int nchunks,
-                                                    const float* __restrict__ hp, int* __restrict__ step_ptr) {
-  __shared__ int s_step;
-  if (threadIdx.x == 0) s_step = step_ptr[0] + 1;  // step being taken (1-based)
-  __syncthreads();
-  Hyper h;
-  h.lr = hp[HP_LR]; h.b1 = hp[HP_BETA1]; h.b2 = hp[HP_BETA2]; h.eps = hp[HP_EPS];
-  h.wd = hp[HP_WD]; h.mom = hp[HP_MOMENTUM]; h.gscale = hp[HP_GRAD_SCALE];
-  h.step = s_step;
-  if (MODE != 0) {
-    const float bc1 = 1.f - __powf(h.b1, static_cast<float>(h.step));
-    const float bc2 = 1.f - __powf(h.b2, static_cast<float>(h.step));
-    h.step_size = h.lr / bc1;
-    h.inv_sqrt_bc2 = rsqrtf(bc2);
-  }
-  const bool use_m = MODE != 0 || h.mom != 0.f;
+struct ChunkRegs {
+  float p[kGroups][4], g[kGroups][4], m[kGroups][4], v[kGroups][4];
+  int e0[kGroups], cnt[kGroups];
+  int tensor;
 
-  for (int c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    const OptimChunk ch = chunks[c];
+  __device__ __forceinline__ void load(const OptimEntry* tab, const OptimChunk& ch, bool use_m) {
+    tensor = ch.tensor;
     const OptimEntry& te = tab[ch.tensor];
     const int end = ch.start + ch.count;
-    float p[kGroups][4], g[kGroups][4], m[kGroups][4], v[kGroups][4];
-    int e0[kGroups], cnt[kGroups];
-    // ---- loads (all issued before the math) ----
 #pragma unroll
     for (int u = 0; u < kGroups; ++u) {
       e0[u] = ch.start + (u * kThreads + threadIdx.x) * 4;
@@ -110,7 +95,10 @@ __global__ __launch_bounds__(kThreads) void k_optim(const OptimEntry* __restrict
         }
       }
     }
-    // ---- math + stores ----
+  }
+
+  __device__ __forceinline__ void finish(const Hyper& h, const OptimEntry* tab, bool use_m) {
+    const OptimEntry& te = tab[tensor];
 #pragma unroll
     for (int u = 0; u < kGroups; ++u) {
       if (cnt[u] == 0) continue;
@@ -136,6 +124,38 @@ __global__ __launch_bounds__(kThreads) void k_optim(const OptimEntry* __restrict
       }
     }
   }
+};
+
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void k_optim(const OptimEntry* __restrict__ tab,
+                                                    const OptimChunk* __restrict__ chunks, int nchunks,
+                                                    const float* __restrict__ hp, int* __restrict__ step_ptr) {
+  __shared__ int s_step;
+  if (threadIdx.x == 0) s_step = step_ptr[0] + 1;  // step being taken (1-based)
+  __syncthreads();
+  Hyper h;
+  h.lr = hp[HP_LR]; h.b1 = hp[HP_BETA1]; h.b2 = hp[HP_BETA2]; h.eps = hp[HP_EPS];
+  h.wd = hp[HP_WD]; h.mom = hp[HP_MOMENTUM]; h.gscale = hp[HP_GRAD_SCALE];
+  h.step = s_step;
+  if (MODE != 0) {
+    const float bc1 = 1.f - __powf(h.b1, static_cast<float>(h.step));
+    const float bc2 = 1.f - __powf(h.b2, static_cast<float>(h.step));
+    h.step_size = h.lr / bc1;
+    h.inv_sqrt_bc2 = rsqrtf(bc2);
+  }
+  const bool use_m = MODE != 0 || h.mom != 0.f;
+
+  // Grid-stride over chunks, software-pipelined: the next chunk's loads are issued before the current
+  // chunk's math and stores, so every block keeps a chunk of loads in flight while it writes.
+  ChunkRegs<MODE> cur, nxt;
+  int c = blockIdx.x;
+  if (c < nchunks) cur.load(tab, chunks[c], use_m);
+  for (; c < nchunks; c += gridDim.x) {
+    const int cn = c + gridDim.x;
+    if (cn < nchunks) nxt.load(tab, chunks[cn], use_m);
+    cur.finish(h, tab, use_m);
+    cur = nxt;
+  }
   // The last block to finish publishes the new step count.  Every block read the old count before its
   // arrival (the value was consumed before the barrier above), and the next launch sees the store
   // across the kernel boundary: a relaxed device-scope ticket is enough (no fence).
@@ -156,7 +176,9 @@ int optim_chunk_elems() { return kChunk; }
 hipError_t multi_tensor_optim(int mode, const OptimEntry* dev_table, const OptimChunk* dev_chunks, int nchunks,
                               const float* dev_hparams, int* dev_step, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
-  dim3 grid(static_cast<unsigned>(nchunks < 2048 ? nchunks : 2048));
+  // ~3 blocks per CU, each walking several chunks with the next one's loads in flight (pipelined loop)
+  constexpr int kMaxBlocks = 768;
+  dim3 grid(static_cast<unsigned>(nchunks < kMaxBlocks ? nchunks : kMaxBlocks));
   if (mode == 0)
     hipLaunchKernelGGL(k_optim<0>, grid, dim3(kThreads), 0, s, dev_table, dev_chunks, nchunks, dev_hparams, dev_step);
   else if (mode == 1)

@@ -64,7 +64,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-graph", action="store_true", help="run the step eagerly (no hipGraph capture)")
     ap.add_argument("--graph-steps", type=int, default=10,
                     help="consecutive training steps recorded into one hipGraph (each reads its own batch)")
-    ap.add_argument("--generic", action="store_true", help="CNN: layer-by-layer kernels instead of the fused step")
+    ap.add_argument("--generic", action="store_true", help="CNN / MLP: layer-by-layer autograd kernels instead of the fused step")
     ap.add_argument("--device", default="auto", choices=["auto", "cpu"], help="cpu: contract/plumbing check only")
     args = ap.parse_args(argv)
     if args.model == "resnet50_hybrid":
@@ -181,9 +181,16 @@ def build_data_parallel(args, ctx, batch) -> Workload:
         from ..models.cnn_fused import FusedCNN
 
         fused = FusedCNN(model)
+        fmlp = None
         ddp = DistributedDataParallel(model, overlap=False, param_order="forward", comm=comm)
     else:
-        ddp = DistributedDataParallel(model, overlap=not use_graph, comm=comm)
+        fmlp = None
+        if args.model == "mlp" and not args.generic and on_gpu:
+            # explicit launch sequence, no autograd: weight + bias gradients of each layer in ONE GEMM
+            from ..models.mlp_fused import FusedMLP
+
+            fmlp = FusedMLP(model)
+        ddp = DistributedDataParallel(model, overlap=not use_graph and fmlp is None, comm=comm)
     # world > 1 on the xGMI data plane: the fused CNN exchanges its gradients inside the slab reduction
     # (PDE_CNN_XCHG=0: all-reduce through the DDP communicator + a separate SGD launch instead)
     xgmi = getattr(comm, "xgmi", None) if fused is not None and os.environ.get("PDE_CNN_XCHG", "1") != "0" else None
@@ -198,6 +205,12 @@ def build_data_parallel(args, ctx, batch) -> Workload:
             ddp.sync_gradients()
             fused.sgd_step(opt, ddp.flat_grad)
             return loss
+        if fmlp is not None:
+            loss = fmlp.forward_backward(x, y)  # gradients written (not accumulated): no zeroing
+            if ctx.world_size > 1:
+                ddp.sync_gradients()
+            opt.step()
+            return loss
         ddp.zero_grad()
         loss = loss_fn(ddp(x), y)
         loss.backward()
@@ -210,7 +223,7 @@ def build_data_parallel(args, ctx, batch) -> Workload:
     if use_graph:
         one, group = _capture(train_step, [batch_fn(j) for j in range(max(1, args.graph_steps))],
                               args.graph_steps, ctx.rank)
-        if one is None and fused is None:  # eager fallback: overlapped buckets (hooks) again
+        if one is None and fused is None and fmlp is None:  # eager fallback: overlapped buckets (hooks) again
             ddp.remove_hooks()
             ddp = DistributedDataParallel(model, overlap=True, comm=comm)
 
@@ -220,7 +233,7 @@ def build_data_parallel(args, ctx, batch) -> Workload:
 
     routed = getattr(comm, "routed", None)
     w = Workload(step, batch * ctx.world_size, f"dp{ctx.world_size}", hipgraph=one is not None,
-                 fused_step=fused is not None, rccl_nranks=nranks,
+                 fused_step=fused is not None or fmlp is not None, rccl_nranks=nranks,
                  steps_per_graph=group.steps if group is not None else (1 if one is not None else 0),
                  allreduce=("xgmi-in-reduce-kernel" if xgmi is not None else
                             "xgmi-oneshot<=%dB+rccl" % comm.threshold) if routed is not None else
