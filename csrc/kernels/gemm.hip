@@ -122,17 +122,44 @@ __device__ __forceinline__ u16x8 load_dense_rc(const Operand& op, int rows, int 
   return v;
 }
 
+// Branch-free 16-B operand load through a buffer descriptor: an invalid slot (out of the tile's rows, past
+// K, or a conv tap in the padding) gets an out-of-range offset and the hardware returns zeros.  With no
+// divergent branches around the loads the compiler can count them (s_waitcnt vmcnt(N)), which is what
+// lets the register ring keep several K-tiles in flight (FAST loaders; operand extents < 2 GB).
+constexpr uint32_t kOob = 0x80000000u;
+__device__ __forceinline__ u16x8 bload16(__amdgpu_buffer_rsrc_t r, bool ok, long elem_off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, ok ? static_cast<uint32_t>(elem_off * 2) : kOob, 0, 0);
+  return __builtin_bit_cast(u16x8, v);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t operand_rsrc(const Operand& op, int kind, int rows, int K,
+                                                               bool kc) {
+  long elems;
+  if (kind == 0)
+    elems = kc ? static_cast<long>(rows - 1) * op.ld_r + K : static_cast<long>(K - 1) * op.ld_k + rows;
+  else
+    elems = static_cast<long>(op.g.N) * op.g.H * op.g.W * op.g.C;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(op.ptr), 0, static_cast<int>(elems * 2), 0x00020000);
+}
+
 // K-contiguous operand (kinds 0, 1, 3): each slot loads 8 consecutive K elements of one row.
-template <int BROWS, int BK>
+template <int BROWS, int BK, int KIND>  // KIND >= 0: compile-time operand kind, branch-free FAST loads
 struct KcLoader {
+  static constexpr bool FAST = KIND >= 0;
+  __device__ static __forceinline__ int kind_of(const Operand& op) {
+    if constexpr (KIND >= 0) return KIND;
+    else return op.kind;
+  }
   static constexpr int kVecs = BROWS * BK / 8;
   static constexpr int kPer = (kVecs + kThreads - 1) / kThreads;
   int k0[kPer];                 // the slot's current reduction index
   int c[kPer], kw[kPer], kh[kPer];
   int by[kPer], bx[kPer];       // kind 1: oy*s - pad, ox*s - pad;  kind 3: h + pad, w + pad
   long nb[kPer];                // image base offset in elements; -1: row out of range
+  __amdgpu_buffer_rsrc_t rsrc;  // FAST: descriptor over the operand's valid extent
 
-  __device__ __forceinline__ void init(const Operand& op, int rows, int row0, int kbeg) {
+  __device__ __forceinline__ void init(const Operand& op, int rows, int row0, int kbeg, int K) {
+    if constexpr (FAST) rsrc = operand_rsrc(op, KIND, rows, K, true);
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int v = threadIdx.x + i * kThreads;
@@ -140,7 +167,7 @@ struct KcLoader {
       k0[i] = kbeg + kv * 8;
       nb[i] = -1;
       c[i] = kw[i] = kh[i] = by[i] = bx[i] = 0;
-      if (op.kind == 0 || v >= kVecs) continue;
+      if (kind_of(op) == 0 || v >= kVecs) continue;
       const ConvGeom& g = op.g;
       c[i] = k0[i] % g.C;  // C % 8 == 0: the slot's 8 elements share (kh, kw)
       const int rs = k0[i] / g.C;
@@ -151,7 +178,7 @@ struct KcLoader {
         const int HWo = g.Ho * g.Wo;
         const int n = r / HWo, rem = r - n * HWo, oy = rem / g.Wo, ox = rem - oy * g.Wo;
         nb[i] = static_cast<long>(n) * g.H * g.W * g.C;
-        if (op.kind == 1) {
+        if (kind_of(op) == 1) {
           by[i] = oy * g.stride - g.pad;
           bx[i] = ox * g.stride - g.pad;
         } else {  // kind 3: (oy, ox) are dx coordinates; dy has dims H x W
@@ -166,7 +193,7 @@ struct KcLoader {
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       k0[i] += BK;
-      if (op.kind != 0) {
+      if (kind_of(op) != 0) {
         c[i] += BK;
         while (c[i] >= op.g.C) {
           c[i] -= op.g.C;
@@ -181,19 +208,56 @@ struct KcLoader {
 
   __device__ __forceinline__ void load(const Operand& op, int rows, int K, int row0, bool vec_ok,
                                        u16x8 (&regs)[kPer]) {
+    if constexpr (FAST) {
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int v = threadIdx.x + i * kThreads;
+        bool ok = v < kVecs && k0[i] < K;
+        long off;
+        if (kind_of(op) == 0) {
+          const int r = row0 + v / (BK / 8);
+          ok = ok && r < rows;
+          off = static_cast<long>(r) * op.ld_r + k0[i];
+        } else {
+          const ConvGeom& g = op.g;
+          int iy, ix;
+          if (kind_of(op) == 1) {
+            iy = by[i] + kh[i];
+            ix = bx[i] + kw[i];
+          } else {
+            iy = by[i] - kh[i];
+            ix = bx[i] - kw[i];
+            ok = ok && iy >= 0 && ix >= 0;
+            if (g.stride == 2) {
+              ok = ok && ((iy | ix) & 1) == 0;
+              iy >>= 1;
+              ix >>= 1;
+            } else if (g.stride > 2) {
+              ok = ok && (iy % g.stride) == 0 && (ix % g.stride) == 0;
+              iy /= g.stride;
+              ix /= g.stride;
+            }
+          }
+          ok = ok && nb[i] >= 0 && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+          off = nb[i] + (static_cast<long>(iy) * g.W + ix) * g.C + c[i];
+        }
+        regs[i] = bload16(rsrc, ok, off);
+      }
+      return;
+    }
     const uint16_t* p = static_cast<const uint16_t*>(op.ptr);
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int v = threadIdx.x + i * kThreads;
       u16x8 val = zero8();
       if (v < kVecs && k0[i] < K) {
-        if (op.kind == 0) {
+        if (kind_of(op) == 0) {
           val = load_dense_kc(op, rows, K, row0 + v / (BK / 8), k0[i], vec_ok);
         } else if (nb[i] >= 0) {
           const ConvGeom& g = op.g;
           int iy, ix;
           bool ok = true;
-          if (op.kind == 1) {
+          if (kind_of(op) == 1) {
             iy = by[i] + kh[i];
             ix = bx[i] + kw[i];
           } else {
@@ -234,16 +298,23 @@ struct KcLoader {
 // Row-contiguous operand (kinds 0 and 2): each slot loads 8 consecutive ROW elements at one k.
 // Kind 2 (weight-gradient B operand): rows are (kh, kw, c) of the conv (fixed per slot), k is the output
 // pixel (n, oy, ox), advanced incrementally.
-template <int BROWS, int BK>
+template <int BROWS, int BK, int KIND>  // KIND >= 0: compile-time operand kind, branch-free FAST loads
 struct RcLoader {
+  static constexpr bool FAST = KIND >= 0;
+  __device__ static __forceinline__ int kind_of(const Operand& op) {
+    if constexpr (KIND >= 0) return KIND;
+    else return op.kind;
+  }
   static constexpr int kVecs = BROWS * BK / 8;
   static constexpr int kPer = (kVecs + kThreads - 1) / kThreads;
   int k[kPer];
   int c0[kPer], kw[kPer], kh[kPer];
   int n[kPer], oy[kPer], ox[kPer];
   bool rok[kPer];
+  __amdgpu_buffer_rsrc_t rsrc;  // FAST: descriptor over the operand's valid extent
 
-  __device__ __forceinline__ void init(const Operand& op, int rows, int row0, int kbeg) {
+  __device__ __forceinline__ void init(const Operand& op, int rows, int row0, int kbeg, int K) {
+    if constexpr (FAST) rsrc = operand_rsrc(op, KIND, rows, K, false);
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int v = threadIdx.x + i * kThreads;
@@ -252,7 +323,7 @@ struct RcLoader {
       k[i] = kbeg + kk;
       rok[i] = v < kVecs && r0 < rows;
       c0[i] = kw[i] = kh[i] = n[i] = oy[i] = ox[i] = 0;
-      if (op.kind != 2 || !rok[i]) continue;
+      if (kind_of(op) != 2 || !rok[i]) continue;
       const ConvGeom& g = op.g;
       c0[i] = r0 % g.C;
       const int rs = r0 / g.C;
@@ -270,7 +341,7 @@ struct RcLoader {
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       k[i] += BK;
-      if (op.kind == 2) {
+      if (kind_of(op) == 2) {
         ox[i] += BK;
         while (ox[i] >= op.g.Wo) {
           ox[i] -= op.g.Wo;
@@ -285,13 +356,34 @@ struct RcLoader {
 
   __device__ __forceinline__ void load(const Operand& op, int rows, int K, int row0, bool vec_ok,
                                        u16x8 (&regs)[kPer]) {
+    if constexpr (FAST) {
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int v = threadIdx.x + i * kThreads;
+        bool ok = v < kVecs && k[i] < K;
+        long off;
+        if (kind_of(op) == 0) {
+          const int r0 = row0 + (v % (BROWS / 8)) * 8;  // FAST dense: rows % 8 == 0
+          ok = ok && r0 < rows;
+          off = static_cast<long>(k[i]) * op.ld_k + r0;
+        } else {
+          const ConvGeom& g = op.g;
+          const int iy = oy[i] * g.stride - g.pad + kh[i];
+          const int ix = ox[i] * g.stride - g.pad + kw[i];
+          ok = ok && rok[i] && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+          off = ((static_cast<long>(n[i]) * g.H + iy) * g.W + ix) * g.C + c0[i];
+        }
+        regs[i] = bload16(rsrc, ok, off);
+      }
+      return;
+    }
     const uint16_t* p = static_cast<const uint16_t*>(op.ptr);
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int v = threadIdx.x + i * kThreads;
       u16x8 val = zero8();
       if (v < kVecs && k[i] < K) {
-        if (op.kind == 0) {
+        if (kind_of(op) == 0) {
           val = load_dense_rc(op, rows, K, row0 + (v % (BROWS / 8)) * 8, k[i], vec_ok);
         } else if (rok[i]) {
           const ConvGeom& g = op.g;
@@ -319,8 +411,8 @@ struct RcLoader {
   }
 };
 
-template <int BROWS, int BK, bool KC>
-using Loader = typename std::conditional<KC, KcLoader<BROWS, BK>, RcLoader<BROWS, BK>>::type;
+template <int BROWS, int BK, bool KC, int KIND>
+using Loader = typename std::conditional<KC, KcLoader<BROWS, BK, KIND>, RcLoader<BROWS, BK, KIND>>::type;
 
 __device__ __forceinline__ float apply_epi(float v, int epi, int m, int n, const GemmArgs& a) {
   if ((epi & EPI_BIAS) && n < a.nbias) v += a.bias[n];
@@ -472,7 +564,7 @@ __device__ __forceinline__ void write_slab_and_reduce(const GemmArgs& args, cons
   if (threadIdx.x == 0) __hip_atomic_store(args.tickets + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC, int STAGES>
+template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC, int AKIND, int BKIND, int STAGES>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles_m, int tiles_n,
                                                         int k_per_split, int a_vec, int b_vec) {
   static_assert(WM * WN == 4, "4 waves per block");
@@ -516,13 +608,16 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  using LA = Loader<BM, BK, AKC>;
-  using LB = Loader<BN, BK, BKC>;
+  using LA = Loader<BM, BK, AKC, AKIND>;
+  using LB = Loader<BN, BK, BKC, BKIND>;
+  // FAST (both kinds compile-time): every load is issued unconditionally (past the end it is masked to
+  // zeros with no memory traffic), so the waits before the LDS stores are counted, not vmcnt(0)
+  constexpr bool FASTK = AKIND >= 0 && BKIND >= 0;
   LA la;
   LB lb;
   const bool avec = a_vec != 0, bvec = b_vec != 0;
-  la.init(args.a, args.M, m0, kbeg);
-  lb.init(args.b, args.N, n0, kbeg);
+  la.init(args.a, args.M, m0, kbeg, args.K);
+  lb.init(args.b, args.N, n0, kbeg, args.K);
   // Register ring of S K-tiles: the loads of tile t + S are issued at iteration t (before its MFMAs), so
   // S tiles of global round trips are in flight; tile t + 1 is written to the other LDS buffer after the
   // MFMAs of tile t.  Reduction bound for the loaders is kend (zero fill past the split's end).
@@ -533,7 +628,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles
     lb.load(args.b, args.N, kend, n0, bvec, rb[0]);
 #pragma unroll
     for (int u = 1; u < S; ++u) {
-      if (u < nk) {
+      if (FASTK || u < nk) {
         la.advance(args.a);
         lb.advance(args.b);
         la.load(args.a, args.M, kend, m0, avec, ra[u]);
@@ -549,13 +644,13 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles
 #pragma unroll
     for (int u = 0; u < S; ++u) {
       const int t = kt + u;
+      if (FASTK || t + S < nk) {  // refill this slot (its tile went to LDS one iteration ago)
+        la.advance(args.a);
+        lb.advance(args.b);
+        la.load(args.a, args.M, kend, m0, avec, ra[u]);
+        lb.load(args.b, args.N, kend, n0, bvec, rb[u]);
+      }
       if (t < nk) {
-        if (t + S < nk) {  // refill this slot (its tile went to LDS one iteration ago)
-          la.advance(args.a);
-          lb.advance(args.b);
-          la.load(args.a, args.M, kend, m0, avec, ra[u]);
-          lb.load(args.b, args.N, kend, n0, bvec, rb[u]);
-        }
         const uint16_t* As = smem + (t & 1) * (LDS_A + LDS_B);
         const uint16_t* Bs = As + LDS_A;
         bf16x8 af[FM], bfr[FN];
@@ -800,6 +895,40 @@ int* split_tickets(int tiles, hipStream_t s) {
   return t;
 }
 
+// FAST instantiations: (A kind, B kind) pairs that occur -- K-contiguous A: dense, im2col, dgrad gather;
+// row-contiguous A: dense (dy^T); K-contiguous B: dense weights; row-contiguous B: dense, im2col^T.
+constexpr int kFastStages = 3;
+template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC, int AK, int BKN>
+void launch_fast1(dim3 grid, hipStream_t s, const GemmArgs& ka, int tm, int tn, int kps, int av, int bv) {
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AKC, BKC, AK, BKN, kFastStages>), grid, dim3(kThreads), 0, s,
+                     ka, tm, tn, kps, av, bv);
+}
+template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC, int AK>
+bool launch_fast_b(dim3 grid, hipStream_t s, const GemmArgs& ka, int tm, int tn, int kps, int av, int bv) {
+  const int bk = ka.b.kind;
+  if (bk == 0) {
+    launch_fast1<BM, BN, BK, WM, WN, AKC, BKC, AK, 0>(grid, s, ka, tm, tn, kps, av, bv);
+    return true;
+  }
+  if constexpr (!BKC) {
+    if (bk == 2) {
+      launch_fast1<BM, BN, BK, WM, WN, AKC, BKC, AK, 2>(grid, s, ka, tm, tn, kps, av, bv);
+      return true;
+    }
+  }
+  return false;
+}
+template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC>
+bool launch_fast(dim3 grid, hipStream_t s, const GemmArgs& ka, int tm, int tn, int kps, int av, int bv) {
+  const int ak = ka.a.kind;
+  if (ak == 0) return launch_fast_b<BM, BN, BK, WM, WN, AKC, BKC, 0>(grid, s, ka, tm, tn, kps, av, bv);
+  if constexpr (AKC) {
+    if (ak == 1) return launch_fast_b<BM, BN, BK, WM, WN, AKC, BKC, 1>(grid, s, ka, tm, tn, kps, av, bv);
+    if (ak == 3) return launch_fast_b<BM, BN, BK, WM, WN, AKC, BKC, 3>(grid, s, ka, tm, tn, kps, av, bv);
+  }
+  return false;
+}
+
 template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC>
 hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
   const int tm = ceil_div(a.M, BM), tn = ceil_div(a.N, BN);
@@ -819,12 +948,32 @@ hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
   const bool in_kernel = splitk > 1 && splitk <= kMaxInKernelSplits &&
                          static_cast<long>(splitk) * a.M * a.N * 4 < (1L << 31);  // buffer offsets
   ka.tickets = in_kernel ? split_tickets(tm * tn, s) : nullptr;
-  // register-ring depth (K-tiles in flight).  Depth 4 on the small tiles measured neutral on the MLP and
-  // ResNet-50 (r2g: 0.302 vs 0.296 ms, 5.89 vs 5.80 ms) and adds spills to the 128x128 tile, so 1: the
-  // loads of tile t+1 overlap the MFMAs of tile t.
-  constexpr int STAGES = 1;
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AKC, BKC, STAGES>), grid, dim3(kThreads), 0, s, ka, tm, tn,
-                     kps, av, bv);
+  // FAST: both operands loaded branch-free through buffer descriptors (gathers always; dense operands when
+  // every 16-B group is whole and aligned, extents < 2 GB) with compile-time operand kinds -- then the loads
+  // are counted and a register ring of kFastStages K-tiles stays in flight.  The generic loaders' divergent scalar fallbacks make the
+  // compiler wait for every load (vmcnt(0)) before each LDS store, so a deeper ring buys nothing there
+  // (measured r2g), and they run at depth 1.
+  auto fast_ok = [&](const Operand& o, bool kc, int rows) {
+    long elems;
+    if (o.kind != 0) {
+      elems = static_cast<long>(o.g.N) * o.g.H * o.g.W * o.g.C;
+    } else {
+      if (!vec_ok(o, kc)) return false;
+      if (kc ? (a.K % 8 != 0) : (rows % 8 != 0)) return false;
+      elems = kc ? static_cast<long>(rows - 1) * o.ld_r + a.K : static_cast<long>(a.K - 1) * o.ld_k + rows;
+    }
+    return elems * 2 < (1L << 31) - 16;
+  };
+  static const bool generic_only = std::getenv("PDE_GEMM_GENERIC") != nullptr;  // A/B switch
+  constexpr bool kFastTile = BM * BN < 128 * 128;  // the 128x128 tile already spills: generic only
+  const bool fast = kFastTile && !generic_only && fast_ok(a.a, AKC, a.M) && fast_ok(a.b, BKC, a.N);
+  bool launched = false;
+  if constexpr (kFastTile) {
+    if (fast) launched = launch_fast<BM, BN, BK, WM, WN, AKC, BKC>(grid, s, ka, tm, tn, kps, av, bv);
+  }
+  if (!launched)
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AKC, BKC, -1, -1, 1>), grid, dim3(kThreads), 0, s, ka, tm,
+                       tn, kps, av, bv);
   if (splitk > 1 && ka.tickets == nullptr) {
     const long total = static_cast<long>(a.M) * a.N;
     if (a.N % 4 == 0 && total / 4 < (1L << 30) && (reinterpret_cast<uintptr_t>(a.workspace) & 15) == 0) {
