@@ -565,7 +565,7 @@ __device__ __forceinline__ void write_slab_and_reduce(const GemmArgs& args, cons
 }
 
 template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC, int AKIND, int BKIND, int STAGES>
-__global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs args, int tiles_m, int tiles_n,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu((BM * BN >= 128 * 128) ? 1 : 4))) void gemm_kernel(GemmArgs args, int tiles_m, int tiles_n,
                                                         int k_per_split, int a_vec, int b_vec) {
   static_assert(WM * WN == 4, "4 waves per block");
   static_assert(BK == 32, "swz_chunk assumes 4 16-byte K-chunks (64 B) per LDS row");
@@ -897,7 +897,7 @@ int* split_tickets(int tiles, hipStream_t s) {
 
 // FAST instantiations: (A kind, B kind) pairs that occur -- K-contiguous A: dense, im2col, dgrad gather;
 // row-contiguous A: dense (dy^T); K-contiguous B: dense weights; row-contiguous B: dense, im2col^T.
-constexpr int kFastStages = 3;
+constexpr int kFastStages = 4;
 template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC, int AK, int BKN>
 void launch_fast1(dim3 grid, hipStream_t s, const GemmArgs& ka, int tm, int tn, int kps, int av, int bv) {
   hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AKC, BKC, AK, BKN, kFastStages>), grid, dim3(kThreads), 0, s,
