@@ -135,8 +135,8 @@ __device__ __forceinline__ u16x8 bload16(__amdgpu_buffer_rsrc_t r, bool ok, long
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t operand_rsrc(const Operand& op, int kind, int rows, int K,
                                                                bool kc) {
   long elems;
-  if (kind == 0)
-    elems = kc ? static_cast<long>(rows - 1) * op.ld_r + K : static_cast<long>(K - 1) * op.ld_k + rows;
+  if (kind == 0)  // row-contiguous: whole 8-row groups (rows past the end are padding, host-checked)
+    elems = kc ? static_cast<long>(rows - 1) * op.ld_r + K : static_cast<long>(K - 1) * op.ld_k + (rows + 7) / 8 * 8;
   else
     elems = static_cast<long>(op.g.N) * op.g.H * op.g.W * op.g.C;
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(op.ptr), 0, static_cast<int>(elems * 2), 0x00020000);
@@ -363,7 +363,7 @@ struct RcLoader {
         bool ok = v < kVecs && k[i] < K;
         long off;
         if (kind_of(op) == 0) {
-          const int r0 = row0 + (v % (BROWS / 8)) * 8;  // FAST dense: rows % 8 == 0
+          const int r0 = row0 + (v % (BROWS / 8)) * 8;  // FAST dense: the 8-row group is allocated
           ok = ok && r0 < rows;
           off = static_cast<long>(k[i]) * op.ld_k + r0;
         } else {
@@ -959,8 +959,11 @@ hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
       elems = static_cast<long>(o.g.N) * o.g.H * o.g.W * o.g.C;
     } else {
       if (!vec_ok(o, kc)) return false;
-      if (kc ? (a.K % 8 != 0) : (rows % 8 != 0)) return false;
-      elems = kc ? static_cast<long>(rows - 1) * o.ld_r + a.K : static_cast<long>(a.K - 1) * o.ld_k + rows;
+      // K-contiguous: whole 8-element K groups; row-contiguous: whole 8-row groups, or a row pitch that
+      // holds the padded group (the loads past `rows` only feed outputs beyond M / N, never stored)
+      if (kc ? (a.K % 8 != 0) : (rows % 8 != 0 && o.ld_k < (rows + 7) / 8 * 8)) return false;
+      elems = kc ? static_cast<long>(rows - 1) * o.ld_r + a.K
+                 : static_cast<long>(a.K - 1) * o.ld_k + (rows + 7) / 8 * 8;
     }
     return elems * 2 < (1L << 31) - 16;
   };
