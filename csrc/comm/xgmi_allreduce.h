@@ -39,8 +39,9 @@ class XgmiAllreduce {
 
   std::string ipc_handle() const;                   // this rank's exported allocation
   void open(const std::vector<std::string>& handles);  // all ranks' handles, in rank order
-  // dst[i] = scale * sum_r src_r[i]; fp32; src may alias dst; n * 4 <= max_bytes; stream-ordered
-  void allreduce(const float* src, float* dst, int64_t n, float scale, hipStream_t s);
+  // dst[i] = scale * sum_r src_r[i]; fp32; src may alias dst; n * 4 <= max_bytes; stream-ordered.
+  // wire_bf16: the exchanged copies are bf16 (cast fused into the staging; fp32 sum and output)
+  void allreduce(const float* src, float* dst, int64_t n, float scale, hipStream_t s, bool wire_bf16 = false);
   XgmiView view() const;  // device view for kernels that fold the exchange in (xgmi_device.h)
   int error();   // 0, or 1 when some workgroup timed out waiting for a peer (synchronises the device)
   void close();

@@ -15,13 +15,21 @@ namespace {
 
 constexpr int kThreads = 256;
 
+__device__ __forceinline__ uint16_t bf16_bits(float f) {  // round to nearest even
+  const uint32_t u = __float_as_uint(f);
+  return static_cast<uint16_t>((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bf16_float(uint16_t b) { return __uint_as_float(static_cast<uint32_t>(b) << 16); }
+
 void hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("xgmi allreduce: ") + what + ": " + hipGetErrorString(e));
 }
 
 // grid = one workgroup per chunk of `chunk` elements (the same grid on every rank for the same n: the
 // per-workgroup epochs must advance in step across ranks).
-template <int NR, bool VEC>
+// WIRE_BF16: the staged chunk is bf16 (cast fused into the staging store, half the bytes over xGMI); the
+// rank-order sum is fp32 either way.
+template <int NR, bool VEC, bool WIRE_BF16>
 __global__ __launch_bounds__(kThreads) void k_xgmi_oneshot(const float* src, float* dst, int64_t n, float scale,
                                                             XgmiView xv, int64_t chunk) {
   __shared__ uint32_t s_epoch;
@@ -34,7 +42,18 @@ __global__ __launch_bounds__(kThreads) void k_xgmi_oneshot(const float* src, flo
   float* mine = xgmi_slot(xv, xv.rank, epoch);
 
   // 1. stage this workgroup's chunk into my exported slot
-  if (VEC) {
+  if constexpr (WIRE_BF16) {
+    uint16_t* mine16 = reinterpret_cast<uint16_t*>(mine);
+    if (VEC) {
+      for (int64_t i = lo + 4 * tid; i < hi; i += 4 * kThreads) {
+        const float4 v = *reinterpret_cast<const float4*>(src + i);
+        *reinterpret_cast<ushort4*>(mine16 + i) = make_ushort4(bf16_bits(v.x), bf16_bits(v.y), bf16_bits(v.z),
+                                                               bf16_bits(v.w));
+      }
+    } else {
+      for (int64_t i = lo + tid; i < hi; i += kThreads) mine16[i] = bf16_bits(src[i]);
+    }
+  } else if (VEC) {
     for (int64_t i = lo + 4 * tid; i < hi; i += 4 * kThreads)
       *reinterpret_cast<float4*>(mine + i) = *reinterpret_cast<const float4*>(src + i);
   } else {
@@ -43,6 +62,36 @@ __global__ __launch_bounds__(kThreads) void k_xgmi_oneshot(const float* src, flo
   // 2.-3. publish my chunk to every peer and wait for theirs
   if (xgmi_publish_and_wait(xv, b, epoch, &s_fail)) {
     // 4. sum the chunk over all ranks' slots in rank order (bit-identical on every rank)
+    if constexpr (WIRE_BF16) {
+      const uint16_t* s16[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) s16[r] = reinterpret_cast<const uint16_t*>(xgmi_slot(xv, r, epoch));
+      if (VEC) {
+        for (int64_t i = lo + 4 * tid; i < hi; i += 4 * kThreads) {
+          ushort4 u[NR];
+#pragma unroll
+          for (int r = 0; r < NR; ++r) u[r] = *reinterpret_cast<const ushort4*>(s16[r] + i);
+          float4 acc = make_float4(bf16_float(u[0].x), bf16_float(u[0].y), bf16_float(u[0].z), bf16_float(u[0].w));
+#pragma unroll
+          for (int r = 1; r < NR; ++r) {
+            acc.x += bf16_float(u[r].x);
+            acc.y += bf16_float(u[r].y);
+            acc.z += bf16_float(u[r].z);
+            acc.w += bf16_float(u[r].w);
+          }
+          *reinterpret_cast<float4*>(dst + i) = make_float4(acc.x * scale, acc.y * scale, acc.z * scale, acc.w * scale);
+        }
+      } else {
+        for (int64_t i = lo + tid; i < hi; i += kThreads) {
+          float acc = bf16_float(s16[0][i]);
+#pragma unroll
+          for (int r = 1; r < NR; ++r) acc += bf16_float(s16[r][i]);
+          dst[i] = acc * scale;
+        }
+      }
+      xgmi_finish(xv, b, epoch);
+      return;
+    }
     const float* slots[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) slots[r] = xgmi_slot(xv, r, epoch);
@@ -87,13 +136,21 @@ __global__ void k_scale(const float* src, float* dst, int64_t n, float scale) {
     dst[i] = src[i] * scale;
 }
 
-template <int NR>
-void launch(bool vec, dim3 grid, hipStream_t s, const float* src, float* dst, int64_t n, float scale,
-            const XgmiView& v, int64_t chunk) {
+template <int NR, bool W>
+void launch_w(bool vec, dim3 grid, hipStream_t s, const float* src, float* dst, int64_t n, float scale,
+              const XgmiView& v, int64_t chunk) {
   if (vec)
-    hipLaunchKernelGGL((k_xgmi_oneshot<NR, true>), grid, dim3(kThreads), 0, s, src, dst, n, scale, v, chunk);
+    hipLaunchKernelGGL((k_xgmi_oneshot<NR, true, W>), grid, dim3(kThreads), 0, s, src, dst, n, scale, v, chunk);
   else
-    hipLaunchKernelGGL((k_xgmi_oneshot<NR, false>), grid, dim3(kThreads), 0, s, src, dst, n, scale, v, chunk);
+    hipLaunchKernelGGL((k_xgmi_oneshot<NR, false, W>), grid, dim3(kThreads), 0, s, src, dst, n, scale, v, chunk);
+}
+template <int NR>
+void launch(bool vec, bool wire_bf16, dim3 grid, hipStream_t s, const float* src, float* dst, int64_t n, float scale,
+            const XgmiView& v, int64_t chunk) {
+  if (wire_bf16)
+    launch_w<NR, true>(vec, grid, s, src, dst, n, scale, v, chunk);
+  else
+    launch_w<NR, false>(vec, grid, s, src, dst, n, scale, v, chunk);
 }
 
 }  // namespace
@@ -148,7 +205,8 @@ void XgmiAllreduce::open(const std::vector<std::string>& handles) {
   opened_ = true;
 }
 
-void XgmiAllreduce::allreduce(const float* src, float* dst, int64_t n, float scale, hipStream_t s) {
+void XgmiAllreduce::allreduce(const float* src, float* dst, int64_t n, float scale, hipStream_t s,
+                              bool wire_bf16) {
   if (n <= 0) return;
   if (n * 4 > max_bytes_) throw std::invalid_argument("xgmi allreduce: bucket exceeds max_bytes");
   if (size_ == 1) {
@@ -167,13 +225,13 @@ void XgmiAllreduce::allreduce(const float* src, float* dst, int64_t n, float sca
                    (reinterpret_cast<uintptr_t>(dst) % 16 == 0);
   const dim3 grid(static_cast<unsigned>((n + chunk - 1) / chunk));
   switch (size_) {
-    case 2: launch<2>(vec, grid, s, src, dst, n, scale, v, chunk); break;
-    case 3: launch<3>(vec, grid, s, src, dst, n, scale, v, chunk); break;
-    case 4: launch<4>(vec, grid, s, src, dst, n, scale, v, chunk); break;
-    case 5: launch<5>(vec, grid, s, src, dst, n, scale, v, chunk); break;
-    case 6: launch<6>(vec, grid, s, src, dst, n, scale, v, chunk); break;
-    case 7: launch<7>(vec, grid, s, src, dst, n, scale, v, chunk); break;
-    default: launch<8>(vec, grid, s, src, dst, n, scale, v, chunk); break;
+    case 2: launch<2>(vec, wire_bf16, grid, s, src, dst, n, scale, v, chunk); break;
+    case 3: launch<3>(vec, wire_bf16, grid, s, src, dst, n, scale, v, chunk); break;
+    case 4: launch<4>(vec, wire_bf16, grid, s, src, dst, n, scale, v, chunk); break;
+    case 5: launch<5>(vec, wire_bf16, grid, s, src, dst, n, scale, v, chunk); break;
+    case 6: launch<6>(vec, wire_bf16, grid, s, src, dst, n, scale, v, chunk); break;
+    case 7: launch<7>(vec, wire_bf16, grid, s, src, dst, n, scale, v, chunk); break;
+    default: launch<8>(vec, wire_bf16, grid, s, src, dst, n, scale, v, chunk); break;
   }
   hip_check(hipGetLastError(), "oneshot launch");
   ++calls_;

@@ -55,11 +55,15 @@ class _CpuWork:
 
 
 class _GpuWork:
+    """An RCCL bucket all-reduce on the current stream.  ``wait()`` does not block the host: everything
+    that consumes the bucket is stream-ordered behind the collective.  Liveness is checked once per step
+    instead (:meth:`RoundComm.step_done`, one step behind) and at commit points (:meth:`RoundComm.drain`)."""
+
     def __init__(self, comm, event):
         self.comm, self.event = comm, event
 
     def wait(self):
-        self.comm.wait_event(self.event)
+        return True
 
 
 class RoundComm:
@@ -81,6 +85,7 @@ class RoundComm:
             self.rccl = C.RcclComm()
             self.rccl.init(uid, rank, size, device.index, True)
         self.supports_avg = self.rccl is not None
+        self._steps = []  # end-of-step events not yet checked on the host (GPU data plane)
 
     # -- data plane ------------------------------------------------------------------------------
     def allreduce_async(self, t: torch.Tensor, avg: bool = False):
@@ -108,6 +113,23 @@ class RoundComm:
         except RuntimeError as exc:
             raise PeerFailure(str(exc)) from exc
         return t
+
+    def step_done(self, lag: int = 1):
+        """Mark the end of a training step.  The host checks the step ``lag`` steps back (its collectives
+        finished, or a failure surfaces as :class:`PeerFailure`), so it never stalls on the step it just
+        enqueued -- one liveness wait per step instead of one host sync per bucket."""
+        if self.rccl is None:
+            return
+        ev = torch.cuda.Event()
+        ev.record()
+        self._steps.append(ev)
+        while len(self._steps) > lag:
+            self.wait_event(self._steps.pop(0))
+
+    def drain(self):
+        """Commit point: every enqueued step has finished (or a failure surfaces)."""
+        while self._steps:
+            self.wait_event(self._steps.pop(0))
 
     def wait_event(self, ev):
         """Host-side liveness wait for an RCCL collective: returns when it finished; aborts the
@@ -153,6 +175,12 @@ class RoundComm:
             self.rccl.abort()
 
     def close(self, abort: bool = False):
+        if self.rccl is not None and not abort:
+            try:
+                self.drain()
+            except PeerFailure:
+                abort = True
+        self._steps = []
         if self.rccl is not None:
             if abort:
                 self.rccl.abort()
@@ -273,15 +301,18 @@ def run_elastic(args):
                     loss = criterion(ddp(source), targets)
                     loss.backward()
                     optimizer.step()
+                    comm.step_done()
                     fault.maybe_fault(step, rank)
                     step += 1
                     pos["seen"] += per_step
                     since += 1
                     if since % commit_every == 0:
+                        comm.drain()
                         commit.save()
                         if comm.agree(rdzv.hosts_updated()):
                             raise MembershipChanged()
                 pos["epoch"], pos["seen"] = epoch + 1, 0
+                comm.drain()
                 commit.save()
                 _test(model, test_data, dev, comm, log)
                 if rank == 0 and epoch % args.save_every == 0:

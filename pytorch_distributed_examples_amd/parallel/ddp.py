@@ -14,7 +14,8 @@ Mirrors ``torch.nn.parallel.DistributedDataParallel`` as used by the reference
 * bucket sizes follow :mod:`.xgmi` (sized for 7 point-to-point links, not DDP's 25 MiB default);
 * ``overlap=False`` skips the hooks and reduces every bucket in :meth:`sync_gradients` -- the form used
   inside a captured hipGraph step;
-* ``grad_dtype=torch.bfloat16`` halves the bytes on the wire (bucket cast -> all-reduce -> cast back);
+* ``grad_dtype=torch.bfloat16`` halves the bytes on the wire (bucket cast -> all-reduce -> cast back; on
+  the xGMI data plane the casts are fused into the one-shot all-reduce kernel and DDP copies nothing);
 * ``comm=`` swaps the c10d group for another communicator (``size``, ``supports_avg``,
   ``allreduce_async(t, avg) -> work``, ``broadcast_(t, src)``), e.g. the per-round RCCL communicator of
   :mod:`..elastic.rewire` that is aborted and rebuilt in-process on a membership change.
@@ -140,6 +141,11 @@ class DistributedDataParallel(nn.Module):
         return hook
 
     def _launch(self, b: int):
+        if self._bf16_bufs is not None and getattr(self.comm, "supports_bf16_wire", False):
+            # the communicator casts on the wire itself (fused into the xGMI one-shot kernel): no copies here
+            work = self.comm.allreduce_async(self._bucket_flat[b], avg=self._use_avg, wire_bf16=True)
+            self._works.append((-1 - b, work))
+            return
         if self._bf16_bufs is not None:
             buf = self._bf16_bufs[b]
             buf.copy_(self._bucket_flat[b])
@@ -160,7 +166,7 @@ class DistributedDataParallel(nn.Module):
     def _complete(self):
         for b, work in self._works:
             work.wait()
-            if self._bf16_bufs is not None:
+            if self._bf16_bufs is not None and b >= 0:  # b < 0: reduced in place with a bf16 wire
                 self._bucket_flat[b].copy_(self._bf16_bufs[b])
         if not self._use_avg and self.world > 1:
             self.flat_grad.mul_(1.0 / self.world)

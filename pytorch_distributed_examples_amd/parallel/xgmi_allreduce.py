@@ -52,8 +52,10 @@ class XgmiAllreduce:
     def max_bytes(self) -> int:
         return self.impl.max_bytes
 
-    def allreduce_(self, t: torch.Tensor, avg: bool = False) -> torch.Tensor:
-        self.impl.allreduce_(t, 1.0 / self.size if avg else 1.0)
+    def allreduce_(self, t: torch.Tensor, avg: bool = False, wire_bf16: bool = False) -> torch.Tensor:
+        """In-place fp32 all-reduce; ``wire_bf16``: peers exchange bf16 copies (cast fused into the staging,
+        half the xGMI bytes), the sum and the result stay fp32."""
+        self.impl.allreduce_(t, 1.0 / self.size if avg else 1.0, wire_bf16)
         return t
 
     def view(self) -> list:
@@ -88,15 +90,23 @@ class RoutedComm:
         self.rccl, self.xgmi = rccl, xgmi
         self.size, self.rank = rccl.size, rccl.rank
         self.supports_avg = True
+        self.supports_bf16_wire = True
         self.threshold = min(int(threshold_bytes), xgmi.max_bytes)
         self.routed = {"xgmi": 0, "rccl": 0}
 
-    def allreduce_async(self, t: torch.Tensor, avg: bool = False):
+    def allreduce_async(self, t: torch.Tensor, avg: bool = False, wire_bf16: bool = False):
+        """``wire_bf16`` (fp32 ``t``): reduce bf16 copies -- fused into the one-shot kernel on the xGMI path;
+        on RCCL a cast into a bf16 scratch, a bf16 all-reduce, and the cast back."""
         if t.dtype == torch.float32 and t.numel() * 4 <= self.threshold:
-            self.xgmi.allreduce_(t, avg)
+            self.xgmi.allreduce_(t, avg, wire_bf16)
             self.routed["xgmi"] += 1
             return _Done()
         self.routed["rccl"] += 1
+        if wire_bf16 and t.dtype == torch.float32:
+            w = t.to(torch.bfloat16)
+            self.rccl.allreduce_async(w, avg)
+            t.copy_(w)  # stream-ordered behind the collective
+            return _Done()
         return self.rccl.allreduce_async(t, avg)
 
     def allreduce_(self, t: torch.Tensor, avg: bool = False) -> torch.Tensor:

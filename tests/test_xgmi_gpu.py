@@ -37,6 +37,13 @@ for n in (1, 7, 1000, 21840, 262144, 1 << 20):
     xs = [torch.empty(n) for _ in range(N)]
     dist.all_gather(xs, x.cpu())
     assert all(torch.equal(v, xs[0]) for v in xs), n
+# bf16 wire: the staged copies are bf16 (cast fused), the rank-order sum fp32
+for n in (7, 1000, 21840, 1 << 20):
+    x = rank_data(r, n, n + 7).to(dev)
+    xa.allreduce_(x, wire_bf16=True)
+    torch.cuda.synchronize()
+    ref = sum(rank_data(k, n, n + 7).bfloat16().float() for k in range(N))
+    assert torch.allclose(x.cpu(), ref, rtol=1e-6, atol=1e-6), n
 # unaligned views (scalar path) and averaging
 big = rank_data(r, 1001, 5).to(dev)
 v = big[1:]
@@ -92,6 +99,13 @@ ddp.sync_gradients()
 torch.cuda.synchronize()
 assert torch.allclose(ddp.flat_grad, torch.full_like(ddp.flat_grad, (N - 1) / 2)), ddp.flat_grad[:4]
 assert comm.routed["xgmi"] >= 1
+# bf16-wire DDP buckets: reduced in place by the one-shot kernel, no cast copies in DDP
+ddp16 = DistributedDataParallel(torch.nn.Linear(16, 8).to(dev), overlap=False, comm=comm, grad_dtype=torch.bfloat16)
+ddp16.zero_grad()
+ddp16.flat_grad.fill_(float(r))
+ddp16.sync_gradients()
+torch.cuda.synchronize()
+assert torch.allclose(ddp16.flat_grad, torch.full_like(ddp16.flat_grad, (N - 1) / 2)), ddp16.flat_grad[:4]
 xa.check()
 # fused CNN: the gradient exchange inside the slab-reduction kernel (+ fused SGD) against local gradients
 # all-reduced over gloo + the separate SGD launch; both replicas start from the same weights.
