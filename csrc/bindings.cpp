@@ -718,7 +718,7 @@ Tensor embbag_bwd(const Tensor& dy, const Tensor& idx, const Tensor& off, int64_
   const int B = off.size(0), D = dy.size(1);
   Tensor dw = at::zeros({num, D}, dy.options());
   check(pde::embbag_bwd(dy.data_ptr<float>(), idx.data_ptr<int64_t>(), off.data_ptr<int64_t>(), B, idx.numel(), D,
-                        dw.data_ptr<float>(), cur_stream()),
+                        dw.data_ptr<float>(), num, cur_stream()),
         "embbag_bwd");
   return dw;
 }

@@ -199,7 +199,9 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
 hipError_t cnn_sgd_fused(float* params, const float* grads, const float* hp, void* frag, hipStream_t s,
                          int* step = nullptr);  // step: the optimiser's device step counter (+1 per call)
 
+// dw (+)= EmbeddingBag-sum gradient; deterministic (row-owner scan) for tables with rows * L <= 2^26 and
+// D <= 256, fp32 atomics beyond
 hipError_t embbag_bwd(const float* dy, const int64_t* idx, const int64_t* off, int B, long L, int D, float* dw,
-                      hipStream_t s);
+                      long rows, hipStream_t s);
 
 }  // namespace pde

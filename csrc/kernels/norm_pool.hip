@@ -514,13 +514,26 @@ __global__ void k_dropout_bwd(const uint16_t* __restrict__ dy, const uint8_t* __
 
 // ---------------------------------------------------------------------------------------------
 // EmbeddingBag (mode=sum): one wave per bag, lanes over the embedding dim.
+// EmbeddingBag (sum mode), one wave per bag.  For D <= 32 the wave splits into G = 64 / Dp lane groups
+// (Dp = D rounded up to a power of two): group g sums indices s+g, s+g+G, ... and the groups are combined
+// with a fixed xor-shuffle tree, so every lane works and the result is deterministic.
 __global__ void k_embbag_fwd(const float* __restrict__ w, const int64_t* __restrict__ idx,
-                             const int64_t* __restrict__ off, int B, long L, int D, float* __restrict__ out) {
+                             const int64_t* __restrict__ off, int B, long L, int D, int Dp,
+                             float* __restrict__ out) {
   const int bag = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (bag >= B) return;
+  if (bag >= B) return;  // wave-uniform
   const long s = off[bag];
   const long e = bag + 1 < B ? off[bag + 1] : L;
+  if (Dp <= 32) {
+    const int G = 64 / Dp, g = lane / Dp, d = lane % Dp;
+    float acc = 0.f;
+    if (d < D)
+      for (long j = s + g; j < e; j += G) acc += w[idx[j] * D + d];
+    for (int m = Dp; m < 64; m <<= 1) acc += __shfl_xor(acc, m);
+    if (g == 0 && d < D) out[static_cast<long>(bag) * D + d] = acc;
+    return;
+  }
   for (int d = lane; d < D; d += 64) {
     float acc = 0.f;
     for (long j = s; j < e; ++j) acc += w[idx[j] * D + d];
@@ -528,9 +541,44 @@ __global__ void k_embbag_fwd(const float* __restrict__ w, const int64_t* __restr
   }
 }
 
-// dW[idx[j], :] += dy[bag(j), :]  (fp32 atomics; the table is tiny and rows are 64 B)
-__global__ void k_embbag_bwd(const float* __restrict__ dy, const int64_t* __restrict__ idx,
-                             const int64_t* __restrict__ off, int B, long L, int D, float* __restrict__ dw) {
+// dW[r, :] += sum over positions j with idx[j] == r (increasing j) of dy[bag(j), :] -- deterministic: one
+// wave owns table row r, ballots the matching positions 64 at a time and adds them in index order (the bag
+// of a position by binary search over the offsets).  O(rows x L) scanning: used for parameter-server-sized
+// tables (host picks k_embbag_bwd_atomic beyond that).
+__global__ void k_embbag_bwd_det(const float* __restrict__ dy, const int64_t* __restrict__ idx,
+                                 const int64_t* __restrict__ off, int B, long L, int D, long rows,
+                                 float* __restrict__ dw) {
+  const long row = static_cast<long>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;  // wave-uniform
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};  // D <= 256: lane d, d + 64, d + 128, d + 192
+  for (long base = 0; base < L; base += 64) {
+    const long j = base + lane;
+    unsigned long long m = __ballot(j < L && idx[j] == row);
+    while (m) {
+      const int bit = __ffsll(static_cast<long long>(m)) - 1;
+      m &= m - 1;
+      const long jj = base + bit;
+      int lo = 0, hi = B - 1;  // last bag with off[bag] <= jj
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= jj) lo = mid;
+        else hi = mid - 1;
+      }
+      const float* src = dy + static_cast<long>(lo) * D;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (lane + 64 * q < D) acc[q] += src[lane + 64 * q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (lane + 64 * q < D) dw[row * D + lane + 64 * q] += acc[q];
+}
+
+// Large tables: dW[idx[j], :] += dy[bag(j), :] with fp32 atomics (order-dependent rounding).
+__global__ void k_embbag_bwd_atomic(const float* __restrict__ dy, const int64_t* __restrict__ idx,
+                                    const int64_t* __restrict__ off, int B, long L, int D, float* __restrict__ dw) {
   const int bag = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (bag >= B) return;
@@ -646,12 +694,19 @@ hipError_t dropout_bwd(const uint16_t* dy, const uint8_t* mask, uint16_t* dx, lo
 }
 hipError_t embbag_fwd(const float* w, const int64_t* idx, const int64_t* off, int B, long L, int D, float* out,
                       hipStream_t s) {
-  hipLaunchKernelGGL(k_embbag_fwd, dim3(ceil_div(B, 4)), dim3(256), 0, s, w, idx, off, B, L, D, out);
+  int Dp = 1;
+  while (Dp < D) Dp <<= 1;
+  hipLaunchKernelGGL(k_embbag_fwd, dim3(ceil_div(B, 4)), dim3(256), 0, s, w, idx, off, B, L, D, Dp, out);
   return hipGetLastError();
 }
 hipError_t embbag_bwd(const float* dy, const int64_t* idx, const int64_t* off, int B, long L, int D, float* dw,
-                      hipStream_t s) {
-  hipLaunchKernelGGL(k_embbag_bwd, dim3(ceil_div(B, 4)), dim3(256), 0, s, dy, idx, off, B, L, D, dw);
+                      long rows, hipStream_t s) {
+  if (D <= 256 && rows > 0 && rows * L <= (1L << 26)) {  // deterministic row-owner scan
+    hipLaunchKernelGGL(k_embbag_bwd_det, dim3(static_cast<unsigned>((rows + 3) / 4)), dim3(256), 0, s, dy, idx, off,
+                       B, L, D, rows, dw);
+  } else {
+    hipLaunchKernelGGL(k_embbag_bwd_atomic, dim3(ceil_div(B, 4)), dim3(256), 0, s, dy, idx, off, B, L, D, dw);
+  }
   return hipGetLastError();
 }
 

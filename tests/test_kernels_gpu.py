@@ -227,11 +227,16 @@ def test_dropout(gpu):
     assert torch.equal(x.grad.float() != 0, keep)
 
 
-def test_embedding_bag(gpu):
+@pytest.mark.parametrize("rows,D,L", [(100, 16, 40), (100, 16, 3000), (37, 7, 500), (64, 100, 700),
+                                       (300000, 16, 400)])
+def test_embedding_bag(gpu, rows, D, L):
+    """Lane-grouped forward (D <= 32), wide rows, and both backward paths: the deterministic row-owner
+    scan (bit-identical across runs) and the atomic path for large tables (rows * L > 2^26)."""
     torch.manual_seed(5)
-    w = torch.randn(100, 16, device=gpu, requires_grad=True)
-    idx = torch.randint(0, 100, (40,), device=gpu)
-    off = torch.tensor([0, 3, 9, 20, 31], device=gpu)
+    w = torch.randn(rows, D, device=gpu, requires_grad=True)
+    idx = torch.randint(0, min(rows, 100), (L,), device=gpu)  # repeated rows: accumulation order matters
+    off = torch.sort(torch.randint(0, L, (8,), device=gpu)).values
+    off[0] = 0
     y = OF.embedding_bag_sum(w, idx, off)
     w2 = w.detach().clone().requires_grad_()
     yr = F.embedding_bag(idx, w2, off, mode="sum")
@@ -240,6 +245,11 @@ def test_embedding_bag(gpu):
     y.backward(g)
     yr.backward(g)
     assert rel_err(w.grad, w2.grad) < 1e-5
+    if rows * L <= (1 << 26):
+        g1 = w.grad.clone()
+        w.grad = None
+        OF.embedding_bag_sum(w, idx, off).backward(g)
+        assert torch.equal(w.grad, g1)
 
 
 @pytest.mark.parametrize("kind", ["sgd", "adam", "adamw"])
