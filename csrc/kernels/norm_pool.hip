@@ -5,6 +5,9 @@
 // deterministic; running-stat update with unbiased variance) -> fused normalize(+residual)(+ReLU).
 // Backward = partials of (sum dy, sum dy*xhat) with the ReLU mask applied on the fly -> finalize ->
 // fused dx (+ residual grad).  Every pass streams 16 B (8 channels) per lane.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.cuh"
 #include "pde_kernels.h"
 
@@ -269,6 +272,212 @@ __global__ void k_bn_bwd_apply(const uint16_t* __restrict__ dy, const uint16_t* 
     }
     reinterpret_cast<u16x8*>(dx)[i] = o;
     if (dres) reinterpret_cast<u16x8*>(dres)[i] = orr;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Two-kernel BatchNorm: the statistics pass finalizes in the same launch.  Grid = (row chunks) x (64-channel
+// groups); every block stores its partials write-through (sc1), drains, and takes a per-channel-group ticket;
+// the block that draws the last ticket acquires (agent scope) and combines that group's partials in fixed
+// row-chunk order (deterministic) -- cdna_hip_programming.md §6 Guideline 16, recipe R1 in counter form.
+// Saves the separate finalize launch in both directions (6 -> 4 kernels per BatchNorm layer).
+constexpr int kBnCG = 64;  // channels per group: 8 channel-vector lanes x 8 channels
+
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Block-collective tail shared by both passes: partial (s1, s2)[64] -> ws, ticket, and on the last arrival
+// the per-channel totals over all row chunks in fixed order into tot1/tot2 (LDS).  Returns true on the block
+// that finalizes.
+__device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], const float (&s2)[8], float* ws, int C,
+                                                       int* ticket, float (*red)[32][kBnCG + 1], float* tot1,
+                                                       float* tot2, int* s_last) {
+  const int tid = threadIdx.x, tv = tid & 7, tr = tid >> 3;
+  const int rb = blockIdx.x, nrb = gridDim.x, cbase = blockIdx.y * kBnCG;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][tr][tv * 8 + j] = s1[j];
+    red[1][tr][tv * 8 + j] = s2[j];
+  }
+  __syncthreads();
+  if (tid < 2 * kBnCG) {
+    const int which = tid / kBnCG, ch = tid % kBnCG;
+    float v = 0.f;
+    for (int r = 0; r < 32; ++r) v += red[which][r][ch];
+    if (cbase + ch < C) st_sc1(ws + (static_cast<long>(rb) * 2 + which) * C + cbase + ch, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) *s_last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nrb - 1;
+  __syncthreads();
+  if (!*s_last) return false;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // 4 lanes per (which, channel) over the row chunks, combined in lane order
+  {
+    const int q = tid >> 6, ch = tid & 63;
+    float a1 = 0.f, a2 = 0.f;
+    if (cbase + ch < C) {
+      // 8 chunks per trip with all 16 loads issued before the adds (the tail is latency-bound)
+      int b = q;
+      for (; b + 28 < nrb; b += 32) {
+        float u1[8], u2[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          u1[k] = ws[(static_cast<long>(b + 4 * k) * 2) * C + cbase + ch];
+          u2[k] = ws[(static_cast<long>(b + 4 * k) * 2 + 1) * C + cbase + ch];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          a1 += u1[k];
+          a2 += u2[k];
+        }
+      }
+      for (; b < nrb; b += 4) {
+        a1 += ws[(static_cast<long>(b) * 2) * C + cbase + ch];
+        a2 += ws[(static_cast<long>(b) * 2 + 1) * C + cbase + ch];
+      }
+    }
+    red[0][q][ch] = a1;
+    red[1][q][ch] = a2;
+  }
+  __syncthreads();
+  if (tid < kBnCG) {
+    tot1[tid] = ((red[0][0][tid] + red[0][1][tid]) + red[0][2][tid]) + red[0][3][tid];
+    tot2[tid] = ((red[1][0][tid] + red[1][1][tid]) + red[1][2][tid]) + red[1][3][tid];
+  }
+  if (tid == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+  __syncthreads();
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_bn_stats_fin(const uint16_t* __restrict__ x, int P, int C, int rpb,
+                                                      float* __restrict__ ws, int* __restrict__ tickets,
+                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      float eps, float momentum, float* __restrict__ running_mean,
+                                                      float* __restrict__ running_var, float* __restrict__ save_mean,
+                                                      float* __restrict__ save_invstd, float* __restrict__ scale,
+                                                      float* __restrict__ shift) {
+  __shared__ float red[2][32][kBnCG + 1];
+  __shared__ float tot1[kBnCG], tot2[kBnCG];
+  __shared__ int s_last;
+  const int tid = threadIdx.x, tv = tid & 7, tr = tid >> 3;
+  const int c0 = blockIdx.y * kBnCG + tv * 8;
+  const bool cok = c0 < C;
+  float s1[8], s2[8], piv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = piv[j] = 0.f;
+  if (cok) {
+    load8(x + c0, piv);  // shift by row 0 (same pivot in every block)
+    const int r1 = min(P, (blockIdx.x + 1) * rpb);
+    int r = blockIdx.x * rpb + tr;
+    for (; r + 3 * 32 < r1; r += 4 * 32) {
+      u16x8 u[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) u[q] = *reinterpret_cast<const u16x8*>(x + static_cast<long>(r + 32 * q) * C + c0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float d = bf2f(u[q][j]) - piv[j]; s1[j] += d; s2[j] += d * d; }
+    }
+    for (; r < r1; r += 32) {
+      float v[8];
+      load8(x + static_cast<long>(r) * C + c0, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = v[j] - piv[j]; s1[j] += d; s2[j] += d * d; }
+    }
+  }
+  if (!bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last)) return;
+  if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
+    const int c = blockIdx.y * kBnCG + tid;
+    const double n = static_cast<double>(P);
+    const double mean_s = static_cast<double>(tot1[tid]) / n;
+    double var = static_cast<double>(tot2[tid]) / n - mean_s * mean_s;
+    if (var < 0.0) var = 0.0;
+    const float mean = static_cast<float>(mean_s) + bf2f(x[c]);
+    const float invstd = rsqrtf(static_cast<float>(var) + eps);
+    save_mean[c] = mean;
+    save_invstd[c] = invstd;
+    const float g = gamma ? gamma[c] : 1.f;
+    const float b = beta ? beta[c] : 0.f;
+    scale[c] = g * invstd;
+    shift[c] = b - mean * g * invstd;
+    if (running_mean) {
+      const float unbiased = P > 1 ? static_cast<float>(var * n / (n - 1.0)) : static_cast<float>(var);
+      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bn_bwd_reduce_fin(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const uint16_t* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ invstd, int P, int C, int rpb, int relu,
+    float* __restrict__ ws, int* __restrict__ tickets, const float* __restrict__ gamma, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, int accum, float* __restrict__ coef) {
+  __shared__ float red[2][32][kBnCG + 1];
+  __shared__ float tot1[kBnCG], tot2[kBnCG];
+  __shared__ int s_last;
+  const int tid = threadIdx.x, tv = tid & 7, tr = tid >> 3;
+  const int c0 = blockIdx.y * kBnCG + tv * 8;
+  const bool cok = c0 < C;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  if (cok) {
+    float mu[8], is[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j]; }
+    const int r1 = min(P, (blockIdx.x + 1) * rpb);
+    int r = blockIdx.x * rpb + tr;
+    for (; r + 32 < r1; r += 2 * 32) {
+      u16x8 ud[2], ux[2], uy[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const long off = static_cast<long>(r + 32 * q) * C + c0;
+        ud[q] = *reinterpret_cast<const u16x8*>(dy + off);
+        ux[q] = *reinterpret_cast<const u16x8*>(x + off);
+        if (relu) uy[q] = *reinterpret_cast<const u16x8*>(y + off);
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float d = bf2f(ud[q][j]);
+          if (relu && !(bf2f(uy[q][j]) > 0.f)) d = 0.f;
+          s1[j] += d;
+          s2[j] += d * (bf2f(ux[q][j]) - mu[j]) * is[j];
+        }
+    }
+    for (; r < r1; r += 32) {
+      const long off = static_cast<long>(r) * C + c0;
+      float d[8], xv[8];
+      load8(dy + off, d);
+      load8(x + off, xv);
+      if (relu) {
+        float yv[8];
+        load8(y + off, yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s1[j] += d[j]; s2[j] += d[j] * (xv[j] - mu[j]) * is[j]; }
+    }
+  }
+  if (!bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last)) return;
+  if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
+    const int c = blockIdx.y * kBnCG + tid;
+    const float t1 = tot1[tid], t2 = tot2[tid];
+    if (dgamma) dgamma[c] = accum ? dgamma[c] + t2 : t2;
+    if (dbeta) dbeta[c] = accum ? dbeta[c] + t1 : t1;
+    const float a = (gamma ? gamma[c] : 1.f) * invstd[c];
+    coef[c] = a;
+    coef[C + c] = a * t1 / static_cast<float>(P);
+    coef[2 * C + c] = a * t2 / static_cast<float>(P);
   }
 }
 
@@ -605,9 +814,49 @@ int bn_blocks(int P, int C, int& rows_per_block) {
 
 }  // namespace
 
+// Fused-finalize grid: row chunks x 64-channel groups, ~512 blocks, >= 32 rows per chunk, <= 64 chunks (r2i: 128 chunks
+// made the finalizing tail 0.14 ms/step slower; 64 chunks measure level with the 3-pass form at 106 fewer
+// launches per step)
+// (the finalizing block reads chunks x 2 x 64 partials).
+int bn_fin_grid(int P, int C, int& rpb) {
+  const int ncg = (C + kBnCG - 1) / kBnCG;
+  int nrb = std::max(1, std::min(64, 512 / ncg));
+  nrb = std::min(nrb, std::max(1, P / 32));
+  rpb = ceil_div(P, nrb);
+  return ceil_div(P, rpb);
+}
+
+// Per-channel-group arrival counters: one zeroed array per device, handed out in a rolling window (each
+// launch leaves its counters at 0).  Allocated on the first call outside a graph capture; until then (or
+// with PDE_BN_3PASS=1) BatchNorm uses the separate finalize kernels.
+int* bn_tickets(int n, hipStream_t s) {
+  constexpr int kSlots = 1 << 20;
+  static int* base[64] = {};
+  static int next[64] = {};
+  static const bool off = std::getenv("PDE_BN_3PASS") != nullptr;
+  if (off || n > kSlots) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (base[dev] == nullptr) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+    void* p = nullptr;
+    if (hipMalloc(&p, sizeof(int) * kSlots) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, sizeof(int) * kSlots) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(p);
+      return nullptr;
+    }
+    base[dev] = static_cast<int*>(p);
+  }
+  if (next[dev] + n > kSlots) next[dev] = 0;
+  int* t = base[dev] + next[dev];
+  next[dev] += n;
+  return t;
+}
+
 int bn_workspace_blocks(int P, int C) {
   int rpb;
-  return bn_blocks(P, C, rpb);
+  return std::max(bn_blocks(P, C, rpb), bn_fin_grid(P, C, rpb));
 }
 
 hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, const float* beta, float eps,
@@ -615,10 +864,18 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
                         float* save_invstd, float* scale_shift, float* ws, const uint16_t* res, int relu,
                         uint16_t* y, hipStream_t s) {
   int rpb;
-  const int nblk = bn_blocks(P, C, rpb);
-  hipLaunchKernelGGL(k_bn_stats, dim3(nblk), dim3(256), 0, s, x, P, C, rpb, ws);
-  hipLaunchKernelGGL(k_bn_finalize, dim3(ceil_div(C, 4)), dim3(256), 0, s, x, ws, nblk, P, C, gamma, beta, eps,
-                     momentum, running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C);
+  int* tk = bn_tickets(ceil_div(C, kBnCG), s);
+  if (tk != nullptr) {
+    const int nrb = bn_fin_grid(P, C, rpb);
+    hipLaunchKernelGGL(k_bn_stats_fin, dim3(nrb, ceil_div(C, kBnCG)), dim3(256), 0, s, x, P, C, rpb, ws, tk, gamma,
+                       beta, eps, momentum, running_mean, running_var, save_mean, save_invstd, scale_shift,
+                       scale_shift + C);
+  } else {
+    const int nblk = bn_blocks(P, C, rpb);
+    hipLaunchKernelGGL(k_bn_stats, dim3(nblk), dim3(256), 0, s, x, P, C, rpb, ws);
+    hipLaunchKernelGGL(k_bn_finalize, dim3(ceil_div(C, 4)), dim3(256), 0, s, x, ws, nblk, P, C, gamma, beta, eps,
+                       momentum, running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C);
+  }
   const long nvec = static_cast<long>(P) * C / 8;
   hipLaunchKernelGGL(k_bn_apply, dim3(stream_grid(nvec, 256)), dim3(256), 0, s, x, scale_shift, scale_shift + C,
                      res, y, nvec, C, relu);
@@ -637,10 +894,17 @@ hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, cons
                   const float* gamma, int P, int C, int relu, float* dgamma, float* dbeta, int accum_params, float* ws,
                   float* coef, uint16_t* dx, uint16_t* dres, hipStream_t s) {
   int rpb;
-  const int nblk = bn_blocks(P, C, rpb);
-  hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(nblk), dim3(256), 0, s, dy, x, y, mean, invstd, P, C, rpb, relu, ws);
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(ceil_div(C, 4)), dim3(256), 0, s, ws, nblk, P, C, gamma, invstd,
-                     dgamma, dbeta, accum_params, coef);
+  int* tk = bn_tickets(ceil_div(C, kBnCG), s);
+  if (tk != nullptr) {
+    const int nrb = bn_fin_grid(P, C, rpb);
+    hipLaunchKernelGGL(k_bn_bwd_reduce_fin, dim3(nrb, ceil_div(C, kBnCG)), dim3(256), 0, s, dy, x, y, mean, invstd,
+                       P, C, rpb, relu, ws, tk, gamma, dgamma, dbeta, accum_params, coef);
+  } else {
+    const int nblk = bn_blocks(P, C, rpb);
+    hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(nblk), dim3(256), 0, s, dy, x, y, mean, invstd, P, C, rpb, relu, ws);
+    hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(ceil_div(C, 4)), dim3(256), 0, s, ws, nblk, P, C, gamma, invstd,
+                       dgamma, dbeta, accum_params, coef);
+  }
   const long nvec = static_cast<long>(P) * C / 8;
   hipLaunchKernelGGL(k_bn_bwd_apply, dim3(stream_grid(nvec, 256)), dim3(256), 0, s, dy, x, y, mean, invstd, coef,
                      nvec, C, relu, dx, dres);
