@@ -85,6 +85,16 @@ int split_cap(const pde::GemmArgs& a) {
   return cap < 1 ? 1 : static_cast<int>(cap);
 }
 
+// GEMM pairing (gemm_pair_begin / gemm_pair_end): while a pair is being collected, run_gemm records the
+// GEMM (with its workspace) instead of launching it; gemm_pair_end launches the two recorded GEMMs as one
+// pde::gemm_bf16_pair.  Used for a layer's dgrad + wgrad (ops/functional.py, models/mlp_fused.py).
+struct PendingGemm {
+  pde::GemmArgs args;
+  Tensor ws;
+};
+thread_local bool g_collect = false;
+thread_local std::vector<PendingGemm> g_pending;
+
 void run_gemm(pde::GemmArgs& a, const Tensor& like, int max_split) {
   Tensor ws;
   a.workspace = nullptr;
@@ -95,7 +105,30 @@ void run_gemm(pde::GemmArgs& a, const Tensor& like, int max_split) {
     a.workspace = ws.data_ptr<float>();
     a.splitk = max_split;
   }
+  if (g_collect) {
+    TORCH_CHECK(g_pending.size() < 2, "gemm pair: more than two GEMMs collected");
+    g_pending.push_back({a, ws});
+    return;
+  }
   check(pde::gemm_bf16(a, cur_stream()), "gemm");
+}
+
+void gemm_pair_begin() {
+  TORCH_CHECK(!g_collect && g_pending.empty(), "gemm_pair_begin: a pair is already being collected");
+  g_collect = true;
+}
+
+// Launch what was collected (2 GEMMs: one paired launch; fewer: ordinary launches).  abort=true drops it.
+void gemm_pair_end(bool abort) {
+  g_collect = false;
+  std::vector<PendingGemm> q;
+  q.swap(g_pending);
+  if (abort) return;
+  if (q.size() == 2) {
+    check(pde::gemm_bf16_pair(q[0].args, q[1].args, cur_stream()), "gemm_pair");
+  } else {
+    for (auto& p : q) check(pde::gemm_bf16(p.args, cur_stream()), "gemm");
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -855,6 +888,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_fwd_out", &linear_fwd_out);
   m.def("linear_dgrad_out", &linear_dgrad_out);
   m.def("linear_wgrad_bias", &linear_wgrad_bias);
+  m.def("gemm_pair_begin", &gemm_pair_begin);
+  m.def("gemm_pair_end", &gemm_pair_end, py::arg("abort") = false);
   m.def("cast_rows_ones", &cast_rows_ones);
   m.def("ce_bwd", &ce_bwd);
   m.def("log_softmax_fwd", &log_softmax_fwd);

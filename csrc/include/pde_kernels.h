@@ -67,6 +67,10 @@ struct GemmArgs {
 };
 
 hipError_t gemm_bf16(const GemmArgs& args, hipStream_t stream);
+// Two independent GEMMs (a layer's dgrad and wgrad) in one launch when both run on the 64x64 FAST tile, their
+// split-K slab reductions in one more; otherwise two ordinary gemm_bf16 launches (problem 0 first).
+hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t stream);
+bool gemm_pair_enabled();
 
 // ---------------------------------------------------------------------------------------------
 // Elementwise / layout (elementwise.hip)

@@ -459,10 +459,9 @@ constexpr int SMEM_BYTES_OF() { return 2 * (BM + BN) * 32 * 2; }  // gemm_kernel
 template <int BM, int BN, int FM, int FN, int WTM, int WTN>
 __device__ __forceinline__ void write_slab_and_reduce(const GemmArgs& args, const f32x4 (&acc)[FM][FN],
                                                       uint16_t* smem, int m0, int n0, int kz, int wm, int wn,
-                                                      int lane) {
+                                                      int lane, int splits, int slot) {
   float* ws = args.workspace;
   const long MN = static_cast<long>(args.M) * args.N;
-  const int splits = gridDim.z;
   // one buffer descriptor over all slabs (host checks splits*M*N*4 < 2^31)
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(ws, 0, static_cast<int>(splits * MN * 4), 0x00020000);
   constexpr int SC1 = 16;  // aux bit: write-through store / L1-bypassing load
@@ -508,7 +507,7 @@ __device__ __forceinline__ void write_slab_and_reduce(const GemmArgs& args, cons
   __syncthreads();
   int* last = reinterpret_cast<int*>(smem);  // staging reads are behind the barrier: LDS is free
   if (threadIdx.x == 0) {
-    const int t = __hip_atomic_fetch_add(args.tickets + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int t = __hip_atomic_fetch_add(args.tickets + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last[0] = t == splits - 1;
   }
   __syncthreads();
@@ -561,23 +560,25 @@ __device__ __forceinline__ void write_slab_and_reduce(const GemmArgs& args, cons
       store_out(apply_epi(v, args.epi, m, n, args), args.epi, m, n, args);
     }
   }
-  if (threadIdx.x == 0) __hip_atomic_store(args.tickets + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store(args.tickets + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// One output tile (and K slice kz of nz) of a GEMM: the body of gemm_kernel, also run by gemm_pair_kernel for
+// either of its two problems.  `orig` is the block's tile slot within its problem, `smem` the block's LDS
+// (SMEM_BYTES_OF<BM, BN>() bytes).
 template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC, int AKIND, int BKIND, int STAGES>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu((BM * BN >= 128 * 128) ? 1 : 4))) void gemm_kernel(GemmArgs args, int tiles_m, int tiles_n,
-                                                        int k_per_split, int a_vec, int b_vec) {
+__device__ __forceinline__ void gemm_tile(const GemmArgs& args, int tiles_m, int tiles_n, int k_per_split, int a_vec,
+                                          int b_vec, const int orig, const int kz, const int nz, uint16_t* smem) {
   static_assert(WM * WN == 4, "4 waves per block");
   static_assert(BK == 32, "swz_chunk assumes 4 16-byte K-chunks (64 B) per LDS row");
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int LDS_A = BM * BK, LDS_B = BN * BK;
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (LDS_A + LDS_B)];
-  static_assert(sizeof(smem) == SMEM_BYTES_OF<BM, BN>(), "split-K staging size");
+  constexpr int SMEM_BYTES = SMEM_BYTES_OF<BM, BN>();
+  static_assert(2 * (LDS_A + LDS_B) * 2 == SMEM_BYTES, "split-K staging size");
 
   // XCD-aware tile id remap (bijective; see cdna_hip_programming.md §5 "XCD swizzle").
   const int ntiles = tiles_m * tiles_n;
-  const int orig = blockIdx.x;
   int tile = orig;
   if (ntiles > 8) {
     const int q = ntiles / 8, r = ntiles % 8, xcd = orig % 8;
@@ -593,7 +594,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu((BM * 
   const int tn = (tile % group_sz) / gm;
 
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kz = blockIdx.z;
   const int kbeg = kz * k_per_split;
   const int kend = min(args.K, kbeg + k_per_split);
   const int nk = (kend - kbeg + BK - 1) / BK;
@@ -690,13 +690,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu((BM * 
   // Epilogue. C/D map of 16x16x32: col = lane & 15, row = (lane >> 4) * 4 + reg.  A lane's outputs are 4
   // rows of one column, so direct stores are 2-byte (bf16) / 4-byte (slab) scatters.  Where the tile fits
   // the (now idle) LDS, it is staged there and written back as 16-byte row vectors instead.
-  const bool split = gridDim.z > 1;
+  const bool split = nz > 1;
   float* ws = args.workspace;
   if (split && args.tickets != nullptr) {
-    write_slab_and_reduce<BM, BN, FM, FN, WTM, WTN>(args, acc, smem, m0, n0, kz, wm, wn, lane);
+    write_slab_and_reduce<BM, BN, FM, FN, WTM, WTN>(args, acc, smem, m0, n0, kz, wm, wn, lane, nz, orig);
     return;
   }
-  constexpr int SMEM_BYTES = static_cast<int>(sizeof(smem));
   const bool vec_bf16 = !split && !(args.epi & (EPI_OIHW | EPI_OUT_F32)) && args.N % 8 == 0 && args.ldo % 8 == 0 &&
                         (reinterpret_cast<uintptr_t>(args.out) & 15) == 0;
   const bool vec_f32 = split && args.N % 4 == 0 && (reinterpret_cast<uintptr_t>(ws) & 15) == 0;
@@ -810,6 +809,41 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu((BM * 
   }
 }
 
+template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC, int AKIND, int BKIND, int STAGES>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu((BM * BN >= 128 * 128) ? 1 : 4))) void gemm_kernel(GemmArgs args, int tiles_m, int tiles_n,
+                                                        int k_per_split, int a_vec, int b_vec) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM_BYTES_OF<BM, BN>() / 2];
+  gemm_tile<BM, BN, BK, WM, WN, AKC, BKC, AKIND, BKIND, STAGES>(args, tiles_m, tiles_n, k_per_split, a_vec, b_vec,
+                                                                blockIdx.x, blockIdx.z, gridDim.z, smem);
+}
+
+// Two independent GEMMs in ONE launch (a layer's data gradient and weight gradient): blocks [0, nb0) run
+// problem 0's (tile, K-slice) grid, the rest problem 1's.  Both use the 64x64 FAST configuration; the
+// operand kinds are per problem.  At the reference's small per-GPU batches each backward GEMM alone leaves
+// CUs idle (ResNet-50 layer4: 512 output rows; the MLP: 128) and pays its own launch boundary; the pair
+// fills the chip with both grids and costs one boundary.  (A second HIP stream does not help here: a
+// branched hipGraph is launched node by node on ROCm, measured 12 % slower for ResNet-50 -- ops/streams.py.)
+struct PairDims {
+  int tm[2], tn[2], kps[2], av[2], bv[2], nz[2];
+};
+template <bool AKC0, bool BKC0, int AK0, int BK0, bool AKC1, bool BKC1, int AK1, int BK1>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void gemm_pair_kernel(
+    GemmArgs a0, GemmArgs a1, PairDims d) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM_BYTES_OF<64, 64>() / 2];
+  const int t0 = d.tm[0] * d.tn[0];
+  const int nb0 = t0 * d.nz[0];
+  int b = blockIdx.x;
+  if (b < nb0) {
+    gemm_tile<64, 64, 32, 2, 2, AKC0, BKC0, AK0, BK0, 4>(a0, d.tm[0], d.tn[0], d.kps[0], d.av[0], d.bv[0], b % t0,
+                                                         b / t0, d.nz[0], smem);
+  } else {
+    b -= nb0;
+    const int t1 = d.tm[1] * d.tn[1];
+    gemm_tile<64, 64, 32, 2, 2, AKC1, BKC1, AK1, BK1, 4>(a1, d.tm[1], d.tn[1], d.kps[1], d.av[1], d.bv[1], b % t1,
+                                                         b / t1, d.nz[1], smem);
+  }
+}
+
 // Split-K slab reduction, scalar form (N % 4 != 0).
 __global__ void gemm_splitk_reduce(GemmArgs args, int splits) {
   const long total = static_cast<long>(args.M) * args.N;
@@ -828,12 +862,12 @@ __global__ void gemm_splitk_reduce(GemmArgs args, int splits) {
 // output with LANES slab-lanes each (thread = column + COLS x lane); partials meet in LDS in a fixed
 // order (deterministic), then the epilogue runs on the 4 outputs of each column.
 template <int LANES>
-__global__ __launch_bounds__(256) void gemm_splitk_reduce4(GemmArgs args, int splits) {
+__device__ __forceinline__ void splitk_reduce4_block(const GemmArgs& args, int splits, int block) {
   constexpr int COLS = 256 / LANES;
   __shared__ f32x4 part[LANES][COLS];
   const int total4 = args.M * (args.N / 4);
   const int col = threadIdx.x % COLS, sl = threadIdx.x / COLS;
-  const int c4 = blockIdx.x * COLS + col;
+  const int c4 = block * COLS + col;
   const f32x4* w4 = reinterpret_cast<const f32x4*>(args.workspace);
   f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
   if (c4 < total4) {
@@ -859,6 +893,18 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce4(GemmArgs args, int sp
 #pragma unroll
     for (int j = 0; j < 4; ++j) store_out(apply_epi(v[j], args.epi, m, n + j, args), args.epi, m, n + j, args);
   }
+}
+template <int LANES>
+__global__ __launch_bounds__(256) void gemm_splitk_reduce4(GemmArgs args, int splits) {
+  splitk_reduce4_block<LANES>(args, splits, blockIdx.x);
+}
+// the slab reductions of a GEMM pair in one launch (blocks [0, nb0): problem 0)
+template <int L0, int L1>
+__global__ __launch_bounds__(256) void gemm_splitk_reduce4_pair(GemmArgs a0, int s0, int nb0, GemmArgs a1, int s1) {
+  if (static_cast<int>(blockIdx.x) < nb0)
+    splitk_reduce4_block<L0>(a0, s0, blockIdx.x);
+  else
+    splitk_reduce4_block<L1>(a1, s1, blockIdx.x - nb0);
 }
 
 // Per-tile arrival counters for the in-kernel split-K reduction: one zeroed device array per GPU, handed
@@ -929,19 +975,62 @@ bool launch_fast(dim3 grid, hipStream_t s, const GemmArgs& ka, int tm, int tn, i
   return false;
 }
 
+// Slab reduction of a split-K GEMM: the vector form's slab-lane count follows the split count.
+bool reduce_vec_ok(const GemmArgs& a) {
+  const long total = static_cast<long>(a.M) * a.N;
+  return a.N % 4 == 0 && total / 4 < (1L << 30) && (reinterpret_cast<uintptr_t>(a.workspace) & 15) == 0;
+}
+int reduce_lanes(int splitk) { return splitk <= 2 ? 1 : (splitk <= 16 ? 4 : 16); }
+void launch_reduce(const GemmArgs& a, int splitk, hipStream_t s) {
+  const long total = static_cast<long>(a.M) * a.N;
+  if (reduce_vec_ok(a)) {
+    const long t4 = total / 4;
+    const int lanes = reduce_lanes(splitk);
+    if (lanes == 1)
+      hipLaunchKernelGGL(gemm_splitk_reduce4<1>, dim3(ceil_div(t4, 256)), dim3(256), 0, s, a, splitk);
+    else if (lanes == 4)
+      hipLaunchKernelGGL(gemm_splitk_reduce4<4>, dim3(ceil_div(t4, 64)), dim3(256), 0, s, a, splitk);
+    else
+      hipLaunchKernelGGL(gemm_splitk_reduce4<16>, dim3(ceil_div(t4, 16)), dim3(256), 0, s, a, splitk);
+  } else {
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(stream_grid(total, 256)), dim3(256), 0, s, a, splitk);
+  }
+}
+
+// Vector (16 B) loads are legal when the contiguous dimension and the other stride keep every 8-element
+// group 16-byte aligned.
+int vec_ok(const Operand& o, bool kc) {
+  if (o.kind != 0) return 1;
+  if (kc) return (o.ld_k == 1 && o.ld_r % 8 == 0 && (reinterpret_cast<uintptr_t>(o.ptr) & 15) == 0) ? 1 : 0;
+  return (o.ld_r == 1 && o.ld_k % 8 == 0 && (reinterpret_cast<uintptr_t>(o.ptr) & 15) == 0) ? 1 : 0;
+}
+// FAST: the operand can be loaded branch-free through a buffer descriptor (gathers always; dense operands
+// when every 16-B group is whole and aligned, extents < 2 GB).
+bool fast_ok(const GemmArgs& a, const Operand& o, bool kc, int rows) {
+  long elems;
+  if (o.kind != 0) {
+    elems = static_cast<long>(o.g.N) * o.g.H * o.g.W * o.g.C;
+  } else {
+    if (!vec_ok(o, kc)) return false;
+    // K-contiguous: whole 8-element K groups; row-contiguous: whole 8-row groups, or a row pitch that
+    // holds the padded group (the loads past `rows` only feed outputs beyond M / N, never stored)
+    if (kc ? (a.K % 8 != 0) : (rows % 8 != 0 && o.ld_k < (rows + 7) / 8 * 8)) return false;
+    elems = kc ? static_cast<long>(rows - 1) * o.ld_r + a.K
+               : static_cast<long>(a.K - 1) * o.ld_k + (rows + 7) / 8 * 8;
+  }
+  return elems * 2 < (1L << 31) - 16;
+}
+bool generic_only() {
+  static const bool g = std::getenv("PDE_GEMM_GENERIC") != nullptr;  // A/B switch
+  return g;
+}
+
 template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC>
 hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
   const int tm = ceil_div(a.M, BM), tn = ceil_div(a.N, BN);
   int kps = ceil_div(a.K, splitk);
   kps = ceil_div(kps, BK) * BK;
   splitk = ceil_div(a.K, kps);
-  // Vector (16 B) loads are legal when the contiguous dimension and the other stride keep
-  // every 8-element group 16-byte aligned.
-  auto vec_ok = [](const Operand& o, bool kc) {
-    if (o.kind != 0) return 1;
-    if (kc) return (o.ld_k == 1 && o.ld_r % 8 == 0 && (reinterpret_cast<uintptr_t>(o.ptr) & 15) == 0) ? 1 : 0;
-    return (o.ld_r == 1 && o.ld_k % 8 == 0 && (reinterpret_cast<uintptr_t>(o.ptr) & 15) == 0) ? 1 : 0;
-  };
   const int av = vec_ok(a.a, AKC), bv = vec_ok(a.b, BKC);
   dim3 grid(tm * tn, 1, splitk);
   GemmArgs ka = a;
@@ -953,23 +1042,8 @@ hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
   // are counted and a register ring of kFastStages K-tiles stays in flight.  The generic loaders' divergent scalar fallbacks make the
   // compiler wait for every load (vmcnt(0)) before each LDS store, so a deeper ring buys nothing there
   // (measured r2g), and they run at depth 1.
-  auto fast_ok = [&](const Operand& o, bool kc, int rows) {
-    long elems;
-    if (o.kind != 0) {
-      elems = static_cast<long>(o.g.N) * o.g.H * o.g.W * o.g.C;
-    } else {
-      if (!vec_ok(o, kc)) return false;
-      // K-contiguous: whole 8-element K groups; row-contiguous: whole 8-row groups, or a row pitch that
-      // holds the padded group (the loads past `rows` only feed outputs beyond M / N, never stored)
-      if (kc ? (a.K % 8 != 0) : (rows % 8 != 0 && o.ld_k < (rows + 7) / 8 * 8)) return false;
-      elems = kc ? static_cast<long>(rows - 1) * o.ld_r + a.K
-                 : static_cast<long>(a.K - 1) * o.ld_k + (rows + 7) / 8 * 8;
-    }
-    return elems * 2 < (1L << 31) - 16;
-  };
-  static const bool generic_only = std::getenv("PDE_GEMM_GENERIC") != nullptr;  // A/B switch
   constexpr bool kFastTile = BM * BN < 128 * 128;  // the 128x128 tile already spills: generic only
-  const bool fast = kFastTile && !generic_only && fast_ok(a.a, AKC, a.M) && fast_ok(a.b, BKC, a.N);
+  const bool fast = kFastTile && !generic_only() && fast_ok(a, a.a, AKC, a.M) && fast_ok(a, a.b, BKC, a.N);
   bool launched = false;
   if constexpr (kFastTile) {
     if (fast) launched = launch_fast<BM, BN, BK, WM, WN, AKC, BKC>(grid, s, ka, tm, tn, kps, av, bv);
@@ -977,20 +1051,7 @@ hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
   if (!launched)
     hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AKC, BKC, -1, -1, 1>), grid, dim3(kThreads), 0, s, ka, tm,
                        tn, kps, av, bv);
-  if (splitk > 1 && ka.tickets == nullptr) {
-    const long total = static_cast<long>(a.M) * a.N;
-    if (a.N % 4 == 0 && total / 4 < (1L << 30) && (reinterpret_cast<uintptr_t>(a.workspace) & 15) == 0) {
-      const long t4 = total / 4;
-      if (splitk <= 2)
-        hipLaunchKernelGGL(gemm_splitk_reduce4<1>, dim3(ceil_div(t4, 256)), dim3(256), 0, s, a, splitk);
-      else if (splitk <= 16)
-        hipLaunchKernelGGL(gemm_splitk_reduce4<4>, dim3(ceil_div(t4, 64)), dim3(256), 0, s, a, splitk);
-      else
-        hipLaunchKernelGGL(gemm_splitk_reduce4<16>, dim3(ceil_div(t4, 16)), dim3(256), 0, s, a, splitk);
-    } else {
-      hipLaunchKernelGGL(gemm_splitk_reduce, dim3(stream_grid(total, 256)), dim3(256), 0, s, a, splitk);
-    }
-  }
+  if (splitk > 1 && ka.tickets == nullptr) launch_reduce(a, splitk, s);
   return hipGetLastError();
 }
 
@@ -1019,15 +1080,16 @@ const TilePolicy& tile_policy() {
   return p;
 }
 
-template <bool AKC, bool BKC>
-hipError_t dispatch_tiles(const GemmArgs& a, hipStream_t s) {
+enum TileCfg { kTile128x32, kTile32x128, kTile128, kTile64 };
+// The tile configuration and split-K count of a GEMM (split-K only where a workspace was provided:
+// a.splitk slabs, never exceeded).
+TileCfg choose_tiles(const GemmArgs& a, int& split) {
   const TilePolicy& tp = tile_policy();
   const long t128 = static_cast<long>(ceil_div(a.M, 128)) * ceil_div(a.N, 128);
   const long t64 = static_cast<long>(ceil_div(a.M, 64)) * ceil_div(a.N, 64);
   const bool small = static_cast<long>(a.M) * a.N <= tp.small_mn;
   const long target = small ? tp.small_split_target : tp.split_target;
   const int min_kt = small ? tp.small_split_min_kt : tp.split_min_kt;
-  // Split-K only where a workspace was provided (a.splitk slabs: never exceeded).
   auto pick_split = [&](long tiles, int bk) {
     if (a.workspace == nullptr || a.splitk <= 1) return 1;
     int sk = 1;
@@ -1035,21 +1097,73 @@ hipError_t dispatch_tiles(const GemmArgs& a, hipStream_t s) {
     return sk;
   };
   if (a.N <= 32) {
-    const long t = static_cast<long>(ceil_div(a.M, 128)) * ceil_div(a.N, 32);
-    return launch_cfg<128, 32, 32, 4, 1, AKC, BKC>(a, s, pick_split(t, 32));
+    split = pick_split(static_cast<long>(ceil_div(a.M, 128)) * ceil_div(a.N, 32), 32);
+    return kTile128x32;
   }
   if (a.M <= 32) {
-    const long t = static_cast<long>(ceil_div(a.M, 32)) * ceil_div(a.N, 128);
-    return launch_cfg<32, 128, 32, 1, 4, AKC, BKC>(a, s, pick_split(t, 32));
+    split = pick_split(static_cast<long>(ceil_div(a.M, 32)) * ceil_div(a.N, 128), 32);
+    return kTile32x128;
   }
-  if (t128 >= tp.t128_min) return launch_cfg<128, 128, 32, 2, 2, AKC, BKC>(a, s, pick_split(t128, 32));
-  return launch_cfg<64, 64, 32, 2, 2, AKC, BKC>(a, s, pick_split(t64, 32));
+  if (t128 >= tp.t128_min) {
+    split = pick_split(t128, 32);
+    return kTile128;
+  }
+  split = pick_split(t64, 32);
+  return kTile64;
+}
+
+template <bool AKC, bool BKC>
+hipError_t dispatch_tiles(const GemmArgs& a, hipStream_t s) {
+  int split = 1;
+  switch (choose_tiles(a, split)) {
+    case kTile128x32: return launch_cfg<128, 32, 32, 4, 1, AKC, BKC>(a, s, split);
+    case kTile32x128: return launch_cfg<32, 128, 32, 1, 4, AKC, BKC>(a, s, split);
+    case kTile128: return launch_cfg<128, 128, 32, 2, 2, AKC, BKC>(a, s, split);
+    default: return launch_cfg<64, 64, 32, 2, 2, AKC, BKC>(a, s, split);
+  }
 }
 
 bool is_kc(const Operand& o) {
   if (o.kind == 1 || o.kind == 3) return true;
   if (o.kind == 2) return false;
   return o.ld_k == 1;
+}
+
+// ---- GEMM pairs ------------------------------------------------------------------------------------
+constexpr int kind_code(bool akc, bool bkc, int ak, int bk) { return (akc ? 1 : 0) | (bkc ? 2 : 0) | (ak << 2) | (bk << 4); }
+int kind_code_of(const GemmArgs& a) { return kind_code(is_kc(a.a), is_kc(a.b), a.a.kind, a.b.kind); }
+
+// Launch plan of one pair member: false unless the single-GEMM dispatch would run it on the 64x64 FAST tile
+// (so the pair computes exactly what two separate launches would).
+bool pair_member_plan(const GemmArgs& a, int& tm, int& tn, int& kps, int& split, int& av, int& bv) {
+  if (a.M <= 0 || a.N <= 0 || generic_only()) return false;
+  if (choose_tiles(a, split) != kTile64) return false;
+  const bool akc = is_kc(a.a), bkc = is_kc(a.b);
+  if (!fast_ok(a, a.a, akc, a.M) || !fast_ok(a, a.b, bkc, a.N)) return false;
+  tm = ceil_div(a.M, 64);
+  tn = ceil_div(a.N, 64);
+  kps = ceil_div(ceil_div(a.K, split), 32) * 32;
+  split = ceil_div(a.K, kps);
+  av = vec_ok(a.a, akc);
+  bv = vec_ok(a.b, bkc);
+  return true;
+}
+
+template <bool AKC1, bool BKC1, int AK1, int BK1>
+bool launch_pair_k0(int k0, dim3 grid, hipStream_t s, const GemmArgs& a0, const GemmArgs& a1, const PairDims& d) {
+  switch (k0) {  // data-gradient kinds: dgrad gather / dense dy x {dgrad layout, forward copy read transposed}
+#define PDE_PAIR(AKC0, BKC0, AK0, BK0)                                                                          \
+  case kind_code(AKC0, BKC0, AK0, BK0):                                                                         \
+    hipLaunchKernelGGL((gemm_pair_kernel<AKC0, BKC0, AK0, BK0, AKC1, BKC1, AK1, BK1>), grid, dim3(kThreads), 0, s, \
+                       a0, a1, d);                                                                              \
+    return true;
+    PDE_PAIR(true, true, 3, 0)
+    PDE_PAIR(true, true, 0, 0)
+    PDE_PAIR(true, false, 0, 0)
+    PDE_PAIR(true, false, 3, 0)
+#undef PDE_PAIR
+    default: return false;
+  }
 }
 
 }  // namespace
@@ -1061,6 +1175,56 @@ hipError_t gemm_bf16(const GemmArgs& a, hipStream_t s) {
   if (akc && !bkc) return dispatch_tiles<true, false>(a, s);
   if (!akc && bkc) return dispatch_tiles<false, true>(a, s);
   return dispatch_tiles<false, false>(a, s);
+}
+
+bool gemm_pair_enabled() {
+  static const bool on = !(std::getenv("PDE_GEMM_PAIR") && std::getenv("PDE_GEMM_PAIR")[0] == '0');
+  return on;
+}
+
+hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
+  PairDims d{};
+  int sp0 = 1, sp1 = 1;
+  const bool ok = gemm_pair_enabled() &&
+                  pair_member_plan(a0, d.tm[0], d.tn[0], d.kps[0], sp0, d.av[0], d.bv[0]) &&
+                  pair_member_plan(a1, d.tm[1], d.tn[1], d.kps[1], sp1, d.av[1], d.bv[1]) &&
+                  (sp0 == 1 || reduce_vec_ok(a0)) && (sp1 == 1 || reduce_vec_ok(a1));
+  const int k0 = ok ? kind_code_of(a0) : -1, k1 = ok ? kind_code_of(a1) : -1;
+  d.nz[0] = sp0;
+  d.nz[1] = sp1;
+  const long blocks = static_cast<long>(d.tm[0]) * d.tn[0] * sp0 + static_cast<long>(d.tm[1]) * d.tn[1] * sp1;
+  bool launched = false;
+  if (ok && blocks < (1L << 31)) {
+    GemmArgs g0 = a0, g1 = a1;
+    g0.tickets = g1.tickets = nullptr;  // pair: split-K partials always go through the reduce launch
+    const dim3 grid(static_cast<unsigned>(blocks));
+    switch (k1) {  // weight-gradient kinds: dy^T x {im2col^T gather, dense activation}
+      case kind_code(false, false, 0, 2): launched = launch_pair_k0<false, false, 0, 2>(k0, grid, s, g0, g1, d); break;
+      case kind_code(false, false, 0, 0): launched = launch_pair_k0<false, false, 0, 0>(k0, grid, s, g0, g1, d); break;
+      default: break;
+    }
+  }
+  if (!launched) {  // not a pairable configuration: two ordinary launches, problem 0 first
+    hipError_t e = gemm_bf16(a0, s);
+    if (e != hipSuccess) return e;
+    return gemm_bf16(a1, s);
+  }
+  if (sp0 > 1 && sp1 > 1) {
+    const int l0 = reduce_lanes(sp0), l1 = reduce_lanes(sp1);
+    const int nb0 = static_cast<int>(ceil_div(static_cast<long>(a0.M) * a0.N / 4, 256 / l0));
+    const int nb1 = static_cast<int>(ceil_div(static_cast<long>(a1.M) * a1.N / 4, 256 / l1));
+    const dim3 g(nb0 + nb1);
+#define PDE_RED(L0, L1) \
+  if (l0 == L0 && l1 == L1) hipLaunchKernelGGL((gemm_splitk_reduce4_pair<L0, L1>), g, dim3(256), 0, s, a0, sp0, nb0, a1, sp1);
+    PDE_RED(1, 1) PDE_RED(1, 4) PDE_RED(1, 16) PDE_RED(4, 1) PDE_RED(4, 4) PDE_RED(4, 16) PDE_RED(16, 1) PDE_RED(16, 4)
+    PDE_RED(16, 16)
+#undef PDE_RED
+  } else if (sp0 > 1) {
+    launch_reduce(a0, sp0, s);
+  } else if (sp1 > 1) {
+    launch_reduce(a1, sp1, s);
+  }
+  return hipGetLastError();
 }
 
 }  // namespace pde

@@ -20,6 +20,7 @@ import contextlib
 import torch
 
 from . import core
+from ..ops import streams
 from .exceptions import HorovodInternalError
 
 
@@ -102,6 +103,8 @@ class _DistributedOptimizerMixin:
     def _allreduce_grad(self, p):
         name = self._param_names.get(p)
         g = p.grad
+        if g.is_cuda:  # the gradient may still be in flight on the wgrad side stream (ops/streams.py)
+            streams.join(g.device)
         if not g.is_contiguous():
             p.grad = g = g.contiguous()
         op = self._op

@@ -12,7 +12,8 @@ Per step, for L linear layers (7 for the reference 5x1024 model):
   (``linear_wgrad_bias``) -- no column-sum kernel; weight and bias gradients land directly in the
   parameters' ``.grad`` (the DDP flat buffer), no zeroing, no accumulation copies;
 * L-1 data-gradient GEMMs with the producer's ReLU mask applied in the epilogue (threshold_backward
-  fused); the first layer's input gradient is never computed.
+  fused); the first layer's input gradient is never computed.  Each layer's dgrad and weight-gradient
+  GEMMs go out as ONE paired launch (``OF.gemm_pair``), so the two small grids fill the chip together.
 
 The layer-by-layer autograd path (``MLP.forward`` + ``backward()``) runs the same GEMMs plus autograd's
 grad-zeroing, copies, casts and one bias column-sum per layer (≈60 launches per step vs ≈30 here).
@@ -28,6 +29,7 @@ import torch
 
 from .. import _native
 from ..ops import functional as OF
+from ..ops import streams
 
 
 def _pad8(n: int) -> int:
@@ -77,13 +79,29 @@ class FusedMLP:
             out = acts[i + 1][:, :L.out_features] if i < last else logits
             C.linear_fwd_out(acts[i][:, :L.in_features], w, L.bias.detach(), i < last, out)
         loss, dy = C.ce_fused(logits, y.long().contiguous())
+        side = streams.active_for(x)
         for i in range(last, -1, -1):
             L = self.layers[i]
             gw, gb = self._grads(L)
-            C.linear_wgrad_bias(dy, acts[i][:, :L.in_features + 1], gw, gb, accumulate)
+            if side:
+                # (opt-in, ops/streams.py) weight + bias gradient on the side stream, concurrent with the dgrad
+                # chain (forked before the dgrad is enqueued so the fork point does not wait for it)
+                with streams.fork(dy, join_at_backward_end=False):
+                    C.linear_wgrad_bias(dy, acts[i][:, :L.in_features + 1], gw, gb, accumulate)
+            elif i > 0:
+                # dgrad + weight/bias gradient as ONE paired GEMM launch (dgrad tiles first)
+                with OF.gemm_pair():
+                    C.linear_dgrad_out(dy, OF._bf16_weight(L.weight), acts[i][:, :L.in_features], dys[i - 1])
+                    C.linear_wgrad_bias(dy, acts[i][:, :L.in_features + 1], gw, gb, accumulate)
+                dy = dys[i - 1]
+                continue
+            else:
+                C.linear_wgrad_bias(dy, acts[i][:, :L.in_features + 1], gw, gb, accumulate)
             if i > 0:
                 C.linear_dgrad_out(dy, OF._bf16_weight(L.weight), acts[i][:, :L.in_features], dys[i - 1])
                 dy = dys[i - 1]
+        if side:
+            streams.join(x.device)
         return loss
 
     def launches_per_step(self) -> int:

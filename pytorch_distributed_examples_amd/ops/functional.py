@@ -23,6 +23,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import _native
+from . import streams
 
 # ---------------------------------------------------------------------------------------------
 # compute-copy cache
@@ -93,6 +94,23 @@ def pad8(c: int) -> int:
 
 def _C():
     return _native.C()
+
+
+# ---------------------------------------------------------------------------------------------
+# GEMM pairing
+# ---------------------------------------------------------------------------------------------
+class gemm_pair:
+    """Context manager: the (at most two) GEMM ops issued inside are launched together as ONE paired launch
+    when the block exits (``pde::gemm_bf16_pair``: the first op's tiles are scheduled first; both grids fill
+    the chip together and pay one launch boundary).  Ops inside must not read each other's outputs; non-GEMM
+    kernels issued inside run immediately (before the pair).  ``PDE_GEMM_PAIR=0`` launches them one by one."""
+
+    def __enter__(self):
+        _C().gemm_pair_begin()
+        return self
+
+    def __exit__(self, exc_type, *exc):
+        _C().gemm_pair_end(exc_type is not None)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -227,18 +245,37 @@ class _LinearFn(torch.autograd.Function):
         if ctx.relu:
             dy = _C().relu_bwd(dy, y)
         dx = dw = db = None
+        weight, bias = ctx.params
+        wsink = _grad_sink(weight) if ctx.needs_input_grad[1] else None
+        bsink = _grad_sink(bias) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        if wsink is not None and ctx.needs_input_grad[0] and not streams.active_for(dy):
+            # dgrad + wgrad as ONE paired GEMM launch (the dgrad's tiles first: it feeds the next layer)
+            with gemm_pair():
+                dx = _C().linear_dgrad(dy, wb, x if ctx.mask_input_grad else None)
+                _C().linear_wgrad(dy, x, wsink, True)
+            if bsink is not None:
+                _C().colsum(dy, -1, bsink, True)
+            elif ctx.has_bias and ctx.needs_input_grad[2]:
+                db = _C().colsum(dy, -1, None, False)
+            return dx, None, db, None, None, None, None
+        if wsink is not None and (bsink is not None or not ctx.has_bias or not ctx.needs_input_grad[2]) \
+                and ctx.needs_input_grad[0] and streams.active_for(dy):
+            # weight / bias gradients go straight into .grad on the side stream, concurrent with the dgrad
+            with streams.fork(dy, x):
+                _C().linear_wgrad(dy, x, wsink, True)
+                if bsink is not None:
+                    _C().colsum(dy, -1, bsink, True)
+            dx = _C().linear_dgrad(dy, wb, x if ctx.mask_input_grad else None)
+            return dx, None, None, None, None, None, None
         if ctx.needs_input_grad[0]:
             dx = _C().linear_dgrad(dy, wb, x if ctx.mask_input_grad else None)
-        weight, bias = ctx.params
         if ctx.needs_input_grad[1]:
-            sink = _grad_sink(weight)
-            dw = _C().linear_wgrad(dy, x, sink, sink is not None)
-            if sink is not None:
+            dw = _C().linear_wgrad(dy, x, wsink, wsink is not None)
+            if wsink is not None:
                 dw = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            sink = _grad_sink(bias)
-            db = _C().colsum(dy, -1, sink, sink is not None)
-            if sink is not None:
+            db = _C().colsum(dy, -1, bsink, bsink is not None)
+            if bsink is not None:
                 db = None
         return dx, dw, db, None, None, None, None
 
@@ -288,6 +325,22 @@ class _Conv2dFn(torch.autograd.Function):
         if ctx.relu:
             dy = _C().relu_bwd(dy, y)
         dx = dw = db = None
+        wsink = _grad_sink(weight) if ctx.needs_input_grad[1] else None
+        bsink = _grad_sink(ctx.bias) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        side = (wsink is not None and ctx.needs_input_grad[0] and streams.active_for(dy)
+                and (bsink is not None or not ctx.has_bias or not ctx.needs_input_grad[2]))
+        if side:
+            # the weight (and bias) gradient is off the critical path: side stream, issued BEFORE the dgrad so
+            # the fork point does not wait for it (ops/streams.py)
+            with streams.fork(dy, x):
+                _C().conv_wgrad(dy, x, r, s, stride, pad, co, ci, wsink, True)
+                if bsink is not None:
+                    _C().colsum(dy, co, bsink, True)
+        paired = wsink is not None and ctx.needs_input_grad[0] and not side
+        if paired:
+            # dgrad + wgrad as ONE paired GEMM launch (dgrad tiles first); the dgrad op is issued first
+            pair = gemm_pair()
+            pair.__enter__()
         if ctx.needs_input_grad[0]:
             # residual fork: the other branch's gradient (stored by the block's last BatchNorm) is added in the
             # dgrad epilogue instead of by a separate autograd add
@@ -302,16 +355,28 @@ class _Conv2dFn(torch.autograd.Function):
                     wd = _cached(weight, ("conv_dgrad", cp, cop),
                                  lambda: _C().conv_w_dgrad(weight.detach().contiguous(), cp, cop))
                 dx = _C().conv_dgrad(dy, wd, h, w, r, s, stride, pad, other, False, other is not None)
+        if paired:
+            try:
+                _C().conv_wgrad(dy, x, r, s, stride, pad, co, ci, wsink, True)
+            except BaseException as exc:
+                pair.__exit__(type(exc), exc, None)
+                raise
+            pair.__exit__(None, None, None)
+            if ctx.has_bias and ctx.needs_input_grad[2]:
+                db = _C().colsum(dy, co, bsink, bsink is not None)
+                if bsink is not None:
+                    db = None
+            return dx, None, db, None, None, None, None
+        if side:
+            return dx, None, None, None, None, None, None
         if ctx.needs_input_grad[1]:
             # OIHW epilogue: the GEMM writes the parameter's layout (and adds into .grad when it exists)
-            sink = _grad_sink(weight)
-            dw = _C().conv_wgrad(dy, x, r, s, stride, pad, co, ci, sink, sink is not None)
-            if sink is not None:
+            dw = _C().conv_wgrad(dy, x, r, s, stride, pad, co, ci, wsink, wsink is not None)
+            if wsink is not None:
                 dw = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            sink = _grad_sink(ctx.bias)
-            db = _C().colsum(dy, co, sink, sink is not None)
-            if sink is not None:
+            db = _C().colsum(dy, co, bsink, bsink is not None)
+            if bsink is not None:
                 db = None
         return dx, dw, db, None, None, None, None
 

@@ -18,6 +18,7 @@ import torch
 
 from .. import _native
 from . import functional as OF
+from . import streams
 
 _MODES = {"sgd": 0, "adam": 1, "adamw": 2}
 
@@ -103,6 +104,7 @@ class _FusedBase(torch.optim.Optimizer):
                 continue
             if params[0].is_cuda:
                 C = C or _native.C()
+                streams.join(params[0].device)  # gradients written on the wgrad side stream
                 st = self._group_dev(gi, group, params)
                 C.optim_step(st["table"], st["chunks"], st["nchunks"], _MODES[self.KIND], st["hp"], st["step"])
                 if st["nconv"]:

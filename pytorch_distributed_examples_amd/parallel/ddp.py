@@ -28,6 +28,7 @@ import torch
 import torch.distributed as dist
 from torch import nn
 
+from ..ops import streams
 from . import xgmi
 
 
@@ -141,6 +142,8 @@ class DistributedDataParallel(nn.Module):
         return hook
 
     def _launch(self, b: int):
+        if self.flat_grad.is_cuda:  # weight gradients may still be running on the side stream (ops/streams.py)
+            streams.join(self.flat_grad.device)
         if self._bf16_bufs is not None and getattr(self.comm, "supports_bf16_wire", False):
             # the communicator casts on the wire itself (fused into the xGMI one-shot kernel): no copies here
             work = self.comm.allreduce_async(self._bucket_flat[b], avg=self._use_avg, wire_bf16=True)
