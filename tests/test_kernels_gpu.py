@@ -117,11 +117,13 @@ def test_colsum(gpu, M, N):
 
 
 # shapes: one 64-channel slice; C < 64 (partial slice, groups not dividing 256); C % 64 != 0 (ragged
-# last slice, several slices); many rows (256 row chunks per slice -> widest last-block combine)
+# last slice, several slices); many rows (256 row chunks per slice -> widest last-block combine); odd row
+# counts per chunk (P = 1000, 3600).
 @pytest.mark.parametrize("relu,res,n,c,h", [(False, False, 8, 64, 16), (True, False, 8, 64, 16),
                                             (True, True, 8, 64, 16), (True, False, 4, 24, 10),
                                             (False, True, 2, 200, 9), (True, True, 32, 64, 64),
-                                            (False, False, 2, 2048, 4)])
+                                            (False, False, 2, 2048, 4), (True, True, 10, 96, 10),
+                                            (True, True, 16, 64, 32), (False, True, 4, 200, 30)])
 def test_batchnorm(gpu, relu, res, n, c, h):
     torch.manual_seed(2)
     x = torch.randn(n, c, h, h, device=gpu) * 3 + 1
