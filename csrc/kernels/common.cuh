@@ -36,10 +36,10 @@ __device__ __forceinline__ float wave_max(float v) {
 inline int ceil_div(long a, long b) { return static_cast<int>((a + b - 1) / b); }
 
 // Grid size for a grid-stride memory-bound kernel: enough blocks to fill 256 CUs, capped.
-inline int stream_grid(long n, int block, int per_thread = 1) {
+inline int stream_grid(long n, int block, int per_thread = 1, long cap = 2048) {
   long blocks = (n + static_cast<long>(block) * per_thread - 1) / (static_cast<long>(block) * per_thread);
   if (blocks < 1) blocks = 1;
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > cap) blocks = cap;
   return static_cast<int>(blocks);
 }
 

@@ -41,6 +41,10 @@ namespace pde {
 namespace {
 
 constexpr int kThreads = 256;
+// K-tiles in flight in the FAST loaders' register ring (-DPDE_FAST_STAGES=N to sweep)
+#ifndef PDE_FAST_STAGES
+#define PDE_FAST_STAGES 4
+#endif
 
 // LDS images are unpadded K-contiguous rows (BK = 32 -> 64 B, four 16-byte K-chunks) with an XOR swizzle
 // of the chunk index: chunk c of row r lives at c ^ H[(r >> 2) & 3] ^ ((r >> 4) & 3), H = {0, 3, 2, 1}.
@@ -453,8 +457,14 @@ __device__ __forceinline__ void store_out(float v, int epi, int m, int n, const 
 // one lane takes a relaxed agent-scope ticket; the reducer reads every slab with sc1 loads (L1 bypassed,
 // so no acquire).  The reducer resets the ticket (the array starts zeroed, so every launch finds 0).
 constexpr int kMaxInKernelSplits = 8;  // more slabs per tile: the serial combine loses to a reduce launch
+// K-tiles staged per LDS buffer and consumed per barrier (-DPDE_GEMM_SUB=N to sweep): the MFMAs of kSub
+// consecutive 32-deep K-tiles run between two barriers, each K-tile keeping its own swizzled image.
+#ifndef PDE_GEMM_SUB
+#define PDE_GEMM_SUB 1
+#endif
+constexpr int kSub = PDE_GEMM_SUB;
 template <int BM, int BN>
-constexpr int SMEM_BYTES_OF() { return 2 * (BM + BN) * 32 * 2; }  // gemm_kernel's LDS (BK = 32, bf16)
+constexpr int SMEM_BYTES_OF() { return 2 * kSub * (BM + BN) * 32 * 2; }  // gemm_kernel's LDS (BK = 32, bf16)
 
 template <int BM, int BN, int FM, int FN, int WTM, int WTN>
 __device__ __forceinline__ void write_slab_and_reduce(const GemmArgs& args, const f32x4 (&acc)[FM][FN],
@@ -575,7 +585,10 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args, int tiles_m, int
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int LDS_A = BM * BK, LDS_B = BN * BK;
   constexpr int SMEM_BYTES = SMEM_BYTES_OF<BM, BN>();
-  static_assert(2 * (LDS_A + LDS_B) * 2 == SMEM_BYTES, "split-K staging size");
+  constexpr int KSUB = (STAGES % kSub == 0) ? kSub : 1;  // the register ring holds whole K-tile groups
+  constexpr int SUBT = LDS_A + LDS_B;                    // one K-tile image (A then B)
+  constexpr int BUF = KSUB * SUBT;                       // one LDS buffer: KSUB K-tile images
+  static_assert(2 * BUF * 2 <= SMEM_BYTES, "LDS budget");
 
   // XCD-aware tile id remap (bijective; see cdna_hip_programming.md §5 "XCD swizzle").
   const int ntiles = tiles_m * tiles_n;
@@ -635,52 +648,70 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args, int tiles_m, int
         lb.load(args.b, args.N, kend, n0, bvec, rb[u]);
       }
     }
-    la.store(smem, ra[0]);
-    lb.store(smem + LDS_A, rb[0]);
+#pragma unroll
+    for (int q = 0; q < KSUB; ++q) {
+      if (q < nk) {
+        la.store(smem + q * SUBT, ra[q]);
+        lb.store(smem + q * SUBT + LDS_A, rb[q]);
+      }
+    }
   }
   __syncthreads();
 
+  // one K-tile's MFMAs from its LDS image
+  auto mma_tile = [&](const uint16_t* As) {
+    const uint16_t* Bs = As + LDS_A;
+    bf16x8 af[FM], bfr[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if constexpr (AKC) {
+        const int row = wm * WTM + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + row * BK + swz_chunk(row, lane >> 4) * 8);
+      } else {
+        af[i] = rc_frag<BM>(As, wm * WTM + i * 16, lane);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      if constexpr (BKC) {
+        const int row = wn * WTN + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + swz_chunk(row, lane >> 4) * 8);
+      } else {
+        bfr[j] = rc_frag<BN>(Bs, wn * WTN + j * 16, lane);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  };
+
   for (int kt = 0; kt < nk; kt += S) {
 #pragma unroll
-    for (int u = 0; u < S; ++u) {
-      const int t = kt + u;
-      if (FASTK || t + S < nk) {  // refill this slot (its tile went to LDS one iteration ago)
-        la.advance(args.a);
-        lb.advance(args.b);
-        la.load(args.a, args.M, kend, m0, avec, ra[u]);
-        lb.load(args.b, args.N, kend, n0, bvec, rb[u]);
+    for (int u = 0; u < S; u += KSUB) {
+      const int t = kt + u;  // first K-tile of this group (its KSUB images are in LDS buffer (t / KSUB) & 1)
+#pragma unroll
+      for (int q = 0; q < KSUB; ++q) {
+        if (FASTK || t + q + S < nk) {  // refill these slots (their tiles went to LDS one group ago)
+          la.advance(args.a);
+          lb.advance(args.b);
+          la.load(args.a, args.M, kend, m0, avec, ra[u + q]);
+          lb.load(args.b, args.N, kend, n0, bvec, rb[u + q]);
+        }
       }
       if (t < nk) {
-        const uint16_t* As = smem + (t & 1) * (LDS_A + LDS_B);
-        const uint16_t* Bs = As + LDS_A;
-        bf16x8 af[FM], bfr[FN];
+        const uint16_t* buf = smem + ((t / KSUB) & 1) * BUF;
 #pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          if constexpr (AKC) {
-            const int row = wm * WTM + i * 16 + (lane & 15);
-            af[i] = *reinterpret_cast<const bf16x8*>(As + row * BK + swz_chunk(row, lane >> 4) * 8);
-          } else {
-            af[i] = rc_frag<BM>(As, wm * WTM + i * 16, lane);
+        for (int q = 0; q < KSUB; ++q)
+          if (q == 0 || t + q < nk) mma_tile(buf + q * SUBT);
+        uint16_t* nxt = smem + (((t / KSUB) + 1) & 1) * BUF;
+#pragma unroll
+        for (int q = 0; q < KSUB; ++q) {
+          if (t + KSUB + q < nk) {
+            la.store(nxt + q * SUBT, ra[(u + KSUB + q) % S]);
+            lb.store(nxt + q * SUBT + LDS_A, rb[(u + KSUB + q) % S]);
           }
-        }
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          if constexpr (BKC) {
-            const int row = wn * WTN + j * 16 + (lane & 15);
-            bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + swz_chunk(row, lane >> 4) * 8);
-          } else {
-            bfr[j] = rc_frag<BN>(Bs, wn * WTN + j * 16, lane);
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        if (t + 1 < nk) {
-          uint16_t* nxt = smem + ((t + 1) & 1) * (LDS_A + LDS_B);
-          la.store(nxt, ra[(u + 1) % S]);
-          lb.store(nxt + LDS_A, rb[(u + 1) % S]);
         }
         __syncthreads();
       }
@@ -834,12 +865,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   const int nb0 = t0 * d.nz[0];
   int b = blockIdx.x;
   if (b < nb0) {
-    gemm_tile<64, 64, 32, 2, 2, AKC0, BKC0, AK0, BK0, 4>(a0, d.tm[0], d.tn[0], d.kps[0], d.av[0], d.bv[0], b % t0,
+    gemm_tile<64, 64, 32, 2, 2, AKC0, BKC0, AK0, BK0, PDE_FAST_STAGES>(a0, d.tm[0], d.tn[0], d.kps[0], d.av[0], d.bv[0], b % t0,
                                                          b / t0, d.nz[0], smem);
   } else {
     b -= nb0;
     const int t1 = d.tm[1] * d.tn[1];
-    gemm_tile<64, 64, 32, 2, 2, AKC1, BKC1, AK1, BK1, 4>(a1, d.tm[1], d.tn[1], d.kps[1], d.av[1], d.bv[1], b % t1,
+    gemm_tile<64, 64, 32, 2, 2, AKC1, BKC1, AK1, BK1, PDE_FAST_STAGES>(a1, d.tm[1], d.tn[1], d.kps[1], d.av[1], d.bv[1], b % t1,
                                                          b / t1, d.nz[1], smem);
   }
 }
@@ -943,7 +974,7 @@ int* split_tickets(int tiles, hipStream_t s) {
 
 // FAST instantiations: (A kind, B kind) pairs that occur -- K-contiguous A: dense, im2col, dgrad gather;
 // row-contiguous A: dense (dy^T); K-contiguous B: dense weights; row-contiguous B: dense, im2col^T.
-constexpr int kFastStages = 4;
+constexpr int kFastStages = PDE_FAST_STAGES;
 template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC, int AK, int BKN>
 void launch_fast1(dim3 grid, hipStream_t s, const GemmArgs& ka, int tm, int tn, int kps, int av, int bv) {
   hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AKC, BKC, AK, BKN, kFastStages>), grid, dim3(kThreads), 0, s,

@@ -281,7 +281,11 @@ __global__ void k_bn_bwd_apply(const uint16_t* __restrict__ dy, const uint16_t* 
 // the block that draws the last ticket acquires (agent scope) and combines that group's partials in fixed
 // row-chunk order (deterministic) -- cdna_hip_programming.md §6 Guideline 16, recipe R1 in counter form.
 // Saves the separate finalize launch in both directions (6 -> 4 kernels per BatchNorm layer).
-constexpr int kBnCG = 64;  // channels per group: 8 channel-vector lanes x 8 channels
+constexpr int kBnCG = 64;       // channels per group: 8 channel-vector lanes x 8 channels
+constexpr int kBnThreads = 512;  // 64 row lanes x 8 channel-vector lanes
+constexpr int kBnRows = kBnThreads / 8;
+constexpr int kBnQ = kBnThreads / kBnCG;  // lanes per (channel) in the finalizing combine
+constexpr int kBnUnroll = 8;     // rows per lane per trip, all loads issued before the math
 
 __device__ __forceinline__ void st_sc1(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -291,7 +295,7 @@ __device__ __forceinline__ void st_sc1(float* p, float v) {
 // the per-channel totals over all row chunks in fixed order into tot1/tot2 (LDS).  Returns true on the block
 // that finalizes.
 __device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], const float (&s2)[8], float* ws, int C,
-                                                       int* ticket, float (*red)[32][kBnCG + 1], float* tot1,
+                                                       int* ticket, float (*red)[kBnRows][kBnCG + 1], float* tot1,
                                                        float* tot2, int* s_last) {
   const int tid = threadIdx.x, tv = tid & 7, tr = tid >> 3;
   const int rb = blockIdx.x, nrb = gridDim.x, cbase = blockIdx.y * kBnCG;
@@ -304,7 +308,7 @@ __device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], con
   if (tid < 2 * kBnCG) {
     const int which = tid / kBnCG, ch = tid % kBnCG;
     float v = 0.f;
-    for (int r = 0; r < 32; ++r) v += red[which][r][ch];
+    for (int r = 0; r < kBnRows; ++r) v += red[which][r][ch];
     if (cbase + ch < C) st_sc1(ws + (static_cast<long>(rb) * 2 + which) * C + cbase + ch, v);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -317,19 +321,19 @@ __device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], con
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  // 4 lanes per (which, channel) over the row chunks, combined in lane order
+  // kBnQ lanes per (which, channel) over the row chunks, combined in lane order
   {
     const int q = tid >> 6, ch = tid & 63;
     float a1 = 0.f, a2 = 0.f;
     if (cbase + ch < C) {
       // 8 chunks per trip with all 16 loads issued before the adds (the tail is latency-bound)
       int b = q;
-      for (; b + 28 < nrb; b += 32) {
+      for (; b + 7 * kBnQ < nrb; b += 8 * kBnQ) {
         float u1[8], u2[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          u1[k] = ws[(static_cast<long>(b + 4 * k) * 2) * C + cbase + ch];
-          u2[k] = ws[(static_cast<long>(b + 4 * k) * 2 + 1) * C + cbase + ch];
+          u1[k] = ws[(static_cast<long>(b + kBnQ * k) * 2) * C + cbase + ch];
+          u2[k] = ws[(static_cast<long>(b + kBnQ * k) * 2 + 1) * C + cbase + ch];
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -337,7 +341,7 @@ __device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], con
           a2 += u2[k];
         }
       }
-      for (; b < nrb; b += 4) {
+      for (; b < nrb; b += kBnQ) {
         a1 += ws[(static_cast<long>(b) * 2) * C + cbase + ch];
         a2 += ws[(static_cast<long>(b) * 2 + 1) * C + cbase + ch];
       }
@@ -347,22 +351,28 @@ __device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], con
   }
   __syncthreads();
   if (tid < kBnCG) {
-    tot1[tid] = ((red[0][0][tid] + red[0][1][tid]) + red[0][2][tid]) + red[0][3][tid];
-    tot2[tid] = ((red[1][0][tid] + red[1][1][tid]) + red[1][2][tid]) + red[1][3][tid];
+    float v1 = red[0][0][tid], v2 = red[1][0][tid];
+#pragma unroll
+    for (int q = 1; q < kBnQ; ++q) {
+      v1 += red[0][q][tid];
+      v2 += red[1][q][tid];
+    }
+    tot1[tid] = v1;
+    tot2[tid] = v2;
   }
   if (tid == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
   __syncthreads();
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_bn_stats_fin(const uint16_t* __restrict__ x, int P, int C, int rpb,
+__global__ __launch_bounds__(kBnThreads) void k_bn_stats_fin(const uint16_t* __restrict__ x, int P, int C, int rpb,
                                                       float* __restrict__ ws, int* __restrict__ tickets,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       float eps, float momentum, float* __restrict__ running_mean,
                                                       float* __restrict__ running_var, float* __restrict__ save_mean,
                                                       float* __restrict__ save_invstd, float* __restrict__ scale,
                                                       float* __restrict__ shift) {
-  __shared__ float red[2][32][kBnCG + 1];
+  __shared__ float red[2][kBnRows][kBnCG + 1];
   __shared__ float tot1[kBnCG], tot2[kBnCG];
   __shared__ int s_last;
   const int tid = threadIdx.x, tv = tid & 7, tr = tid >> 3;
@@ -375,16 +385,18 @@ __global__ __launch_bounds__(256) void k_bn_stats_fin(const uint16_t* __restrict
     load8(x + c0, piv);  // shift by row 0 (same pivot in every block)
     const int r1 = min(P, (blockIdx.x + 1) * rpb);
     int r = blockIdx.x * rpb + tr;
-    for (; r + 3 * 32 < r1; r += 4 * 32) {
-      u16x8 u[4];
+    constexpr int U = kBnUnroll;
+    for (; r + (U - 1) * kBnRows < r1; r += U * kBnRows) {
+      u16x8 u[U];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) u[q] = *reinterpret_cast<const u16x8*>(x + static_cast<long>(r + 32 * q) * C + c0);
+      for (int q = 0; q < U; ++q)
+        u[q] = *reinterpret_cast<const u16x8*>(x + static_cast<long>(r + kBnRows * q) * C + c0);
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < U; ++q)
 #pragma unroll
         for (int j = 0; j < 8; ++j) { const float d = bf2f(u[q][j]) - piv[j]; s1[j] += d; s2[j] += d * d; }
     }
-    for (; r < r1; r += 32) {
+    for (; r < r1; r += kBnRows) {
       float v[8];
       load8(x + static_cast<long>(r) * C + c0, v);
 #pragma unroll
@@ -414,12 +426,12 @@ __global__ __launch_bounds__(256) void k_bn_stats_fin(const uint16_t* __restrict
   }
 }
 
-__global__ __launch_bounds__(256) void k_bn_bwd_reduce_fin(
+__global__ __launch_bounds__(kBnThreads) void k_bn_bwd_reduce_fin(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const uint16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, int P, int C, int rpb, int relu,
     float* __restrict__ ws, int* __restrict__ tickets, const float* __restrict__ gamma, float* __restrict__ dgamma,
     float* __restrict__ dbeta, int accum, float* __restrict__ coef) {
-  __shared__ float red[2][32][kBnCG + 1];
+  __shared__ float red[2][kBnRows][kBnCG + 1];
   __shared__ float tot1[kBnCG], tot2[kBnCG];
   __shared__ int s_last;
   const int tid = threadIdx.x, tv = tid & 7, tr = tid >> 3;
@@ -434,17 +446,18 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce_fin(
     for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j]; }
     const int r1 = min(P, (blockIdx.x + 1) * rpb);
     int r = blockIdx.x * rpb + tr;
-    for (; r + 32 < r1; r += 2 * 32) {
-      u16x8 ud[2], ux[2], uy[2];
+    constexpr int U = kBnUnroll / 2;  // 3 tensors per row: 12 x 16-B loads in flight per lane
+    for (; r + (U - 1) * kBnRows < r1; r += U * kBnRows) {
+      u16x8 ud[U], ux[U], uy[U];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const long off = static_cast<long>(r + 32 * q) * C + c0;
+      for (int q = 0; q < U; ++q) {
+        const long off = static_cast<long>(r + kBnRows * q) * C + c0;
         ud[q] = *reinterpret_cast<const u16x8*>(dy + off);
         ux[q] = *reinterpret_cast<const u16x8*>(x + off);
         if (relu) uy[q] = *reinterpret_cast<const u16x8*>(y + off);
       }
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+      for (int q = 0; q < U; ++q)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           float d = bf2f(ud[q][j]);
@@ -453,7 +466,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_reduce_fin(
           s2[j] += d * (bf2f(ux[q][j]) - mu[j]) * is[j];
         }
     }
-    for (; r < r1; r += 32) {
+    for (; r < r1; r += kBnRows) {
       const long off = static_cast<long>(r) * C + c0;
       float d[8], xv[8];
       load8(dy + off, d);
@@ -820,8 +833,10 @@ int bn_blocks(int P, int C, int& rows_per_block) {
 // (the finalizing block reads chunks x 2 x 64 partials).
 int bn_fin_grid(int P, int C, int& rpb) {
   const int ncg = (C + kBnCG - 1) / kBnCG;
-  int nrb = std::max(1, std::min(64, 512 / ncg));
-  nrb = std::min(nrb, std::max(1, P / 32));
+  static const int kChunks = std::getenv("PDE_BN_CHUNKS") ? std::atoi(std::getenv("PDE_BN_CHUNKS")) : 64;
+  static const int kTarget = std::getenv("PDE_BN_BLOCKS") ? std::atoi(std::getenv("PDE_BN_BLOCKS")) : 512;
+  int nrb = std::max(1, std::min(kChunks, kTarget / ncg));
+  nrb = std::min(nrb, std::max(1, P / kBnRows));
   rpb = ceil_div(P, nrb);
   return ceil_div(P, rpb);
 }
@@ -854,6 +869,8 @@ int* bn_tickets(int n, hipStream_t s) {
   return t;
 }
 
+const long kBnApplyCap = std::getenv("PDE_BN_APPLY_CAP") ? std::atol(std::getenv("PDE_BN_APPLY_CAP")) : 8192;
+
 int bn_workspace_blocks(int P, int C) {
   int rpb;
   return std::max(bn_blocks(P, C, rpb), bn_fin_grid(P, C, rpb));
@@ -867,7 +884,7 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
   int* tk = bn_tickets(ceil_div(C, kBnCG), s);
   if (tk != nullptr) {
     const int nrb = bn_fin_grid(P, C, rpb);
-    hipLaunchKernelGGL(k_bn_stats_fin, dim3(nrb, ceil_div(C, kBnCG)), dim3(256), 0, s, x, P, C, rpb, ws, tk, gamma,
+    hipLaunchKernelGGL(k_bn_stats_fin, dim3(nrb, ceil_div(C, kBnCG)), dim3(kBnThreads), 0, s, x, P, C, rpb, ws, tk, gamma,
                        beta, eps, momentum, running_mean, running_var, save_mean, save_invstd, scale_shift,
                        scale_shift + C);
   } else {
@@ -877,8 +894,9 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
                        momentum, running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C);
   }
   const long nvec = static_cast<long>(P) * C / 8;
-  hipLaunchKernelGGL(k_bn_apply, dim3(stream_grid(nvec, 256)), dim3(256), 0, s, x, scale_shift, scale_shift + C,
-                     res, y, nvec, C, relu);
+  // one 16-B vector per lane (up to 8192 blocks): a single memory round trip, no grid-stride second trip
+  hipLaunchKernelGGL(k_bn_apply, dim3(stream_grid(nvec, 256, 1, kBnApplyCap)), dim3(256), 0, s, x, scale_shift,
+                     scale_shift + C, res, y, nvec, C, relu);
   return hipGetLastError();
 }
 
@@ -897,7 +915,7 @@ hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, cons
   int* tk = bn_tickets(ceil_div(C, kBnCG), s);
   if (tk != nullptr) {
     const int nrb = bn_fin_grid(P, C, rpb);
-    hipLaunchKernelGGL(k_bn_bwd_reduce_fin, dim3(nrb, ceil_div(C, kBnCG)), dim3(256), 0, s, dy, x, y, mean, invstd,
+    hipLaunchKernelGGL(k_bn_bwd_reduce_fin, dim3(nrb, ceil_div(C, kBnCG)), dim3(kBnThreads), 0, s, dy, x, y, mean, invstd,
                        P, C, rpb, relu, ws, tk, gamma, dgamma, dbeta, accum_params, coef);
   } else {
     const int nblk = bn_blocks(P, C, rpb);
@@ -906,8 +924,8 @@ hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, cons
                        dgamma, dbeta, accum_params, coef);
   }
   const long nvec = static_cast<long>(P) * C / 8;
-  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(stream_grid(nvec, 256)), dim3(256), 0, s, dy, x, y, mean, invstd, coef,
-                     nvec, C, relu, dx, dres);
+  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(stream_grid(nvec, 256, 1, kBnApplyCap)), dim3(256), 0, s, dy, x, y, mean,
+                     invstd, coef, nvec, C, relu, dx, dres);
   return hipGetLastError();
 }
 

@@ -13,6 +13,8 @@
 // the weight it just wrote (linear weights, and 1x1 conv weights whose OIHW layout IS the implicit-GEMM
 // layout), with contiguous 8-byte stores -- so those layers run no per-step cast / layout kernel.  The
 // step counter is int32[2] = {steps taken, arrival counter}: the last block to finish advances it.
+#include <cstdlib>
+
 #include "common.cuh"
 #include "pde_kernels.h"
 
@@ -177,7 +179,7 @@ hipError_t multi_tensor_optim(int mode, const OptimEntry* dev_table, const Optim
                               const float* dev_hparams, int* dev_step, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
   // ~3 blocks per CU, each walking several chunks with the next one's loads in flight (pipelined loop)
-  constexpr int kMaxBlocks = 768;
+  static const int kMaxBlocks = std::getenv("PDE_OPTIM_BLOCKS") ? std::atoi(std::getenv("PDE_OPTIM_BLOCKS")) : 768;
   dim3 grid(static_cast<unsigned>(nchunks < kMaxBlocks ? nchunks : kMaxBlocks));
   if (mode == 0)
     hipLaunchKernelGGL(k_optim<0>, grid, dim3(kThreads), 0, s, dev_table, dev_chunks, nchunks, dev_hparams, dev_step);

@@ -10,6 +10,7 @@ import importlib
 import os
 
 _mods: dict[str, object] = {}
+_DEBUG_SYNC = [os.environ.get("PDE_DEBUG_SYNC", "0") == "1"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -35,9 +36,48 @@ def _load(name: str):
     return mod
 
 
+class _SyncChecked:
+    """Debug view of a native module (``PDE_DEBUG_SYNC=1`` / ``--debug-sync``): every call is
+    followed by a device synchronize and a HIP last-error check that raises with the op's name, so an
+    asynchronous fault, an out-of-bounds access or a missing stream dependency is pinned to the launch that
+    caused it instead of surfacing at some later synchronization.  Inside a stream capture the checks are
+    skipped (synchronizing would invalidate the capture)."""
+
+    def __init__(self, mod):
+        self._mod = mod
+
+    def __getattr__(self, name):
+        fn = getattr(self._mod, name)
+        if not callable(fn) or name in ("clear_last_error",):
+            return fn
+        mod = self._mod
+
+        def checked(*a, **k):
+            out = fn(*a, **k)
+            import torch
+
+            if torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+                torch.cuda.synchronize()
+                err = mod.clear_last_error() if hasattr(mod, "clear_last_error") else 0
+                if err:
+                    raise RuntimeError(f"native op {name!r} left HIP error {err} (PDE_DEBUG_SYNC)")
+            return out
+
+        return checked
+
+
+def set_debug_sync(flag: bool) -> None:
+    _DEBUG_SYNC[0] = bool(flag)
+
+
+def debug_sync() -> bool:
+    return _DEBUG_SYNC[0]
+
+
 def C():
     """The gfx950 kernel extension (GEMM/conv/BN/pool/loss/optimizer/...)."""
-    return _load("_C")
+    mod = _load("_C")
+    return _SyncChecked(mod) if _DEBUG_SYNC[0] else mod
 
 
 def comm():

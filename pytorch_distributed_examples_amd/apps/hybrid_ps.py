@@ -32,6 +32,8 @@ from ..ops import layers as L
 from ..parallel.ddp import DistributedDataParallel
 from ..parallel.dist import free_port
 from ..rpc import DistributedOptimizer, RemoteModule, dist_autograd
+from ..utils import config as rtconfig
+from ..utils.config import add_runtime_args
 
 NUM_EMBEDDINGS = 100
 EMBEDDING_DIM = 16
@@ -231,7 +233,11 @@ def main(argv=None):
     ap.add_argument("--split-size", type=int, default=8)
     ap.add_argument("--schedule", default="gpipe", choices=["gpipe", "1f1b"])
     ap.add_argument("--image", type=int, default=128)
+    add_runtime_args(ap)
     args = ap.parse_args(argv)
+    _cfg = rtconfig.apply(rtconfig.from_args(args))
+    if hasattr(args, "device"):
+        args.device = rtconfig.device_for(_cfg, args.device)
     if args.model == "resnet50":
         world = int(os.environ.get("WORLD_SIZE", "1"))
         dp = args.dp or max(1, world // args.stages)

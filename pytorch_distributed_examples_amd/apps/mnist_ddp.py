@@ -37,6 +37,8 @@ from ..ops.optim import FusedAdam, FusedSGD
 from ..parallel import dist as pdist
 from ..parallel.ddp import DistributedDataParallel
 from ..utils.log import RankLogger, MetricsWriter
+from ..utils import config as rtconfig
+from ..utils.config import add_runtime_args
 
 
 def load_train_objs(model_name: str, device, train_size: int, test_size: int):
@@ -58,7 +60,7 @@ def load_train_objs(model_name: str, device, train_size: int, test_size: int):
 
 class Trainer:
     def __init__(self, ctx, model, train_data, test_data, make_opt, criterion, save_every, snapshot_path,
-                 log, metrics=None, save_optimizer=True, fused=False):
+                 log, metrics=None, save_optimizer=True, fused=False, ddp_kwargs=None):
         self.ctx = ctx
         self.global_rank = int(os.environ.get("RANK", ctx.rank))
         self.local_rank = int(os.environ.get("LOCAL_RANK", ctx.local_rank))
@@ -84,9 +86,10 @@ class Trainer:
             if ctx.device.type != "cuda":
                 raise SystemExit("--fused runs the gfx950 training kernel: it needs a GPU")
             self.fused = FusedCNN(self.model)
-            self.ddp = DistributedDataParallel(self.model, overlap=False, param_order="forward", comm=data_plane(ctx))
+            self.ddp = DistributedDataParallel(self.model, overlap=False, param_order="forward", comm=data_plane(ctx),
+                                               **(ddp_kwargs or {}))
         else:
-            self.ddp = DistributedDataParallel(self.model)
+            self.ddp = DistributedDataParallel(self.model, **(ddp_kwargs or {}))
 
     def _load_snapshot(self, path):
         snap = load_snapshot(path)
@@ -189,7 +192,10 @@ def main(argv=None):
                         help="survive membership changes in-process (RCCL communicator re-wire); launch with "
                              "python -m pytorch_distributed_examples_amd.launch.hvdrun")
     parser.add_argument("--commit_every", type=int, default=10, help="--rewire: steps between in-memory commits")
+    add_runtime_args(parser, style="underscore")
     args = parser.parse_args(argv)
+    cfg = rtconfig.apply(rtconfig.from_args(args))
+    args.device = rtconfig.device_for(cfg, args.device)
 
     start = time.time()
     if args.rewire:
@@ -205,7 +211,8 @@ def main(argv=None):
         train_data = ShardedLoader(train_set, args.batch_size, ctx.world_size, ctx.rank, shuffle=True)
         test_data = ShardedLoader(test_set, args.batch_size, ctx.world_size, ctx.rank, shuffle=False)
         trainer = Trainer(ctx, model, train_data, test_data, make_opt, criterion, args.save_every,
-                          args.snapshot_path, log, metrics, fused=args.fused and args.model == "cnn")
+                          args.snapshot_path, log, metrics, fused=args.fused and args.model == "cnn",
+                          ddp_kwargs=cfg.ddp_kwargs())
         trainer.train(args.total_epochs)
         pdist.shutdown()
     end = time.time()

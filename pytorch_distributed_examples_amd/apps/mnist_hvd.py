@@ -24,6 +24,8 @@ from ..data.synthetic import mnist_splits
 from ..models.cnn import Net
 from ..ops import functional as OF
 from ..ops.optim import FusedSGD
+from ..utils import config as rtconfig
+from ..utils.config import add_runtime_args
 
 
 def main(argv=None):
@@ -36,7 +38,11 @@ def main(argv=None):
     ap.add_argument("--log-interval", type=int, default=5)
     ap.add_argument("--fused", action="store_true", help="fused whole-network training kernel (GPU)")
     ap.add_argument("--compression", default="none", choices=["none", "fp16", "bf16"])
+    add_runtime_args(ap)
     args = ap.parse_args(argv)
+    _cfg = rtconfig.apply(rtconfig.from_args(args))
+    if hasattr(args, "device"):
+        args.device = rtconfig.device_for(_cfg, args.device)
 
     hvd.init(device="cpu" if args.device == "cpu" else None)
     dev = hvd.core._ctx.device
@@ -52,7 +58,8 @@ def main(argv=None):
         fused.grad_buffer()
     optimizer = FusedSGD(model.parameters(), lr=args.lr)
     optimizer = hvd.DistributedOptimizer(optimizer, named_parameters=model.named_parameters(),
-                                         compression=getattr(hvd.Compression, args.compression))
+                                         compression=getattr(hvd.Compression, "bf16" if args.compression == "none"
+                                                             and _cfg.grad_dtype == "bf16" else args.compression))
     hvd.broadcast_parameters(model.state_dict(), root_rank=0)
 
     t0 = time.time()

@@ -29,6 +29,8 @@ from ..elastic import fault
 from ..models.cnn import Net
 from ..ops import functional as OF
 from ..ops.optim import FusedAdamW
+from ..utils import config as rtconfig
+from ..utils.config import add_runtime_args
 
 
 def main(argv=None):
@@ -40,7 +42,11 @@ def main(argv=None):
     ap.add_argument("--train-size", type=int, default=60000)
     ap.add_argument("--test-size", type=int, default=10000)
     ap.add_argument("--device", default="auto", choices=["auto", "cpu", "gpu"])
+    add_runtime_args(ap)
     args = ap.parse_args(argv)
+    _cfg = rtconfig.apply(rtconfig.from_args(args))
+    if hasattr(args, "device"):
+        args.device = rtconfig.device_for(_cfg, args.device)
     epochs, batches_per_commit, lr = args.epochs, args.batches_per_commit, args.lr
 
     hvd.init(device="cpu" if args.device == "cpu" else None)

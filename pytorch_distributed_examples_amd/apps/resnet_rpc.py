@@ -27,6 +27,8 @@ from torch import nn, optim
 from ..models.resnet import ResNetShard1, ResNetShard2
 from ..parallel.dist import free_port
 from ..rpc import DistributedOptimizer, RemotePipeline, dist_autograd
+from ..utils import config as rtconfig
+from ..utils.config import add_runtime_args
 
 NUM_CLASSES = 1000
 
@@ -97,7 +99,11 @@ def main(argv=None):
     ap.add_argument("--image-h", type=int, default=128)
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    add_runtime_args(ap)
     args = ap.parse_args(argv)
+    _cfg = rtconfig.apply(rtconfig.from_args(args))
+    if hasattr(args, "device"):
+        args.device = rtconfig.device_for(_cfg, args.device)
     world_size = 3
     for num_split in args.splits:
         tik = time.time()

@@ -245,6 +245,7 @@ def run_elastic(args):
     from ..elastic.snapshot import save_snapshot
     from ..parallel import dist as pdist
     from ..parallel.ddp import DistributedDataParallel
+    from ..utils import config as rtconfig
     from ..utils.log import RankLogger
 
     if "PDE_ELASTIC_STORE" not in os.environ:
@@ -283,7 +284,7 @@ def run_elastic(args):
                 optimizer.load_state_dict(state["opt"])
             if ddp is not None:
                 ddp.remove_hooks()
-            ddp = DistributedDataParallel(model, comm=comm)
+            ddp = DistributedDataParallel(model, comm=comm, **rtconfig.from_args(args).ddp_kwargs())
             commit.save()
             train_data = ShardedLoader(train_set, args.batch_size, size, rank, shuffle=True)
             test_data = ShardedLoader(test_set, args.batch_size, size, rank, shuffle=False)
