@@ -460,7 +460,7 @@ constexpr int kMaxInKernelSplits = 8;  // more slabs per tile: the serial combin
 // K-tiles staged per LDS buffer and consumed per barrier (-DPDE_GEMM_SUB=N to sweep): the MFMAs of kSub
 // consecutive 32-deep K-tiles run between two barriers, each K-tile keeping its own swizzled image.
 #ifndef PDE_GEMM_SUB
-#define PDE_GEMM_SUB 1
+#define PDE_GEMM_SUB 2
 #endif
 constexpr int kSub = PDE_GEMM_SUB;
 template <int BM, int BN>

@@ -78,6 +78,16 @@ def init_distributed(backend: str | None = None, device: str | None = None, time
             init_method = "env://"
         kw = dict(backend=backend, init_method=init_method, rank=rank, world_size=world_size,
                   timeout=datetime.timedelta(seconds=timeout_s))
+        if (init_method == "env://" and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True"
+                and "TORCHELASTIC_RESTART_COUNT" in os.environ):
+            # torchrun restarts reuse the agent's TCPStore (same MASTER_PORT), and torch's env:// handler adds
+            # no per-attempt prefix: a restarted rank could read the PREVIOUS attempt's gloo / RCCL rendezvous
+            # keys of a dead peer ("Connection refused", then a hang in connectFullMesh -- measured on this
+            # container, ~1 restart in 4).  Every attempt gets its own key space.
+            store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world_size,
+                                  is_master=False, timeout=kw["timeout"])
+            kw.pop("init_method")
+            kw["store"] = dist.PrefixStore(f"/pde/attempt_{os.environ['TORCHELASTIC_RESTART_COUNT']}", store)
         if backend == "nccl" and use_gpu:
             kw["device_id"] = dev
         dist.init_process_group(**kw)
