@@ -1093,8 +1093,11 @@ hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
 // small_mn elements (cheap fp32 slabs: the MLP's linears) split further (small_* knobs).
 // PDE_GEMM_* environment variables override the knobs for tuning sweeps (read once).
 struct TilePolicy {
-  long t128_min = 2048, split_target = 512, small_mn = 262144, small_split_target = 512;
-  int split_min_kt = 16, small_split_min_kt = 4;  // r2j sweep (FAST loaders): ResNet-50 4.66 -> 4.48 ms
+  // r2j sweep (FAST loaders): ResNet-50 4.66 -> 4.48 ms; r2m sweep after dgrad/wgrad pairing (a paired
+  // launch already fills the chip with two grids, so each member needs less split-K): split targets
+  // 512 -> 256 blocks, small outputs >= 8 K-tiles per split -- ResNet-50 3.97 -> 3.84 ms, MLP 0.235 -> 0.228 ms
+  long t128_min = 2048, split_target = 256, small_mn = 262144, small_split_target = 256;
+  int split_min_kt = 16, small_split_min_kt = 8;
   TilePolicy() {
     auto env_l = [](const char* n, long& v) { if (const char* e = std::getenv(n)) v = std::atol(e); };
     auto env_i = [](const char* n, int& v) { if (const char* e = std::getenv(n)) v = std::atoi(e); };

@@ -157,3 +157,38 @@ def test_hvd_aborted_communicator_raises(gpu):
         assert torch.equal(hvd.allreduce(t, op=hvd.Sum), t)
     finally:
         hvd.shutdown()
+
+
+def test_rccl_abort_and_reinit_rounds(gpu):
+    """The in-process re-wire's GPU data plane (elastic/rewire.py RoundComm) at world 1: a round's communicator
+    carries stream-ordered all-reduces checked by the host-side liveness wait, is ABORTED (what a survivor does
+    on a peer failure), and the next round builds a fresh communicator from a new unique id on the same device
+    and keeps working -- three rounds in one process."""
+    from pytorch_distributed_examples_amd import _native
+    from pytorch_distributed_examples_amd.elastic.rewire import RoundComm
+
+    C = _native.comm()
+
+    class _Rdzv:  # no membership change published
+        def hosts_updated(self):
+            return False
+
+    for rnd in range(3):
+        rc = RoundComm.__new__(RoundComm)  # the round's data plane only (its gloo control plane needs peers)
+        rc.rdzv, rc.rank, rc.size, rc.device = _Rdzv(), 0, 1, gpu
+        rc.timeout_s, rc.grace_s, rc._steps = 30.0, 2.0, []
+        rc.rccl = C.RcclComm()
+        rc.rccl.init(C.rccl_unique_id(), 0, 1, gpu.index, True)
+        rc.supports_avg = True
+        t = torch.full((4096,), float(rnd + 1), device=gpu)
+        for _ in range(3):
+            rc.allreduce_async(t, avg=True)
+            rc.step_done(lag=1)  # host checks the previous step's event (liveness wait)
+        rc.drain()
+        assert rc.rccl.async_error() in (0, 7)
+        assert torch.equal(t.cpu(), torch.full((4096,), float(rnd + 1)))
+        if rnd < 2:
+            rc.abort()  # survivor path: abort, never destroy
+            rc.rccl = None
+        else:
+            rc.rccl.destroy()  # (RoundComm.close would also tear down the round's gloo group)
