@@ -827,14 +827,15 @@ int bn_blocks(int P, int C, int& rows_per_block) {
 
 }  // namespace
 
-// Fused-finalize grid: row chunks x 64-channel groups, ~512 blocks, >= 32 rows per chunk, <= 64 chunks (r2i: 128 chunks
+// Fused-finalize grid: row chunks x 64-channel groups, ~256 blocks of 512 threads, >= 64 rows per chunk, <= 64 chunks (r2i: 128 chunks
 // made the finalizing tail 0.14 ms/step slower; 64 chunks measure level with the 3-pass form at 106 fewer
 // launches per step)
 // (the finalizing block reads chunks x 2 x 64 partials).
 int bn_fin_grid(int P, int C, int& rpb) {
   const int ncg = (C + kBnCG - 1) / kBnCG;
   static const int kChunks = std::getenv("PDE_BN_CHUNKS") ? std::atoi(std::getenv("PDE_BN_CHUNKS")) : 64;
-  static const int kTarget = std::getenv("PDE_BN_BLOCKS") ? std::atoi(std::getenv("PDE_BN_BLOCKS")) : 512;
+  // r2m sweep at 512 threads per block: 256 blocks (one per CU, 8 waves) 3.83 -> 3.79 ms/step
+  static const int kTarget = std::getenv("PDE_BN_BLOCKS") ? std::atoi(std::getenv("PDE_BN_BLOCKS")) : 256;
   int nrb = std::max(1, std::min(kChunks, kTarget / ncg));
   nrb = std::min(nrb, std::max(1, P / kBnRows));
   rpb = ceil_div(P, nrb);
@@ -869,7 +870,7 @@ int* bn_tickets(int n, hipStream_t s) {
   return t;
 }
 
-const long kBnApplyCap = std::getenv("PDE_BN_APPLY_CAP") ? std::atol(std::getenv("PDE_BN_APPLY_CAP")) : 8192;
+const long kBnApplyCap = std::getenv("PDE_BN_APPLY_CAP") ? std::atol(std::getenv("PDE_BN_APPLY_CAP")) : 2048;
 
 int bn_workspace_blocks(int P, int C) {
   int rpb;
@@ -894,7 +895,7 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
                        momentum, running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C);
   }
   const long nvec = static_cast<long>(P) * C / 8;
-  // one 16-B vector per lane (up to 8192 blocks): a single memory round trip, no grid-stride second trip
+  // (grid cap swept 2048 / 4096 / 8192 blocks: level, r2m)
   hipLaunchKernelGGL(k_bn_apply, dim3(stream_grid(nvec, 256, 1, kBnApplyCap)), dim3(256), 0, s, x, scale_shift,
                      scale_shift + C, res, y, nvec, C, relu);
   return hipGetLastError();
