@@ -1098,6 +1098,9 @@ struct TilePolicy {
   // 512 -> 256 blocks, small outputs >= 8 K-tiles per split -- ResNet-50 3.97 -> 3.84 ms, MLP 0.235 -> 0.228 ms
   long t128_min = 2048, split_target = 256, small_mn = 262144, small_split_target = 256;
   int split_min_kt = 16, small_split_min_kt = 8;
+  // 128x64 tile (64x32 per wave: 25 % less LDS traffic per MFMA than the 64x64 tile's 32x32 wave tiles) for
+  // unpaired GEMMs with at least wide_min 64x64 tiles (0: off)
+  long wide_min = 0;
   TilePolicy() {
     auto env_l = [](const char* n, long& v) { if (const char* e = std::getenv(n)) v = std::atol(e); };
     auto env_i = [](const char* n, int& v) { if (const char* e = std::getenv(n)) v = std::atoi(e); };
@@ -1107,6 +1110,7 @@ struct TilePolicy {
     env_l("PDE_GEMM_SMALL_MN", small_mn);
     env_l("PDE_GEMM_SMALL_SPLIT_TARGET", small_split_target);
     env_i("PDE_GEMM_SMALL_SPLIT_MIN_KT", small_split_min_kt);
+    env_l("PDE_GEMM_WIDE_MIN", wide_min);
   }
 };
 const TilePolicy& tile_policy() {
@@ -1114,10 +1118,10 @@ const TilePolicy& tile_policy() {
   return p;
 }
 
-enum TileCfg { kTile128x32, kTile32x128, kTile128, kTile64 };
+enum TileCfg { kTile128x32, kTile32x128, kTile128, kTile64, kTile128x64 };
 // The tile configuration and split-K count of a GEMM (split-K only where a workspace was provided:
-// a.splitk slabs, never exceeded).
-TileCfg choose_tiles(const GemmArgs& a, int& split) {
+// a.splitk slabs, never exceeded).  `wide`: the 128x64 tile may be chosen (single launches; pairs keep 64x64).
+TileCfg choose_tiles(const GemmArgs& a, int& split, bool wide = false) {
   const TilePolicy& tp = tile_policy();
   const long t128 = static_cast<long>(ceil_div(a.M, 128)) * ceil_div(a.N, 128);
   const long t64 = static_cast<long>(ceil_div(a.M, 64)) * ceil_div(a.N, 64);
@@ -1142,6 +1146,10 @@ TileCfg choose_tiles(const GemmArgs& a, int& split) {
     split = pick_split(t128, 32);
     return kTile128;
   }
+  if (wide && tp.wide_min > 0 && t64 >= tp.wide_min) {
+    split = pick_split(static_cast<long>(ceil_div(a.M, 128)) * ceil_div(a.N, 64), 32);
+    return kTile128x64;
+  }
   split = pick_split(t64, 32);
   return kTile64;
 }
@@ -1149,7 +1157,8 @@ TileCfg choose_tiles(const GemmArgs& a, int& split) {
 template <bool AKC, bool BKC>
 hipError_t dispatch_tiles(const GemmArgs& a, hipStream_t s) {
   int split = 1;
-  switch (choose_tiles(a, split)) {
+  switch (choose_tiles(a, split, true)) {
+    case kTile128x64: return launch_cfg<128, 64, 32, 2, 2, AKC, BKC>(a, s, split);
     case kTile128x32: return launch_cfg<128, 32, 32, 4, 1, AKC, BKC>(a, s, split);
     case kTile32x128: return launch_cfg<32, 128, 32, 1, 4, AKC, BKC>(a, s, split);
     case kTile128: return launch_cfg<128, 128, 32, 2, 2, AKC, BKC>(a, s, split);
