@@ -118,18 +118,53 @@ void gemm_pair_begin() {
   g_collect = true;
 }
 
+// Deferred weight-gradient reductions (gemm_pair_end(defer=true)): the second GEMM of a pair (a weight
+// gradient accumulated into .grad, read only by the optimizer / all-reduce) leaves its split-K slabs for
+// ONE batched reduce launch, gemm_flush_deferred(), at the end of backward (ops/functional.py).  The slabs
+// stay alive here until then; the flush runs on the stream that produced them.
+struct DeferredReduce {
+  pde::ReduceJob job;
+  Tensor ws;
+};
+std::vector<DeferredReduce> g_deferred;
+
 // Launch what was collected (2 GEMMs: one paired launch; fewer: ordinary launches).  abort=true drops it.
-void gemm_pair_end(bool abort) {
+// defer=true: the second GEMM's slab reduction is deferred to gemm_flush_deferred (returns true if it was).
+bool gemm_pair_end(bool abort, bool defer) {
   g_collect = false;
   std::vector<PendingGemm> q;
   q.swap(g_pending);
-  if (abort) return;
+  if (abort) return false;
   if (q.size() == 2) {
-    check(pde::gemm_bf16_pair(q[0].args, q[1].args, cur_stream()), "gemm_pair");
+    int sp1 = 0;
+    check(pde::gemm_bf16_pair(q[0].args, q[1].args, cur_stream(), defer ? &sp1 : nullptr), "gemm_pair");
+    if (sp1 > 1) {
+      const pde::GemmArgs& a = q[1].args;
+      pde::ReduceJob j{};
+      j.workspace = a.workspace; j.out = a.out; j.bias_grad = a.bias_grad; j.ldo = a.ldo;
+      j.M = a.M; j.N = a.N; j.splits = sp1; j.epi = a.epi;
+      j.oihw_ci = a.oihw_ci; j.oihw_rs = a.oihw_rs; j.oihw_cp = a.oihw_cp; j.bias_col = a.bias_col;
+      g_deferred.push_back({j, q[1].ws});
+      return true;
+    }
   } else {
     for (auto& p : q) check(pde::gemm_bf16(p.args, cur_stream()), "gemm");
   }
+  return false;
 }
+
+// One batched launch for every deferred reduction (no-op when none is pending).
+int gemm_flush_deferred() {
+  std::vector<DeferredReduce> d;
+  d.swap(g_deferred);
+  if (d.empty()) return 0;
+  std::vector<pde::ReduceJob> jobs;
+  jobs.reserve(d.size());
+  for (auto& x : d) jobs.push_back(x.job);
+  check(pde::gemm_reduce_jobs(jobs.data(), static_cast<int>(jobs.size()), cur_stream()), "gemm_reduce_jobs");
+  return static_cast<int>(d.size());  // the slabs are released after the launch (stream-ordered reuse)
+}
+int gemm_deferred_count() { return static_cast<int>(g_deferred.size()); }
 
 // ------------------------------------------------------------------------------------------------
 // Dense GEMMs (nn.Linear)
@@ -889,7 +924,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_dgrad_out", &linear_dgrad_out);
   m.def("linear_wgrad_bias", &linear_wgrad_bias);
   m.def("gemm_pair_begin", &gemm_pair_begin);
-  m.def("gemm_pair_end", &gemm_pair_end, py::arg("abort") = false);
+  m.def("gemm_pair_end", &gemm_pair_end, py::arg("abort") = false, py::arg("defer") = false);
+  m.def("gemm_flush_deferred", &gemm_flush_deferred);
+  m.def("gemm_deferred_count", &gemm_deferred_count);
   m.def("cast_rows_ones", &cast_rows_ones);
   m.def("ce_bwd", &ce_bwd);
   m.def("log_softmax_fwd", &log_softmax_fwd);

@@ -69,8 +69,21 @@ struct GemmArgs {
 hipError_t gemm_bf16(const GemmArgs& args, hipStream_t stream);
 // Two independent GEMMs (a layer's dgrad and wgrad) in one launch when both run on the 64x64 FAST tile, their
 // split-K slab reductions in one more; otherwise two ordinary gemm_bf16 launches (problem 0 first).
-hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t stream);
+// defer_split1 != nullptr: problem 1's split-K slab reduction is NOT launched; its split count is returned
+// there (0 / 1: nothing deferred) and the caller reduces it later with gemm_reduce_jobs.
+hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t stream, int* defer_split1 = nullptr);
 bool gemm_pair_enabled();
+// A deferred split-K slab reduction (vector form: N % 4 == 0, 16-B aligned slabs) with the fp32 epilogue of
+// its GEMM (accumulate, OIHW remap, ones-column bias gradient).
+struct ReduceJob {
+  float* workspace;
+  void* out;
+  float* bias_grad;
+  long ldo;
+  int M, N, splits, epi, oihw_ci, oihw_rs, oihw_cp, bias_col;
+};
+constexpr int kMaxReduceJobs = 24;
+hipError_t gemm_reduce_jobs(const ReduceJob* jobs, int n, hipStream_t stream);
 
 // ---------------------------------------------------------------------------------------------
 // Elementwise / layout (elementwise.hip)

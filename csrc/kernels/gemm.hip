@@ -30,6 +30,7 @@
 //     cdna_hip_programming.md §5 "in-launch split-K reduction") -- measured slower here, see split_tickets.
 //   * Epilogue options: bias, ReLU, ReLU-mask (backward), fp32 / bf16 output, accumulate, and an OIHW
 //     remap that writes a conv weight gradient straight into the parameter's [Co][Ci][R][S] fp32 grad.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -938,6 +939,33 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce4_pair(GemmArgs a0, int
     splitk_reduce4_block<L1>(a1, s1, blockIdx.x - nb0);
 }
 
+// Deferred weight-gradient slab reductions, batched: up to kMaxReduceJobs split-K GEMMs whose outputs are
+// only read later (weight gradients accumulated into .grad) reduce in ONE launch at the end of backward
+// instead of one launch per layer.  The job table travels by value in the kernel arguments (no host
+// buffer the hipGraph would have to keep alive); block b reduces job j for b in [first[j], first[j+1]).
+struct ReduceJobs {
+  ReduceJob job[kMaxReduceJobs];
+  int first[kMaxReduceJobs + 1];
+  int n;
+};
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_jobs(ReduceJobs t) {
+  int j = 0;
+  while (j + 1 < t.n && static_cast<int>(blockIdx.x) >= t.first[j + 1]) ++j;
+  const ReduceJob& r = t.job[j];
+  GemmArgs a{};
+  a.M = r.M; a.N = r.N; a.out = r.out; a.ldo = r.ldo; a.epi = r.epi; a.workspace = r.workspace;
+  a.oihw_ci = r.oihw_ci; a.oihw_rs = r.oihw_rs; a.oihw_cp = r.oihw_cp;
+  a.bias_grad = r.bias_grad; a.bias_col = r.bias_col;
+  // the same slab-lane count as the immediate reduction of this split count: identical summation order
+  const int b = blockIdx.x - t.first[j];
+  if (r.splits <= 2)
+    splitk_reduce4_block<1>(a, r.splits, b);
+  else if (r.splits <= 16)
+    splitk_reduce4_block<4>(a, r.splits, b);
+  else
+    splitk_reduce4_block<16>(a, r.splits, b);
+}
+
 // Per-tile arrival counters for the in-kernel split-K reduction: one zeroed device array per GPU, handed
 // out in rolling windows (consecutive launches on one stream may share slots -- each launch leaves its
 // tickets at 0 -- and the window keeps launches on different streams apart).  Allocated on first use
@@ -1220,12 +1248,29 @@ hipError_t gemm_bf16(const GemmArgs& a, hipStream_t s) {
   return dispatch_tiles<false, false>(a, s);
 }
 
+hipError_t gemm_reduce_jobs(const ReduceJob* jobs, int n, hipStream_t s) {
+  for (int base = 0; base < n; base += kMaxReduceJobs) {
+    ReduceJobs t{};
+    t.n = std::min(kMaxReduceJobs, n - base);
+    int blocks = 0;
+    for (int j = 0; j < t.n; ++j) {
+      t.job[j] = jobs[base + j];
+      t.first[j] = blocks;
+      blocks += ceil_div(static_cast<long>(t.job[j].M) * t.job[j].N / 4, 256 / reduce_lanes(t.job[j].splits));
+    }
+    t.first[t.n] = blocks;
+    hipLaunchKernelGGL(gemm_splitk_reduce_jobs, dim3(blocks), dim3(256), 0, s, t);
+  }
+  return hipGetLastError();
+}
+
 bool gemm_pair_enabled() {
   static const bool on = !(std::getenv("PDE_GEMM_PAIR") && std::getenv("PDE_GEMM_PAIR")[0] == '0');
   return on;
 }
 
-hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
+hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s, int* defer_split1) {
+  if (defer_split1 != nullptr) *defer_split1 = 0;
   PairDims d{};
   int sp0 = 1, sp1 = 1;
   const bool ok = gemm_pair_enabled() &&
@@ -1251,6 +1296,10 @@ hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s)
     hipError_t e = gemm_bf16(a0, s);
     if (e != hipSuccess) return e;
     return gemm_bf16(a1, s);
+  }
+  if (defer_split1 != nullptr && sp1 > 1) {  // problem 1's slabs are reduced later by gemm_reduce_jobs
+    *defer_split1 = sp1;
+    sp1 = 1;
   }
   if (sp0 > 1 && sp1 > 1) {
     const int l0 = reduce_lanes(sp0), l1 = reduce_lanes(sp1);

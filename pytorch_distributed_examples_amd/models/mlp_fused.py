@@ -90,7 +90,7 @@ class FusedMLP:
                     C.linear_wgrad_bias(dy, acts[i][:, :L.in_features + 1], gw, gb, accumulate)
             elif i > 0:
                 # dgrad + weight/bias gradient as ONE paired GEMM launch (dgrad tiles first)
-                with OF.gemm_pair():
+                with OF.gemm_pair(defer_second=True):
                     C.linear_dgrad_out(dy, OF._bf16_weight(L.weight), acts[i][:, :L.in_features], dys[i - 1])
                     C.linear_wgrad_bias(dy, acts[i][:, :L.in_features + 1], gw, gb, accumulate)
                 dy = dys[i - 1]
@@ -100,8 +100,8 @@ class FusedMLP:
             if i > 0:
                 C.linear_dgrad_out(dy, OF._bf16_weight(L.weight), acts[i][:, :L.in_features], dys[i - 1])
                 dy = dys[i - 1]
-        if side:
-            streams.join(x.device)
+        # the deferred weight-gradient reductions: one batched launch (and the side stream, if used)
+        streams.join(x.device)
         return loss
 
     def launches_per_step(self) -> int:

@@ -103,14 +103,20 @@ class gemm_pair:
     """Context manager: the (at most two) GEMM ops issued inside are launched together as ONE paired launch
     when the block exits (``pde::gemm_bf16_pair``: the first op's tiles are scheduled first; both grids fill
     the chip together and pay one launch boundary).  Ops inside must not read each other's outputs; non-GEMM
-    kernels issued inside run immediately (before the pair).  ``PDE_GEMM_PAIR=0`` launches them one by one."""
+    kernels issued inside run immediately (before the pair).  ``PDE_GEMM_PAIR=0`` launches them one by one.
+    ``defer_second=True``: the second op is a weight gradient accumulated into ``.grad``; its split-K slab
+    reduction joins the step's single batched reduction (:func:`.streams.flush_deferred`)."""
+
+    def __init__(self, defer_second: bool = False):
+        self.defer = defer_second and streams.defer_enabled()
 
     def __enter__(self):
         _C().gemm_pair_begin()
         return self
 
     def __exit__(self, exc_type, *exc):
-        _C().gemm_pair_end(exc_type is not None)
+        if _C().gemm_pair_end(exc_type is not None, self.defer):
+            streams.note_deferred_reduce()
 
 
 # ---------------------------------------------------------------------------------------------
@@ -250,7 +256,7 @@ class _LinearFn(torch.autograd.Function):
         bsink = _grad_sink(bias) if ctx.has_bias and ctx.needs_input_grad[2] else None
         if wsink is not None and ctx.needs_input_grad[0] and not streams.active_for(dy):
             # dgrad + wgrad as ONE paired GEMM launch (the dgrad's tiles first: it feeds the next layer)
-            with gemm_pair():
+            with gemm_pair(defer_second=True):
                 dx = _C().linear_dgrad(dy, wb, x if ctx.mask_input_grad else None)
                 _C().linear_wgrad(dy, x, wsink, True)
             if bsink is not None:
@@ -339,7 +345,7 @@ class _Conv2dFn(torch.autograd.Function):
         paired = wsink is not None and ctx.needs_input_grad[0] and not side
         if paired:
             # dgrad + wgrad as ONE paired GEMM launch (dgrad tiles first); the dgrad op is issued first
-            pair = gemm_pair()
+            pair = gemm_pair(defer_second=True)
             pair.__enter__()
         if ctx.needs_input_grad[0]:
             # residual fork: the other branch's gradient (stored by the block's last BatchNorm) is added in the

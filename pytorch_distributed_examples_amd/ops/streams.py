@@ -100,8 +100,50 @@ def _join_onto(idx: int, stream: torch.cuda.Stream) -> None:
         _PENDING[idx] = False
 
 
+# ---- deferred weight-gradient reductions ---------------------------------------------------------------
+# The paired backward GEMMs (ops/functional.py ``gemm_pair(defer=True)``) leave the split-K slab reduction of
+# their weight gradient pending; ONE batched launch reduces all of them (pde::gemm_reduce_jobs) when the
+# gradients are first needed: at the end of the backward pass (engine final callback) or earlier at any
+# gradient reader that joins (DDP bucket launch, Horovod hook, fused optimizer).  That replaces one reduce
+# launch per layer with one per step.  ``PDE_DEFER_WGRAD_REDUCE=0`` reduces every pair right away.
+_DEFER_ENABLED = [os.environ.get("PDE_DEFER_WGRAD_REDUCE", "1") != "0"]
+_DEFERRED: dict = {"stream": None}
+
+
+def defer_enabled() -> bool:
+    return _DEFER_ENABLED[0]
+
+
+def note_deferred_reduce() -> None:
+    """A weight-gradient reduction was deferred on the current stream (queues the end-of-backward flush)."""
+    if _DEFERRED["stream"] is None:
+        _DEFERRED["stream"] = torch.cuda.current_stream()
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(flush_deferred)
+        except RuntimeError:  # not inside a backward pass: the launch sequence flushes explicitly
+            pass
+
+
+def flush_deferred(stream: torch.cuda.Stream | None = None) -> None:
+    """Launch the pending weight-gradient reductions (on the stream that produced them); ``stream`` then
+    waits for them when it is a different stream."""
+    s = _DEFERRED["stream"]
+    if s is None:
+        return
+    _DEFERRED["stream"] = None
+    from .. import _native
+
+    with torch.cuda.stream(s):
+        _native.C().gemm_flush_deferred()
+    if stream is not None and stream != s:
+        stream.wait_stream(s)
+
+
 def join(device=None, stream: torch.cuda.Stream | None = None) -> None:
-    """Make ``stream`` (default: the current stream of ``device``) wait for all side-stream work so far."""
+    """Make ``stream`` (default: the current stream of ``device``) see every gradient issued so far: pending
+    deferred weight-gradient reductions are launched, side-stream work is waited for."""
+    if _DEFERRED["stream"] is not None:
+        flush_deferred(stream if stream is not None else torch.cuda.current_stream())
     if not _PENDING:
         return
     if device is None:

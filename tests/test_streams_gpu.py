@@ -197,3 +197,46 @@ def test_linear_dgrad_wgrad_pair_bitwise(gpu, batch):
     ref_gw = dy.float().t() @ x_ext[:, :k].float()
     assert ((outs[1][1] - ref_gw).norm() / ref_gw.norm()).item() < 1e-3
     assert torch.allclose(outs[1][2], dy.float().sum(0), rtol=1e-3, atol=1e-2)
+
+
+# ---- deferred, batched weight-gradient reductions (ops/streams.py flush_deferred) ------------------------------
+def _with_defer(flag, fn):
+    old = streams._DEFER_ENABLED[0]
+    streams._DEFER_ENABLED[0] = flag
+    try:
+        return fn()
+    finally:
+        streams._DEFER_ENABLED[0] = old
+
+
+def test_deferred_wgrad_reduce_bitwise_resnet(gpu):
+    """ResNet-50 (both shards, batch 32 at 64px: split-K weight gradients in every stage) -- gradients after
+    backward() with the per-step batched reduction equal the per-layer reductions bit for bit, and nothing is
+    left pending after backward returns."""
+    torch.manual_seed(0)
+    m = ResNet50().to(gpu)
+    x = torch.randn(32, 3, 64, 64, device=gpu)
+    t = torch.randn(32, 1000, device=gpu)
+    g_now = _with_defer(False, lambda: _grads(m, x, t, OF.mse_loss, side=False))
+    g_def = _with_defer(True, lambda: _grads(m, x, t, OF.mse_loss, side=False))
+    assert OF._C().gemm_deferred_count() == 0
+    for (n, _), a, b in zip(m.named_parameters(), g_now, g_def):
+        assert torch.equal(a, b), n
+
+
+def test_deferred_wgrad_reduce_bitwise_fused_mlp(gpu):
+    from pytorch_distributed_examples_amd.models.mlp_fused import FusedMLP
+
+    torch.manual_seed(0)
+    m = MLP(hidden_layers=5, features=1024).to(gpu)
+    f = FusedMLP(m)
+    x = torch.randn(128, 1, 28, 28, device=gpu)
+    y = torch.randint(0, 10, (128,), device=gpu)
+    out = []
+    for flag in (False, True):
+        _with_defer(flag, lambda: f.forward_backward(x, y))
+        torch.cuda.synchronize()
+        out.append([p.grad.clone() for p in m.parameters()])
+    assert OF._C().gemm_deferred_count() == 0
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
