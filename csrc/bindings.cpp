@@ -292,15 +292,23 @@ void cast_rows_ones(const Tensor& x, Tensor& out) {
   check(pde::cast_rows_bf16(x.data_ptr<float>(), B, K, u16(out), out.stride(0), 1, cur_stream()), "cast_rows_ones");
 }
 
-// (mean cross-entropy loss, d loss / d logits as bf16) in one launch
-std::vector<Tensor> ce_fused(const Tensor& x, const Tensor& tgt) {
+// (mean cross-entropy loss, d loss / d logits as bf16) in one launch.  dx_out: a [B, >= V] bf16 row view to
+// write d logits into (its columns past V are left as they are, e.g. the zero padding of a K = 16 operand).
+std::vector<Tensor> ce_fused(const Tensor& x, const Tensor& tgt, const optional<Tensor>& dx_out) {
   CHECK_IN(x); CHECK_IN(tgt);
   TORCH_CHECK(tgt.scalar_type() == at::kLong, "targets must be int64");
   const int B = x.size(0), V = x.size(1);
   Tensor loss = at::empty({}, x.options().dtype(at::kFloat));
-  Tensor dx = at::empty({B, V}, x.options().dtype(at::kBFloat16));
+  Tensor dx;
+  if (dx_out.has_value() && dx_out->defined()) {
+    dx = *dx_out;
+    CHECK_ROWS(dx); CHECK_BF16(dx);
+    TORCH_CHECK(dx.size(0) == B && dx.stride(0) >= V, "ce_fused: dx_out must be [B, >= V] rows");
+  } else {
+    dx = at::empty({B, V}, x.options().dtype(at::kBFloat16));
+  }
   check(pde::ce_fused(x.data_ptr(), x.scalar_type() == at::kFloat, tgt.data_ptr<int64_t>(), B, V,
-                      loss.data_ptr<float>(), u16(dx), cur_stream()),
+                      loss.data_ptr<float>(), u16(dx), static_cast<int>(dx.stride(0)), cur_stream()),
         "ce_fused");
   return {loss, dx};
 }
@@ -919,7 +927,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("accumulate") = false);
   m.def("relu_bwd", &relu_bwd);
   m.def("ce_fwd", &ce_fwd);
-  m.def("ce_fused", &ce_fused);
+  m.def("ce_fused", &ce_fused, py::arg("x"), py::arg("tgt"), py::arg("dx_out") = py::none());
   m.def("linear_fwd_out", &linear_fwd_out);
   m.def("linear_dgrad_out", &linear_dgrad_out);
   m.def("linear_wgrad_bias", &linear_wgrad_bias);

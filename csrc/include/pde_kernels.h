@@ -130,7 +130,7 @@ hipError_t ce_bwd(const void* x, int x_f32, const int64_t* tgt, const float* lse
                   int mode, void* dx, int dx_f32, hipStream_t s);
 // Mean cross-entropy and its input gradient in one launch (mode 0 of ce_fwd/ce_bwd with d loss = 1):
 // loss[0] = mean_b (lse_b - x[b, t_b]),  dx[b, v] = (softmax(x_b)_v - [v == t_b]) / B  (bf16).
-hipError_t ce_fused(const void* x, int x_f32, const int64_t* tgt, int B, int V, float* loss, uint16_t* dx,
+hipError_t ce_fused(const void* x, int x_f32, const int64_t* tgt, int B, int V, float* loss, uint16_t* dx, int ldx,
                     hipStream_t s);
 hipError_t log_softmax_fwd(const void* x, int x_f32, int B, int V, float* y, hipStream_t s);
 hipError_t log_softmax_bwd(const float* dy, const float* y, int B, int V, void* dx, int dx_f32, hipStream_t s);

@@ -84,7 +84,7 @@ __global__ void k_ce_bwd(const void* x, int f32, const int64_t* __restrict__ tgt
 
 // Fused mean cross-entropy forward + backward (one block; thread per row)
 __global__ void k_ce_fused(const void* x, int f32, const int64_t* __restrict__ tgt, int B, int V,
-                           float* __restrict__ loss, uint16_t* __restrict__ dx) {
+                           float* __restrict__ loss, uint16_t* __restrict__ dx, int ldx) {
   __shared__ float red[16];
   const float inv_b = 1.f / static_cast<float>(B);
   float acc = 0.f;
@@ -93,7 +93,8 @@ __global__ void k_ce_fused(const void* x, int f32, const int64_t* __restrict__ t
     const int t = static_cast<int>(tgt[b]);
     const float l = row_lse(x, f32, base, V);
     acc += l - ld(x, f32, base + t);
-    for (int v = 0; v < V; ++v) dx[base + v] = f2bf((__expf(ld(x, f32, base + v) - l) - (v == t ? 1.f : 0.f)) * inv_b);
+    uint16_t* drow = dx + static_cast<long>(b) * ldx;  // (row pitch ldx >= V: columns past V are untouched)
+    for (int v = 0; v < V; ++v) drow[v] = f2bf((__expf(ld(x, f32, base + v) - l) - (v == t ? 1.f : 0.f)) * inv_b);
   }
   const float tot = block_sum(acc, red);
   if (threadIdx.x == 0) loss[0] = tot * inv_b;
@@ -175,9 +176,9 @@ hipError_t ce_bwd(const void* x, int f32, const int64_t* tgt, const float* lse, 
                      mode, dx, dx_f32);
   return hipGetLastError();
 }
-hipError_t ce_fused(const void* x, int f32, const int64_t* tgt, int B, int V, float* loss, uint16_t* dx,
+hipError_t ce_fused(const void* x, int f32, const int64_t* tgt, int B, int V, float* loss, uint16_t* dx, int ldx,
                     hipStream_t s) {
-  hipLaunchKernelGGL(k_ce_fused, dim3(1), dim3(kLossThreads), 0, s, x, f32, tgt, B, V, loss, dx);
+  hipLaunchKernelGGL(k_ce_fused, dim3(1), dim3(kLossThreads), 0, s, x, f32, tgt, B, V, loss, dx, ldx);
   return hipGetLastError();
 }
 hipError_t log_softmax_fwd(const void* x, int f32, int B, int V, float* y, hipStream_t s) {

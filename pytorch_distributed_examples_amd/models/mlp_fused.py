@@ -56,7 +56,10 @@ class FusedMLP:
                 acts.append(h)
             logits = torch.empty(B, self.layers[-1].out_features, dtype=torch.float32, device=dev)
             dys = [torch.empty(B, L.out_features, **bf) for L in self.layers[:-1]]
-            self._bufs[key] = (acts, logits, dys)
+            # d logits with its row padded to a multiple of 8 (zero columns, never written): the last layer's
+            # dgrad then has K = 16 instead of 10 and runs on the FAST GEMM path with the zero-padded weight copy
+            dlog = torch.zeros(B, _pad8(self.layers[-1].out_features), **bf)
+            self._bufs[key] = (acts, logits, dys, dlog)
         return self._bufs[key]
 
     def _grads(self, L):
@@ -71,14 +74,16 @@ class FusedMLP:
         added) into each parameter's ``.grad``."""
         C = _native.C()
         B = x.shape[0]
-        acts, logits, dys = self._buffers(B, x.device)
+        acts, logits, dys, dlog = self._buffers(B, x.device)
         C.cast_rows_ones(x.reshape(B, -1).float().contiguous(), acts[0])
         last = len(self.layers) - 1
         for i, L in enumerate(self.layers):
             w = OF._bf16_weight(L.weight)
             out = acts[i + 1][:, :L.out_features] if i < last else logits
             C.linear_fwd_out(acts[i][:, :L.in_features], w, L.bias.detach(), i < last, out)
-        loss, dy = C.ce_fused(logits, y.long().contiguous())
+        nout = self.layers[-1].out_features
+        loss, dy = C.ce_fused(logits, y.long().contiguous(), dlog)
+        dy = dlog[:, :nout]
         side = streams.active_for(x)
         for i in range(last, -1, -1):
             L = self.layers[i]
@@ -90,8 +95,12 @@ class FusedMLP:
                     C.linear_wgrad_bias(dy, acts[i][:, :L.in_features + 1], gw, gb, accumulate)
             elif i > 0:
                 # dgrad + weight/bias gradient as ONE paired GEMM launch (dgrad tiles first)
+                wpad = OF._maintained(L.weight, "bf16_pad") if i == last else None
                 with OF.gemm_pair(defer_second=True):
-                    C.linear_dgrad_out(dy, OF._bf16_weight(L.weight), acts[i][:, :L.in_features], dys[i - 1])
+                    if wpad is not None:  # K padded to 16: zero columns of d logits x zero rows of the weight
+                        C.linear_dgrad_out(dlog, wpad, acts[i][:, :L.in_features], dys[i - 1])
+                    else:
+                        C.linear_dgrad_out(dy, OF._bf16_weight(L.weight), acts[i][:, :L.in_features], dys[i - 1])
                     C.linear_wgrad_bias(dy, acts[i][:, :L.in_features + 1], gw, gb, accumulate)
                 dy = dys[i - 1]
                 continue

@@ -183,7 +183,15 @@ def maintain_compute_copies(p: torch.Tensor):
             d["conv_fwd"] = torch.empty(cop, r * s * cp, dtype=torch.bfloat16, device=p.device)
             d["conv_dgrad"] = torch.empty(cp, r * s * cop, dtype=torch.bfloat16, device=p.device)
     elif getattr(p, "_pde_linear", False) and p.dim() == 2:
-        d["bf16"] = torch.empty(p.shape, dtype=torch.bfloat16, device=p.device)
+        out_f = p.shape[0]
+        if out_f % 8 == 0:
+            d["bf16"] = torch.empty(p.shape, dtype=torch.bfloat16, device=p.device)
+        else:
+            # rows padded to a multiple of 8 with zeros (written once, never by the optimizer): the dgrad GEMM
+            # can take the padded copy as a K = pad8(out) operand on the FAST path (models/mlp_fused.py)
+            pad = torch.zeros(pad8(out_f), p.shape[1], dtype=torch.bfloat16, device=p.device)
+            d["bf16_pad"] = pad
+            d["bf16"] = pad[:out_f]
     else:
         return None
     _derive_copies(p, d)
