@@ -96,7 +96,7 @@ class FusedMLP:
             elif i > 0:
                 # dgrad + weight/bias gradient as ONE paired GEMM launch (dgrad tiles first)
                 wpad = OF._maintained(L.weight, "bf16_pad") if i == last else None
-                with OF.gemm_pair(defer_second=True):
+                with OF.gemm_pair(defer_second=True, flush_by_caller=True):
                     if wpad is not None:  # K padded to 16: zero columns of d logits x zero rows of the weight
                         C.linear_dgrad_out(dlog, wpad, acts[i][:, :L.in_features], dys[i - 1])
                     else:

@@ -107,8 +107,9 @@ class gemm_pair:
     ``defer_second=True``: the second op is a weight gradient accumulated into ``.grad``; its split-K slab
     reduction joins the step's single batched reduction (:func:`.streams.flush_deferred`)."""
 
-    def __init__(self, defer_second: bool = False):
+    def __init__(self, defer_second: bool = False, flush_by_caller: bool = False):
         self.defer = defer_second and streams.defer_enabled()
+        self.flush_by_caller = flush_by_caller
 
     def __enter__(self):
         _C().gemm_pair_begin()
@@ -116,7 +117,7 @@ class gemm_pair:
 
     def __exit__(self, exc_type, *exc):
         if _C().gemm_pair_end(exc_type is not None, self.defer):
-            streams.note_deferred_reduce()
+            streams.note_deferred_reduce(self.flush_by_caller)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -114,14 +114,18 @@ def defer_enabled() -> bool:
     return _DEFER_ENABLED[0]
 
 
-def note_deferred_reduce() -> None:
-    """A weight-gradient reduction was deferred on the current stream (queues the end-of-backward flush)."""
+def note_deferred_reduce(flush_by_caller: bool = False) -> None:
+    """A weight-gradient reduction was deferred on the current stream: queue the end-of-backward flush.
+    Outside a regular autograd backward pass (e.g. a distributed-autograd engine that takes no final callbacks)
+    it is flushed right away, unless ``flush_by_caller`` (an explicit launch sequence that joins itself)."""
     if _DEFERRED["stream"] is None:
         _DEFERRED["stream"] = torch.cuda.current_stream()
+        if flush_by_caller:
+            return
         try:
             torch.autograd.Variable._execution_engine.queue_callback(flush_deferred)
-        except RuntimeError:  # not inside a backward pass: the launch sequence flushes explicitly
-            pass
+        except RuntimeError:  # no backward pass to hook: never leave gradients unreduced
+            flush_deferred()
 
 
 def flush_deferred(stream: torch.cuda.Stream | None = None) -> None:
