@@ -79,8 +79,10 @@ def test_fused_mlp_side_stream_bitwise(gpu):
 
 
 def test_resnet_graph_step_with_side_stream(gpu):
-    """A captured training step (forward, backward with forked wgrads, SGD) replays to the same weights as
-    the same steps run eagerly on one stream."""
+    """A captured training step (forward, backward with the default paired dgrad + wgrad launches and the
+    deferred batched wgrad reduction, SGD) replays to the same weights as the same steps run eagerly.  (With
+    PDE_WGRAD_STREAM=1 the same test covers the side-stream fork / join inside the capture: passed on MI355X
+    while that was the default, r2k.)"""
     from pytorch_distributed_examples_amd.utils.graph import CapturedStep
 
     torch.manual_seed(0)
