@@ -414,6 +414,11 @@ Tensor cast_f32(const Tensor& x) {
   check(pde::cast_bf16_f32(u16(x), y.data_ptr<float>(), x.numel(), cur_stream()), "cast_f32");
   return y;
 }
+void cast_f32_into(const Tensor& x, Tensor& y) {
+  CHECK_IN(x); CHECK_BF16(x); CHECK_IN(y); CHECK_F32(y);
+  TORCH_CHECK(x.numel() == y.numel(), "cast_f32_into: size mismatch");
+  check(pde::cast_bf16_f32(u16(x), y.data_ptr<float>(), x.numel(), cur_stream()), "cast_f32_into");
+}
 Tensor nchw_to_nhwc(const Tensor& x, int Cp) {
   CHECK_IN(x); CHECK_F32(x);
   const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
@@ -812,9 +817,10 @@ Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, 
   CHECK_IN(images); CHECK_IN(tgt); CHECK_IN(params); CHECK_IN(rng); CHECK_IN(grads);
   pde::XgmiView xv{};
   const bool have_xv = xgmi_view.has_value();
-  if (have_xv) {  // XgmiAllreduce.view(): base[8], state, timeout_ticks, flag_bytes, slot_bytes, rank, size, blocks
+  if (have_xv) {  // XgmiAllreduce.view(): base[8], state, timeout_ticks, flag_bytes, slot_bytes, rank, size, blocks,
+                  // read_delay_ticks
     const auto& w = *xgmi_view;
-    TORCH_CHECK(w.size() == pde::kXgmiMaxRanks + 7, "cnn_train: malformed xgmi view");
+    TORCH_CHECK(w.size() == pde::kXgmiMaxRanks + 8, "cnn_train: malformed xgmi view");
     for (int r = 0; r < pde::kXgmiMaxRanks; ++r) xv.base[r] = reinterpret_cast<char*>(w[r]);
     xv.state = reinterpret_cast<uint32_t*>(w[8]);
     xv.timeout_ticks = static_cast<uint64_t>(w[9]);
@@ -823,6 +829,7 @@ Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, 
     xv.rank = static_cast<int>(w[12]);
     xv.size = static_cast<int>(w[13]);
     xv.blocks = static_cast<int>(w[14]);
+    xv.read_delay_ticks = static_cast<uint64_t>(w[15]);
     TORCH_CHECK(!accumulate, "cnn_train: the xGMI gradient exchange replaces accumulation");
   }
   CHECK_F32(images); CHECK_F32(params); CHECK_F32(grads);
@@ -916,6 +923,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cast_bf16", &cast_bf16);
   m.def("cast_bf16_into", &cast_bf16_into);
   m.def("cast_f32", &cast_f32);
+  m.def("cast_f32_into", &cast_f32_into);
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
   m.def("conv_layout_table", &conv_layout_table, py::arg("ws"), py::arg("fwds"), py::arg("dgrads"),
         py::arg("cps"), py::arg("cops"));
@@ -944,6 +952,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("optim_table", &optim_table);
   m.def("optim_step", &optim_step);
   m.def("bn_fwd", &bn_fwd);
+  // 1 if a one-launch BatchNorm wait timed out since the last reset (synchronises the device)
+  m.def("bn_error", [](bool reset) { return pde::bn_error(reset ? 1 : 0); }, py::arg("reset") = true);
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("mean"), py::arg("invstd"),
         py::arg("gamma"), py::arg("relu"), py::arg("want_dres"), py::arg("dg_out") = py::none(),

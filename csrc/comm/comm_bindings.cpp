@@ -5,11 +5,13 @@
 
 #include "comm_manager.h"
 #include "fusion_engine.h"
+#include "p2p_ring.h"
 #include "xgmi_allreduce.h"
 
 namespace {
 
 using pde::FusionEngine;
+using pde::P2PRing;
 using pde::RcclComm;
 using pde::XgmiAllreduce;
 
@@ -144,14 +146,38 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              w.push_back(v.rank);
              w.push_back(v.size);
              w.push_back(v.blocks);
+             w.push_back(static_cast<int64_t>(v.read_delay_ticks));
              return w;
            })
+      .def("set_read_delay_us", &XgmiAllreduce::set_read_delay_us)
       .def("error", [](XgmiAllreduce& x) { py::gil_scoped_release nogil; return x.error(); })
       .def("close", [](XgmiAllreduce& x) { py::gil_scoped_release nogil; x.close(); })
       .def_property_readonly("rank", &XgmiAllreduce::rank)
       .def_property_readonly("size", &XgmiAllreduce::size)
       .def_property_readonly("max_bytes", &XgmiAllreduce::max_bytes)
       .def_property_readonly("calls", &XgmiAllreduce::calls);
+
+  py::class_<P2PRing, std::shared_ptr<P2PRing>>(m, "P2PRing")
+      .def(py::init<int, int64_t, double>(), py::arg("device"), py::arg("slot_bytes"), py::arg("timeout_s") = 60.0)
+      .def("ipc_handle", [](P2PRing& r) { return py::bytes(r.ipc_handle()); })
+      .def("open", [](P2PRing& r, py::bytes h) { r.open(std::string(h)); })
+      // both stream-ordered on the caller's CURRENT stream, hipGraph-capturable; raw bytes of the tensor
+      .def("send",
+           [](P2PRing& r, const at::Tensor& t) {
+             check_gpu(t);
+             r.send(t.data_ptr(), static_cast<int64_t>(t.numel() * t.element_size()), cur(t));
+           })
+      .def("recv",
+           [](P2PRing& r, at::Tensor& t) {
+             check_gpu(t);
+             r.recv(t.data_ptr(), static_cast<int64_t>(t.numel() * t.element_size()), cur(t));
+             return t;
+           })
+      .def("error", [](P2PRing& r) { py::gil_scoped_release nogil; return r.error(); })
+      .def("close", [](P2PRing& r) { py::gil_scoped_release nogil; r.close(); })
+      .def_property_readonly("slot_bytes", &P2PRing::slot_bytes)
+      .def_property_readonly("sent", &P2PRing::sent)
+      .def_property_readonly("received", &P2PRing::received);
 
   py::class_<FusionEngine, std::shared_ptr<FusionEngine>>(m, "FusionEngine")
       .def(py::init<int, int, int64_t, const std::string&, double>(), py::arg("rank"), py::arg("size"),

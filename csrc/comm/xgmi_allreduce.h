@@ -9,10 +9,11 @@
 //   4. reads the same chunk from all N slots over xGMI (7 links in parallel) and sums them in rank order.
 // Every rank sums identical values in the same order, so the result is bit-identical on all ranks.
 //
-// Synchronisation is epoch based and needs no reset between calls: each workgroup keeps its own
-// monotonically increasing epoch in device memory (so the kernel is hipGraph-capturable and replays
-// advance it), flags are written with the epoch value, staging alternates between two slots (a peer can
-// be at most one call ahead: it cannot pass the next call's flag wait without this rank).  Spins are
+// Synchronisation is epoch based and needs no reset between calls: every call has ONE epoch, kept in
+// device memory and advanced by the call's last finishing workgroup (so the kernel is hipGraph-capturable
+// and replays advance it; calls of different sizes keep every workgroup on the same epoch), flags are
+// written with the epoch value, staging alternates between two slots (a peer can be at most one call
+// ahead: it cannot pass the next call's flag wait without this rank).  Spins are
 // bounded by s_memrealtime; a timeout sets an error word and the workgroup drains (never a hung grid).
 //
 // Memory: one hipExtMallocWithFlags(hipDeviceMallocUncached) allocation per rank = [flags | slot0 | slot1],
@@ -43,6 +44,8 @@ class XgmiAllreduce {
   // wire_bf16: the exchanged copies are bf16 (cast fused into the staging; fp32 sum and output)
   void allreduce(const float* src, float* dst, int64_t n, float scale, hipStream_t s, bool wire_bf16 = false);
   XgmiView view() const;  // device view for kernels that fold the exchange in (xgmi_device.h)
+  // test hook: every workgroup of this rank stalls `us` microseconds between its flag wait and its peer reads
+  void set_read_delay_us(double us) { read_delay_ticks_ = static_cast<uint64_t>(us * 100.0); }
   int error();   // 0, or 1 when some workgroup timed out waiting for a peer (synchronises the device)
   void close();
   int rank() const { return rank_; }
@@ -54,8 +57,9 @@ class XgmiAllreduce {
   int rank_, size_, device_, blocks_;
   int64_t max_bytes_, slot_bytes_, flag_bytes_;
   uint64_t timeout_ticks_;
+  uint64_t read_delay_ticks_ = 0;
   char* local_ = nullptr;       // my exported allocation
-  uint32_t* state_ = nullptr;   // [blocks] epochs + [1] error word (device-local)
+  uint32_t* state_ = nullptr;   // kXgmiStateWords: call epoch, done count, error word (device-local)
   std::vector<char*> peers_;    // mapped bases, peers_[rank_] == local_
   bool opened_ = false;
   int64_t calls_ = 0;

@@ -25,8 +25,8 @@ void hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("xgmi allreduce: ") + what + ": " + hipGetErrorString(e));
 }
 
-// grid = one workgroup per chunk of `chunk` elements (the same grid on every rank for the same n: the
-// per-workgroup epochs must advance in step across ranks).
+// grid = one workgroup per chunk of `chunk` elements (the same grid on every rank for the same n: workgroup
+// b waits for the peers' flags of workgroup b).  The epoch is per call (xgmi_epoch), not per workgroup.
 // WIRE_BF16: the staged chunk is bf16 (cast fused into the staging store, half the bytes over xGMI); the
 // rank-order sum is fp32 either way.
 template <int NR, bool VEC, bool WIRE_BF16>
@@ -61,6 +61,7 @@ __global__ __launch_bounds__(kThreads) void k_xgmi_oneshot(const float* src, flo
   }
   // 2.-3. publish my chunk to every peer and wait for theirs
   if (xgmi_publish_and_wait(xv, b, epoch, &s_fail)) {
+    xgmi_read_delay(xv);
     // 4. sum the chunk over all ranks' slots in rank order (bit-identical on every rank)
     if constexpr (WIRE_BF16) {
       const uint16_t* s16[NR];
@@ -169,9 +170,9 @@ XgmiAllreduce::XgmiAllreduce(int rank, int size, int device, int64_t max_bytes, 
   local_ = static_cast<char*>(p);
   hip_check(hipMemset(local_, 0, bytes), "zero flags");
   void* st = nullptr;
-  hip_check(hipMalloc(&st, static_cast<size_t>(blocks + 1) * 4), "hipMalloc state");
+  hip_check(hipMalloc(&st, kXgmiStateWords * 4), "hipMalloc state");
   state_ = static_cast<uint32_t*>(st);
-  hip_check(hipMemset(state_, 0, static_cast<size_t>(blocks + 1) * 4), "zero state");
+  hip_check(hipMemset(state_, 0, kXgmiStateWords * 4), "zero state");
   hip_check(hipDeviceSynchronize(), "sync after init");  // flags are zero before any peer can map them
   peers_.assign(size, nullptr);
   peers_[rank] = local_;
@@ -243,6 +244,7 @@ XgmiView XgmiAllreduce::view() const {
   for (int r = 0; r < size_; ++r) v.base[r] = peers_[r];
   v.state = state_;
   v.timeout_ticks = timeout_ticks_;
+  v.read_delay_ticks = read_delay_ticks_;
   v.flag_bytes = flag_bytes_;
   v.slot_bytes = slot_bytes_;
   v.rank = rank_;
@@ -255,7 +257,7 @@ int XgmiAllreduce::error() {
   uint32_t e = 0;
   hip_check(hipSetDevice(device_), "hipSetDevice");
   hip_check(hipDeviceSynchronize(), "sync");
-  hip_check(hipMemcpy(&e, state_ + blocks_, 4, hipMemcpyDeviceToHost), "read error word");
+  hip_check(hipMemcpy(&e, state_ + kXgmiStateError, 4, hipMemcpyDeviceToHost), "read error word");
   return static_cast<int>(e);
 }
 

@@ -14,9 +14,16 @@
 
 namespace pde {
 
-// Workgroup b's epoch for this call (block-collective: every thread gets it through LDS).
+// This call's epoch (block-collective: every thread gets it through LDS).  ONE epoch per call for all
+// workgroups -- whatever the grid size -- so the staging-slot parity is the same for every byte of a call:
+// consecutive calls with different sizes (or kernels sharing the instance) never hand the same slot range
+// to two calls in flight.  Why that is enough: rank A can write slot (e & 1) of call e + 2 only after its
+// call e + 1 saw every peer's flags of e + 1, i.e. after every peer LAUNCHED call e + 1, which on a peer's
+// stream starts only when its call e -- all of its reads of slot (e & 1) -- has completed.
 __device__ __forceinline__ uint32_t xgmi_epoch(const XgmiView& v, int b, uint32_t* s_epoch) {
-  if (threadIdx.x == 0) *s_epoch = v.state[b] + 1u;
+  (void)b;
+  if (threadIdx.x == 0)
+    *s_epoch = __hip_atomic_load(v.state + kXgmiStateEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   __syncthreads();
   return *s_epoch;
 }
@@ -50,7 +57,7 @@ __device__ __forceinline__ bool xgmi_publish_and_wait(const XgmiView& v, int b, 
     while (static_cast<int32_t>(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks) {
         *s_fail = 1;
-        __hip_atomic_store(v.state + v.blocks, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(v.state + kXgmiStateError, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -65,9 +72,25 @@ __device__ __forceinline__ bool xgmi_publish_and_wait(const XgmiView& v, int b, 
   return *s_fail == 0;
 }
 
-// Workgroup b's epoch advances (read again by the same workgroup index next call, on every rank).
+// Test hook: hold this workgroup between the flag wait and its peer reads (a slow reader).
+__device__ __forceinline__ void xgmi_read_delay(const XgmiView& v) {
+  if (v.read_delay_ticks == 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < v.read_delay_ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+// Block-collective, once per workgroup after its last peer read: the workgroup that finishes last advances
+// the call's epoch (the next kernel using the view reads it; kernel boundaries order the store).
 __device__ __forceinline__ void xgmi_finish(const XgmiView& v, int b, uint32_t epoch) {
-  if (threadIdx.x == 0) v.state[b] = epoch;
+  (void)b;
+  __syncthreads();  // every wave's peer reads are issued before the workgroup counts itself done
+  if (threadIdx.x == 0) {
+    const uint32_t n = __hip_atomic_fetch_add(v.state + kXgmiStateDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (n == gridDim.x - 1) {
+      __hip_atomic_store(v.state + kXgmiStateDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(v.state + kXgmiStateEpoch, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 }  // namespace pde

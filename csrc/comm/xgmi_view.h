@@ -7,11 +7,17 @@
 namespace pde {
 
 constexpr int kXgmiMaxRanks = 8;
+// device-local state words (XgmiView::state)
+constexpr int kXgmiStateEpoch = 0;  // epoch of the last completed call (one epoch per call, all workgroups)
+constexpr int kXgmiStateDone = 1;   // workgroups of the running call that have finished
+constexpr int kXgmiStateError = 2;  // 1 once a workgroup timed out waiting for a peer
+constexpr int kXgmiStateWords = 4;
 
 struct XgmiView {
   char* base[kXgmiMaxRanks];  // every rank's mapped [flags | slot0 | slot1] allocation (base[rank] = mine)
-  uint32_t* state;            // [blocks] per-workgroup epochs + [1] error word, device-local
+  uint32_t* state;            // kXgmiStateWords words, device-local
   uint64_t timeout_ticks;     // s_memrealtime ticks (100 MHz) before a waiting workgroup gives up
+  uint64_t read_delay_ticks;  // test hook (set_read_delay_us): stall before the peer reads
   int64_t flag_bytes, slot_bytes;
   int rank, size, blocks;     // a kernel using the view may run at most `blocks` workgroups
 };

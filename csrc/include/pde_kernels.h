@@ -169,6 +169,8 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
                         float momentum, float* running_mean, float* running_var, float* save_mean,
                         float* save_invstd, float* scale_shift, float* ws, const uint16_t* res, int relu,
                         uint16_t* y, hipStream_t s);
+// 1 when a one-launch BatchNorm wait timed out (a block of the grid was never resident); reset clears it
+int bn_error(int reset);
 hipError_t bn_apply(const uint16_t* x, int P, int C, const float* scale, const float* shift, const uint16_t* res,
                     int relu, uint16_t* y, hipStream_t s);
 // dgamma / dbeta are written, or added to when accum_params != 0 (direct accumulation into .grad).

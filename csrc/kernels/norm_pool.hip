@@ -495,6 +495,266 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_reduce_fin(
 }
 
 // ---------------------------------------------------------------------------------------------
+// ONE-launch BatchNorm (forward and backward): statistics pass -> per-channel-group ticket -> the group's
+// last arriver finalizes and raises the group's generation flag -> every block of the group waits for the
+// flag and applies the normalization (forward: y = relu?(x*scale + shift + res); backward: dx, dres) to its
+// own row chunk.  Halves the BatchNorm launches of a ResNet-50 step (4 -> 2 per layer) and the apply pass
+// re-reads a chunk its block has just streamed (L2).
+//
+// Co-residency: the grid is <= 256 blocks of 512 threads (bn_fin_grid) and the host caps it at 2 x CUs,
+// one-per-CU capacity being ~4 blocks; a kernel on a stream starts only once its predecessor finished, so
+// every block of the grid is resident and the waits complete.  Hand-off (cdna_hip_programming.md §6
+// Guideline 16): finalizer plain stores -> every storing wave s_waitcnt vmcnt(0) -> barrier -> lane-0
+// agent release -> s_waitcnt vmcnt(0) -> relaxed flag store; waiters: relaxed poll of the flag -> ONE agent
+// acquire -> s_waitcnt vmcnt(0) -> barrier -> plain loads.  Flags are generation counters (read at kernel
+// start, before the block's own ticket, hence before any increment of this launch), so they need no reset
+// and hipGraph replays just count up.  Spins are bounded (2 s): a timeout sets the BatchNorm error word.
+constexpr uint64_t kBnWaitTicks = 200000000ull;  // s_memrealtime 100 MHz: 2 s
+
+// Lane 0 reads the group's generation at kernel start (the block reads s_gen after the next barrier).
+__device__ __forceinline__ void bn_gen_start(const uint32_t* flag, uint32_t* s_gen) {
+  if (threadIdx.x == 0) *s_gen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The finalizing block, after its threads stored the group's coefficients: publish generation gen + 1.
+__device__ __forceinline__ void bn_publish(uint32_t* flag, uint32_t gen) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(flag, gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Every other block of the group: wait (bounded) for generation gen + 1, then acquire.
+__device__ __forceinline__ void bn_wait(const uint32_t* flag, uint32_t gen, int* err) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kBnWaitTicks) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
+    const uint16_t* __restrict__ x, int P, int C, int rpb, float* __restrict__ ws, int* __restrict__ tickets,
+    uint32_t* __restrict__ flags, int* __restrict__ err, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float momentum, float* __restrict__ running_mean,
+    float* __restrict__ running_var, float* __restrict__ save_mean, float* __restrict__ save_invstd,
+    float* __restrict__ scale, float* __restrict__ shift, const uint16_t* __restrict__ res, int relu,
+    uint16_t* __restrict__ y) {
+  __shared__ float red[2][kBnRows][kBnCG + 1];
+  __shared__ float tot1[kBnCG], tot2[kBnCG];
+  __shared__ int s_last;
+  __shared__ uint32_t s_gen;
+  const int tid = threadIdx.x, tv = tid & 7, tr = tid >> 3;
+  const int c0 = blockIdx.y * kBnCG + tv * 8;
+  const bool cok = c0 < C;
+  bn_gen_start(flags + blockIdx.y, &s_gen);
+  const int r1 = min(P, (blockIdx.x + 1) * rpb);
+  float s1[8], s2[8], piv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = piv[j] = 0.f;
+  if (cok) {
+    load8(x + c0, piv);  // shift by row 0 (same pivot in every block)
+    int r = blockIdx.x * rpb + tr;
+    constexpr int U = kBnUnroll;
+    for (; r + (U - 1) * kBnRows < r1; r += U * kBnRows) {
+      u16x8 u[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q) u[q] = *reinterpret_cast<const u16x8*>(x + static_cast<long>(r + kBnRows * q) * C + c0);
+#pragma unroll
+      for (int q = 0; q < U; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float d = bf2f(u[q][j]) - piv[j]; s1[j] += d; s2[j] += d * d; }
+    }
+    for (; r < r1; r += kBnRows) {
+      float v[8];
+      load8(x + static_cast<long>(r) * C + c0, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = v[j] - piv[j]; s1[j] += d; s2[j] += d * d; }
+    }
+  }
+  // (bn_partials_and_ticket's first barrier also publishes s_gen to the block)
+  if (bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last)) {
+    if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
+      const int c = blockIdx.y * kBnCG + tid;
+      const double n = static_cast<double>(P);
+      const double mean_s = static_cast<double>(tot1[tid]) / n;
+      double var = static_cast<double>(tot2[tid]) / n - mean_s * mean_s;
+      if (var < 0.0) var = 0.0;
+      const float mean = static_cast<float>(mean_s) + bf2f(x[c]);
+      const float invstd = rsqrtf(static_cast<float>(var) + eps);
+      save_mean[c] = mean;
+      save_invstd[c] = invstd;
+      const float g = gamma ? gamma[c] : 1.f;
+      const float b = beta ? beta[c] : 0.f;
+      scale[c] = g * invstd;
+      shift[c] = b - mean * g * invstd;
+      if (running_mean) {
+        const float unbiased = P > 1 ? static_cast<float>(var * n / (n - 1.0)) : static_cast<float>(var);
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+      }
+    }
+    bn_publish(flags + blockIdx.y, s_gen);
+    __syncthreads();
+  } else {
+    bn_wait(flags + blockIdx.y, s_gen, err);
+  }
+  if (!cok) return;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; }
+  int r = blockIdx.x * rpb + tr;
+  constexpr int U = 4;
+  for (; r + (U - 1) * kBnRows < r1; r += U * kBnRows) {
+    u16x8 u[U], q[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const long off = static_cast<long>(r + kBnRows * k) * C + c0;
+      u[k] = *reinterpret_cast<const u16x8*>(x + off);
+      if (res) q[k] = *reinterpret_cast<const u16x8*>(res + off);
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = bf2f(u[k][j]) * sc[j] + sh[j];
+        if (res) t += bf2f(q[k][j]);
+        if (relu) t = fmaxf(t, 0.f);
+        o[j] = f2bf(t);
+      }
+      *reinterpret_cast<u16x8*>(y + static_cast<long>(r + kBnRows * k) * C + c0) = o;
+    }
+  }
+  for (; r < r1; r += kBnRows) {
+    const long off = static_cast<long>(r) * C + c0;
+    float v[8], rv[8];
+    load8(x + off, v);
+    if (res) load8(res + off, rv);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = v[j] * sc[j] + sh[j];
+      if (res) t += rv[j];
+      if (relu) t = fmaxf(t, 0.f);
+      o[j] = f2bf(t);
+    }
+    *reinterpret_cast<u16x8*>(y + off) = o;
+  }
+}
+
+__global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const uint16_t* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ invstd, int P, int C, int rpb, int relu,
+    float* __restrict__ ws, int* __restrict__ tickets, uint32_t* __restrict__ flags, int* __restrict__ err,
+    const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta, int accum,
+    float* __restrict__ coef, uint16_t* __restrict__ dx, uint16_t* __restrict__ dres) {
+  __shared__ float red[2][kBnRows][kBnCG + 1];
+  __shared__ float tot1[kBnCG], tot2[kBnCG];
+  __shared__ int s_last;
+  __shared__ uint32_t s_gen;
+  const int tid = threadIdx.x, tv = tid & 7, tr = tid >> 3;
+  const int c0 = blockIdx.y * kBnCG + tv * 8;
+  const bool cok = c0 < C;
+  bn_gen_start(flags + blockIdx.y, &s_gen);
+  const int r1 = min(P, (blockIdx.x + 1) * rpb);
+  float s1[8], s2[8], mu[8], is[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = mu[j] = is[j] = 0.f;
+  if (cok) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j]; }
+    int r = blockIdx.x * rpb + tr;
+    constexpr int U = kBnUnroll / 2;  // 3 tensors per row: 12 x 16-B loads in flight per lane
+    for (; r + (U - 1) * kBnRows < r1; r += U * kBnRows) {
+      u16x8 ud[U], ux[U], uy[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        const long off = static_cast<long>(r + kBnRows * q) * C + c0;
+        ud[q] = *reinterpret_cast<const u16x8*>(dy + off);
+        ux[q] = *reinterpret_cast<const u16x8*>(x + off);
+        if (relu) uy[q] = *reinterpret_cast<const u16x8*>(y + off);
+      }
+#pragma unroll
+      for (int q = 0; q < U; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float d = bf2f(ud[q][j]);
+          if (relu && !(bf2f(uy[q][j]) > 0.f)) d = 0.f;
+          s1[j] += d;
+          s2[j] += d * (bf2f(ux[q][j]) - mu[j]) * is[j];
+        }
+    }
+    for (; r < r1; r += kBnRows) {
+      const long off = static_cast<long>(r) * C + c0;
+      float d[8], xv[8];
+      load8(dy + off, d);
+      load8(x + off, xv);
+      if (relu) {
+        float yv[8];
+        load8(y + off, yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s1[j] += d[j]; s2[j] += d[j] * (xv[j] - mu[j]) * is[j]; }
+    }
+  }
+  if (bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last)) {
+    if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
+      const int c = blockIdx.y * kBnCG + tid;
+      const float t1 = tot1[tid], t2 = tot2[tid];
+      if (dgamma) dgamma[c] = accum ? dgamma[c] + t2 : t2;
+      if (dbeta) dbeta[c] = accum ? dbeta[c] + t1 : t1;
+      const float a = (gamma ? gamma[c] : 1.f) * invstd[c];
+      coef[c] = a;
+      coef[C + c] = a * t1 / static_cast<float>(P);
+      coef[2 * C + c] = a * t2 / static_cast<float>(P);
+    }
+    bn_publish(flags + blockIdx.y, s_gen);
+    __syncthreads();
+  } else {
+    bn_wait(flags + blockIdx.y, s_gen, err);
+  }
+  if (!cok) return;
+  float ca[8], cb[8], cc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { ca[j] = coef[c0 + j]; cb[j] = coef[C + c0 + j]; cc[j] = coef[2 * C + c0 + j]; }
+  for (int r = blockIdx.x * rpb + tr; r < r1; r += kBnRows) {
+    const long off = static_cast<long>(r) * C + c0;
+    float d[8], xv[8];
+    load8(dy + off, d);
+    load8(x + off, xv);
+    if (relu) {
+      float yv[8];
+      load8(y + off, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+    }
+    u16x8 o, orr;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xh = (xv[j] - mu[j]) * is[j];
+      o[j] = f2bf(ca[j] * d[j] - cb[j] - cc[j] * xh);
+      orr[j] = f2bf(d[j]);
+    }
+    *reinterpret_cast<u16x8*>(dx + off) = o;
+    if (dres) *reinterpret_cast<u16x8*>(dres + off) = orr;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Max pooling, NHWC, any C (scalar channel loop for C % 8 != 0, the MNIST CNN's 10 / 20 channels).
 // Saves the argmax window index (uint8) for the backward gather.
 __global__ void k_maxpool_fwd(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, uint8_t* __restrict__ idx,
@@ -845,29 +1105,59 @@ int bn_fin_grid(int P, int C, int& rpb) {
 // Per-channel-group arrival counters: one zeroed array per device, handed out in a rolling window (each
 // launch leaves its counters at 0).  Allocated on the first call outside a graph capture; until then (or
 // with PDE_BN_3PASS=1) BatchNorm uses the separate finalize kernels.
-int* bn_tickets(int n, hipStream_t s) {
+int* bn_ticket_base(hipStream_t s, int** err) {
   constexpr int kSlots = 1 << 20;
   static int* base[64] = {};
-  static int next[64] = {};
-  static const bool off = std::getenv("PDE_BN_3PASS") != nullptr;
-  if (off || n > kSlots) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   if (base[dev] == nullptr) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
     void* p = nullptr;
-    if (hipMalloc(&p, sizeof(int) * kSlots) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, sizeof(int) * kSlots) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    const size_t bytes = sizeof(int) * (kSlots + 64);  // + the error word of the one-launch kernels
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
       (void)hipFree(p);
       return nullptr;
     }
     base[dev] = static_cast<int*>(p);
   }
-  if (next[dev] + n > kSlots) next[dev] = 0;
-  int* t = base[dev] + next[dev];
-  next[dev] += n;
+  if (err != nullptr) *err = base[dev] + kSlots;
+  return base[dev];
+}
+
+// Rolling windows over the zeroed array: [0, kHalf) arrival tickets (every launch leaves them at 0), [kHalf,
+// kSlots) generation flags of the one-launch kernels (any value; never handed out as tickets).
+int* bn_window(int n, hipStream_t s, int which) {
+  constexpr int kSlots = 1 << 20, kHalf = kSlots / 2;
+  static int next[64][2] = {};
+  static const bool off = std::getenv("PDE_BN_3PASS") != nullptr;
+  if (off || n > kHalf) return nullptr;
+  int* base = bn_ticket_base(s, nullptr);
+  if (base == nullptr) return nullptr;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int& nx = next[dev][which];
+  if (nx + n > kHalf) nx = 0;
+  int* t = base + which * kHalf + nx;
+  nx += n;
   return t;
+}
+int* bn_tickets(int n, hipStream_t s) { return bn_window(n, s, 0); }
+uint32_t* bn_flags(int n, hipStream_t s) { return reinterpret_cast<uint32_t*>(bn_window(n, s, 1)); }
+
+// One-launch BatchNorm (k_bn_fwd_fused / k_bn_bwd_fused): on unless PDE_BN_FUSED=0, and only for grids the
+// chip holds at once (every block must be resident for the flag waits).
+bool bn_one_launch(int blocks) {
+  static const bool off = std::getenv("PDE_BN_FUSED") != nullptr && std::getenv("PDE_BN_FUSED")[0] == '0';
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    hipDeviceProp_t prop{};
+    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+              ? prop.multiProcessorCount : 1;
+  }
+  return !off && blocks <= 2 * cus;
 }
 
 const long kBnApplyCap = std::getenv("PDE_BN_APPLY_CAP") ? std::atol(std::getenv("PDE_BN_APPLY_CAP")) : 2048;
@@ -882,10 +1172,22 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
                         float* save_invstd, float* scale_shift, float* ws, const uint16_t* res, int relu,
                         uint16_t* y, hipStream_t s) {
   int rpb;
-  int* tk = bn_tickets(ceil_div(C, kBnCG), s);
+  const int ncg = ceil_div(C, kBnCG);
+  int* err = nullptr;
+  const int nrb1 = bn_fin_grid(P, C, rpb);
+  if (bn_one_launch(nrb1 * ncg) && bn_ticket_base(s, &err) != nullptr) {
+    int* tk = bn_tickets(ncg, s);
+    uint32_t* fl = bn_flags(ncg, s);  // generation flags of the channel groups
+    if (tk != nullptr && fl != nullptr) {
+      hipLaunchKernelGGL(k_bn_fwd_fused, dim3(nrb1, ncg), dim3(kBnThreads), 0, s, x, P, C, rpb, ws, tk, fl, err, gamma, beta, eps, momentum, running_mean,
+                         running_var, save_mean, save_invstd, scale_shift, scale_shift + C, res, relu, y);
+      return hipGetLastError();
+    }
+  }
+  int* tk = bn_tickets(ncg, s);
   if (tk != nullptr) {
     const int nrb = bn_fin_grid(P, C, rpb);
-    hipLaunchKernelGGL(k_bn_stats_fin, dim3(nrb, ceil_div(C, kBnCG)), dim3(kBnThreads), 0, s, x, P, C, rpb, ws, tk, gamma,
+    hipLaunchKernelGGL(k_bn_stats_fin, dim3(nrb, ncg), dim3(kBnThreads), 0, s, x, P, C, rpb, ws, tk, gamma,
                        beta, eps, momentum, running_mean, running_var, save_mean, save_invstd, scale_shift,
                        scale_shift + C);
   } else {
@@ -901,6 +1203,16 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
   return hipGetLastError();
 }
 
+int bn_error(int reset) {
+  int* err = nullptr;
+  if (bn_ticket_base(nullptr, &err) == nullptr || err == nullptr) return 0;
+  int v = 0;
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&v, err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  if (reset && v != 0) (void)hipMemset(err, 0, sizeof(int));
+  return v;
+}
+
 hipError_t bn_apply(const uint16_t* x, int P, int C, const float* scale, const float* shift, const uint16_t* res,
                     int relu, uint16_t* y, hipStream_t s) {
   const long nvec = static_cast<long>(P) * C / 8;
@@ -913,10 +1225,23 @@ hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, cons
                   const float* gamma, int P, int C, int relu, float* dgamma, float* dbeta, int accum_params, float* ws,
                   float* coef, uint16_t* dx, uint16_t* dres, hipStream_t s) {
   int rpb;
-  int* tk = bn_tickets(ceil_div(C, kBnCG), s);
+  const int ncg = ceil_div(C, kBnCG);
+  int* err = nullptr;
+  const int nrb1 = bn_fin_grid(P, C, rpb);
+  if (bn_one_launch(nrb1 * ncg) && bn_ticket_base(s, &err) != nullptr) {
+    int* tk = bn_tickets(ncg, s);
+    uint32_t* fl = bn_flags(ncg, s);
+    if (tk != nullptr && fl != nullptr) {
+      hipLaunchKernelGGL(k_bn_bwd_fused, dim3(nrb1, ncg), dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, P, C, rpb,
+                         relu, ws, tk, fl, err, gamma, dgamma, dbeta, accum_params,
+                         coef, dx, dres);
+      return hipGetLastError();
+    }
+  }
+  int* tk = bn_tickets(ncg, s);
   if (tk != nullptr) {
     const int nrb = bn_fin_grid(P, C, rpb);
-    hipLaunchKernelGGL(k_bn_bwd_reduce_fin, dim3(nrb, ceil_div(C, kBnCG)), dim3(kBnThreads), 0, s, dy, x, y, mean, invstd,
+    hipLaunchKernelGGL(k_bn_bwd_reduce_fin, dim3(nrb, ncg), dim3(kBnThreads), 0, s, dy, x, y, mean, invstd,
                        P, C, rpb, relu, ws, tk, gamma, dgamma, dbeta, accum_params, coef);
   } else {
     const int nblk = bn_blocks(P, C, rpb);

@@ -32,7 +32,7 @@ EXTENSIONS = {
         ["bindings.cpp"],
     ),
     "_comm": (
-        ["comm/pack.hip", "comm/xgmi_allreduce.hip"],
+        ["comm/pack.hip", "comm/xgmi_allreduce.hip", "comm/p2p_ring.hip"],
         ["comm/comm_manager.cpp", "comm/fusion_engine.cpp", "comm/comm_bindings.cpp"],
     ),
 }
@@ -65,13 +65,39 @@ def _headers() -> list[Path]:
     return sorted(CSRC.rglob("*.h")) + sorted(CSRC.rglob("*.cuh"))
 
 
+_INC_DIRS = [CSRC / "include", CSRC / "kernels", CSRC / "comm"]
+
+
+def _deps(src: Path, seen: set | None = None) -> set:
+    """In-tree headers ``src`` includes (``#include "..."``, recursively) -- an object is rebuilt only
+    when one of ITS headers changed, not any header of the tree."""
+    seen = set() if seen is None else seen
+    try:
+        text = src.read_text(errors="ignore")
+    except OSError:
+        return seen
+    for line in text.splitlines():
+        line = line.strip()
+        if not line.startswith("#include \""):
+            continue
+        name = line.split('"')[1]
+        for d in [src.parent, *_INC_DIRS]:
+            h = (d / name).resolve()
+            if h.exists():
+                if h not in seen:
+                    seen.add(h)
+                    _deps(h, seen)
+                break
+    return seen
+
+
 def _stale(obj: Path, src: Path, headers: list[Path]) -> bool:
     if not obj.exists():
         return True
     t = obj.stat().st_mtime
     if src.stat().st_mtime > t:
         return True
-    return any(h.stat().st_mtime > t for h in headers)
+    return any(h.stat().st_mtime > t for h in _deps(src))
 
 
 def _run(cmd: list[str]) -> None:

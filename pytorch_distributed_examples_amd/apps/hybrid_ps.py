@@ -49,7 +49,8 @@ class HybridModel(nn.Module):
         self.device = device
 
     def forward(self, indices, offsets):
-        emb_lookup = self.remote_emb_module.forward(indices, offsets)
+        # on GPUs the looked-up rows arrive in this GPU's HBM over the P2P ring (no host round trip)
+        emb_lookup = self.remote_emb_module.forward(indices, offsets, out_device=self.device)
         return self.fc(emb_lookup.to(self.device), out_f32=True)
 
 
@@ -78,7 +79,9 @@ def _run_trainer(remote_emb_module, rank, epochs, device_str):
         if epoch % 5 == 0:
             print(f"Training done for epoch {epoch} (trainer {rank}, loss {loss.item():.4f})", flush=True)
     dt = time.perf_counter() - t0
-    print(f"trainer {rank}: {steps} steps, {dt / steps * 1e3:.2f} ms/step", flush=True)
+    plane = "p2p-ring" if remote_emb_module.uses_ring(device) else "rpc-host"
+    print(f"trainer {rank}: {steps} steps, {dt / steps * 1e3:.2f} ms/step (embedding data plane: {plane})",
+          flush=True)
     return steps
 
 
@@ -105,8 +108,9 @@ def run_worker(rank, world_size, epochs, ports, use_gpu):
     elif rank <= 1:  # trainers: DDP group of 2 next to the RPC agent (:155-166)
         if use_gpu:
             torch.cuda.set_device(rank % ngpu)
-        dist.init_process_group("nccl" if use_gpu else "gloo", rank=rank, world_size=2,
-                                init_method=f"tcp://127.0.0.1:{pg_port}")
+        # PDE_BACKEND=gloo: trainers sharing one GPU (RCCL refuses two ranks on one device)
+        dist.init_process_group(os.environ.get("PDE_BACKEND") or ("nccl" if use_gpu else "gloo"), rank=rank,
+                                world_size=2, init_method=f"tcp://127.0.0.1:{pg_port}")
         rpc.init_rpc(f"trainer{rank}", rank=rank, world_size=world_size, rpc_backend_options=options)
     else:  # parameter server
         rpc.init_rpc("ps", rank=rank, world_size=world_size, rpc_backend_options=options)
@@ -176,12 +180,33 @@ class ResNetPipelineDP:
     def images_per_step(self) -> int:
         return self.batch * self.dp
 
-    def step(self):
+    @property
+    def capturable(self) -> bool:
+        """The whole step can record into one hipGraph: GPU stage channels (ring / RCCL, not host staging)
+        and a stream-ordered data-parallel communicator (or none at dp 1)."""
+        if self.ctx.device.type != "cuda" or (self.dp > 1 and self.comm is None):
+            return False
+        return all(ch is None or ch.mode != "host" for ch in (self.engine.prev, self.engine.next))
+
+    def check(self):
+        """Raise if a stage channel timed out (synchronises the device)."""
+        self.engine.check()
+
+    def step(self, timer=None):
+        """One training step; ``timer`` (utils.log.PhaseTimer, eager steps only): this stage's fwd / bwd /
+        recv-wait / comm / opt device times."""
+        from ..utils.log import NO_PHASES
+
+        t = timer or NO_PHASES
+        self.engine.timer = t
         self.ddp.zero_grad()
         loss = self.engine.train_step(self.xs if self.stage == 0 else None, self.ys if self.last else None,
                                       self.n_mb)
-        self.ddp.sync_gradients()
-        self.opt.step()
+        with t.phase("comm"):
+            self.ddp.sync_gradients()
+        with t.phase("opt"):
+            self.opt.step()
+        self.engine.timer = NO_PHASES
         return loss if loss is not None else self._zero
 
     def close(self):

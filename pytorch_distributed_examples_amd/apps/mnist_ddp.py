@@ -137,6 +137,11 @@ class Trainer:
             n += source.shape[0]
         if self.ctx.device.type == "cuda":
             torch.cuda.synchronize()
+            # a one-shot xGMI exchange that timed out drops its result (replicas would silently diverge):
+            # read the device error word at this existing sync point, before the test pass and any snapshot
+            check = getattr(self.ddp.comm, "check", None)
+            if check is not None:
+                check()
         dt = time.perf_counter() - t0
         img_s = pdist.sum_over_ranks(n / dt, self.ctx.device)
         if self.metrics is not None:

@@ -8,7 +8,8 @@ one-hot labels of 1000 classes on ``randn(32,3,128,128)`` batches (:191-217), di
 line for split sizes 4 and 8 (:258-262).
 
 MI355X-first: stage k lives on GPU k-1 (NHWC bf16 MFMA kernels), the stage-1 -> stage-2 activation
-(m x 16 x 16 x 512 bf16) moves GPU->GPU over RCCL instead of ``to_here()`` through the CPU; the
+(m x 16 x 16 x 512 bf16) moves GPU->GPU over xGMI (the IPC receive ring of csrc/comm/p2p_ring.hip; RCCL
+send/recv with ``PDE_P2P=rccl``) instead of ``to_here()`` through the CPU; the
 ``Forward 2`` print (quirk Q12) is behind ``--verbose``.  A separate port is used per spawn (the reference
 reuses 29500 for both spawns).
 """
@@ -82,8 +83,9 @@ def run_worker(rank, world_size, num_split, args, rpc_port, pg_port):
             # CPU configuration: split the cores between the stage processes (each stage computes in
             # its executor thread; oversubscribed OpenMP teams spin against each other otherwise)
             torch.set_num_threads(max(1, (os.cpu_count() or 2) // (world_size - 1)))
-        dist.init_process_group("nccl" if use_gpu else "gloo", init_method=f"tcp://127.0.0.1:{pg_port}",
-                                rank=rank - 1, world_size=world_size - 1)
+        # PDE_BACKEND=gloo: both stages on one GPU (rehearsal); the stage data plane is the P2P ring either way
+        dist.init_process_group(os.environ.get("PDE_BACKEND") or ("nccl" if use_gpu else "gloo"),
+                                init_method=f"tcp://127.0.0.1:{pg_port}", rank=rank - 1, world_size=world_size - 1)
         rpc.init_rpc(f"worker{rank}", rank=rank, world_size=world_size, rpc_backend_options=options)
     rpc.shutdown()
     if rank != 0:

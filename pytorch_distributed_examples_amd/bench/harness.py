@@ -33,6 +33,7 @@ import torch
 import torch.distributed as dist
 
 from ..parallel import dist as pdist
+from ..utils.log import NO_PHASES, PhaseTimer
 
 # BASELINE.json names one metric for the whole suite; ``config`` says which of its workloads this run measured.
 METRIC = "images/sec (whole node) MNIST DDP + ResNet50 RPC-MP at 1/2/4/8 MI355X"
@@ -195,28 +196,41 @@ def build_data_parallel(args, ctx, batch) -> Workload:
     # (PDE_CNN_XCHG=0: all-reduce through the DDP communicator + a separate SGD launch instead)
     xgmi = getattr(comm, "xgmi", None) if fused is not None and os.environ.get("PDE_CNN_XCHG", "1") != "0" else None
 
-    def train_step(x, y):
+    def train_step(x, y, t=NO_PHASES):
+        # ``t``: PhaseTimer of the phase measurement (eager steps after the timed region), else a no-op
         if fused is not None:
             if ctx.world_size == 1:
-                return fused.forward_backward(x, y, grad_out=ddp.flat_grad, sgd=opt)
+                with t.phase("fused_fwd_bwd_reduce_sgd"):
+                    return fused.forward_backward(x, y, grad_out=ddp.flat_grad, sgd=opt)
             if xgmi is not None:  # all-reduce folded into the slab reduction: still 2 launches per step
-                return fused.forward_backward(x, y, grad_out=ddp.flat_grad, sgd=opt, xgmi=xgmi)
-            loss = fused.forward_backward(x, y, grad_out=ddp.flat_grad)
-            ddp.sync_gradients()
-            fused.sgd_step(opt, ddp.flat_grad)
+                with t.phase("fused_fwd_bwd_xchg_sgd"):
+                    return fused.forward_backward(x, y, grad_out=ddp.flat_grad, sgd=opt, xgmi=xgmi)
+            with t.phase("fused_fwd_bwd_reduce"):
+                loss = fused.forward_backward(x, y, grad_out=ddp.flat_grad)
+            with t.phase("comm"):
+                ddp.sync_gradients()
+            with t.phase("opt"):
+                fused.sgd_step(opt, ddp.flat_grad)
             return loss
         if fmlp is not None:
-            loss = fmlp.forward_backward(x, y)  # gradients written (not accumulated): no zeroing
+            with t.phase("fwd_bwd"):
+                loss = fmlp.forward_backward(x, y)  # gradients written (not accumulated): no zeroing
             if ctx.world_size > 1:
-                ddp.sync_gradients()
-            opt.step()
+                with t.phase("comm"):
+                    ddp.sync_gradients()
+            with t.phase("opt"):
+                opt.step()
             return loss
         ddp.zero_grad()
-        loss = loss_fn(ddp(x), y)
-        loss.backward()
+        with t.phase("fwd"):
+            loss = loss_fn(ddp(x), y)
+        with t.phase("bwd"):
+            loss.backward()
         if not ddp.overlap:  # graph mode: buckets reduced after backward on the capturing stream
-            ddp.sync_gradients()
-        opt.step()
+            with t.phase("comm"):
+                ddp.sync_gradients()
+        with t.phase("opt"):
+            opt.step()
         return loss
 
     one = group = None
@@ -241,6 +255,12 @@ def build_data_parallel(args, ctx, batch) -> Workload:
     w.group = group
     if routed is not None:
         w.check = comm.xgmi.check  # raises if any one-shot call timed out waiting for a peer
+
+    def phase_step(i, timer):
+        x, y = batch_fn(i)
+        return train_step(x, y, timer)
+
+    w.phase_step = phase_step
     return w
 
 
@@ -253,7 +273,7 @@ def build_pipeline(args, ctx, batch) -> Workload:
     nranks = _data_plane_check(ctx, None)
     pipe = ResNetPipelineDP(ctx, batch, args.split_size, args.image or 128, args.schedule, tag="bench")
     one = None
-    if not args.no_graph and on_gpu and ctx.backend == "nccl":
+    if not args.no_graph and pipe.capturable:
         one, _ = _capture(pipe.step, [()], 1, ctx.rank)
 
     def step(i):
@@ -264,6 +284,9 @@ def build_pipeline(args, ctx, batch) -> Workload:
                  split_size=args.split_size, microbatches=pipe.n_mb, schedule=args.schedule)
     w.loss_rank = pipe.stages - 1
     w.close = pipe.close
+    w.check = pipe.check
+    w.phase_step = lambda i, timer: pipe.step(timer)
+    w.per_stage = True
     return w
 
 
@@ -328,6 +351,33 @@ def _report_loss(work, ctx, loss):
     return float(t.item())
 
 
+PHASE_STEPS = 3
+
+
+def _measure_phases(work, ctx, args):
+    """Per-phase device milliseconds per step, from PHASE_STEPS eager steps run AFTER the
+    timed region (a captured hipGraph has no host-visible phase boundaries; eager steps add host launch
+    gaps between phases, which these device-time spans exclude).  Data parallel: rank 0's phases.  Pipeline:
+    one entry per stage of the first pipeline (fwd / bwd compute, recv_wait = time the stage's stream spends
+    in receive kernels waiting for its neighbour, comm = stage all-reduce, opt)."""
+    if not hasattr(work, "phase_step"):
+        return None
+    timer = PhaseTimer(ctx.device)
+    try:
+        for k in range(PHASE_STEPS):
+            work.phase_step(args.warmup + args.steps + k, timer)
+            timer.steps += 1
+        local = timer.summary()
+    except Exception as exc:  # noqa: BLE001 - diagnostics never cost the headline line
+        local = {"error": repr(exc)[:200]}
+    if getattr(work, "per_stage", False) and ctx.world_size > 1:
+        allp = [None] * ctx.world_size
+        dist.all_gather_object(allp, local)
+        stages = [dict(stage=s, **allp[s]) for s in range(min(2, ctx.world_size))]
+        return {"method": f"hipEvents, {PHASE_STEPS} eager steps after the timed region", "stages": stages}
+    return {"method": f"hipEvents, {PHASE_STEPS} eager steps after the timed region", "rank0_ms": local}
+
+
 def main(argv=None):
     args = parse_args(argv)
     batch = args.batch or DEFAULT_BATCH[args.model]
@@ -354,6 +404,7 @@ def main(argv=None):
         work.check()
     dt = pdist.max_over_ranks(dt, ctx.device)
     final_loss = _report_loss(work, ctx, loss)
+    phases = _measure_phases(work, ctx, args) if os.environ.get("PDE_BENCH_PHASES", "1") != "0" else None
     value = work.images_per_step * args.steps / dt
     secondary = None
     mode = os.environ.get("PDE_BENCH_SECONDARY", "1")  # 0: off; force: also on CPU/gloo (plumbing tests)
@@ -368,6 +419,8 @@ def main(argv=None):
                "image": "1x28x28" if args.model in ("cnn", "mlp") else f"3x{args.image or 128}x{args.image or 128}",
                "parallelism": work.parallelism, "final_loss": round(final_loss, 4)}
         cfg.update(work.info)
+        if phases is not None:
+            cfg["phases"] = phases
         if secondary is not None:
             cfg["secondary"] = secondary
         print(json.dumps({

@@ -14,8 +14,10 @@ Mirrors ``torch.nn.parallel.DistributedDataParallel`` as used by the reference
 * bucket sizes follow :mod:`.xgmi` (sized for 7 point-to-point links, not DDP's 25 MiB default);
 * ``overlap=False`` skips the hooks and reduces every bucket in :meth:`sync_gradients` -- the form used
   inside a captured hipGraph step;
-* ``grad_dtype=torch.bfloat16`` halves the bytes on the wire (bucket cast -> all-reduce -> cast back; on
-  the xGMI data plane the casts are fused into the one-shot all-reduce kernel and DDP copies nothing);
+* ``grad_dtype=torch.bfloat16`` halves the bytes on the wire: on the xGMI data plane the casts are fused
+  into the one-shot all-reduce kernel and DDP copies nothing; on RCCL each bucket is cast by our HIP kernel
+  into a persistent bf16 buffer, all-reduced in place (bf16, AVG in-collective) and cast back by our kernel
+  into the flat fp32 gradient -- no allocation and no ATen kernel per bucket;
 * ``comm=`` swaps the c10d group for another communicator (``size``, ``supports_avg``,
   ``allreduce_async(t, avg) -> work``, ``broadcast_(t, src)``), e.g. the per-round RCCL communicator of
   :mod:`..elastic.rewire` that is aborted and rebuilt in-process on a membership change.
@@ -50,6 +52,17 @@ def _flat_broadcast(tensors, src, group, comm=None):
                 n = t.numel()
                 t.copy_(flat[off:off + n].view_as(t))
                 off += n
+
+
+def _cast(src: torch.Tensor, dst: torch.Tensor) -> None:
+    """fp32 <-> bf16 bucket cast: our HIP kernels on GPU (pytorch_distributed_examples_amd._C), ATen on CPU."""
+    if src.is_cuda:
+        from .. import _native
+
+        C = _native.C()
+        (C.cast_bf16_into if src.dtype == torch.float32 else C.cast_f32_into)(src, dst)
+    else:
+        dst.copy_(src)
 
 
 class DistributedDataParallel(nn.Module):
@@ -144,14 +157,15 @@ class DistributedDataParallel(nn.Module):
     def _launch(self, b: int):
         if self.flat_grad.is_cuda:  # weight gradients may still be running on the side stream (ops/streams.py)
             streams.join(self.flat_grad.device)
-        if self._bf16_bufs is not None and getattr(self.comm, "supports_bf16_wire", False):
+        fused_wire = getattr(self.comm, "fuses_bf16_wire", None)
+        if self._bf16_bufs is not None and fused_wire is not None and fused_wire(self._bucket_flat[b]):
             # the communicator casts on the wire itself (fused into the xGMI one-shot kernel): no copies here
             work = self.comm.allreduce_async(self._bucket_flat[b], avg=self._use_avg, wire_bf16=True)
             self._works.append((-1 - b, work))
             return
         if self._bf16_bufs is not None:
             buf = self._bf16_bufs[b]
-            buf.copy_(self._bucket_flat[b])
+            _cast(self._bucket_flat[b], buf)
         else:
             buf = self._bucket_flat[b]
         if self.comm is not None:
@@ -170,7 +184,7 @@ class DistributedDataParallel(nn.Module):
         for b, work in self._works:
             work.wait()
             if self._bf16_bufs is not None and b >= 0:  # b < 0: reduced in place with a bf16 wire
-                self._bucket_flat[b].copy_(self._bf16_bufs[b])
+                _cast(self._bf16_bufs[b], self._bucket_flat[b])
         if not self._use_avg and self.world > 1:
             self.flat_grad.mul_(1.0 / self.world)
         self._reset_state()

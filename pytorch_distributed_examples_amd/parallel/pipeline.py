@@ -4,9 +4,12 @@ Replaces the reference's RPC data path (rpc/model_parallel_ResNet50.py:167-178: 
 pulled with ``RRef.to_here()`` as a CPU tensor, three process hops per micro-batch) with a
 stage-per-GPU engine:
 
-* activations and activation-gradients stay in HBM and move GPU->GPU with RCCL ``send``/``recv`` on a
-  dedicated 2-rank communicator per neighbouring stage pair (one direct xGMI link), stream-ordered with
-  the producing kernels (no host synchronisation, no ``.cpu()``, quirk Q13 fixed);
+* activations and activation-gradients stay in HBM and move GPU->GPU over the one direct xGMI link of a
+  neighbouring stage pair: by default through an IPC-mapped receive ring that the sender's kernel writes
+  directly (csrc/comm/p2p_ring.hip: epoch flags, credits, bounded spins -- and rehearsable with two
+  processes on ONE GPU), or with ``PDE_P2P=rccl`` RCCL ``send``/``recv`` on dedicated 2-rank
+  communicators; stream-ordered with the producing kernels either way (no host synchronisation, no
+  ``.cpu()``, quirk Q13 fixed), so a whole pipelined step records into one hipGraph;
 * stage boundaries carry bf16 NHWC activations (ResNet-50 at the layer2|layer3 cut: m x 16 x 16 x 512,
   4x fewer bytes than the reference's fp32 tensors);
 * explicit schedules: ``gpipe`` (all forwards, then all backwards -- the reference's fill/drain) and
@@ -20,25 +23,50 @@ owns targets and the loss.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
 from .. import _native
+from ..utils.log import NO_PHASES
+
+
+def p2p_mode(device: torch.device) -> str:
+    """Data plane of the stage channels: ``ring`` (IPC receive ring over xGMI, default on GPUs), ``rccl``
+    (RCCL send/recv; needs the nccl backend) or ``host`` (gloo through host memory: CPU, or forced)."""
+    if device.type != "cuda":
+        return "host"
+    mode = os.environ.get("PDE_P2P", "ring")
+    if mode == "rccl" and dist.get_backend() != "nccl":
+        return "host"
+    return mode if mode in ("ring", "rccl", "host") else "ring"
 
 
 class P2PChannel:
     """Point-to-point channel between two neighbouring stage processes (ranks lo < hi of the default group).
 
-    GPU data plane: TWO 2-rank RCCL communicators, one per direction -- ``down`` carries lo -> hi
-    traffic (activations), ``up`` carries hi -> lo traffic (activation gradients).  RCCL executes the
-    operations of one communicator in issue order whatever stream they are enqueued on, so with a single
+    GPU data plane, ``ring`` (default): each side exports one IPC-mapped receive ring in its HBM
+    (csrc/comm/p2p_ring.hip); ``send`` is ONE kernel that writes the tensor straight into the peer's ring
+    slot over xGMI and raises per-workgroup flags there, ``recv`` is ONE kernel that waits for them, copies
+    the slot into a fresh tensor and returns a credit to the sender.  Sequence numbers live on the device,
+    so the kernels are capturable and every hipGraph replay moves the next messages.  Two processes on one
+    GPU map each other's rings exactly like two GPUs of a node: the pipeline data plane is rehearsed on
+    single-GPU boxes (tests/test_pipeline_gpu.py).
+
+    ``rccl``: TWO 2-rank RCCL communicators, one per direction -- ``down`` carries lo -> hi traffic
+    (activations), ``up`` carries hi -> lo traffic (activation gradients).  RCCL executes the operations
+    of one communicator in issue order whatever stream they are enqueued on, so with a single
     communicator the 1F1B steady state (stage 0: send a1, recv g0; stage 1: send g0, recv a1) would pair
     a send with a send and deadlock.  With one communicator per direction every communicator only ever
     sees send on one side and recv on the other, in the same order.  Unique ids go through the default
-    store; ``send``/``recv`` are stream-ordered (capturable into a hipGraph, no host synchronisation).
+    store.
 
-    CPU configuration (and ``PDE_BACKEND=gloo`` rehearsals of a multi-rank GPU job on one card): gloo
-    ``isend``/``recv`` with one tag per direction; device tensors are staged through host memory."""
+    Either way ``send``/``recv`` are stream-ordered (capturable into a hipGraph, no host synchronisation);
+    sends run on a dedicated side stream so the compute stream never waits for the peer.
+
+    CPU configuration (``host``): gloo ``isend``/``recv`` with one tag per direction; device tensors are
+    staged through host memory."""
 
     TAG_DOWN, TAG_UP = 11, 12
 
@@ -50,18 +78,29 @@ class P2PChannel:
         self.peer_local = 1 - self.local_rank
         self.device = device
         self.down = self.up = None
+        self.ring = None
         self._meta = {}
         self._pending = []
         self._inflight = []  # tensors sent on the side stream: kept alive until flush() joins the streams
         self._send_stream = None
-        self.rccl = device.type == "cuda" and dist.get_backend() == "nccl"
+        self.mode = p2p_mode(device)
+        self.rccl = self.mode == "rccl"
+        self._store = store or (dist.distributed_c10d._get_default_store() if self.mode != "host" else None)
+        self._key = f"pde/p2p/{tag}/{self.lo}-{self.hi}"
+        if self.mode == "ring":
+            C = _native.comm()
+            slot = int(float(os.environ.get("PDE_P2P_SLOT_MB", "16")) * (1 << 20))
+            self.ring = C.P2PRing(device.index, slot, float(os.environ.get("PDE_P2P_TIMEOUT_S", "60")))
+            self._store.set(f"{self._key}/ring/{self.local_rank}", self.ring.ipc_handle())
+            self.ring.open(self._store.get(f"{self._key}/ring/{self.peer_local}"))
+            return
         if not self.rccl:
             return
-        store = store or dist.distributed_c10d._get_default_store()
+        store = self._store
         C = _native.comm()
         comms = []
         for direction in ("down", "up"):  # same creation order on both ranks
-            key = f"pde/p2p/{tag}/{self.lo}-{self.hi}/{direction}"
+            key = f"{self._key}/{direction}"
             if self.local_rank == 0:
                 store.set(key, C.rccl_unique_id())
             uid = store.get(key)
@@ -81,12 +120,20 @@ class P2PChannel:
         lo_side = self.local_rank == 0
         return self.TAG_DOWN if (lo_side == sending) else self.TAG_UP
 
+    def _gpu_send(self, t: torch.Tensor):
+        if self.ring is not None:
+            if t.data_ptr() % 16:  # the ring kernel copies 16-B vectors
+                t = t.clone()
+            self.ring.send(t)  # slot-sized pieces for large tensors (p2p_ring.hip)
+        else:
+            self._send_comm().send(t, self.peer_local)
+
     def send(self, t: torch.Tensor):
-        """Asynchronous send.  RCCL: enqueued on a dedicated send stream (after the producer's work), so
-        the compute stream never waits for the peer to post its receive.  gloo: isend, completed in
+        """Asynchronous send.  GPU: enqueued on a dedicated send stream (after the producer's work), so
+        the compute stream never waits for the peer to post its receive.  host: isend, completed in
         :meth:`flush`."""
         t = t.contiguous()
-        if not self.rccl:
+        if self.mode == "host":
             src = t.cpu() if t.is_cuda else t
             self._pending.append((dist.isend(src, self.peer, tag=self._tag(True)), src))
             return
@@ -95,7 +142,7 @@ class P2PChannel:
         cur = torch.cuda.current_stream(self.device)
         self._send_stream.wait_stream(cur)
         with torch.cuda.stream(self._send_stream):
-            self._send_comm().send(t, self.peer_local)
+            self._gpu_send(t)
         if torch.cuda.is_current_stream_capturing():
             # inside a hipGraph capture: no allocator stream bookkeeping; the tensor stays referenced
             # until flush() has joined the send stream back into the capturing stream
@@ -104,7 +151,7 @@ class P2PChannel:
             t.record_stream(self._send_stream)
 
     def flush(self):
-        """Complete outstanding sends (gloo) / order the compute stream after them (RCCL)."""
+        """Complete outstanding sends (host) / order the compute stream after them (GPU)."""
         for work, _ in self._pending:
             work.wait()
         self._pending = []
@@ -114,16 +161,23 @@ class P2PChannel:
 
     def recv(self, shape, dtype) -> torch.Tensor:
         t = torch.empty(shape, dtype=dtype, device=self.device)
-        if not self.rccl:
+        if self.mode == "host":
             if t.is_cuda:
                 h = torch.empty(shape, dtype=dtype)
                 dist.recv(h, self.peer, tag=self._tag(False))
                 t.copy_(h)
             else:
                 dist.recv(t, self.peer, tag=self._tag(False))
+        elif self.ring is not None:
+            self.ring.recv(t)
         else:
             self._recv_comm().recv(t, self.peer_local)
         return t
+
+    def check(self):
+        """Raise if a ring wait timed out (synchronises the device)."""
+        if self.ring is not None and self.ring.error():
+            raise RuntimeError(f"p2p ring {self._key}: a send/recv timed out waiting for the peer")
 
     def send_meta(self, t: torch.Tensor):
         """Shape/dtype handshake (first micro-batch only), 8 int64s over the same channel."""
@@ -144,6 +198,13 @@ class P2PChannel:
             if c is not None:
                 c.destroy()
         self.down = self.up = None
+        if self.ring is not None:
+            # the peer writes into my ring and ACKs into my ctrl word: both sides drain, meet, then unmap
+            torch.cuda.synchronize(self.device)
+            self._store.set(f"{self._key}/closed/{self.local_rank}", "1")
+            self._store.get(f"{self._key}/closed/{self.peer_local}")
+            self.ring.close()
+            self.ring = None
 
 
 class PipelineEngine:
@@ -169,6 +230,7 @@ class PipelineEngine:
             setattr(self, which, ch)
         self._fwd_meta = None  # (shape, dtype) of activations received from prev
         self._bwd_meta = None
+        self.timer = NO_PHASES  # utils.log.PhaseTimer: per-stage fwd / bwd / recv-wait times (bench)
 
     # -- primitives --------------------------------------------------------------------------------
     def _recv_act(self):
@@ -184,10 +246,15 @@ class PipelineEngine:
         self.next.send(y.detach())
 
     def _forward(self, mb, inputs, targets, n_mb, state):
-        x = inputs[mb] if self.first else self._recv_act()
-        y = self.module(x)
+        if self.first:
+            x = inputs[mb]
+        else:
+            with self.timer.phase("recv_wait"):
+                x = self._recv_act()
+        with self.timer.phase("fwd"):
+            y = self.module(x)
+            loss = self.loss_fn(y, targets[mb]) / n_mb if self.last else None
         if self.last:
-            loss = self.loss_fn(y, targets[mb]) / n_mb
             state["loss"].append(loss.detach())
             state["saved"][mb] = (x, loss, None)
         else:
@@ -197,10 +264,13 @@ class PipelineEngine:
     def _backward(self, mb, state):
         x, y, _ = state["saved"].pop(mb)
         if self.last:
-            y.backward()
+            with self.timer.phase("bwd"):
+                y.backward()
         else:
-            g = self.next.recv(y.shape, y.dtype)
-            torch.autograd.backward(y, g)
+            with self.timer.phase("recv_wait"):
+                g = self.next.recv(y.shape, y.dtype)
+            with self.timer.phase("bwd"):
+                torch.autograd.backward(y, g)
         if not self.first:
             self.prev.send(x.grad)
 
@@ -252,6 +322,11 @@ class PipelineEngine:
         if self._fwd_meta is None:
             self._fwd_meta = self.prev.recv_meta()
         return self._fwd_meta
+
+    def check(self):
+        for ch in (self.prev, self.next):
+            if ch is not None:
+                ch.check()
 
     def close(self):
         for ch in (self.prev, self.next):

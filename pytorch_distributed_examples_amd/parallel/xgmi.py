@@ -10,13 +10,18 @@ overlap with backward wants *several* buckets.  The reference relies on DDP's de
 
 Policy (sizes in bytes of the reduced dtype):
 * ``world == 1``: one bucket (no communication at all).
-* floor = ``CHANNEL_MIN_BYTES * links * channels_per_link`` -- every link's channels get >= 256 KiB.
+* floor = ``CHANNEL_MIN_BYTES * channels`` (channels = 2 per active link, or RCCL's pinned
+  ``NCCL_MIN_NCHANNELS``) -- every channel's slice of every bucket is >= 256 KiB, so at world 8 each bucket
+  splits into >= 14 channel-sized chunks over the 7 links (tests/test_ddp_cpu.py checks the plan); a
+  trailing remainder below the floor is merged into the previous bucket.
 * small models (total < 2 x floor, e.g. the 87 KB MNIST CNN, the 544 B hybrid fc): ONE bucket, reduced
   once after backward (latency-bound: a second collective would only add ~10-30 us of launch+sync).
 * otherwise ``~4`` buckets (first one half-size so the last layer's gradients start moving early),
   each clamped to [floor, 64 MiB].
 """
 from __future__ import annotations
+
+import os
 
 CHANNEL_MIN_BYTES = 256 * 1024
 CHANNELS_PER_LINK = 2
@@ -28,8 +33,17 @@ def active_links(world: int) -> int:
     return max(1, min(world - 1, 7))
 
 
+def channels(world: int) -> int:
+    """Channels the collective spreads a bucket over: RCCL's own minimum when the job pins it
+    (``NCCL_MIN_NCHANNELS``), else ``CHANNELS_PER_LINK`` per active xGMI link."""
+    env = os.environ.get("NCCL_MIN_NCHANNELS")
+    if env and env.isdigit() and int(env) > 0:
+        return max(int(env), active_links(world))
+    return active_links(world) * CHANNELS_PER_LINK
+
+
 def bucket_floor(world: int) -> int:
-    return CHANNEL_MIN_BYTES * active_links(world) * CHANNELS_PER_LINK
+    return CHANNEL_MIN_BYTES * channels(world)
 
 
 def plan_buckets(sizes_bytes: list[int], world: int, cap_bytes: int | None = None) -> list[list[int]]:
@@ -50,18 +64,22 @@ def plan_buckets(sizes_bytes: list[int], world: int, cap_bytes: int | None = Non
         first_cap = max(floor, cap // 2)
     else:
         cap = first_cap = max(1, cap_bytes)
+        floor = 0
     buckets: list[list[int]] = []
     cur: list[int] = []
     cur_bytes = 0
     for i, b in enumerate(sizes_bytes):
         limit = first_cap if not buckets else cap
-        if cur and cur_bytes + b > limit:
+        if cur and cur_bytes + b > limit and cur_bytes >= floor:  # never close a bucket below the floor
             buckets.append(cur)
             cur, cur_bytes = [], 0
         cur.append(i)
         cur_bytes += b
     if cur:
-        buckets.append(cur)
+        if buckets and cur_bytes < floor:
+            buckets[-1].extend(cur)  # a remainder below the floor rides with the previous bucket
+        else:
+            buckets.append(cur)
     return buckets
 
 

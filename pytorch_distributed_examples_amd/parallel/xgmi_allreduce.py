@@ -33,13 +33,15 @@ DEFAULT_THRESHOLD = int(os.environ.get("PDE_XGMI_THRESHOLD", str(1 << 20)))
 
 class XgmiAllreduce:
     def __init__(self, device: torch.device, group=None, max_bytes: int = 4 << 20, blocks: int = 256,
-                 timeout_s: float = 5.0):
+                 timeout_s: float = 5.0, read_delay_us: float = 0.0):
         assert device.type == "cuda", "the xGMI all-reduce is a GPU data plane"
         self.device = device
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.size = dist.get_world_size(group) if dist.is_initialized() else 1
         C = _native.comm()
         self.impl = C.XgmiAllreduce(self.rank, self.size, device.index, int(max_bytes), int(blocks), float(timeout_s))
+        if read_delay_us:  # test hook: a slow reader (tests/test_xgmi_gpu.py)
+            self.impl.set_read_delay_us(float(read_delay_us))
         if self.size > 1:
             store = dist.distributed_c10d._get_default_store()
             ranks = dist.get_process_group_ranks(group) if group is not None else list(range(self.size))
@@ -90,28 +92,43 @@ class RoutedComm:
         self.rccl, self.xgmi = rccl, xgmi
         self.size, self.rank = rccl.size, rccl.rank
         self.supports_avg = True
-        self.supports_bf16_wire = True
         self.threshold = min(int(threshold_bytes), xgmi.max_bytes)
         self.routed = {"xgmi": 0, "rccl": 0}
+        self._scratch: dict = {}  # persistent bf16 wire buffers of RCCL-routed fp32 tensors
+
+    def fuses_bf16_wire(self, t: torch.Tensor) -> bool:
+        """True when ``allreduce_async(t, wire_bf16=True)`` casts inside the one-shot kernel (the bucket
+        takes the xGMI path); DDP casts larger buckets itself into persistent bf16 buffers for RCCL."""
+        return t.dtype == torch.float32 and t.numel() * 4 <= self.threshold
 
     def allreduce_async(self, t: torch.Tensor, avg: bool = False, wire_bf16: bool = False):
         """``wire_bf16`` (fp32 ``t``): reduce bf16 copies -- fused into the one-shot kernel on the xGMI path;
-        on RCCL a cast into a bf16 scratch, a bf16 all-reduce, and the cast back."""
+        on RCCL our cast kernels into / out of a persistent bf16 scratch around a bf16 all-reduce."""
         if t.dtype == torch.float32 and t.numel() * 4 <= self.threshold:
             self.xgmi.allreduce_(t, avg, wire_bf16)
             self.routed["xgmi"] += 1
             return _Done()
         self.routed["rccl"] += 1
         if wire_bf16 and t.dtype == torch.float32:
-            w = t.to(torch.bfloat16)
+            C = _native.C()
+            key = (t.data_ptr(), t.numel())
+            w = self._scratch.get(key)
+            if w is None:
+                w = self._scratch[key] = torch.empty(t.numel(), dtype=torch.bfloat16, device=t.device)
+            C.cast_bf16_into(t.reshape(-1), w)
             self.rccl.allreduce_async(w, avg)
-            t.copy_(w)  # stream-ordered behind the collective
+            C.cast_f32_into(w, t.reshape(-1))  # stream-ordered behind the collective
             return _Done()
         return self.rccl.allreduce_async(t, avg)
 
     def allreduce_(self, t: torch.Tensor, avg: bool = False) -> torch.Tensor:
         self.allreduce_async(t, avg)
         return t
+
+    def check(self) -> None:
+        """Raise if a one-shot exchange timed out (its result was dropped); synchronises the device -- call
+        it at existing sync points (epoch end, before snapshots)."""
+        self.xgmi.check()
 
     def broadcast_(self, t: torch.Tensor, src: int) -> torch.Tensor:
         return self.rccl.broadcast_(t, src)

@@ -49,3 +49,62 @@ class StepTimer:
         if self._name is not None:
             self.totals[self._name] = self.totals.get(self._name, 0.0) + time.perf_counter() - self._t
             self._name = None
+
+
+class PhaseTimer:
+    """Per-phase device time of eager steps (fwd / bwd / comm wait / optimizer, and per
+    pipeline stage: forward / backward compute and the time a stage's stream spends in receive waits).
+
+    ``with timer.phase("fwd"): ...`` records a HIP event pair on the current stream around the work (on
+    CPU: wall time); :meth:`summary` synchronises once and returns milliseconds per phase, summed over the
+    recorded steps and divided by ``steps``.  A captured hipGraph has no host-visible phase boundaries, so
+    the bench measures phases on a few eager steps after its timed region."""
+
+    def __init__(self, device=None):
+        import torch
+
+        self.cuda = device is not None and torch.device(device).type == "cuda"
+        self.marks: list = []
+        self.steps = 0
+
+    def phase(self, name: str):
+        import contextlib
+
+        import torch
+
+        @contextlib.contextmanager
+        def cm():
+            if self.cuda:
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                yield
+                e.record()
+                self.marks.append((name, s, e))
+            else:
+                t0 = time.perf_counter()
+                yield
+                self.marks.append((name, t0, time.perf_counter()))
+
+        return cm()
+
+    def summary(self) -> dict:
+        import torch
+
+        if self.cuda:
+            torch.cuda.synchronize()
+        out: dict[str, float] = {}
+        for name, s, e in self.marks:
+            ms = s.elapsed_time(e) if self.cuda else (e - s) * 1e3
+            out[name] = out.get(name, 0.0) + ms
+        n = max(1, self.steps)
+        return {k: round(v / n, 4) for k, v in out.items()}
+
+
+class _NoPhase:
+    def phase(self, name: str):
+        import contextlib
+
+        return contextlib.nullcontext()
+
+
+NO_PHASES = _NoPhase()

@@ -23,6 +23,31 @@ def test_bucket_policy():
     assert xgmi.plan_buckets([10, 10, 10], world=2, cap_bytes=15) == [[0], [1], [2]]
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("model", ["mlp_fp32", "mlp_bf16", "resnet_stage2_bf16", "resnet50_fp32"])
+def test_bucket_plan_fills_every_link(world, model):
+    """every multi-bucket plan gives each bucket >= 7 channel-sized (>= 256 KiB)
+    chunks at world 8 -- RCCL's channels over all 7 xGMI links carry traffic -- and >= 2 chunks per active
+    link at any world; the trailing remainder is merged, never a sub-floor bucket."""
+    from pytorch_distributed_examples_amd.models.mlp import reference_mlp
+    from pytorch_distributed_examples_amd.models.resnet import ResNet50, ResNetShard2
+
+    net = {"mlp_fp32": reference_mlp, "mlp_bf16": reference_mlp, "resnet_stage2_bf16": ResNetShard2,
+           "resnet50_fp32": ResNet50}[model]()
+    el = 2 if model.endswith("bf16") else 4
+    sizes = [p.numel() * el for p in reversed(list(net.parameters()))]
+    plan = xgmi.plan_buckets(sizes, world=world)
+    assert sorted(i for b in plan for i in b) == list(range(len(sizes)))
+    if len(plan) == 1:
+        assert sum(sizes) < 2 * xgmi.bucket_floor(world)  # only latency-bound models stay in one bucket
+        return
+    for b in plan:
+        chunks = sum(sizes[i] for i in b) // xgmi.CHANNEL_MIN_BYTES
+        assert chunks >= 2 * xgmi.active_links(world), (model, world, chunks)
+        if world == 8:
+            assert chunks >= 7
+
+
 def _ddp_worker(rank, world, mode):
     import torch.distributed as dist
 

@@ -161,6 +161,46 @@ def test_batchnorm(gpu, relu, res, n, c, h):
     assert torch.equal(y2, y)
     y2.float().backward(gy.permute(0, 2, 3, 1))
     assert rel_err(gamma.grad, g2.grad) < 2e-2
+    assert OF._C().bn_error(True) == 0  # no one-launch BatchNorm wait timed out
+
+
+def test_batchnorm_one_launch_graph_replays(gpu):
+    """The one-launch BatchNorm kernels (stats -> ticket finalize -> generation flag -> apply) captured in
+    a hipGraph: every replay counts the channel groups' flags up and must reproduce the eager results bit
+    for bit (forward y, running stats trajectory, and backward dx / dgamma / dbeta / residual grad)."""
+    torch.manual_seed(5)
+    n, c, h = 8, 256, 8
+    x = (torch.randn(n, h, h, c, device=gpu) * 2 + 0.5).bfloat16()
+    r = torch.randn(n, h, h, c, device=gpu).bfloat16()
+    gamma = torch.rand(c, device=gpu) + 0.5
+    beta = torch.randn(c, device=gpu)
+    gy = torch.randn(n, h, h, c, device=gpu).bfloat16()
+
+    def step(rm, rv):
+        xg, rg = x.clone().requires_grad_(), r.clone().requires_grad_()
+        g_, b_ = gamma.clone().requires_grad_(), beta.clone().requires_grad_()
+        y = OF.batch_norm(xg, g_, b_, rm, rv, True, 0.1, 1e-5, rg, True)
+        y.backward(gy)
+        return y.detach(), xg.grad, rg.grad, g_.grad, b_.grad
+
+    rm0, rv0 = torch.zeros(c, device=gpu), torch.ones(c, device=gpu)
+    eager = [step(rm0, rv0) for _ in range(3)]
+    rm1, rv1 = torch.zeros(c, device=gpu), torch.ones(c, device=gpu)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step(torch.zeros(c, device=gpu), torch.ones(c, device=gpu))  # warm-up (allocates the ticket windows)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        outs = step(rm1, rv1)
+    for k in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        for a, b in zip(outs, eager[k]):
+            assert torch.equal(a, b), k
+    assert torch.equal(rm1, rm0) and torch.equal(rv1, rv0)
+    assert OF._C().bn_error(True) == 0
 
 
 # c = 16: 8-channel vector kernels; c = 10: scalar kernels (MNIST CNN channel counts)

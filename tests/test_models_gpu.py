@@ -181,7 +181,8 @@ def test_cnn_trains(gpu):
     assert sum(losses[-5:]) / 5 < losses[0] * 0.7, losses
 
 
-def _mixed_reference_loss(m, x, y):
+def _mixed_reference_loss(m, x, y, mask2=None, mask1=None):
+    """``mask2`` [N, 20] (Dropout2d, already x 1/(1-p)) on conv2's output, ``mask1`` [N, 50] on relu(fc1)."""
     import torch.nn.functional as F
 
     def st(t):  # bf16-rounded value, identity gradient
@@ -190,9 +191,108 @@ def _mixed_reference_loss(m, x, y):
     c1 = F.conv2d(st(x), st(m.conv1.weight), m.conv1.bias)
     r1 = st(F.relu(F.max_pool2d(c1, 2)))
     c2 = F.conv2d(r1, st(m.conv2.weight), m.conv2.bias)
+    if mask2 is not None:
+        c2 = c2 * mask2[:, :, None, None]
     r2 = F.relu(F.max_pool2d(c2, 2)).flatten(1)
     h = F.relu(F.linear(r2, m.fc1.weight, m.fc1.bias))
+    if mask1 is not None:
+        h = h * mask1
     return F.nll_loss(F.log_softmax(F.linear(h, m.fc2.weight, m.fc2.bias), 1), y)
+
+
+def _cnn_hash_u01(seed: int, ids):
+    """Host copy of cnn_fused.hip's counter hash (splitmix64 finaliser over seed + golden * (id + 1))."""
+    import numpy as np
+
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + np.uint64(0x9E3779B97F4A7C15) * (np.asarray(ids, dtype=np.uint64) + np.uint64(1))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z >> np.uint64(40)).astype(np.float64) / 16777216.0
+
+
+def _cnn_masks(counter: int, n: int, p2: float, p1: float):
+    """The training kernel's Dropout2d [n, 20] and dropout [n, 50] multipliers for RNG counter ``counter``."""
+    import numpy as np
+
+    seed = (counter * 0xD1B54A32D192ED03) % (1 << 64)
+    u2 = _cnn_hash_u01(seed ^ 0x5BD1E995, np.arange(n * 20)).reshape(n, 20)
+    u1 = _cnn_hash_u01(seed ^ 0x27D4EB2F, np.arange(n * 50)).reshape(n, 50)
+    m2 = np.where(u2 >= np.float32(p2), np.float32(1.0) / np.float32(1.0 - p2), 0.0).astype(np.float32)
+    m1 = np.where(u1 >= np.float32(p1), np.float32(1.0) / np.float32(1.0 - p1), 0.0).astype(np.float32)
+    return torch.from_numpy(m2), torch.from_numpy(m1)
+
+
+@pytest.mark.parametrize("p2,p1", [(0.5, 0.5), (0.25, 0.6)])
+def test_fused_cnn_dropout_masks(gpu, p2, p1):
+    """Training-mode dropout of the headline kernel (cnn_fused.hip P0/P2/P3): the kernel's loss and every
+    gradient must match a CPU reference that applies the SAME hash masks -- Dropout2d constant per (image,
+    channel) on conv2's output, elementwise dropout on relu(fc1), both scaled by 1/(1-p) and the same in
+    forward and backward.  Also: keep rates within 2 % of 1-p, a wrong seed does NOT match (the check
+    discriminates), and successive hipGraph replays draw fresh masks (the counter advances per step)."""
+    from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
+
+    torch.manual_seed(0)
+    n = 512
+    m_cpu = Net().train()
+    m_gpu = copy.deepcopy(m_cpu).to(gpu).train()
+    fused = FusedCNN(m_gpu)
+    x = torch.randn(n, 1, 28, 28)
+    y = torch.randint(0, 10, (n,))
+    xg, yg = x.to(gpu), y.to(gpu)
+    ctr = OF._rng_counter(xg.device)
+    ctr.fill_(12345)
+
+    m2, m1 = _cnn_masks(12345, n, p2, p1)
+    assert abs((m2 > 0).float().mean().item() - (1 - p2)) < 0.02
+    assert abs((m1 > 0).float().mean().item() - (1 - p1)) < 0.02
+
+    def reference(mask2, mask1):
+        ref = copy.deepcopy(m_cpu)
+        loss = _mixed_reference_loss(ref, x, y, mask2, mask1)
+        loss.backward()
+        return loss.item(), torch.cat([p.grad.reshape(-1) for p in ref.parameters()])
+
+    def errs(g, ref_g):
+        out, off = {}, 0
+        for name, p in m_cpu.named_parameters():
+            k = p.numel()
+            out[name] = rel_err(g[off:off + k].cpu(), ref_g[off:off + k])
+            off += k
+        return out
+
+    g = torch.zeros(fused.flat.numel(), device=gpu)
+    loss = fused.forward_backward(xg, yg, grad_out=g, p_drop2=p2, p_drop1=p1).item()
+    assert int(ctr.item()) == 12346  # the reduction advanced the counter for the next step
+    l_ref, g_ref = reference(m2, m1)
+    assert abs(loss - l_ref) < 1e-2, (loss, l_ref)
+    e = errs(g, g_ref)
+    assert all(v < 3e-2 for v in e.values()), e
+    # negative control: the next counter's masks must NOT explain this step
+    w2, w1 = _cnn_masks(12346, n, p2, p1)
+    l_w, g_w = reference(w2, w1)
+    assert max(errs(g, g_w).values()) > 0.2
+
+    # hipGraph: one captured step, two replays -> masks of counters 12346 and 12347
+    ctr.fill_(12346)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fused.forward_backward(xg, yg, grad_out=g, p_drop2=p2, p_drop1=p1)  # warm-up: counter -> 12347
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        gl = fused.forward_backward(xg, yg, grad_out=g, p_drop2=p2, p_drop1=p1)
+    ctr.fill_(12346)
+    for k in (12346, 12347):
+        graph.replay()
+        torch.cuda.synchronize()
+        l_ref, g_ref = reference(*_cnn_masks(k, n, p2, p1))
+        assert abs(gl.item() - l_ref) < 1e-2, (k, gl.item(), l_ref)
+        e = errs(g, g_ref)
+        assert all(v < 3e-2 for v in e.values()), (k, e)
+    assert int(ctr.item()) == 12348
 
 
 def test_fused_cnn_matches_reference(gpu):

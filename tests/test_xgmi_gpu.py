@@ -76,6 +76,30 @@ for _ in range(4):
 torch.cuda.synchronize()
 assert torch.allclose(t, torch.full_like(t, vals[0]), rtol=1e-6), (t[:4], vals[0])
 xa.check()
+# consecutive calls of DIFFERENT sizes (grids 1..128 workgroups, fp32 and bf16 wires) queued with no host
+# sync in between, while the last rank is a slow reader (read_delay_us holds each of its
+# workgroups between the flag wait and the peer reads): no call may see a later call's staged bytes
+# (ADVICE r2: per-workgroup epochs diverged across sizes and let call k+1 overwrite a slot still being read)
+slow = XgmiAllreduce(dev, max_bytes=4 << 20, timeout_s=20.0,
+                     read_delay_us=(300.0 if r == N - 1 else 0.0))
+sizes = [1000, 262144, 7, 21840, 65536, 1 << 20, 300, 131072] * 3
+outs = []
+torch.cuda.synchronize()
+dist.barrier()
+for i, n in enumerate(sizes):
+    x = rank_data(r, n, 50 + i).to(dev, non_blocking=False)
+    slow.allreduce_(x, wire_bf16=(i % 3 == 2))
+    outs.append(x)
+torch.cuda.synchronize()
+slow.check()
+for i, (n, x) in enumerate(zip(sizes, outs)):
+    if i % 3 == 2:
+        ref = sum(rank_data(k, n, 50 + i).bfloat16().float() for k in range(N))
+        assert torch.allclose(x.cpu(), ref, rtol=1e-6, atol=1e-6), ("bf16", i, n)
+    else:
+        ref = sum(rank_data(k, n, 50 + i) for k in range(N))
+        assert torch.allclose(x.cpu(), ref, rtol=1e-5, atol=1e-5), (i, n)
+slow.close()
 # DDP over the routing communicator: the small bucket takes the xGMI path
 from pytorch_distributed_examples_amd.parallel.ddp import DistributedDataParallel
 from pytorch_distributed_examples_amd.parallel.xgmi_allreduce import RoutedComm
