@@ -44,7 +44,8 @@ def _launch_ranks(n: int, argv) -> int:
 def main() -> None:
     argv = sys.argv[1:]
     n = _requested_gpus(argv)
-    if n > 1 and "WORLD_SIZE" not in os.environ:
+    elastic = "elastic_cnn" in argv  # its own launcher (the elastic driver), never torchrun
+    if n > 1 and "WORLD_SIZE" not in os.environ and not elastic:
         # parent: no torch import, no GPU context -- the ranks own the GPUs
         sys.exit(_launch_ranks(n, argv))
     os.environ.setdefault("OMP_NUM_THREADS", "1")

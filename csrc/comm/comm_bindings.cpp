@@ -52,6 +52,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            },
            py::arg("uid"), py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("blocking") = true)
       .def("abort", [](RcclComm& c) { py::gil_scoped_release nogil; c.abort(); })
+      .def("shrink_from",
+           [](RcclComm& c, RcclComm& parent, const std::vector<int>& exclude, bool abort_parent) {
+             py::gil_scoped_release nogil;
+             return c.shrink_from(parent, exclude, abort_parent);
+           },
+           py::arg("parent"), py::arg("exclude"), py::arg("abort_parent") = false)
+      .def_static("shrink_supported", &RcclComm::shrink_supported)
       .def("destroy", [](RcclComm& c) { py::gil_scoped_release nogil; c.destroy(); })
       .def_property_readonly("valid", &RcclComm::valid)
       .def_property_readonly("rank", &RcclComm::rank)

@@ -1,6 +1,8 @@
 // RCCL communicator manager: see comm_manager.h.
 #include "comm_manager.h"
 
+#include <dlfcn.h>
+
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -117,6 +119,52 @@ void RcclComm::init(const std::string& uid, int rank, int size, int device, bool
   } else {
     check(r, "ncclCommInitRankConfig");
   }
+}
+
+// ncclCommShrink appeared in RCCL 2.27; torch's bundled librccl (2.26.x) does not export it, and this module
+// binds to the librccl torch already loaded, so the symbol is looked up at run time.
+using ShrinkFn = ncclResult_t (*)(ncclComm_t, int*, int, ncclComm_t*, ncclConfig_t*, int);
+static ShrinkFn shrink_fn() {
+  static ShrinkFn fn = reinterpret_cast<ShrinkFn>(dlsym(RTLD_DEFAULT, "ncclCommShrink"));
+  return fn;
+}
+
+bool RcclComm::shrink_supported() { return shrink_fn() != nullptr; }
+
+int RcclComm::shrink_from(RcclComm& parent, const std::vector<int>& exclude, bool abort_parent) {
+  if (parent.comm_ == nullptr) throw std::runtime_error("pde rccl: shrink from an invalid communicator");
+  if (comm_ != nullptr) abort();
+  hip_check(hipSetDevice(parent.device_), "hipSetDevice");
+  if (stream_ == nullptr) {
+    int lo = 0, hi = 0;
+    hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priority range");
+    hip_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "comm stream");
+  }
+  std::vector<int> ex(exclude);
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  ncclComm_t out = nullptr;
+  if (ShrinkFn fn = shrink_fn()) {
+    // survivors only: the excluded (dead) ranks do not take part; ABORT first tears down in-flight work
+    check(fn(parent.comm_, ex.data(), static_cast<int>(ex.size()), &out, &cfg,
+             abort_parent ? NCCL_SHRINK_ABORT : NCCL_SHRINK_DEFAULT), "ncclCommShrink");
+    comm_ = out;
+    device_ = parent.device_;
+    check(ncclCommUserRank(comm_, &rank_), "ncclCommUserRank");
+    check(ncclCommCount(comm_, &size_), "ncclCommCount");
+    return 1;
+  }
+  // graceful shrink without ncclCommShrink (every parent rank alive and calling): the leaving ranks pass
+  // NCCL_SPLIT_NOCOLOR -- a split keeps the parent's topology and skips the unique-id exchange
+  bool leaving = false;
+  for (int r : ex) leaving = leaving || r == parent.rank_;
+  check(ncclCommSplit(parent.comm_, leaving ? NCCL_SPLIT_NOCOLOR : 0, parent.rank_, &out, &cfg), "ncclCommSplit");
+  comm_ = out;
+  device_ = parent.device_;
+  if (comm_ != nullptr) {
+    check(ncclCommUserRank(comm_, &rank_), "ncclCommUserRank");
+    check(ncclCommCount(comm_, &size_), "ncclCommCount");
+  }
+  return 2;
 }
 
 void RcclComm::abort() {

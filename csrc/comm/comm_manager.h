@@ -33,6 +33,12 @@ class RcclComm {
   // communicator config so a later abort() never waits on a dead peer.
   void init(const std::string& uid, int rank, int size, int device, bool blocking = true);
   void abort();    // ncclCommAbort: safe while collectives are hung
+  // Shrink-only membership change: a communicator over `parent` minus `exclude` (parent
+  // ranks).  ncclCommShrink when the loaded RCCL exports it (survivors only; `abort_parent` first aborts
+  // in-flight work) -> returns 1; else ncclCommSplit (every parent rank must call, leavers get no
+  // communicator) -> returns 2.  The parent stays valid (destroy/abort it separately).
+  int shrink_from(RcclComm& parent, const std::vector<int>& exclude, bool abort_parent);
+  static bool shrink_supported();
   void destroy();  // ncclCommDestroy after a clean finish
   bool valid() const { return comm_ != nullptr; }
   int rank() const { return rank_; }

@@ -80,6 +80,8 @@ def _run_trainer(remote_emb_module, rank, epochs, device_str):
             print(f"Training done for epoch {epoch} (trainer {rank}, loss {loss.item():.4f})", flush=True)
     dt = time.perf_counter() - t0
     plane = "p2p-ring" if remote_emb_module.uses_ring(device) else "rpc-host"
+    if remote_emb_module.uses_ring(device):
+        remote_emb_module.close()
     print(f"trainer {rank}: {steps} steps, {dt / steps * 1e3:.2f} ms/step (embedding data plane: {plane})",
           flush=True)
     return steps

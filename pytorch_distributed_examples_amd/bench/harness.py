@@ -8,6 +8,11 @@ Workloads (``--model``), one process per GPU, synthetic data resident in HBM, ra
 * ``mlp`` -- the elastic-DDP script's 5x1024 MLP (pytorch_elastic/mnist_ddp_elastic.py:133-173), batch 128,
   Adam 1e-3, cross-entropy; data parallel.
 * ``resnet50`` -- ResNet-50 at 128x128, batch 32, MSE, SGD 0.05, pure data parallel.
+* ``resnet50_stage`` -- ONE pipeline stage of configs 3/4 at micro-batch size ``--batch`` (default 8, the
+  reference's split size): ``--stage 1`` = stem+layer1+layer2 on images, ``--stage 2`` = layer3+layer4+fc on a
+  [m,16,16,512] bf16 activation with MSE; each step is forward, backward against an upstream gradient
+  (stage 1) / the loss (stage 2, input gradient included: it goes upstream), SGD -- what one stage GPU does
+  per micro-batch, minus the P2P transfers.
 * ``resnet50_pp`` -- BASELINE configs 3 and 4: the 2-stage ResNet-50 of rpc/model_parallel_ResNet50.py
   (stem+layer1+layer2 | layer3+layer4+fc, :85-139), batch 32 split into micro-batches of ``--split-size``
   (the reference's ``split_size`` semantics, :171, quirk Q2), one stage per GPU, activations and their
@@ -40,15 +45,16 @@ METRIC = "images/sec (whole node) MNIST DDP + ResNet50 RPC-MP at 1/2/4/8 MI355X"
 BASELINE_CONFIG = {"cnn": "1: MNIST CNN DDP bf16, RCCL allreduce over xGMI",
                    "mlp": "0/1 workload of mnist_ddp_elastic.py (5x1024 MLP DDP)",
                    "resnet50": "ResNet-50 128px data parallel (no BASELINE config; kernel reference point)",
+                   "resnet50_stage": "one stage of configs 3/4 at micro-batch size (per-stage kernel time)",
                    "resnet50_pp": "3 (world 2: ResNet50 model-parallel across 2 MI355X) / "
                                   "4 (world 8: 2-stage pipeline x 4-way DDP)"}
 # The reference's own numbers, measured on CPU by the survey (no published figures exist).
 # Only same-workload, same-world comparisons are reported.
 REFERENCE_IMG_S = {("mlp", 1): 7452.0, ("mlp", 2): 2630.0, ("mlp", 4): 4620.0,
                    ("resnet50_pp", 2): 18.0}
-DEFAULT_BATCH = {"cnn": 1024, "mlp": 128, "resnet50": 32, "resnet50_pp": 32}
+DEFAULT_BATCH = {"cnn": 1024, "mlp": 128, "resnet50": 32, "resnet50_stage": 8, "resnet50_pp": 32}
 MODEL_NAMES = {"cnn": "mnist_cnn_Net", "mlp": "mnist_mlp_5x1024", "resnet50": "resnet50_128px",
-               "resnet50_pp": "resnet50_128px_2stage"}
+               "resnet50_stage": "resnet50_128px_stage", "resnet50_pp": "resnet50_128px_2stage"}
 
 
 def parse_args(argv=None):
@@ -57,7 +63,14 @@ def parse_args(argv=None):
                     help="ranks (one per GPU); bench.py launches them when run without torchrun")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--model", default="cnn", choices=["cnn", "mlp", "resnet50", "resnet50_pp", "resnet50_hybrid"])
+    ap.add_argument("--model", default="cnn",
+                    choices=["cnn", "mlp", "resnet50", "resnet50_stage", "resnet50_pp", "resnet50_hybrid",
+                             "elastic_cnn"])
+    ap.add_argument("--stage", type=int, default=1, choices=[1, 2], help="resnet50_stage: which pipeline stage")
+    ap.add_argument("--scale-to", type=int, default=None, help="elastic_cnn: world size after the first round")
+    ap.add_argument("--elastic-worker", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--hosts-file", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--report", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--batch", type=int, default=None, help="per-replica batch")
     ap.add_argument("--split-size", type=int, default=8, help="resnet50_pp: micro-batch size (reference: 4 or 8)")
     ap.add_argument("--schedule", default="gpipe", choices=["gpipe", "1f1b"], help="resnet50_pp schedule")
@@ -152,6 +165,33 @@ def build_data_parallel(args, ctx, batch) -> Workload:
             model = reference_mlp().to(dev)
             opt = FusedAdam(model.parameters(), lr=1e-3)
             loss_fn = OF.cross_entropy
+    elif args.model == "resnet50_stage":
+        from ..data.synthetic import resnet_batch
+        from ..models.resnet import ResNetShard1, ResNetShard2
+
+        img = args.image or 128
+        g = torch.Generator().manual_seed(0)
+        model = (ResNetShard1() if args.stage == 1 else ResNetShard2()).to(dev)
+        opt = FusedSGD(model.parameters(), lr=0.05)
+        if args.stage == 1:
+            x, _ = resnet_batch(batch, img, 1000, dev, g)
+            with torch.no_grad():
+                yshape = model(x).shape
+            # the gradient stage 2 would send back for the stage-1 output (train_step: out.backward(dy))
+            dy = (torch.randn(yshape, generator=g) * 1e-3).to(dev, model(x).dtype)
+            loss_fn = None
+            batches = [(x, dy)]
+        else:
+            s1 = ResNetShard1().to(dev)
+            x0, y = resnet_batch(batch, img, 1000, dev, g)
+            with torch.no_grad():
+                act = s1(x0)  # a stage-1 activation of the native layout (NHWC bf16 on GPU)
+            del s1
+            loss_fn = OF.mse_loss
+            batches = [(act.requires_grad_(True), y)]  # its gradient goes upstream: dgrad of layer3's first convs
+
+        def batch_fn(i):
+            return batches[0]
     else:
         from ..data.synthetic import resnet_batch
         from ..models.resnet import ResNet50
@@ -222,10 +262,19 @@ def build_data_parallel(args, ctx, batch) -> Workload:
                 opt.step()
             return loss
         ddp.zero_grad()
-        with t.phase("fwd"):
-            loss = loss_fn(ddp(x), y)
-        with t.phase("bwd"):
-            loss.backward()
+        if x.requires_grad:
+            x.grad = None  # a stage input: its gradient is produced fresh every step (sent upstream)
+        if loss_fn is None:  # a pipeline stage without the loss: backward from the upstream gradient y
+            with t.phase("fwd"):
+                out = ddp(x)
+            with t.phase("bwd"):
+                out.backward(y)
+            loss = None
+        else:
+            with t.phase("fwd"):
+                loss = loss_fn(ddp(x), y)
+            with t.phase("bwd"):
+                loss.backward()
         if not ddp.overlap:  # graph mode: buckets reduced after backward on the capturing stream
             with t.phase("comm"):
                 ddp.sync_gradients()
@@ -246,7 +295,8 @@ def build_data_parallel(args, ctx, batch) -> Workload:
         return one(x, y) if one is not None else train_step(x, y)
 
     routed = getattr(comm, "routed", None)
-    w = Workload(step, batch * ctx.world_size, f"dp{ctx.world_size}", hipgraph=one is not None,
+    extra = {"stage": args.stage} if args.model == "resnet50_stage" else {}
+    w = Workload(step, batch * ctx.world_size, f"dp{ctx.world_size}", **extra, hipgraph=one is not None,
                  fused_step=fused is not None or fmlp is not None, rccl_nranks=nranks,
                  steps_per_graph=group.steps if group is not None else (1 if one is not None else 0),
                  allreduce=("xgmi-in-reduce-kernel" if xgmi is not None else
@@ -380,6 +430,14 @@ def _measure_phases(work, ctx, args):
 
 def main(argv=None):
     args = parse_args(argv)
+    if args.model == "elastic_cnn":  # BASELINE config 2 (bench/elastic.py); bench.py runs it without torchrun
+        from . import elastic
+
+        if args.elastic_worker:
+            return elastic.worker(args)
+        bench_py = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                                "bench.py")
+        sys.exit(elastic.parent(args, bench_py))
     batch = args.batch or DEFAULT_BATCH[args.model]
     ctx = pdist.init_distributed(device="cpu" if args.device == "cpu" else None)
     if args.gpus is not None and args.gpus != ctx.world_size:
@@ -414,7 +472,8 @@ def main(argv=None):
     same_shape = args.image is None and batch == DEFAULT_BATCH[args.model]
     ref = REFERENCE_IMG_S.get((args.model, ctx.world_size)) if same_shape else None
     if ctx.rank == 0:
-        cfg = {"model": MODEL_NAMES[args.model], "baseline_config": BASELINE_CONFIG[args.model],
+        name = MODEL_NAMES[args.model] + (str(args.stage) if args.model == "resnet50_stage" else "")
+        cfg = {"model": name, "baseline_config": BASELINE_CONFIG[args.model],
                "global_batch": work.images_per_step, "seq_len": None,
                "image": "1x28x28" if args.model in ("cnn", "mlp") else f"3x{args.image or 128}x{args.image or 128}",
                "parallelism": work.parallelism, "final_loss": round(final_loss, 4)}

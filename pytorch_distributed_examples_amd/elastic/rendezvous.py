@@ -61,6 +61,14 @@ class RendezvousClient:
                 raise TimeoutError(f"worker {self.wid}: no rendezvous round after {after} within {self.timeout_s}s")
             time.sleep(0.05)
 
+    def members(self, rnd: int | None = None) -> list[str]:
+        """Worker ids of round ``rnd`` (default: the current one) in rank order."""
+        r = self.round if rnd is None else rnd
+        key = f"round/{r}/members"
+        if r < 0 or not self.store.check([key]):
+            return []
+        return self.store.get(key).decode().split(",")
+
     def pg_store(self):
         return dist.PrefixStore(f"pg/{self.round}", self.store)
 

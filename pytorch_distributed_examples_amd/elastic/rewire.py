@@ -67,25 +67,61 @@ class _GpuWork:
 
 
 class RoundComm:
-    """Communicator set of one rendezvous round (see the module docstring)."""
+    """Communicator set of one rendezvous round (see the module docstring).
+
+    ``parent`` (the previous round's RoundComm, not yet torn down): when this round's members are a subset
+    of the parent's -- a shrink -- and the loaded RCCL exports ``ncclCommShrink``, the RCCL communicator is
+    shrunk from the parent's (the dead ranks excluded, in-flight work aborted first) instead of being built
+    from a fresh unique id; ``self.how`` records ``shrink`` / ``init``.  (torch's bundled RCCL 2.26 has no
+    ncclCommShrink: there a shrink re-initialises.)  ``use_rccl=False``: control plane only (the fused CNN
+    exchanges gradients over xGMI inside its reduction kernel)."""
 
     def __init__(self, rdzv: RendezvousClient, rank: int, size: int, device: torch.device,
-                 timeout_s: float = 120.0, grace_s: float = 2.0):
+                 timeout_s: float = 120.0, grace_s: float = 2.0, parent: "RoundComm | None" = None,
+                 use_rccl: bool = True):
         self.rdzv, self.rank, self.size, self.device = rdzv, rank, size, device
         self.timeout_s, self.grace_s = timeout_s, grace_s
+        self.members = rdzv.members()
+        self.how = "none"
         store = rdzv.pg_store()
         dist.init_process_group("gloo", store=store, rank=rank, world_size=size,
                                 timeout=datetime.timedelta(seconds=timeout_s))
         self.rccl = None
-        if device.type == "cuda" and size > 1:
+        if use_rccl and device.type == "cuda" and size > 1:
             C = _native.comm()
-            if rank == 0:
-                store.set("rccl_uid", C.rccl_unique_id())
-            uid = store.get("rccl_uid")
-            self.rccl = C.RcclComm()
-            self.rccl.init(uid, rank, size, device.index, True)
+            excl = self._shrink_plan(parent)
+            if excl is not None and C.RcclComm.shrink_supported():
+                self.rccl = C.RcclComm()
+                self.rccl.shrink_from(parent.rccl, excl, True)
+                self.how = "shrink"
+            else:
+                if rank == 0:
+                    store.set("rccl_uid", C.rccl_unique_id())
+                uid = store.get("rccl_uid")
+                self.rccl = C.RcclComm()
+                self.rccl.init(uid, rank, size, device.index, True)
+                self.how = "init"
+        if parent is not None:
+            parent.release()
         self.supports_avg = self.rccl is not None
         self._steps = []  # end-of-step events not yet checked on the host (GPU data plane)
+
+    def _shrink_plan(self, parent):
+        """Parent ranks to exclude when this round only drops members of the parent's round, else None."""
+        if parent is None or parent.rccl is None or not parent.members or not self.members:
+            return None
+        if not set(self.members) < set(parent.members):
+            return None
+        survivors = [m for m in parent.members if m in self.members]
+        if survivors != self.members:  # the shrunk communicator keeps the parent's rank order
+            return None
+        return [i for i, m in enumerate(parent.members) if m not in self.members]
+
+    def release(self):
+        """Drop the RCCL communicator of a round whose successor was built (shrunk from it or not)."""
+        if self.rccl is not None:
+            self.rccl.abort()
+            self.rccl = None
 
     # -- data plane ------------------------------------------------------------------------------
     def allreduce_async(self, t: torch.Tensor, avg: bool = False):
@@ -174,14 +210,18 @@ class RoundComm:
         if self.rccl is not None:
             self.rccl.abort()
 
-    def close(self, abort: bool = False):
+    def close(self, abort: bool = False, keep_rccl: bool = False):
+        """End of the round.  ``keep_rccl``: leave the RCCL communicator alive as the next round's shrink
+        parent (released by that round); the gloo control group is always torn down."""
         if self.rccl is not None and not abort:
             try:
                 self.drain()
             except PeerFailure:
                 abort = True
         self._steps = []
-        if self.rccl is not None:
+        if self.rccl is not None and keep_rccl:
+            pass
+        elif self.rccl is not None:
             if abort:
                 self.rccl.abort()
             else:
@@ -269,11 +309,13 @@ def run_elastic(args):
     step = 0
     ddp = None
     pid = os.getpid()
+    parent = None  # previous round's communicator set, kept as a possible shrink parent
     while True:
         rnd, rank, size = rdzv.join()
-        comm = RoundComm(rdzv, rank, size, dev)
+        comm = RoundComm(rdzv, rank, size, dev, parent=parent)
+        parent = None
         log = RankLogger(rank)
-        log.print(f"[rewire] round {rnd}: rank {rank} of {size} (pid {pid})", all_ranks=True)
+        log.print(f"[rewire] round {rnd}: rank {rank} of {size} (pid {pid}, rccl {comm.how})", all_ranks=True)
         try:
             # rank 0 is a survivor with the newest commit: everybody adopts its state
             state = comm.broadcast_object({"pos": dict(pos), "opt": _to_cpu(optimizer.state_dict())}
@@ -326,11 +368,15 @@ def run_elastic(args):
         except PeerFailure as exc:
             log.print(f"[rewire] round {rnd}: peer failure ({str(exc).splitlines()[0][:120]}); restoring commit "
                       f"epoch {commit._pos['epoch']} seen {commit._pos['seen']}", all_ranks=True)
-            comm.close(abort=True)
+            keep = comm.rccl is not None and comm.rccl.shrink_supported()
+            comm.close(abort=not keep, keep_rccl=keep)  # a shrink (ABORT flag) tears its work down
+            parent = comm if keep else None
             commit.restore()
         except MembershipChanged:
             log.print(f"[rewire] round {rnd}: membership changed, re-joining", all_ranks=True)
-            comm.close()
+            keep = comm.rccl is not None and comm.rccl.shrink_supported()
+            comm.close(keep_rccl=keep)
+            parent = comm if keep else None
     pdist.shutdown()
 
 
@@ -351,3 +397,176 @@ def _test(model, loader, dev, comm, log):
             raise PeerFailure(str(exc)) from exc
     log.print(f"Global test accuracy: {t[0].item() / max(1.0, t[1].item()) * 100:.2f}%")
     model.train(was)
+
+
+def run_elastic_fused(args, report=None):
+    """``mnist_ddp_elastic.py --rewire --model cnn --fused`` and the elastic bench (BASELINE config 2).
+
+    The fused whole-network CNN step with the gradient exchange over xGMI INSIDE its reduction kernel
+    (``FusedCNN.forward_backward(..., xgmi=...)``: 2 launches per step at any world size) and the SGD update
+    fused in; ``graph_steps`` steps recorded into ONE hipGraph per round (recaptured after every membership
+    change: the xGMI view and the world size are baked in).  No host liveness wait per step: a dead peer
+    makes the exchange time out (bounded spin, error word) and surfaces at the next commit point
+    (``xgmi.check()`` + the gloo ``agree``), every ``commit_every`` graph replays.
+
+    ``report(round, rank, size, info)`` (bench): called by every rank after each round's timed window with
+    img/s and the re-wire latency (membership change seen -> first step of the new round complete)."""
+    import time as _time
+
+    from ..data.synthetic import SyntheticMNIST
+    from ..models.cnn import Net
+    from ..models.cnn_fused import FusedCNN
+    from ..ops.optim import FusedSGD
+    from ..parallel import dist as pdist
+    from ..parallel.xgmi_allreduce import XgmiAllreduce
+    from ..utils.graph import CapturedSteps
+    from ..utils.log import RankLogger
+
+    if "PDE_ELASTIC_STORE" not in os.environ:
+        raise SystemExit("--rewire needs the elastic driver (launch.hvdrun)")
+    rdzv = RendezvousClient()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    on_gpu = torch.cuda.is_available() and getattr(args, "device", "auto") != "cpu"
+    if on_gpu:
+        dev = torch.device("cuda", local % torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+    else:  # CPU plumbing of the same protocol: autograd Net + DDP over the round's gloo group, eager steps
+        dev = torch.device("cpu")
+        torch.set_num_threads(1)
+    torch.manual_seed(0)
+    model = Net().to(dev).train()
+    fused = FusedCNN(model) if on_gpu else None
+    grads = fused.grad_buffer() if on_gpu else None
+    opt = FusedSGD(model.parameters(), lr=0.01)
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+    batch = int(args.batch_size)
+    G = max(1, int(getattr(args, "graph_steps", 10)))
+    data = SyntheticMNIST(max(8 * batch, 1024 if not on_gpu else 16384), device=dev, seed=local + 1)
+    batches = [data.batch(j, batch) for j in range(G)]
+    pos = {"epoch": 0, "seen": 0, "step": 0}
+    commit = Commit(model, opt, pos)
+    commit_every = max(1, int(getattr(args, "commit_every", 10)))  # graph replays between commit points
+    total_steps = int(getattr(args, "total_steps", 0) or 0)  # 0: train args.total_epochs epochs
+    steps_per_epoch = max(1, args.train_size // max(1, batch))
+    changed_at = None
+    pid = os.getpid()
+    while True:
+        rnd, rank, size = rdzv.join()
+        comm = RoundComm(rdzv, rank, size, dev, use_rccl=False)
+        log = RankLogger(rank)
+        xa = None
+        try:
+            # everybody adopts rank 0's weights and position (one 87 KB broadcast over the control plane)
+            if size > 1:
+                if on_gpu:
+                    comm.broadcast_(fused.flat, 0)
+                else:
+                    for p_ in model.parameters():
+                        comm.broadcast_(p_.data, 0)
+            state = comm.broadcast_object(dict(pos) if rank == 0 else None) if size > 1 else dict(pos)
+            pos.clear()
+            pos.update(state)
+            if on_gpu:
+                fused.invalidate()
+                xa = XgmiAllreduce(dev, key=f"rewire/{rnd}") if size > 1 else None
+
+                def train_step(x, y):
+                    return fused.forward_backward(x, y, grad_out=grads, sgd=opt, xgmi=xa)
+
+                graph = CapturedSteps(train_step, batches, warmup=1).capture()
+            else:
+                from ..ops import functional as OF
+                from ..parallel.ddp import DistributedDataParallel
+
+                ddp = DistributedDataParallel(model, comm=comm, overlap=False)
+
+                class _Eager:  # CapturedSteps' replay() surface over eager steps
+                    def replay(self):
+                        out = None
+                        for x, y in batches:
+                            ddp.zero_grad()
+                            out = OF.nll_loss(model(x), y)
+                            out.backward()
+                            ddp.sync_gradients()
+                            opt.step()
+                        return out
+
+                graph = _Eager()
+            sync()
+            rewire_s = _time.perf_counter() - changed_at if changed_at is not None else None
+            changed_at = None
+            plane = f"fused CNN + xGMI exchange, {G} steps per graph" if on_gpu else "CPU autograd + gloo DDP"
+            log.print(f"[rewire] round {rnd}: rank {rank} of {size} (pid {pid}), {plane}" +
+                      (f", re-wired in {rewire_s:.3f}s" if rewire_s is not None else ""), all_ranks=True)
+            commit.save()
+            # timed window of this round (the bench reads it through `report`)
+            warm, timed = int(getattr(args, "round_warmup", 2)), int(getattr(args, "round_replays", 10))
+            for _ in range(warm):
+                graph.replay()
+            sync()
+            comm.agree(False)  # barrier over the control plane
+            t0 = _time.perf_counter()
+            for _ in range(timed):
+                loss = graph.replay()
+            sync()
+            dt = _time.perf_counter() - t0
+            if xa is not None:
+                xa.check()
+            t = torch.tensor([dt])
+            if size > 1:
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            img_s = batch * size * G * timed / float(t.item())
+            pos["step"] += G * (warm + timed)
+            rw = torch.tensor([rewire_s if rewire_s is not None else -1.0])
+            if size > 1:
+                dist.all_reduce(rw, op=dist.ReduceOp.MAX)  # the slowest member's re-wire
+            stop = False
+            if report is not None:
+                stop = bool(report(rnd, rank, size, {
+                    "images_per_s": img_s, "ms_per_step": float(t.item()) / (G * timed) * 1e3,
+                    "rewire_s": float(rw.item()) if rw.item() >= 0 else None, "loss": float(loss.item())}))
+            # keep training; commit points every `commit_every` replays check liveness and membership
+            since = 0
+            while not stop:
+                if total_steps and pos["step"] >= total_steps:
+                    break
+                if not total_steps and pos["step"] >= args.total_epochs * steps_per_epoch:
+                    break
+                graph.replay()
+                pos["step"] += G
+                since += 1
+                if since % commit_every == 0:
+                    sync()
+                    if xa is not None:
+                        try:
+                            xa.check()
+                        except RuntimeError as exc:
+                            raise PeerFailure(str(exc)) from exc
+                    commit.save()
+                    if comm.agree(rdzv.hosts_updated()):
+                        raise MembershipChanged()
+            log.print(f"[rewire] finished {pos['step']} steps in round {rnd} (world {size}, pid {pid})", all_ranks=True)
+            if xa is not None:
+                xa.close()
+            comm.close()
+            break
+        except PeerFailure as exc:
+            changed_at = _time.perf_counter()
+            log.print(f"[rewire] round {rnd}: peer failure ({str(exc).splitlines()[0][:120]}); restoring commit "
+                      f"step {commit._pos['step']}", all_ranks=True)
+            comm.close(abort=True)
+            commit.restore()
+            if fused is not None:
+                fused.invalidate()
+        except MembershipChanged:
+            changed_at = _time.perf_counter()
+            log.print(f"[rewire] round {rnd}: membership changed, re-joining", all_ranks=True)
+            comm.close()
+        finally:
+            if xa is not None and xa.impl is not None:
+                torch.cuda.synchronize()
+                xa.close()
+    pdist.shutdown()

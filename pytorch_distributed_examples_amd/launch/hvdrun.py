@@ -122,6 +122,7 @@ class Driver:
             self.store.set(f"updated/{self.round}", "1")
         r = self.round + 1
         self.store.set(f"round/{r}/size", str(len(members)))
+        self.store.set(f"round/{r}/members", ",".join(members))  # rank order (shrink detection)
         for rank, wid in enumerate(members):
             self.store.set(f"round/{r}/rank/{wid}", str(rank))
         self.store.set("round", str(r))

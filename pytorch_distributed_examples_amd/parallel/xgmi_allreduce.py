@@ -33,7 +33,7 @@ DEFAULT_THRESHOLD = int(os.environ.get("PDE_XGMI_THRESHOLD", str(1 << 20)))
 
 class XgmiAllreduce:
     def __init__(self, device: torch.device, group=None, max_bytes: int = 4 << 20, blocks: int = 256,
-                 timeout_s: float = 5.0, read_delay_us: float = 0.0):
+                 timeout_s: float = 5.0, read_delay_us: float = 0.0, key: str | None = None):
         assert device.type == "cuda", "the xGMI all-reduce is a GPU data plane"
         self.device = device
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -45,7 +45,9 @@ class XgmiAllreduce:
         if self.size > 1:
             store = dist.distributed_c10d._get_default_store()
             ranks = dist.get_process_group_ranks(group) if group is not None else list(range(self.size))
-            key = f"pde/xgmi/{next(_SEQ)}/{'-'.join(map(str, ranks))}"
+            # ``key``: an explicit handshake key (members that joined at different times -- an elastic
+            # round -- have different local counters)
+            key = f"pde/xgmi/{key if key is not None else next(_SEQ)}/{'-'.join(map(str, ranks))}"
             store.set(f"{key}/{self.rank}", self.impl.ipc_handle())
             handles = [store.get(f"{key}/{r}") for r in range(self.size)]
             self.impl.open(handles)

@@ -52,6 +52,18 @@ def _rm_open_ring(srv_rref, caller: str, caller_handle: bytes):
     return srv.submit(run).wait()
 
 
+def _rm_close_ring(srv_rref, caller: str):
+    srv = srv_rref.local_value()
+
+    def run():
+        ring = getattr(srv, "rings", {}).pop(caller, None)
+        if ring is not None:
+            ring.close()
+        return True
+
+    return srv.submit(run).wait()
+
+
 @rpc.functions.async_execution
 def _rm_forward_ring(srv_rref, ctx_id, call_id, caller, args):
     srv = srv_rref.local_value()
@@ -133,6 +145,14 @@ class RemoteModule:
             ring.open(rpc.rpc_sync(self.worker, _rm_open_ring, args=(self.server, me, ring.ipc_handle())))
             self.__dict__["_ring"] = ring
         return ring
+
+    def close(self):
+        """Tear down this process's ring towards the owner (and the owner's side); both drain first."""
+        ring = self.__dict__.pop("_ring", None)
+        if ring is not None:
+            torch.cuda.synchronize()
+            rpc.rpc_sync(self.worker, _rm_close_ring, args=(self.server, rpc.get_worker_info().name))
+            ring.close()
 
     def __getstate__(self):  # the handle travels to other processes; a ring is per process
         d = dict(self.__dict__)

@@ -77,3 +77,27 @@ def test_bench_secondary_pipeline_measurement():
     sec = rec["config"]["secondary"]
     assert "error" not in sec, sec
     assert sec["parallelism"] == "pp2xdp1" and sec["value"] > 0 and sec["global_batch"] == 4
+
+
+def test_bench_elastic_scale_up_cpu():
+    """BASELINE config 2 contract: ``bench.py --model elastic_cnn --gpus 2 --scale-to 4`` starts 2 workers
+    under the elastic driver, scales to 4 mid-run WITHOUT restarting the first two (in-process re-wire),
+    prints one JSON line per round and the final contract line with every round's img/s and re-wire latency."""
+    rc, out = run_cmd(["python", os.path.join(REPO, "bench.py"), "--model", "elastic_cnn", "--gpus", "2",
+                       "--scale-to", "4", "--device", "cpu", "--batch", "32", "--steps", "4", "--warmup", "2",
+                       "--graph-steps", "2"], timeout=600)
+    assert rc == 0, out
+    rounds = [json.loads(ln) for ln in out.splitlines() if ln.startswith('{"event": "round"')]
+    final = [json.loads(ln) for ln in out.splitlines() if ln.startswith('{"metric"')]
+    assert len(final) == 1 and FIELDS <= set(final[0]), out
+    rec = final[0]
+    assert [r["world"] for r in rounds] == [2, 4] and rec["n_gpus"] == 4, out
+    assert rounds[0]["rewire_s"] is None and rounds[1]["rewire_s"] > 0
+    assert all(r["images_per_s"] > 0 for r in rec["config"]["rounds"])
+    # the first round's workers survived the membership change (same pids in both rounds)
+    pids = {}
+    for ln in out.splitlines():
+        if ln.startswith("[rewire] round ") and "(pid " in ln:
+            rnd = int(ln.split()[2].rstrip(":"))
+            pids.setdefault(rnd, set()).add(int(ln.split("(pid ")[1].split(")")[0]))
+    assert pids[0] <= pids[1] and len(pids[1]) == 4, pids

@@ -1,0 +1,32 @@
+"""BASELINE config 2 rehearsed on ONE GPU: the elastic bench scales 1 -> 2 workers mid-run on the fused CNN
+path (whole-step kernel + gradient exchange over xGMI inside the reduction kernel, one hipGraph per round,
+recaptured after the re-wire).  The two workers share the card and map each other's IPC staging buffers
+exactly as two GPUs of a node do.  (3+ processes cannot rehearse this on one card: spinning exchange
+workgroups of the ranks already in their reduction kernel keep a late rank's 122 KB-LDS training kernel from
+being placed -- on a node every rank owns its GPU.)"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_elastic_bench_scale_up_one_gpu(gpu):
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--model", "elastic_cnn", "--gpus", "1", "--scale-to", "2",
+           "--steps", "100", "--warmup", "20", "--graph-steps", "10"]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert res.returncode == 0, (res.stdout[-3000:], res.stderr[-3000:])
+    rounds = [json.loads(ln) for ln in res.stdout.splitlines() if ln.startswith('{"event": "round"')]
+    final = [json.loads(ln) for ln in res.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert [r["world"] for r in rounds] == [1, 2] and len(final) == 1, res.stdout[-3000:]
+    assert rounds[1]["rewire_s"] is not None and rounds[1]["rewire_s"] > 0
+    assert all(r["images_per_s"] > 1e6 for r in rounds), rounds  # fused path (millions of images/s)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", "elastic_rehearsal.jsonl"), "w") as f:
+        for r in rounds + final:
+            f.write(json.dumps(r) + "\n")

@@ -171,7 +171,8 @@ def test_resnet_rpc_pipeline_one_gpu(gpu):
 
 
 _PS = r"""
-import os, sys, torch, torch.distributed.rpc as rpc
+import faulthandler, os, sys, torch, torch.distributed.rpc as rpc
+faulthandler.dump_traceback_later(200, exit=True)  # a hang dumps every thread's stack and exits
 sys.path.insert(0, os.environ["REPO"])
 from torch import nn
 from pytorch_distributed_examples_amd.ops import layers as L
@@ -194,7 +195,9 @@ if rank == 0:
     popt = DistributedOptimizer(torch.optim.SGD, emb.remote_parameters(), lr=1.0)
     idx, off = torch.tensor([1, 2, 3, 4]), torch.tensor([0, 2])
     outs = []
+    print("setup done", flush=True)
     for it in range(3):  # several steps: the ring's sequence numbers advance in both directions
+        print("step", it, flush=True)
         with dist_autograd.context() as cid:
             e = emb(idx, off, out_device=dev)
             assert e.is_cuda and e.device == dev   # rows arrived in this GPU's HBM
@@ -213,6 +216,8 @@ if rank == 0:
     w = rpc.rpc_sync("ps", _table, args=(big.server,))
     ref = torch.nn.functional.embedding_bag(bidx, w, boff, mode="sum")
     assert torch.allclose(e.cpu(), ref, rtol=1e-4, atol=1e-4)
+    emb.close()
+    big.close()
     print("PS_OK", flush=True)
 else:
     rpc.init_rpc("ps", rank=1, world_size=world, rpc_backend_options=opts)
@@ -225,25 +230,39 @@ def test_parameter_server_ring_data_plane_one_gpu(gpu):
     move over the P2P ring (RPC carries only the call and the host indices); Hogwild SGD on the owner."""
     from pytorch_distributed_examples_amd.parallel.dist import free_port
 
-    script = _PS
-    env = dict(os.environ, REPO=REPO, RPC_PORT=str(free_port()))
+    env = dict(os.environ, REPO=REPO, RPC_PORT=str(free_port()), PYTHONUNBUFFERED="1")
+    logdir = os.path.join(REPO, "gpurun_out")
+    os.makedirs(logdir, exist_ok=True)
     with tempfile.NamedTemporaryFile("w", suffix=".py", delete=False) as f:
-        f.write(script)
+        f.write(_PS)
         path = f.name
+    logs = [os.path.join(logdir, f"ps_ring_rank{r}.log") for r in range(2)]
     try:
+        files = [open(lg, "w") for lg in logs]  # progress lands under gpurun_out/ while it runs
         procs = [subprocess.Popen([sys.executable, path], env=dict(env, RANK=str(r), WORLD_SIZE="2"),
-                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
-        outs = [p.communicate(timeout=300) for p in procs]
+                                  stdout=fo, stderr=subprocess.STDOUT, text=True) for r, fo in enumerate(files)]
+        for p in procs:
+            p.wait(timeout=300)
     finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        for fo in files:
+            fo.close()
         os.unlink(path)
-    assert all(p.returncode == 0 for p in procs) and "PS_OK" in outs[0][0], [o[1][-3000:] for o in outs]
+    outs = [open(lg).read() for lg in logs]
+    assert all(p.returncode == 0 for p in procs) and "PS_OK" in outs[0], [o[-3000:] for o in outs]
 
 
 def test_hybrid_ps_script_ring_one_gpu(gpu):
     """rpc/server_model_data_parallel.py on one GPU: 2 trainers + master + ps, trainers' DDP on gloo (two
     ranks on one device), embedding rows and gradients over the P2P ring."""
-    env = dict(os.environ, PDE_BACKEND="gloo")
-    res = subprocess.run([sys.executable, os.path.join(REPO, "rpc", "server_model_data_parallel.py"), "--epochs", "6"],
-                         env=env, capture_output=True, text=True, timeout=600)
-    assert res.returncode == 0, (res.stdout[-3000:], res.stderr[-3000:])
-    assert "Training done for epoch 5" in res.stdout and "embedding data plane: p2p-ring" in res.stdout, res.stdout
+    env = dict(os.environ, PDE_BACKEND="gloo", PYTHONUNBUFFERED="1")
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    log = os.path.join(REPO, "gpurun_out", "hybrid_ps_ring.log")
+    with open(log, "w") as fo:  # progress lands under gpurun_out/ while it runs
+        rc = subprocess.call([sys.executable, os.path.join(REPO, "rpc", "server_model_data_parallel.py"), "--epochs",
+                              "6"], env=env, stdout=fo, stderr=subprocess.STDOUT, timeout=600)
+    out = open(log).read()
+    assert rc == 0, out[-4000:]
+    assert "Training done for epoch 5" in out and "embedding data plane: p2p-ring" in out, out[-4000:]
