@@ -9,6 +9,8 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "pde_kernels.h"
@@ -113,6 +115,34 @@ void run_gemm(pde::GemmArgs& a, const Tensor& like, int max_split) {
   check(pde::gemm_bf16(a, cur_stream()), "gemm");
 }
 
+// ---- conv outputs left as unreduced split-K slabs for the BatchNorm that follows (conv_fwd(defer=true)) ----
+// The one-launch BatchNorm sums the slabs itself (bn_fwd): the GEMM's reduce launch is gone.  Any other op
+// that reads such an output first resolves it (resolve_pending: the plain reduce), so a deferred output is
+// never read unreduced.  The entry keeps the slab workspace alive until it is consumed.
+struct PendingConv {
+  Tensor ws;
+  int splits, M, N;
+};
+std::unordered_map<const void*, PendingConv> g_pending_conv;
+std::mutex g_pending_mu;  // forward ops (main thread) and backward ops (autograd's device thread)
+
+void resolve_pending(const Tensor& t) {
+  if (!t.defined()) return;
+  std::lock_guard<std::mutex> lk(g_pending_mu);
+  if (g_pending_conv.empty()) return;
+  auto it = g_pending_conv.find(t.data_ptr());
+  if (it == g_pending_conv.end()) return;
+  PendingConv pc = std::move(it->second);
+  g_pending_conv.erase(it);
+  check(pde::gemm_reduce_slabs_bf16(pc.ws.data_ptr<float>(), pc.splits, pc.M, pc.N,
+                                    reinterpret_cast<uint16_t*>(t.data_ptr()), cur_stream()),
+        "resolve_pending");
+}
+void resolve_pending(const optional<Tensor>& t) {
+  if (t.has_value()) resolve_pending(*t);
+}
+int pending_conv_count() { return static_cast<int>(g_pending_conv.size()); }
+
 void gemm_pair_begin() {
   TORCH_CHECK(!g_collect && g_pending.empty(), "gemm_pair_begin: a pair is already being collected");
   g_collect = true;
@@ -170,6 +200,7 @@ int gemm_deferred_count() { return static_cast<int>(g_deferred.size()); }
 // Dense GEMMs (nn.Linear)
 // ------------------------------------------------------------------------------------------------
 Tensor linear_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, bool relu, bool out_f32) {
+  resolve_pending(x);
   CHECK_IN(x); CHECK_IN(w); CHECK_BF16(x); CHECK_BF16(w);
   const int M = x.size(0), K = x.size(1), N = w.size(0);
   TORCH_CHECK(w.size(1) == K, "linear_fwd: shape mismatch");
@@ -317,8 +348,9 @@ std::vector<Tensor> ce_fused(const Tensor& x, const Tensor& tgt, const optional<
 // NHWC implicit-GEMM convolution
 // ------------------------------------------------------------------------------------------------
 Tensor conv_fwd(const Tensor& x, const Tensor& wf, const optional<Tensor>& bias, int R, int S, int stride, int pad,
-                bool relu, bool out_f32) {
+                bool relu, bool out_f32, bool defer) {
   CHECK_IN(x); CHECK_IN(wf); CHECK_BF16(x); CHECK_BF16(wf);
+  resolve_pending(x);
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   TORCH_CHECK(C % 8 == 0, "conv_fwd: input channels must be padded to a multiple of 8");
   const int Co = wf.size(0);
@@ -333,6 +365,27 @@ Tensor conv_fwd(const Tensor& x, const Tensor& wf, const optional<Tensor>& bias,
   a.bias = cf32(bias);
   a.nbias = a.bias ? static_cast<int>(bias->numel()) : 0;
   a.epi = (a.bias ? pde::EPI_BIAS : 0) | (relu ? pde::EPI_RELU : 0) | (out_f32 ? pde::EPI_OUT_F32 : 0);
+  if (defer && a.epi == 0 && !g_collect) {
+    // the BatchNorm that follows reduces the split-K slabs itself (bn_fwd): no reduce launch here
+    const int max_split = split_cap(a);
+    Tensor ws;
+    if (max_split > 1) {
+      ws = at::empty({static_cast<long>(max_split) * a.M * a.N}, x.options().dtype(at::kFloat));
+      a.workspace = ws.data_ptr<float>();
+      a.splitk = max_split;
+    } else {
+      a.workspace = nullptr;
+      a.splitk = 1;
+    }
+    int used = 1;
+    a.splits_out = &used;
+    check(pde::gemm_bf16(a, cur_stream()), "conv_fwd");
+    if (used > 1) {
+      std::lock_guard<std::mutex> lk(g_pending_mu);
+      g_pending_conv[y.data_ptr()] = PendingConv{ws, used, a.M, a.N};
+    }
+    return y;
+  }
   run_gemm(a, x, -1);
   return y;
 }
@@ -344,6 +397,7 @@ Tensor conv_fwd(const Tensor& x, const Tensor& wf, const optional<Tensor>& bias,
 Tensor conv_dgrad(const Tensor& dy, const Tensor& wd, int H, int W, int R, int S, int stride, int pad,
                   const optional<Tensor>& aux, bool w_fwd_layout, bool add_aux) {
   CHECK_IN(dy); CHECK_IN(wd); CHECK_BF16(dy); CHECK_BF16(wd);
+  resolve_pending(aux);
   const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
   TORCH_CHECK(Co % 8 == 0, "conv_dgrad: Cout must be a multiple of 8");
   int Ci;
@@ -377,6 +431,7 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wd, int H, int W, int R, int S
 // remap, so no layout kernel runs; with ``out`` (accumulate: +=) it lands directly in the .grad tensor.
 Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int R, int S, int stride, int pad, int Co, int Ci,
                   const optional<Tensor>& out, bool accumulate) {
+  resolve_pending(x);
   CHECK_IN(dy); CHECK_IN(x); CHECK_BF16(dy); CHECK_BF16(x);
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int Ho = dy.size(1), Wo = dy.size(2), Cop = dy.size(3);
@@ -496,6 +551,7 @@ Tensor colsum(const Tensor& x, int64_t ncols, const optional<Tensor>& out, bool 
   return y;
 }
 Tensor relu_bwd(const Tensor& dy, const Tensor& y) {
+  resolve_pending(y);
   CHECK_IN(dy); CHECK_IN(y); CHECK_BF16(dy); CHECK_BF16(y);
   Tensor dx = at::empty_like(dy);
   check(pde::relu_bwd_bf16(u16(dy), u16(y), u16(dx), dy.numel(), cur_stream()), "relu_bwd");
@@ -684,16 +740,30 @@ std::vector<Tensor> bn_fwd(const Tensor& x, const optional<Tensor>& gamma, const
   Tensor y = at::empty_like(x);
   Tensor mean = at::empty({C}, fo), invstd = at::empty({C}, fo), ss = at::empty({2 * C}, fo);
   Tensor ws = at::empty({static_cast<long>(pde::bn_workspace_blocks(P, C)) * 2 * C}, fo);
+  resolve_pending(res);
+  PendingConv pc{};
+  {
+    std::lock_guard<std::mutex> lk(g_pending_mu);
+    auto it = g_pending_conv.find(x.data_ptr());
+    if (it != g_pending_conv.end()) {  // x = a deferred split-K conv output: the BatchNorm reduces its slabs
+      pc = std::move(it->second);
+      g_pending_conv.erase(it);
+    }
+  }
+  TORCH_CHECK(!pc.ws.defined() || (pc.M == P && pc.N == C), "bn_fwd: deferred conv output shape mismatch");
   check(pde::bn_fwd_train(u16(x), P, C, cf32(gamma), cf32(beta), static_cast<float>(eps),
                           static_cast<float>(momentum), f32(running_mean), f32(running_var), mean.data_ptr<float>(),
                           invstd.data_ptr<float>(), ss.data_ptr<float>(), ws.data_ptr<float>(), cu16(res), relu,
-                          u16(y), cur_stream()),
+                          u16(y), cur_stream(), pc.ws.defined() ? pc.ws.data_ptr<float>() : nullptr,
+                          pc.ws.defined() ? pc.splits : 1),
         "bn_fwd");
   return {y, mean, invstd};
 }
 // Inference / eval mode: y = x*scale + shift with scale/shift from running stats (computed in torch).
 Tensor bn_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, const optional<Tensor>& res, bool relu) {
   CHECK_IN(x); CHECK_BF16(x);
+  resolve_pending(x);
+  resolve_pending(res);
   const int C = x.size(-1);
   const int P = x.numel() / C;
   Tensor y = at::empty_like(x);
@@ -708,6 +778,8 @@ std::vector<Tensor> bn_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, c
                            const Tensor& invstd, const optional<Tensor>& gamma, bool relu, bool want_dres,
                            const optional<Tensor>& dg_out, const optional<Tensor>& db_out) {
   CHECK_IN(dy); CHECK_IN(x); CHECK_IN(y); CHECK_BF16(dy);
+  resolve_pending(x);
+  resolve_pending(y);
   const int C = x.size(-1);
   const int P = x.numel() / C;
   auto fo = x.options().dtype(at::kFloat);
@@ -727,6 +799,7 @@ std::vector<Tensor> bn_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, c
 }
 std::vector<Tensor> maxpool_fwd(const Tensor& x, int k, int s, int p, bool relu) {
   CHECK_IN(x); CHECK_BF16(x);
+  resolve_pending(x);
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
   Tensor y = at::empty({N, Ho, Wo, C}, x.options());
@@ -746,6 +819,7 @@ Tensor maxpool_bwd(const Tensor& dy, const Tensor& y, const Tensor& idx, int H, 
   return dx;
 }
 Tensor avgpool_fwd(const Tensor& x) {
+  resolve_pending(x);
   CHECK_IN(x); CHECK_BF16(x);
   const int N = x.size(0), C = x.size(-1);
   const int HW = x.numel() / (static_cast<long>(N) * C);
@@ -914,7 +988,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_dgrad", &linear_dgrad);
   m.def("linear_wgrad", &linear_wgrad, py::arg("dy"), py::arg("x"), py::arg("out") = py::none(),
         py::arg("accumulate") = false);
-  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("wf"), py::arg("bias"), py::arg("R"), py::arg("S"),
+        py::arg("stride"), py::arg("pad"), py::arg("relu"), py::arg("out_f32"), py::arg("defer") = false);
+  m.def("pending_conv_count", &pending_conv_count);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wd"), py::arg("H"), py::arg("W"), py::arg("R"),
         py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("aux") = py::none(), py::arg("w_fwd_layout") = false,
         py::arg("add_aux") = false);

@@ -64,7 +64,13 @@ struct GemmArgs {
   int* tickets;                    // set by gemm_bf16: per-tile arrival counters of the in-kernel split-K reduce
   float* bias_grad;                // EPI_OUT_F32: output column bias_col goes to bias_grad[m] instead (the
   int bias_col;                    //   "ones column" bias gradient of a linear wgrad), columns beyond are dropped
+  int* splits_out;                 // != nullptr: a split-K GEMM leaves its slabs UNREDUCED for a consumer that
+                                   //   sums them itself (the one-launch BatchNorm); the split count used is stored
+                                   //   here (1: the output was written directly)
 };
+// Sum `splits` fp32 slabs [splits][M][N] in z order into bf16 out[M][N] (the plain split-K reduction of a
+// GEMM with no epilogue) -- the fallback when a deferred conv output is read by something else.
+hipError_t gemm_reduce_slabs_bf16(float* ws, int splits, int M, int N, uint16_t* out, hipStream_t s);
 
 hipError_t gemm_bf16(const GemmArgs& args, hipStream_t stream);
 // Two independent GEMMs (a layer's dgrad and wgrad) in one launch when both run on the 64x64 FAST tile, their
@@ -165,10 +171,13 @@ hipError_t multi_tensor_optim(int mode, const OptimEntry* dev_table, const Optim
 // BatchNorm / pooling / dropout / EmbeddingBag (norm_pool.hip).  Activations NHWC bf16, [P = N*H*W][C].
 // ---------------------------------------------------------------------------------------------
 int bn_workspace_blocks(int P, int C);  // ws needs bn_workspace_blocks * 2 * C floats
+// slabs != nullptr (splits > 1): x is the UNREDUCED output of a split-K conv GEMM (GemmArgs::splits_out):
+// the BatchNorm sums the fp32 slabs [splits][P][C] in z order, rounds to bf16, WRITES x and normalizes it --
+// the GEMM's separate slab-reduction launch is gone.
 hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, const float* beta, float eps,
                         float momentum, float* running_mean, float* running_var, float* save_mean,
                         float* save_invstd, float* scale_shift, float* ws, const uint16_t* res, int relu,
-                        uint16_t* y, hipStream_t s);
+                        uint16_t* y, hipStream_t s, const float* slabs = nullptr, int splits = 1);
 // 1 when a one-launch BatchNorm wait timed out (a block of the grid was never resident); reset clears it
 int bn_error(int reset);
 hipError_t bn_apply(const uint16_t* x, int P, int C, const float* scale, const float* shift, const uint16_t* res,

@@ -1093,9 +1093,10 @@ hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
   const int av = vec_ok(a.a, AKC), bv = vec_ok(a.b, BKC);
   dim3 grid(tm * tn, 1, splitk);
   GemmArgs ka = a;
-  const bool in_kernel = splitk > 1 && splitk <= kMaxInKernelSplits &&
+  const bool in_kernel = splitk > 1 && splitk <= kMaxInKernelSplits && a.splits_out == nullptr &&
                          static_cast<long>(splitk) * a.M * a.N * 4 < (1L << 31);  // buffer offsets
   ka.tickets = in_kernel ? split_tickets(tm * tn, s) : nullptr;
+  if (a.splits_out != nullptr) *a.splits_out = splitk;  // the consumer reduces the slabs (no reduce launch)
   // FAST: both operands loaded branch-free through buffer descriptors (gathers always; dense operands when
   // every 16-B group is whole and aligned, extents < 2 GB) with compile-time operand kinds -- then the loads
   // are counted and a register ring of kFastStages K-tiles stays in flight.  The generic loaders' divergent scalar fallbacks make the
@@ -1110,7 +1111,7 @@ hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
   if (!launched)
     hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, AKC, BKC, -1, -1, 1>), grid, dim3(kThreads), 0, s, ka, tm,
                        tn, kps, av, bv);
-  if (splitk > 1 && ka.tickets == nullptr) launch_reduce(a, splitk, s);
+  if (splitk > 1 && ka.tickets == nullptr && a.splits_out == nullptr) launch_reduce(a, splitk, s);
   return hipGetLastError();
 }
 
@@ -1246,6 +1247,18 @@ hipError_t gemm_bf16(const GemmArgs& a, hipStream_t s) {
   if (akc && !bkc) return dispatch_tiles<true, false>(a, s);
   if (!akc && bkc) return dispatch_tiles<false, true>(a, s);
   return dispatch_tiles<false, false>(a, s);
+}
+
+hipError_t gemm_reduce_slabs_bf16(float* ws, int splits, int M, int N, uint16_t* out, hipStream_t s) {
+  GemmArgs a{};
+  a.M = M;
+  a.N = N;
+  a.workspace = ws;
+  a.out = out;
+  a.ldo = N;
+  a.epi = 0;
+  launch_reduce(a, splits, s);
+  return hipGetLastError();
 }
 
 hipError_t gemm_reduce_jobs(const ReduceJob* jobs, int n, hipStream_t s) {

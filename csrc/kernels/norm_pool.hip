@@ -544,13 +544,30 @@ __device__ __forceinline__ void bn_wait(const uint32_t* flag, uint32_t gen, int*
   __syncthreads();
 }
 
+// 8 consecutive channels of one row of the sum over z of fp32 slabs [splits][P*C] (z order).
+__device__ __forceinline__ void slab_row8(const float* __restrict__ slabs, long zs, int splits, long off,
+                                          float (&v)[8]) {
+  const f32x4* p = reinterpret_cast<const f32x4*>(slabs + off);
+  f32x4 a = p[0], b = p[1];
+  for (int z = 1; z < splits; ++z) {
+    const f32x4* q = reinterpret_cast<const f32x4*>(slabs + z * zs + off);
+    a += q[0];
+    b += q[1];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = a[j];
+    v[4 + j] = b[j];
+  }
+}
+
 __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
-    const uint16_t* __restrict__ x, int P, int C, int rpb, float* __restrict__ ws, int* __restrict__ tickets,
+    uint16_t* x, int P, int C, int rpb, float* __restrict__ ws, int* __restrict__ tickets,
     uint32_t* __restrict__ flags, int* __restrict__ err, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float momentum, float* __restrict__ running_mean,
     float* __restrict__ running_var, float* __restrict__ save_mean, float* __restrict__ save_invstd,
     float* __restrict__ scale, float* __restrict__ shift, const uint16_t* __restrict__ res, int relu,
-    uint16_t* __restrict__ y) {
+    uint16_t* __restrict__ y, const float* __restrict__ slabs, int splits) {
   __shared__ float red[2][kBnRows][kBnCG + 1];
   __shared__ float tot1[kBnCG], tot2[kBnCG];
   __shared__ int s_last;
@@ -563,7 +580,25 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
   float s1[8], s2[8], piv[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = piv[j] = 0.f;
-  if (cok) {
+  if (cok && slabs != nullptr) {
+    // x = bf16(sum_z slab_z) in z order (== the GEMM's own reduction), written here, its statistics taken
+    // from the rounded values; the pivot (row 0) is recomputed from the slabs by every block
+    const long zs = static_cast<long>(P) * C;
+    slab_row8(slabs, zs, splits, c0, piv);
+    for (int r = blockIdx.x * rpb + tr; r < r1; r += kBnRows) {
+      float v[8];
+      slab_row8(slabs, zs, splits, static_cast<long>(r) * C + c0, v);
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = f2bf(v[j]);
+        const float d = bf2f(o[j]) - piv[j];
+        s1[j] += d;
+        s2[j] += d * d;
+      }
+      *reinterpret_cast<u16x8*>(x + static_cast<long>(r) * C + c0) = o;  // x: written here, re-read below
+    }
+  } else if (cok) {
     load8(x + c0, piv);  // shift by row 0 (same pivot in every block)
     int r = blockIdx.x * rpb + tr;
     constexpr int U = kBnUnroll;
@@ -591,7 +626,15 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
       const double mean_s = static_cast<double>(tot1[tid]) / n;
       double var = static_cast<double>(tot2[tid]) / n - mean_s * mean_s;
       if (var < 0.0) var = 0.0;
-      const float mean = static_cast<float>(mean_s) + bf2f(x[c]);
+      float pv;
+      if (slabs != nullptr) {  // the pivot row of another block may not be visible yet: from the slabs
+        float a = slabs[c];
+        for (int z = 1; z < splits; ++z) a += slabs[static_cast<long>(z) * P * C + c];
+        pv = bf2f(f2bf(a));
+      } else {
+        pv = bf2f(x[c]);
+      }
+      const float mean = static_cast<float>(mean_s) + pv;
       const float invstd = rsqrtf(static_cast<float>(var) + eps);
       save_mean[c] = mean;
       save_invstd[c] = invstd;
@@ -1170,19 +1213,26 @@ int bn_workspace_blocks(int P, int C) {
 hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, const float* beta, float eps,
                         float momentum, float* running_mean, float* running_var, float* save_mean,
                         float* save_invstd, float* scale_shift, float* ws, const uint16_t* res, int relu,
-                        uint16_t* y, hipStream_t s) {
+                        uint16_t* y, hipStream_t s, const float* slabs, int splits) {
   int rpb;
   const int ncg = ceil_div(C, kBnCG);
   int* err = nullptr;
   const int nrb1 = bn_fin_grid(P, C, rpb);
+  if (splits <= 1) slabs = nullptr;
   if (bn_one_launch(nrb1 * ncg) && bn_ticket_base(s, &err) != nullptr) {
     int* tk = bn_tickets(ncg, s);
     uint32_t* fl = bn_flags(ncg, s);  // generation flags of the channel groups
     if (tk != nullptr && fl != nullptr) {
-      hipLaunchKernelGGL(k_bn_fwd_fused, dim3(nrb1, ncg), dim3(kBnThreads), 0, s, x, P, C, rpb, ws, tk, fl, err, gamma, beta, eps, momentum, running_mean,
-                         running_var, save_mean, save_invstd, scale_shift, scale_shift + C, res, relu, y);
+      hipLaunchKernelGGL(k_bn_fwd_fused, dim3(nrb1, ncg), dim3(kBnThreads), 0, s, const_cast<uint16_t*>(x), P, C,
+                         rpb, ws, tk, fl, err,
+                         gamma, beta, eps, momentum, running_mean, running_var, save_mean, save_invstd, scale_shift,
+                         scale_shift + C, res, relu, y, slabs, splits);
       return hipGetLastError();
     }
+  }
+  if (slabs != nullptr) {  // multi-launch BatchNorm: reduce the conv's slabs into x first
+    const hipError_t e = gemm_reduce_slabs_bf16(const_cast<float*>(slabs), splits, P, C, const_cast<uint16_t*>(x), s);
+    if (e != hipSuccess) return e;
   }
   int* tk = bn_tickets(ncg, s);
   if (tk != nullptr) {

@@ -161,17 +161,24 @@ class ResNetPipelineDP:
         dev = ctx.device
         self.module = (ResNetShard1() if self.stage == 0 else ResNetShard2()).to(dev)
         self.comm = None
+        # stage gradients: bf16 on the wire (our cast kernels around RCCL), reduced on a side stream during
+        # the last micro-batch's backward (PDE_PIPE_DP_OVERLAP=0: one reduce after the pipeline drains)
+        self.overlap = dev.type == "cuda" and self.dp > 1 and os.environ.get("PDE_PIPE_DP_OVERLAP", "1") != "0"
         if dev.type == "cuda" and self.dp > 1 and ctx.backend == "nccl":
             from ..parallel.rccl import StreamComm
 
-            self.comm = StreamComm(dev, group=self.dp_group)
-        self.ddp = DistributedDataParallel(self.module, process_group=self.dp_group, overlap=False,
-                                           broadcast_buffers=False, comm=self.comm)
+            self.comm = StreamComm(dev, group=self.dp_group, side_stream=self.overlap)
+        gd = torch.bfloat16 if (dev.type == "cuda" and os.environ.get("PDE_PIPE_GRAD_DTYPE", "bf16") == "bf16") else None
+        self.ddp = DistributedDataParallel(self.module, process_group=self.dp_group,
+                                           overlap=self.overlap and self.comm is not None,
+                                           broadcast_buffers=False, comm=self.comm, grad_dtype=gd)
         self.opt = FusedSGD(self.module.parameters(), lr=lr)
         prev_rank = ctx.rank - 1 if self.stage > 0 else None
         next_rank = ctx.rank + 1 if not self.last else None
         self.engine = PipelineEngine(self.module, self.stage, self.stages, prev_rank, next_rank, dev,
                                      loss_fn=OF.mse_loss, schedule=schedule, tag=tag)
+        if self.ddp.overlap:
+            self.engine.ddp = self.ddp
         g = torch.Generator().manual_seed(seed + ctx.rank // self.stages)
         x, y = resnet_batch(batch, image, 1000, dev, g)
         self.n_mb = batch // split_size
@@ -205,7 +212,8 @@ class ResNetPipelineDP:
         loss = self.engine.train_step(self.xs if self.stage == 0 else None, self.ys if self.last else None,
                                       self.n_mb)
         with t.phase("comm"):
-            self.ddp.sync_gradients()
+            if not self.ddp.overlap:  # (overlap: the hooks reduced every bucket during the last backward)
+                self.ddp.sync_gradients()
         with t.phase("opt"):
             self.opt.step()
         self.engine.timer = NO_PHASES

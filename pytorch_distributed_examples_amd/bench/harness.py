@@ -76,11 +76,14 @@ def parse_args(argv=None):
     ap.add_argument("--schedule", default="gpipe", choices=["gpipe", "1f1b"], help="resnet50_pp schedule")
     ap.add_argument("--image", type=int, default=None, help="override the image size (CPU plumbing tests)")
     ap.add_argument("--no-graph", action="store_true", help="run the step eagerly (no hipGraph capture)")
-    ap.add_argument("--graph-steps", type=int, default=10,
-                    help="consecutive training steps recorded into one hipGraph (each reads its own batch)")
+    ap.add_argument("--graph-steps", type=int, default=0,
+                    help="consecutive training steps recorded into one hipGraph (each reads its own batch); "
+                         "0 = auto: the largest divisor of --steps up to 50, so the timed steps are whole replays")
     ap.add_argument("--generic", action="store_true", help="CNN / MLP: layer-by-layer autograd kernels instead of the fused step")
     ap.add_argument("--device", default="auto", choices=["auto", "cpu"], help="cpu: contract/plumbing check only")
     args = ap.parse_args(argv)
+    if args.graph_steps <= 0:
+        args.graph_steps = max(d for d in range(1, min(50, max(1, args.steps)) + 1) if args.steps % d == 0)
     if args.model == "resnet50_hybrid":
         args.model = "resnet50_pp"
     return args

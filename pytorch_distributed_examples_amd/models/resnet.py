@@ -39,16 +39,18 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         identity = x
-        # identity shortcut on the GPU: x's two gradients (residual and conv1 branch) meet in conv1's dgrad
+        # on the GPU x's two gradients (residual / downsample branch and conv1 branch) meet in conv1's dgrad
         # epilogue instead of an autograd add (ops.functional.GradJoin)
-        join = OF.GradJoin() if (self.downsample is None and x.is_cuda and torch.is_grad_enabled()) else None
-        out = self.bn1(self.conv1(x, grad_join=join), relu=True)
-        out = self.bn2(self.conv2(out), relu=True)
+        join = OF.GradJoin() if (x.is_cuda and torch.is_grad_enabled() and x.requires_grad) else None
+        t = self.training  # training-mode BatchNorm reduces a split-K conv's slabs itself (bn_follows)
+        out = self.bn1(self.conv1(x, grad_join=join, bn_follows=t), relu=True)
+        out = self.bn2(self.conv2(out, bn_follows=t), relu=True)
         if self.downsample is not None:
             conv, bn = self.downsample[0], self.downsample[1]
-            identity = bn(conv(x))
+            identity = bn(conv(x, grad_to=join, bn_follows=t))
         # relu(bn3(conv3(out)) + identity) in one fused kernel
-        return self.bn3(self.conv3(out), residual=identity, relu=True, residual_grad_to=join)
+        return self.bn3(self.conv3(out, bn_follows=t), residual=identity, relu=True,
+                        residual_grad_to=join if self.downsample is None else None)
 
 
 class _StemReLU(nn.Module):
@@ -95,7 +97,7 @@ class ResNetShard1(nn.Module):
         if x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.shape[1] == 3:
             x = OF.to_native_image(x)
         s = self.seq
-        x = s[1](s[0](x), relu=True)
+        x = s[1](s[0](x, bn_follows=self.training), relu=True)
         x = s[3](x)
         return s[5](s[4](x))
 

@@ -316,15 +316,17 @@ def linear(x, weight, bias=None, relu=False, out_f32=False, consumer_masks=False
 # ---------------------------------------------------------------------------------------------
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, relu, join=None):
+    def forward(ctx, x, weight, bias, stride, pad, relu, join=None, grad_to=None, defer=False):
         ctx.join = join
+        ctx.grad_to = grad_to
         co, ci, r, s = weight.shape
         cp = x.shape[3]
         cop = pad8(co)
         wf = _maintained(weight, "conv_fwd") if cp == pad8(ci) else None
         if wf is None:
             wf = _cached(weight, ("conv_fwd", cp, cop), lambda: _C().conv_w_fwd(weight.detach().contiguous(), cp, cop))
-        y = _C().conv_fwd(x, wf, bias.detach() if bias is not None else None, r, s, stride, pad, relu, False)
+        # defer: a split-K GEMM leaves its slabs for the BatchNorm that follows (it reduces them itself)
+        y = _C().conv_fwd(x, wf, bias.detach() if bias is not None else None, r, s, stride, pad, relu, False, defer)
         ctx.geom = (co, ci, r, s, stride, pad, cp, cop, x.shape[1], x.shape[2])
         ctx.relu = relu
         ctx.has_bias = bias is not None
@@ -370,6 +372,9 @@ class _Conv2dFn(torch.autograd.Function):
                     wd = _cached(weight, ("conv_dgrad", cp, cop),
                                  lambda: _C().conv_w_dgrad(weight.detach().contiguous(), cp, cop))
                 dx = _C().conv_dgrad(dy, wd, h, w, r, s, stride, pad, other, False, other is not None)
+            if ctx.grad_to is not None:  # the other consumer of x adds this gradient in its dgrad epilogue
+                ctx.grad_to.put(dx)
+                dx = None
         if paired:
             try:
                 _C().conv_wgrad(dy, x, r, s, stride, pad, co, ci, wsink, True)
@@ -381,9 +386,9 @@ class _Conv2dFn(torch.autograd.Function):
                 db = _C().colsum(dy, co, bsink, bsink is not None)
                 if bsink is not None:
                     db = None
-            return dx, None, db, None, None, None, None
+            return dx, None, db, None, None, None, None, None, None
         if side:
-            return dx, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None
         if ctx.needs_input_grad[1]:
             # OIHW epilogue: the GEMM writes the parameter's layout (and adds into .grad when it exists)
             dw = _C().conv_wgrad(dy, x, r, s, stride, pad, co, ci, wsink, wsink is not None)
@@ -393,7 +398,7 @@ class _Conv2dFn(torch.autograd.Function):
             db = _C().colsum(dy, co, bsink, bsink is not None)
             if bsink is not None:
                 db = None
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
 class GradJoin:
@@ -404,7 +409,14 @@ class GradJoin:
     ``conv2d(..., grad_join=j)`` makes the BatchNorm backward hand its residual gradient to the join
     (instead of returning it to autograd), and conv1's dgrad GEMM adds it in its epilogue: one bf16 add kernel
     and one gradient tensor fewer per block.  Autograd order is guaranteed by data dependence: conv1's
-    backward needs the gradient that flows back through the BatchNorm."""
+    backward needs the gradient that flows back through the BatchNorm.
+
+    In a block WITH downsample, the block input feeds conv1 and the downsample conv:
+    ``conv2d(x, ..., grad_to=j)`` on the downsample conv hands ITS data gradient to the join and conv1's
+    dgrad adds it -- the bf16 add autograd would run for the two gradients of x.  Order: the downsample
+    branch's nodes are created after conv2/bn2 in forward, so the engine (higher sequence number first among
+    ready nodes) runs the downsample conv's backward before bn2 -> conv2 -> bn1 -> conv1's; ``take`` asserts
+    it."""
 
     __slots__ = ("grad",)
 
@@ -419,14 +431,23 @@ class GradJoin:
         return g
 
 
-def conv2d(x, weight, bias=None, stride=1, padding=0, relu=False, grad_join=None):
+def conv2d(x, weight, bias=None, stride=1, padding=0, relu=False, grad_join=None, grad_to=None, bn_follows=False):
     """2-D convolution.  GPU: ``x`` is NHWC bf16 with C padded to a multiple of 8; output NHWC with
     Cout padded to a multiple of 8 (padded channels are exactly zero).  CPU: NCHW fp32 F.conv2d.
-    ``grad_join``: see :class:`GradJoin` (GPU only; ignored on CPU)."""
+    ``grad_join`` (this conv's dgrad adds the join's gradient) / ``grad_to`` (this conv's input gradient
+    goes to the join instead of autograd): see :class:`GradJoin` (GPU only; ignored on CPU).
+    ``bn_follows``: a training-mode batch_norm consumes the output next -- a split-K GEMM then skips its
+    slab reduction and the one-launch BatchNorm sums the slabs itself (any other reader resolves them)."""
     if not x.is_cuda:
         y = F.conv2d(_emu(x), _emu(weight), bias, stride=stride, padding=padding)
         return _emu(F.relu(y) if relu else y)
-    return _Conv2dFn.apply(x.contiguous(), weight, bias, int(stride), int(padding), relu, grad_join)
+    defer = bool(bn_follows) and bias is None and not relu and _DEFER_CONV[0]
+    return _Conv2dFn.apply(x.contiguous(), weight, bias, int(stride), int(padding), relu, grad_join, grad_to, defer)
+
+
+import os as _os
+
+_DEFER_CONV = [_os.environ.get("PDE_CONV_BN_DEFER", "1") != "0"]  # A/B switch
 
 
 def to_native_image(x: torch.Tensor) -> torch.Tensor:

@@ -58,8 +58,9 @@ class Conv2d(nn.Module):
             bound = 1 / math.sqrt(fan_in)
             nn.init.uniform_(self.bias, -bound, bound)
 
-    def forward(self, x, grad_join=None):
-        return OF.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.relu, grad_join)
+    def forward(self, x, grad_join=None, grad_to=None, bn_follows=False):
+        return OF.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.relu, grad_join, grad_to,
+                         bn_follows)
 
     def extra_repr(self):
         return (f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}, stride={self.stride}, "

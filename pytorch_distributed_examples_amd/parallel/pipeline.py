@@ -231,6 +231,9 @@ class PipelineEngine:
         self._fwd_meta = None  # (shape, dtype) of activations received from prev
         self._bwd_meta = None
         self.timer = NO_PHASES  # utils.log.PhaseTimer: per-stage fwd / bwd / recv-wait times (bench)
+        # a DistributedDataParallel(overlap=True) over this stage's replicas: its bucket all-reduces fire
+        # during the LAST micro-batch's backward (earlier ones run under no_sync), overlapping the rest of it
+        self.ddp = None
 
     # -- primitives --------------------------------------------------------------------------------
     def _recv_act(self):
@@ -262,6 +265,12 @@ class PipelineEngine:
             state["saved"][mb] = (x, y, None)
 
     def _backward(self, mb, state):
+        if self.ddp is not None and mb != state["n_mb"] - 1:
+            with self.ddp.no_sync():
+                return self._backward_mb(mb, state)
+        return self._backward_mb(mb, state)
+
+    def _backward_mb(self, mb, state):
         x, y, _ = state["saved"].pop(mb)
         if self.last:
             with self.timer.phase("bwd"):
@@ -279,7 +288,7 @@ class PipelineEngine:
         """One pipelined forward+backward over ``num_microbatches``; returns the loss (last stage) or
         None.  ``inputs``/``targets`` are lists of micro-batches (stage 0 / last stage)."""
         M = num_microbatches
-        st = {"saved": {}, "loss": []}
+        st = {"saved": {}, "loss": [], "n_mb": M}
         if self.schedule == "gpipe":
             for mb in range(M):
                 self._forward(mb, inputs, targets, M, st)

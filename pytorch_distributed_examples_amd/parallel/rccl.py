@@ -35,8 +35,28 @@ class _StreamWork:
         return True
 
 
+class _SideWork:
+    """An all-reduce enqueued on the communicator's side stream: ``wait()`` makes the CURRENT stream wait
+    for it (an event join -- capturable: a fork/join in the hipGraph), never the host."""
+
+    def __init__(self, event, keep):
+        self.event, self.keep = event, keep
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
+        self.keep = None
+        return True
+
+    def is_completed(self):
+        return self.event.query()
+
+
 class StreamComm:
-    def __init__(self, device: torch.device, group=None):
+    """``side_stream=True``: each all-reduce runs on a dedicated stream forked from the current one, so it
+    overlaps whatever the current stream does next (the remaining backward of a pipeline stage); DDP joins
+    it in ``_complete`` (work.wait())."""
+
+    def __init__(self, device: torch.device, group=None, side_stream: bool = False):
         assert device.type == "cuda", "StreamComm is the GPU data plane"
         self.rank = dist.get_rank(group)
         self.size = dist.get_world_size(group)
@@ -53,10 +73,18 @@ class StreamComm:
         uid = store.get(key)
         self.rccl = C.RcclComm()
         self.rccl.init(uid, self.rank, self.size, device.index, True)
+        self.side = torch.cuda.Stream(device=device) if side_stream else None
 
     def allreduce_async(self, t: torch.Tensor, avg: bool = False):
-        self.rccl.allreduce_(t, _RED_AVG if avg else _RED_SUM)
-        return _StreamWork()
+        if self.side is None:
+            self.rccl.allreduce_(t, _RED_AVG if avg else _RED_SUM)
+            return _StreamWork()
+        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.side):
+            self.rccl.allreduce_(t, _RED_AVG if avg else _RED_SUM)
+            ev = torch.cuda.Event()
+            ev.record()
+        return _SideWork(ev, t)
 
     def allreduce_(self, t: torch.Tensor, avg: bool = False) -> torch.Tensor:
         self.rccl.allreduce_(t, _RED_AVG if avg else _RED_SUM)

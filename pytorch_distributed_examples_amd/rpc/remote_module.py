@@ -138,17 +138,17 @@ class RemoteModule:
         """This process's ring towards the owner (created + handshaken by RPC on first use)."""
         from .. import _native
 
-        ring = self.__dict__.get("_ring")
+        ring = self.__dict__.get("_p2p")
         if ring is None:
             ring = _native.comm().P2PRing(device.index, _ring_slot_bytes(), 60.0)
             me = rpc.get_worker_info().name
             ring.open(rpc.rpc_sync(self.worker, _rm_open_ring, args=(self.server, me, ring.ipc_handle())))
-            self.__dict__["_ring"] = ring
+            self.__dict__["_p2p"] = ring
         return ring
 
     def close(self):
         """Tear down this process's ring towards the owner (and the owner's side); both drain first."""
-        ring = self.__dict__.pop("_ring", None)
+        ring = self.__dict__.pop("_p2p", None)
         if ring is not None:
             torch.cuda.synchronize()
             rpc.rpc_sync(self.worker, _rm_close_ring, args=(self.server, rpc.get_worker_info().name))
@@ -156,7 +156,7 @@ class RemoteModule:
 
     def __getstate__(self):  # the handle travels to other processes; a ring is per process
         d = dict(self.__dict__)
-        d.pop("_ring", None)
+        d.pop("_p2p", None)
         return d
 
     def uses_ring(self, out_device) -> bool:

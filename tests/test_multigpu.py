@@ -194,3 +194,57 @@ def test_pipeline_grads_world_n(gpu, n):
         pytest.skip(f"needs {n} GPUs, box has {torch.cuda.device_count()}")
     res = _torchrun(_PIPE, n)
     assert res.returncode == 0 and res.stdout.count("PIPE_OK") == n, (res.stdout[-3000:], res.stderr[-5000:])
+
+
+_RESNET_PP = r"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["REPO"])
+from pytorch_distributed_examples_amd.parallel import dist as pdist
+from pytorch_distributed_examples_amd.apps.hybrid_ps import ResNetPipelineDP
+from pytorch_distributed_examples_amd.utils.graph import CapturedStep
+ctx = pdist.init_distributed()
+N, r, dev = ctx.world_size, ctx.rank, ctx.device
+for schedule in ("gpipe", "1f1b"):
+    torch.manual_seed(0)
+    pipe = ResNetPipelineDP(ctx, batch=16, split_size=4, image=64, schedule=schedule, lr=0.02, tag="mg" + schedule)
+    assert pipe.capturable, "BASELINE configs 3/4: the whole pipelined step is one hipGraph per rank"
+    graph = CapturedStep(pipe.step, [], warmup=1).capture()
+    losses = [float(graph().item()) for _ in range(4)]
+    pipe.check()
+    flat = torch.cat([p.detach().float().reshape(-1) for p in pipe.module.parameters()])
+    assert torch.isfinite(flat).all()
+    # every data-parallel replica of a stage holds bit-identical weights (stage all-reduce, bf16 wire, overlapped)
+    gathered = [torch.empty_like(flat) for _ in range(N)]
+    dist.all_gather(gathered, flat)
+    for k in range(r % 2, N, 2):
+        assert torch.equal(gathered[k], flat), (schedule, r, k)
+    if r % 2 == 1:
+        assert all(l == l and l < 1e3 for l in losses), losses
+    pipe.close()
+dist.destroy_process_group()
+print("RESNET_PP_OK", r)
+"""
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_resnet_pipeline_dp_world_n(gpu, n):
+    """BASELINE configs 3 (n=2) and 4 (n=8: pp2 x dp4): ResNetPipelineDP captured in a hipGraph, stage
+    activations over the P2P ring, stage gradients all-reduced (bf16 wire, overlapped with the last
+    micro-batch's backward) -- replicas must stay bit-identical, for gpipe and 1f1b."""
+    if torch.cuda.device_count() < n:
+        pytest.skip(f"needs {n} GPUs, box has {torch.cuda.device_count()}")
+    res = _torchrun(_RESNET_PP, n)
+    assert res.returncode == 0 and res.stdout.count("RESNET_PP_OK") == n, (res.stdout[-3000:], res.stderr[-5000:])
+
+
+def test_resnet_rpc_two_gpus(gpu):
+    """rpc/model_parallel_ResNet50.py with each stage on its own GPU (master + 2 stage workers)."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    env = dict(os.environ)
+    env.pop("PDE_BACKEND", None)
+    cmd = [sys.executable, os.path.join(REPO, "rpc", "model_parallel_ResNet50.py"), "--splits", "4", "8",
+           "--num-batches", "3", "--verbose"]
+    res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert res.returncode == 0, (res.stdout[-3000:], res.stderr[-3000:])
+    assert "number of splits = 8, execution time" in res.stdout, res.stdout

@@ -13,6 +13,7 @@ import os
 import subprocess
 import sys
 import tempfile
+import time
 
 import pytest
 
@@ -241,8 +242,11 @@ def test_parameter_server_ring_data_plane_one_gpu(gpu):
         files = [open(lg, "w") for lg in logs]  # progress lands under gpurun_out/ while it runs
         procs = [subprocess.Popen([sys.executable, path], env=dict(env, RANK=str(r), WORLD_SIZE="2"),
                                   stdout=fo, stderr=subprocess.STDOUT, text=True) for r, fo in enumerate(files)]
-        for p in procs:
-            p.wait(timeout=300)
+        t0 = time.time()
+        while any(p.poll() is None for p in procs) and time.time() - t0 < 150:
+            if any(p.poll() not in (None, 0) for p in procs):  # one side failed: the other would wait forever
+                break
+            time.sleep(0.5)
     finally:
         for p in procs:
             if p.poll() is None:

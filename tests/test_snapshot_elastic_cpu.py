@@ -100,3 +100,26 @@ def test_rewire_scale_up_via_discovery(tmp_path):
     assert re.search(r"\[rewire\] round 1: rank 1 of 2", out), out[-3000:]
     fin = re.findall(r"\[rewire\] finished 4 epochs in round (\d+) \(world (\d)", out)
     assert len(fin) == 2 and all(w == "2" for _, w in fin), out[-3000:]
+
+
+def test_round_shrink_plan():
+    """Shrink-only re-wire: a round whose members are a subset of the previous round's, in the
+    same relative order, is built by shrinking the previous RCCL communicator (excluded = the parent ranks
+    that left); growth, reordering or no parent falls back to a fresh init."""
+    from pytorch_distributed_examples_amd.elastic.rewire import RoundComm
+
+    class P:  # a previous round: members in rank order, a live communicator
+        def __init__(self, members):
+            self.members, self.rccl = members, object()
+
+    def plan(parent_members, members):
+        rc = RoundComm.__new__(RoundComm)
+        rc.members = members
+        return rc._shrink_plan(P(parent_members) if parent_members is not None else None)
+
+    assert plan(["a", "b", "c", "d"], ["a", "c", "d"]) == [1]
+    assert plan(["a", "b", "c", "d"], ["b", "c"]) == [0, 3]
+    assert plan(["a", "b", "c"], ["a", "b", "c", "e"]) is None      # growth: fresh init
+    assert plan(["a", "b", "c"], ["a", "b", "c"]) is None           # no change
+    assert plan(["a", "b", "c"], ["c", "a"]) is None                # reordered ranks
+    assert plan(None, ["a"]) is None
