@@ -728,7 +728,7 @@ void optim_step(const Tensor& table, const Tensor& chunks, int64_t nchunks, int 
 // ------------------------------------------------------------------------------------------------
 // BatchNorm / pooling / dropout / EmbeddingBag
 // ------------------------------------------------------------------------------------------------
-// Returns y, save_mean, save_invstd.
+// Returns y, save_mean, save_invstd, scale_shift ([2C] fp32: y = relu?(x*scale + shift + res)).
 std::vector<Tensor> bn_fwd(const Tensor& x, const optional<Tensor>& gamma, const optional<Tensor>& beta,
                            const optional<Tensor>& running_mean, const optional<Tensor>& running_var, double eps,
                            double momentum, const optional<Tensor>& res, bool relu) {
@@ -757,7 +757,7 @@ std::vector<Tensor> bn_fwd(const Tensor& x, const optional<Tensor>& gamma, const
                           u16(y), cur_stream(), pc.ws.defined() ? pc.ws.data_ptr<float>() : nullptr,
                           pc.ws.defined() ? pc.splits : 1),
         "bn_fwd");
-  return {y, mean, invstd};
+  return {y, mean, invstd, ss};
 }
 // Inference / eval mode: y = x*scale + shift with scale/shift from running stats (computed in torch).
 Tensor bn_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, const optional<Tensor>& res, bool relu) {
@@ -773,10 +773,12 @@ Tensor bn_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, const
   return y;
 }
 // Returns dx, dgamma, dbeta, dres (dres undefined unless want_dres).  With dg_out / db_out (both, [C] fp32)
-// the parameter gradients are ADDED into those tensors (direct accumulation into .grad).
+// the parameter gradients are ADDED into those tensors (direct accumulation into .grad).  scale_shift (the
+// forward's, only for a BatchNorm without residual): the ReLU mask comes from x instead of y.
 std::vector<Tensor> bn_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const Tensor& mean,
                            const Tensor& invstd, const optional<Tensor>& gamma, bool relu, bool want_dres,
-                           const optional<Tensor>& dg_out, const optional<Tensor>& db_out) {
+                           const optional<Tensor>& dg_out, const optional<Tensor>& db_out,
+                           const optional<Tensor>& scale_shift) {
   CHECK_IN(dy); CHECK_IN(x); CHECK_IN(y); CHECK_BF16(dy);
   resolve_pending(x);
   resolve_pending(y);
@@ -793,7 +795,8 @@ std::vector<Tensor> bn_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, c
   if (want_dres) dres = at::empty_like(x);
   check(pde::bn_bwd(u16(dy), u16(x), u16(y), mean.data_ptr<float>(), invstd.data_ptr<float>(), cf32(gamma), P, C,
                     relu, dg.data_ptr<float>(), db.data_ptr<float>(), direct ? 1 : 0, ws.data_ptr<float>(),
-                    coef.data_ptr<float>(), u16(dx), want_dres ? u16(dres) : nullptr, cur_stream()),
+                    coef.data_ptr<float>(), u16(dx), want_dres ? u16(dres) : nullptr, cur_stream(),
+                    want_dres ? nullptr : cf32(scale_shift)),
         "bn_bwd");
   return {dx, dg, db, dres};
 }
@@ -1033,7 +1036,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("mean"), py::arg("invstd"),
         py::arg("gamma"), py::arg("relu"), py::arg("want_dres"), py::arg("dg_out") = py::none(),
-        py::arg("db_out") = py::none());
+        py::arg("db_out") = py::none(), py::arg("scale_shift") = py::none());
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);

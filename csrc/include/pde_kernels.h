@@ -183,9 +183,11 @@ int bn_error(int reset);
 hipError_t bn_apply(const uint16_t* x, int P, int C, const float* scale, const float* shift, const uint16_t* res,
                     int relu, uint16_t* y, hipStream_t s);
 // dgamma / dbeta are written, or added to when accum_params != 0 (direct accumulation into .grad).
+// ss (optional, the forward's fp32 scale/shift [2C] of a BatchNorm WITHOUT residual): the ReLU mask is
+// recomputed from x (y is not read by the one-launch kernel)
 hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
                   const float* gamma, int P, int C, int relu, float* dgamma, float* dbeta, int accum_params, float* ws,
-                  float* coef, uint16_t* dx, uint16_t* dres, hipStream_t s);
+                  float* coef, uint16_t* dx, uint16_t* dres, hipStream_t s, const float* ss = nullptr);
 hipError_t maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
                        int k, int st, int p, int relu, hipStream_t s);
 hipError_t maxpool_bwd(const uint16_t* dy, const uint16_t* y, const uint8_t* idx, uint16_t* dx, int N, int H, int W,

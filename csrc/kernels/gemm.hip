@@ -876,6 +876,145 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   }
 }
 
+// ---- Skinny GEMMs: a handful of output tiles over a long K (the MLP's batch-128 linears) ---------------
+// A 128 x 1024 output is 32 tiles of 64x64: too few blocks for 256 CUs, so the tile path splits K across
+// blocks and pays an fp32 slab round trip plus a reduce launch per GEMM.  Here the split is ACROSS THE
+// WAVES of one workgroup: a 16FM x 16FN tile per block (M=128, N=1024: 256 blocks), wave w takes K-steps
+// w, w + NW, ... (32 deep), every lane loads its MFMA fragments straight from global memory (K-contiguous
+// operands: one 16-B buffer load per lane per fragment, all U K-steps of a batch in flight at once;
+// a row-contiguous B -- the dgrad's weight [K][N] -- goes through a wave-private LDS image read back with
+// ds_read_b64_tr_b16), and the NW partial tiles meet in LDS, summed in wave order (deterministic) with the
+// epilogue applied.  One launch, no slabs, no reduce kernel.  Requires dense operands, K-contiguous A, 16-B
+// aligned rows, K % 8 == 0 (host-checked: skinny_ok).
+constexpr int kSkinnyFM = 1, kSkinnyFN = 2, kSkinnyNW = kThreads / 64;
+template <bool BKC>
+constexpr int skinny_u() { return BKC ? 8 : 4; }  // K-steps per wave per batch
+template <int FM, int FN, int NW, bool BKC>
+constexpr int skinny_smem_bytes() {
+  constexpr int img = BKC ? 0 : NW * skinny_u<BKC>() * 32 * 16 * FN * 2;
+  constexpr int red = NW * FM * FN * 64 * 16;
+  return img > red ? img : red;
+}
+template <int FM, int FN, int NW, bool BKC>
+__device__ __forceinline__ void skinny_tile(const GemmArgs& args, int tiles_m, int tiles_n, int orig,
+                                            uint16_t* smem) {
+  constexpr int U = skinny_u<BKC>();
+  constexpr int TM = 16 * FM, TN = 16 * FN;
+  static_assert(BKC || TN == 32 || TN == 64 || TN == 128, "row-contiguous B image widths (rc_swz)");
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // XCD-aware: consecutive tile ids (the tiles_m row tiles of one B column block) on one XCD's L2
+  const int ntiles = tiles_m * tiles_n;
+  int tile = orig;
+  if (ntiles > 8) {
+    const int q = ntiles / 8, r = ntiles % 8, xcd = orig % 8;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  }
+  const int tn = tile / tiles_m, tm = tile - tn * tiles_m;
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int K = args.K, nks = (K + 31) / 32;
+  const auto ra = operand_rsrc(args.a, 0, args.M, K, true);
+  const auto rb = operand_rsrc(args.b, 0, args.N, K, BKC);
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint16_t* img = smem + w * (U * 32 * TN);  // row-contiguous B only: [U][32 k][TN] per wave
+  const int kq = 8 * (lane >> 4);
+  for (int b0 = 0; b0 < nks; b0 += NW * U) {  // uniform trip count: the barriers below are legal
+    u16x8 fa[U][FM], fb[U][FN];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ks = b0 + w + u * NW;
+      const int k = ks * 32 + kq;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int m = m0 + 16 * i + (lane & 15);
+        fa[u][i] = bload16(ra, ks < nks && m < args.M && k < K, static_cast<long>(m) * args.a.ld_r + k);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        if constexpr (BKC) {
+          const int n = n0 + 16 * j + (lane & 15);
+          fb[u][j] = bload16(rb, ks < nks && n < args.N && k < K, static_cast<long>(n) * args.b.ld_r + k);
+        } else {  // chunk c = lane + 64 j of the 32 x TN block: row c / (TN / 8), 8 columns at c % (TN / 8)
+          const int c = lane + 64 * j, kr = c / (TN / 8), n = n0 + (c % (TN / 8)) * 8, kk = ks * 32 + kr;
+          fb[u][j] = bload16(rb, ks < nks && kk < K && n < args.N, static_cast<long>(kk) * args.b.ld_k + n);
+        }
+      }
+    }
+    if constexpr (!BKC) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int c = lane + 64 * j, kr = c / (TN / 8), cc = c % (TN / 8);
+          *reinterpret_cast<u16x8*>(img + u * 32 * TN + kr * TN + ((cc ^ rc_swz<TN>(kr)) << 3)) = fb[u][j];
+        }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (b0 + w + u * NW >= nks) continue;  // wave-uniform
+      bf16x8 bfr[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        if constexpr (BKC) bfr[j] = __builtin_bit_cast(bf16x8, fb[u][j]);
+        else bfr[j] = rc_frag<TN>(img + u * 32 * TN, 16 * j, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[u][i]), bfr[j],
+                                                              acc[i][j], 0, 0, 0);
+    }
+    if constexpr (!BKC) __syncthreads();  // images read before the next batch overwrites them
+  }
+  __syncthreads();  // the LDS is reused for the partial tiles
+  f32x4* red = reinterpret_cast<f32x4*>(smem);  // [NW][FM][FN][64 lanes]
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) red[((w * FM + i) * FN + j) * 64 + lane] = acc[i][j];
+  __syncthreads();
+  // output o = ((i FN + j) 64 + lane') 4 + r: C/D map of 16x16x32 -- column lane' & 15, row 4 (lane' >> 4) + r
+  for (int o = threadIdx.x; o < TM * TN; o += NW * 64) {
+    const int r = o & 3, ln = (o >> 2) & 63, ij = o >> 8;
+    const int i = ij / FN, j = ij - i * FN;
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) v += red[((ww * FM + i) * FN + j) * 64 + ln][r];
+    const int m = m0 + 16 * i + 4 * (ln >> 4) + r, n = n0 + 16 * j + (ln & 15);
+    if (m < args.M && n < args.N) store_out(apply_epi(v, args.epi, m, n, args), args.epi, m, n, args);
+  }
+}
+
+template <bool BKC>
+__global__ __launch_bounds__(kThreads) void gemm_skinny_kernel(GemmArgs args, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[skinny_smem_bytes<kSkinnyFM, kSkinnyFN, kSkinnyNW, BKC>() / 2];
+  skinny_tile<kSkinnyFM, kSkinnyFN, kSkinnyNW, BKC>(args, tiles_m, tiles_n, blockIdx.x, smem);
+}
+
+// A layer's skinny dgrad (problem 0) and its weight gradient on the 64x64 FAST tile (problem 1) in one launch.
+template <bool BKC0, bool AKC1, bool BKC1, int AK1, int BK1>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void gemm_pair_skinny_kernel(
+    GemmArgs a0, int tm0, int tn0, GemmArgs a1, PairDims d) {
+  constexpr int kS = skinny_smem_bytes<kSkinnyFM, kSkinnyFN, kSkinnyNW, BKC0>();
+  constexpr int kT = SMEM_BYTES_OF<64, 64>();
+  __shared__ __attribute__((aligned(16))) uint16_t smem[(kS > kT ? kS : kT) / 2];
+  const int nb0 = tm0 * tn0;
+  const int b = blockIdx.x;
+  if (b < nb0) {
+    skinny_tile<kSkinnyFM, kSkinnyFN, kSkinnyNW, BKC0>(a0, tm0, tn0, b, smem);
+  } else {
+    const int t1 = d.tm[1] * d.tn[1], b1 = b - nb0;
+    gemm_tile<64, 64, 32, 2, 2, AKC1, BKC1, AK1, BK1, PDE_FAST_STAGES>(a1, d.tm[1], d.tn[1], d.kps[1], d.av[1],
+                                                                       d.bv[1], b1 % t1, b1 / t1, d.nz[1], smem);
+  }
+}
+
 // Split-K slab reduction, scalar form (N % 4 != 0).
 __global__ void gemm_splitk_reduce(GemmArgs args, int splits) {
   const long total = static_cast<long>(args.M) * args.N;
@@ -1238,10 +1377,59 @@ bool launch_pair_k0(int k0, dim3 grid, hipStream_t s, const GemmArgs& a0, const 
   }
 }
 
+// Skinny path (skinny_tile): dense operands, K-contiguous A, 16-B aligned rows, whole 8-element K groups, a
+// plain epilogue, and an output the 64x64 tile path would cover with too few blocks for the chip (it would
+// split K across blocks) while K is long enough for the in-block wave split to pay.
+bool skinny_enabled() {
+  static const bool on = !(std::getenv("PDE_GEMM_SKINNY") && std::getenv("PDE_GEMM_SKINNY")[0] == '0');
+  return on;
+}
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+bool skinny_ok(const GemmArgs& a) {
+  if (!skinny_enabled() || generic_only() || a.a.kind != 0 || a.b.kind != 0) return false;
+  if (a.epi & EPI_OIHW || a.bias_grad != nullptr || a.splits_out != nullptr) return false;
+  if (a.a.ld_k != 1 || a.a.ld_r % 8 != 0 || !aligned16(a.a.ptr) || a.K % 8 != 0) return false;
+  const bool bkc = is_kc(a.b);
+  if (bkc ? (a.b.ld_r % 8 != 0) : (a.b.ld_r != 1 || a.b.ld_k % 8 != 0 || a.N % 8 != 0)) return false;
+  if (!aligned16(a.b.ptr)) return false;
+  if (static_cast<long>(a.M) * a.a.ld_r * 2 >= (1L << 31) || static_cast<long>(a.K) * a.N * 2 >= (1L << 31))
+    return false;
+  const long t64 = static_cast<long>(ceil_div(a.M, 64)) * ceil_div(a.N, 64);
+  return t64 < 128 && a.K >= 256 && a.M <= 1024;
+}
+void skinny_grid(const GemmArgs& a, int& tm, int& tn) {
+  tm = ceil_div(a.M, 16 * kSkinnyFM);
+  tn = ceil_div(a.N, 16 * kSkinnyFN);
+}
+hipError_t launch_skinny(const GemmArgs& a, hipStream_t s) {
+  int tm, tn;
+  skinny_grid(a, tm, tn);
+  if (is_kc(a.b))
+    hipLaunchKernelGGL(gemm_skinny_kernel<true>, dim3(tm * tn), dim3(kThreads), 0, s, a, tm, tn);
+  else
+    hipLaunchKernelGGL(gemm_skinny_kernel<false>, dim3(tm * tn), dim3(kThreads), 0, s, a, tm, tn);
+  return hipGetLastError();
+}
+// skinny problem 0 + 64x64 FAST-tile problem 1 (a weight gradient: dy^T x dense activation)
+bool launch_pair_skinny(const GemmArgs& a0, const GemmArgs& a1, const PairDims& d, hipStream_t s) {
+  if (kind_code_of(a1) != kind_code(false, false, 0, 0)) return false;
+  int tm0, tn0;
+  skinny_grid(a0, tm0, tn0);
+  const dim3 grid(static_cast<unsigned>(tm0 * tn0 + d.tm[1] * d.tn[1] * d.nz[1]));
+  if (is_kc(a0.b))
+    hipLaunchKernelGGL((gemm_pair_skinny_kernel<true, false, false, 0, 0>), grid, dim3(kThreads), 0, s, a0, tm0, tn0,
+                       a1, d);
+  else
+    hipLaunchKernelGGL((gemm_pair_skinny_kernel<false, false, false, 0, 0>), grid, dim3(kThreads), 0, s, a0, tm0,
+                       tn0, a1, d);
+  return true;
+}
+
 }  // namespace
 
 hipError_t gemm_bf16(const GemmArgs& a, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0) return hipSuccess;
+  if (skinny_ok(a)) return launch_skinny(a, s);
   const bool akc = is_kc(a.a), bkc = is_kc(a.b);
   if (akc && bkc) return dispatch_tiles<true, true>(a, s);
   if (akc && !bkc) return dispatch_tiles<true, false>(a, s);
@@ -1286,6 +1474,23 @@ hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s,
   if (defer_split1 != nullptr) *defer_split1 = 0;
   PairDims d{};
   int sp0 = 1, sp1 = 1;
+  if (gemm_pair_enabled() && skinny_ok(a0) &&
+      pair_member_plan(a1, d.tm[1], d.tn[1], d.kps[1], sp1, d.av[1], d.bv[1]) && (sp1 == 1 || reduce_vec_ok(a1))) {
+    // skinny dgrad + tile wgrad: problem 0 needs no reduction at all
+    GemmArgs g1 = a1;
+    g1.tickets = nullptr;
+    d.nz[1] = sp1;
+    if (static_cast<long>(d.tm[1]) * d.tn[1] * sp1 < (1L << 30) && launch_pair_skinny(a0, g1, d, s)) {
+      if (defer_split1 != nullptr && sp1 > 1) {
+        *defer_split1 = sp1;
+      } else if (sp1 > 1) {
+        launch_reduce(a1, sp1, s);
+      }
+      return hipGetLastError();
+    }
+  }
+  d = PairDims{};
+  sp1 = 1;
   const bool ok = gemm_pair_enabled() &&
                   pair_member_plan(a0, d.tm[0], d.tn[0], d.kps[0], sp0, d.av[0], d.bv[0]) &&
                   pair_member_plan(a1, d.tm[1], d.tn[1], d.kps[1], sp1, d.av[1], d.bv[1]) &&

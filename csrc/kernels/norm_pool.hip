@@ -697,12 +697,34 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
   }
 }
 
+// ReLU mask of a BatchNorm output, recomputed from its INPUT when the forward had no residual: relu(x*sc+sh)
+// > 0 <=> x*sc + sh > 0 with the forward's own fp32 scale/shift (ss) -- the backward then streams dy and x
+// only, not y.  With a residual (the block's last BN) the saved y decides.
+__device__ __forceinline__ void bn_relu_mask(const u16x8& ux, const uint16_t* __restrict__ y, long off,
+                                             const float (&sc)[8], const float (&sh)[8], bool from_x,
+                                             float (&d)[8]) {
+  if (from_x) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (!(bf2f(ux[j]) * sc[j] + sh[j] > 0.f)) d[j] = 0.f;
+  } else {
+    const u16x8 uy = *reinterpret_cast<const u16x8*>(y + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (!(bf2f(uy[j]) > 0.f)) d[j] = 0.f;
+  }
+}
+
+// RC > 0: a thread's rows of the chunk (<= RC of them) stay in registers between the statistics pass and the
+// apply pass (micro-batch sized tensors), else the apply pass re-reads them (L2).
+template <int RC>
 __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const uint16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, int P, int C, int rpb, int relu,
     float* __restrict__ ws, int* __restrict__ tickets, uint32_t* __restrict__ flags, int* __restrict__ err,
     const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta, int accum,
-    float* __restrict__ coef, uint16_t* __restrict__ dx, uint16_t* __restrict__ dres) {
+    float* __restrict__ coef, uint16_t* __restrict__ dx, uint16_t* __restrict__ dres,
+    const float* __restrict__ ss) {
   __shared__ float red[2][kBnRows][kBnCG + 1];
   __shared__ float tot1[kBnCG], tot2[kBnCG];
   __shared__ int s_last;
@@ -710,48 +732,75 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
   const int tid = threadIdx.x, tv = tid & 7, tr = tid >> 3;
   const int c0 = blockIdx.y * kBnCG + tv * 8;
   const bool cok = c0 < C;
+  const bool from_x = relu && ss != nullptr;
   bn_gen_start(flags + blockIdx.y, &s_gen);
+  const int r0 = blockIdx.x * rpb + tr;
   const int r1 = min(P, (blockIdx.x + 1) * rpb);
-  float s1[8], s2[8], mu[8], is[8];
+  float s1[8], s2[8], mu[8], is[8], sc[8], sh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = mu[j] = is[j] = 0.f;
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = mu[j] = is[j] = sc[j] = sh[j] = 0.f;
+  u16x8 cd[RC > 0 ? RC : 1], cx[RC > 0 ? RC : 1];
   if (cok) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) { mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j]; }
-    int r = blockIdx.x * rpb + tr;
-    constexpr int U = kBnUnroll / 2;  // 3 tensors per row: 12 x 16-B loads in flight per lane
-    for (; r + (U - 1) * kBnRows < r1; r += U * kBnRows) {
-      u16x8 ud[U], ux[U], uy[U];
+    if (from_x) {
 #pragma unroll
-      for (int q = 0; q < U; ++q) {
-        const long off = static_cast<long>(r + kBnRows * q) * C + c0;
-        ud[q] = *reinterpret_cast<const u16x8*>(dy + off);
-        ux[q] = *reinterpret_cast<const u16x8*>(x + off);
-        if (relu) uy[q] = *reinterpret_cast<const u16x8*>(y + off);
-      }
-#pragma unroll
-      for (int q = 0; q < U; ++q)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float d = bf2f(ud[q][j]);
-          if (relu && !(bf2f(uy[q][j]) > 0.f)) d = 0.f;
-          s1[j] += d;
-          s2[j] += d * (bf2f(ux[q][j]) - mu[j]) * is[j];
-        }
+      for (int j = 0; j < 8; ++j) { sc[j] = ss[c0 + j]; sh[j] = ss[C + c0 + j]; }
     }
-    for (; r < r1; r += kBnRows) {
-      const long off = static_cast<long>(r) * C + c0;
-      float d[8], xv[8];
-      load8(dy + off, d);
-      load8(x + off, xv);
-      if (relu) {
-        float yv[8];
-        load8(y + off, yv);
+    if constexpr (RC > 0) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+      for (int k = 0; k < RC; ++k) {  // all of the thread's loads in flight, kept for the apply pass
+        const int r = r0 + k * kBnRows;
+        if (r < r1) {
+          const long off = static_cast<long>(r) * C + c0;
+          cd[k] = *reinterpret_cast<const u16x8*>(dy + off);
+          cx[k] = *reinterpret_cast<const u16x8*>(x + off);
+        }
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { s1[j] += d[j]; s2[j] += d[j] * (xv[j] - mu[j]) * is[j]; }
+      for (int k = 0; k < RC; ++k) {
+        const int r = r0 + k * kBnRows;
+        if (r < r1) {
+          float d[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d[j] = bf2f(cd[k][j]);
+          if (relu) bn_relu_mask(cx[k], y, static_cast<long>(r) * C + c0, sc, sh, from_x, d);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { s1[j] += d[j]; s2[j] += d[j] * (bf2f(cx[k][j]) - mu[j]) * is[j]; }
+        }
+      }
+    } else {
+      int r = r0;
+      constexpr int U = kBnUnroll / 2;
+      for (; r + (U - 1) * kBnRows < r1; r += U * kBnRows) {
+        u16x8 ud[U], ux[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+          const long off = static_cast<long>(r + kBnRows * q) * C + c0;
+          ud[q] = *reinterpret_cast<const u16x8*>(dy + off);
+          ux[q] = *reinterpret_cast<const u16x8*>(x + off);
+        }
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+          float d[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d[j] = bf2f(ud[q][j]);
+          if (relu) bn_relu_mask(ux[q], y, static_cast<long>(r + kBnRows * q) * C + c0, sc, sh, from_x, d);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { s1[j] += d[j]; s2[j] += d[j] * (bf2f(ux[q][j]) - mu[j]) * is[j]; }
+        }
+      }
+      for (; r < r1; r += kBnRows) {
+        const long off = static_cast<long>(r) * C + c0;
+        const u16x8 ud = *reinterpret_cast<const u16x8*>(dy + off);
+        const u16x8 ux = *reinterpret_cast<const u16x8*>(x + off);
+        float d[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = bf2f(ud[j]);
+        if (relu) bn_relu_mask(ux, y, off, sc, sh, from_x, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { s1[j] += d[j]; s2[j] += d[j] * (bf2f(ux[j]) - mu[j]) * is[j]; }
+      }
     }
   }
   if (bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last)) {
@@ -774,26 +823,32 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
   float ca[8], cb[8], cc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { ca[j] = coef[c0 + j]; cb[j] = coef[C + c0 + j]; cc[j] = coef[2 * C + c0 + j]; }
-  for (int r = blockIdx.x * rpb + tr; r < r1; r += kBnRows) {
-    const long off = static_cast<long>(r) * C + c0;
-    float d[8], xv[8];
-    load8(dy + off, d);
-    load8(x + off, xv);
-    if (relu) {
-      float yv[8];
-      load8(y + off, yv);
+  auto apply = [&](const u16x8& ud, const u16x8& ux, long off) {
+    float d[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
-    }
+    for (int j = 0; j < 8; ++j) d[j] = bf2f(ud[j]);
+    if (relu) bn_relu_mask(ux, y, off, sc, sh, from_x, d);
     u16x8 o, orr;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float xh = (xv[j] - mu[j]) * is[j];
+      const float xh = (bf2f(ux[j]) - mu[j]) * is[j];
       o[j] = f2bf(ca[j] * d[j] - cb[j] - cc[j] * xh);
       orr[j] = f2bf(d[j]);
     }
     *reinterpret_cast<u16x8*>(dx + off) = o;
     if (dres) *reinterpret_cast<u16x8*>(dres + off) = orr;
+  };
+  if constexpr (RC > 0) {
+#pragma unroll
+    for (int k = 0; k < RC; ++k) {
+      const int r = r0 + k * kBnRows;
+      if (r < r1) apply(cd[k], cx[k], static_cast<long>(r) * C + c0);
+    }
+  } else {
+    for (int r = r0; r < r1; r += kBnRows) {
+      const long off = static_cast<long>(r) * C + c0;
+      apply(*reinterpret_cast<const u16x8*>(dy + off), *reinterpret_cast<const u16x8*>(x + off), off);
+    }
   }
 }
 
@@ -1273,7 +1328,7 @@ hipError_t bn_apply(const uint16_t* x, int P, int C, const float* scale, const f
 
 hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
                   const float* gamma, int P, int C, int relu, float* dgamma, float* dbeta, int accum_params, float* ws,
-                  float* coef, uint16_t* dx, uint16_t* dres, hipStream_t s) {
+                  float* coef, uint16_t* dx, uint16_t* dres, hipStream_t s, const float* ss) {
   int rpb;
   const int ncg = ceil_div(C, kBnCG);
   int* err = nullptr;
@@ -1282,9 +1337,13 @@ hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, cons
     int* tk = bn_tickets(ncg, s);
     uint32_t* fl = bn_flags(ncg, s);
     if (tk != nullptr && fl != nullptr) {
-      hipLaunchKernelGGL(k_bn_bwd_fused, dim3(nrb1, ncg), dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, P, C, rpb,
-                         relu, ws, tk, fl, err, gamma, dgamma, dbeta, accum_params,
-                         coef, dx, dres);
+      // rows per thread of a chunk: small enough -> kept in registers for the apply pass
+      if (ceil_div(rpb, kBnRows) <= 4)
+        hipLaunchKernelGGL(k_bn_bwd_fused<4>, dim3(nrb1, ncg), dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, P, C,
+                           rpb, relu, ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss);
+      else
+        hipLaunchKernelGGL(k_bn_bwd_fused<0>, dim3(nrb1, ncg), dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, P, C,
+                           rpb, relu, ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss);
       return hipGetLastError();
     }
   }

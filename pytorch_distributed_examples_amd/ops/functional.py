@@ -464,24 +464,26 @@ class _BatchNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, running_mean, running_var, residual, eps, momentum, relu, join=None):
         ctx.join = join
-        y, mean, invstd = _C().bn_fwd(x, gamma.detach() if gamma is not None else None,
-                                      beta.detach() if beta is not None else None, running_mean, running_var,
-                                      eps, momentum, residual, relu)
+        y, mean, invstd, ss = _C().bn_fwd(x, gamma.detach() if gamma is not None else None,
+                                          beta.detach() if beta is not None else None, running_mean,
+                                          running_var, eps, momentum, residual, relu)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.beta = beta
-        ctx.save_for_backward(x, y, mean, invstd, gamma)
+        # without a residual the backward recomputes the ReLU mask from x with the forward's scale/shift
+        ctx.save_for_backward(x, y, mean, invstd, gamma, ss)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, mean, invstd, gamma = ctx.saved_tensors
+        x, y, mean, invstd, gamma, ss = ctx.saved_tensors
         beta = ctx.beta
         dg_sink, db_sink = _grad_sink(gamma), _grad_sink(beta)
         direct = dg_sink is not None and db_sink is not None
         dx, dg, db, dres = _C().bn_bwd(dy.contiguous(), x, y, mean, invstd,
                                        gamma.detach() if gamma is not None else None, ctx.relu, ctx.has_res,
-                                       dg_sink if direct else None, db_sink if direct else None)
+                                       dg_sink if direct else None, db_sink if direct else None,
+                                       None if ctx.has_res else ss)
         if direct:  # dgamma / dbeta were added into .grad by the finalize kernel
             dg = db = None
         if ctx.has_res and ctx.join is not None:  # the residual fork's conv adds it in its dgrad epilogue

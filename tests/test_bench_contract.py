@@ -1,6 +1,7 @@
 """bench.py output contract (one JSON line, required fields), exercised on CPU: 1 rank and 2 ranks
 under torchrun (gloo)."""
 import json
+import re
 import os
 
 from dist_utils import REPO, free_port, run_cmd
@@ -99,5 +100,5 @@ def test_bench_elastic_scale_up_cpu():
     for ln in out.splitlines():
         if ln.startswith("[rewire] round ") and "(pid " in ln:
             rnd = int(ln.split()[2].rstrip(":"))
-            pids.setdefault(rnd, set()).add(int(ln.split("(pid ")[1].split(")")[0]))
+            pids.setdefault(rnd, set()).add(int(re.match(r"\d+", ln.split("(pid ")[1]).group(0)))
     assert pids[0] <= pids[1] and len(pids[1]) == 4, pids

@@ -42,6 +42,26 @@ def test_linear_fwd_bwd(gpu, M, K, N):
     assert rel_err(dw, dy.float().t() @ bf(x)) < 1e-2
 
 
+@pytest.mark.parametrize("M,K,N", [(128, 1024, 1024), (200, 4096, 96), (72, 2056, 40), (1000, 320, 56)])
+def test_skinny_gemm_paths(gpu, M, K, N):
+    """Few output tiles over a long K: the in-block wave split-K kernel (gemm.hip skinny_tile) -- forward
+    (K-contiguous weight, bias + ReLU epilogue), dgrad (row-contiguous weight through the transposing LDS
+    image, ReLU-mask epilogue), several K batches and ragged M / N edges; bitwise deterministic."""
+    C = OF._C()
+    torch.manual_seed(1)
+    x = torch.randn(M, K, device=gpu).bfloat16()
+    w = (torch.randn(N, K, device=gpu) * 0.05).bfloat16()
+    b = torch.randn(N, device=gpu)
+    y = C.linear_fwd(x, w, b, True, False)
+    assert rel_err(y, torch.relu(x.float() @ w.float().t() + b)) < 1e-2
+    assert torch.equal(y, C.linear_fwd(x, w, b, True, False))
+    wt = (torch.randn(K, N, device=gpu) * 0.05).bfloat16()  # dgrad-shaped: dx[M, N] = dy2[M, K] @ wt[K, N]
+    dy2 = torch.randn(M, K, device=gpu).bfloat16()
+    aux = torch.randn(M, N, device=gpu).bfloat16()
+    dx = C.linear_dgrad(dy2, wt, aux)
+    assert rel_err(dx, (dy2.float() @ wt.float()) * (aux.float() > 0)) < 1e-2
+
+
 def test_linear_identity_asymmetric(gpu):
     """A = I with an asymmetric B catches a transposed C write."""
     C = OF._C()

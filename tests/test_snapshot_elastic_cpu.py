@@ -76,8 +76,8 @@ def test_rewire_survives_worker_failure_in_process(tmp_path):
                                 str(tmp_path / "s.pt")], env=env)
     assert rc == 0, out
     assert "[fault-injector] rank 1 step 40" in out and "peer failure" in out, out[-3000:]
-    pids0 = re.findall(r"\[rewire\] round 0: rank 0 of 2 \(pid (\d+)\)", out)
-    pids1 = re.findall(r"\[rewire\] round 1: rank 0 of \d \(pid (\d+)\)", out)
+    pids0 = re.findall(r"\[rewire\] round 0: rank 0 of 2 \(pid (\d+)[,)]", out)
+    pids1 = re.findall(r"\[rewire\] round 1: rank 0 of \d \(pid (\d+)[,)]", out)
     assert pids0 and pids1 and pids0 == pids1, out[-3000:]  # rank 0 survived in-process
     fin = re.findall(r"\[rewire\] finished 3 epochs in round (\d+)", out)
     assert len(fin) == 2 and set(fin) == {"1"}, out[-3000:]
