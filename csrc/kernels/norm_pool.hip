@@ -585,6 +585,8 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
     // from the rounded values; the pivot (row 0) is recomputed from the slabs by every block
     const long zs = static_cast<long>(P) * C;
     slab_row8(slabs, zs, splits, c0, piv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) piv[j] = bf2f(f2bf(piv[j]));  // the ROUNDED row 0, as the finalize uses it
     for (int r = blockIdx.x * rpb + tr; r < r1; r += kBnRows) {
       float v[8];
       slab_row8(slabs, zs, splits, static_cast<long>(r) * C + c0, v);

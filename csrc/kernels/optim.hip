@@ -53,8 +53,21 @@ __device__ __forceinline__ void update(const Hyper& h, float& p, float g, float&
   }
 }
 
+// 16-B state accesses; NT: non-temporal (streaming) loads and stores -- every state byte is touched once per
+// step, so keeping it in L2 / MALL only evicts the GEMMs' operands (A/B: PDE_OPTIM_NT=0)
+template <bool NT>
+__device__ __forceinline__ f32x4 ld4(const float* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  else return *reinterpret_cast<const f32x4*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, const f32x4& v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+  else *reinterpret_cast<f32x4*>(p) = v;
+}
+
 // One chunk's state for one thread: kGroups x 16 B of every state tensor, loaded before any math.
-template <int MODE>
+template <int MODE, bool NT>
 struct ChunkRegs {
   float p[kGroups][4], g[kGroups][4], m[kGroups][4], v[kGroups][4];
   int e0[kGroups], cnt[kGroups];
@@ -71,18 +84,18 @@ struct ChunkRegs {
 #pragma unroll
       for (int k = 0; k < 4; ++k) p[u][k] = g[u][k] = m[u][k] = v[u][k] = 0.f;
       if (cnt[u] == 4 && te.vec) {
-        const f32x4 pv = *reinterpret_cast<const f32x4*>(te.param + e0[u]);
+        const f32x4 pv = ld4<NT>(te.param + e0[u]);
         p[u][0] = pv[0]; p[u][1] = pv[1]; p[u][2] = pv[2]; p[u][3] = pv[3];
         if (te.grad) {
-          const f32x4 gv = *reinterpret_cast<const f32x4*>(te.grad + e0[u]);
+          const f32x4 gv = ld4<NT>(te.grad + e0[u]);
           g[u][0] = gv[0]; g[u][1] = gv[1]; g[u][2] = gv[2]; g[u][3] = gv[3];
         }
         if (use_m) {
-          const f32x4 mv = *reinterpret_cast<const f32x4*>(te.exp_avg + e0[u]);
+          const f32x4 mv = ld4<NT>(te.exp_avg + e0[u]);
           m[u][0] = mv[0]; m[u][1] = mv[1]; m[u][2] = mv[2]; m[u][3] = mv[3];
         }
         if (MODE != 0) {
-          const f32x4 vv = *reinterpret_cast<const f32x4*>(te.exp_avg_sq + e0[u]);
+          const f32x4 vv = ld4<NT>(te.exp_avg_sq + e0[u]);
           v[u][0] = vv[0]; v[u][1] = vv[1]; v[u][2] = vv[2]; v[u][3] = vv[3];
         }
       } else {
@@ -108,9 +121,9 @@ struct ChunkRegs {
       for (int k = 0; k < 4; ++k) update<MODE>(h, p[u][k], g[u][k], m[u][k], v[u][k]);
       const int i = e0[u];
       if (cnt[u] == 4 && te.vec) {
-        *reinterpret_cast<f32x4*>(te.param + i) = f32x4{p[u][0], p[u][1], p[u][2], p[u][3]};
-        if (use_m) *reinterpret_cast<f32x4*>(te.exp_avg + i) = f32x4{m[u][0], m[u][1], m[u][2], m[u][3]};
-        if (MODE != 0) *reinterpret_cast<f32x4*>(te.exp_avg_sq + i) = f32x4{v[u][0], v[u][1], v[u][2], v[u][3]};
+        st4<NT>(te.param + i, f32x4{p[u][0], p[u][1], p[u][2], p[u][3]});
+        if (use_m) st4<NT>(te.exp_avg + i, f32x4{m[u][0], m[u][1], m[u][2], m[u][3]});
+        if (MODE != 0) st4<NT>(te.exp_avg_sq + i, f32x4{v[u][0], v[u][1], v[u][2], v[u][3]});
         if (te.bf16_copy)
           *reinterpret_cast<u16x4*>(te.bf16_copy + i) = u16x4{f2bf(p[u][0]), f2bf(p[u][1]), f2bf(p[u][2]), f2bf(p[u][3])};
       } else {
@@ -128,7 +141,7 @@ struct ChunkRegs {
   }
 };
 
-template <int MODE>
+template <int MODE, bool NT>
 __global__ __launch_bounds__(kThreads) void k_optim(const OptimEntry* __restrict__ tab,
                                                     const OptimChunk* __restrict__ chunks, int nchunks,
                                                     const float* __restrict__ hp, int* __restrict__ step_ptr) {
@@ -149,7 +162,7 @@ __global__ __launch_bounds__(kThreads) void k_optim(const OptimEntry* __restrict
 
   // Grid-stride over chunks, software-pipelined: the next chunk's loads are issued before the current
   // chunk's math and stores, so every block keeps a chunk of loads in flight while it writes.
-  ChunkRegs<MODE> cur, nxt;
+  ChunkRegs<MODE, NT> cur, nxt;
   int c = blockIdx.x;
   if (c < nchunks) cur.load(tab, chunks[c], use_m);
   for (; c < nchunks; c += gridDim.x) {
@@ -180,13 +193,23 @@ hipError_t multi_tensor_optim(int mode, const OptimEntry* dev_table, const Optim
   if (nchunks <= 0) return hipSuccess;
   // ~3 blocks per CU, each walking several chunks with the next one's loads in flight (pipelined loop)
   static const int kMaxBlocks = std::getenv("PDE_OPTIM_BLOCKS") ? std::atoi(std::getenv("PDE_OPTIM_BLOCKS")) : 768;
+  static const bool nt = !(std::getenv("PDE_OPTIM_NT") && std::getenv("PDE_OPTIM_NT")[0] == '0');
   dim3 grid(static_cast<unsigned>(nchunks < kMaxBlocks ? nchunks : kMaxBlocks));
-  if (mode == 0)
-    hipLaunchKernelGGL(k_optim<0>, grid, dim3(kThreads), 0, s, dev_table, dev_chunks, nchunks, dev_hparams, dev_step);
-  else if (mode == 1)
-    hipLaunchKernelGGL(k_optim<1>, grid, dim3(kThreads), 0, s, dev_table, dev_chunks, nchunks, dev_hparams, dev_step);
-  else
-    hipLaunchKernelGGL(k_optim<2>, grid, dim3(kThreads), 0, s, dev_table, dev_chunks, nchunks, dev_hparams, dev_step);
+#define PDE_OPT(M)                                                                                            \
+  if (nt)                                                                                                     \
+    hipLaunchKernelGGL((k_optim<M, true>), grid, dim3(kThreads), 0, s, dev_table, dev_chunks, nchunks,       \
+                       dev_hparams, dev_step);                                                                \
+  else                                                                                                        \
+    hipLaunchKernelGGL((k_optim<M, false>), grid, dim3(kThreads), 0, s, dev_table, dev_chunks, nchunks,      \
+                       dev_hparams, dev_step);
+  if (mode == 0) {
+    PDE_OPT(0)
+  } else if (mode == 1) {
+    PDE_OPT(1)
+  } else {
+    PDE_OPT(2)
+  }
+#undef PDE_OPT
   return hipGetLastError();
 }
 

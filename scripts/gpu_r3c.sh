@@ -15,6 +15,7 @@ run() {  # name, bench args...
   python3 scripts/graph_kernel_table.py "$f" --title "$name: hipGraph replay kernel trace" > gpurun_out/tl_$name.md
   head -14 gpurun_out/tl_$name.md
 }
+run mlp --model mlp --steps 40 --warmup 10 && \
 run resnet50 --model resnet50 --steps 20 --warmup 10 && \
 run stage1_m8 --model resnet50_stage --stage 1 --batch 8 --steps 30 --warmup 10 && \
 run stage2_m8 --model resnet50_stage --stage 2 --batch 8 --steps 30 --warmup 10

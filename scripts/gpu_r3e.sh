@@ -12,6 +12,10 @@ for sk in 1 0; do
   PDE_GEMM_SKINNY=$sk timeout -k 10 200 python bench.py --model mlp --steps 50 --warmup 10 > gpurun_out/r3e_mlp$sk.log 2>&1 || { tail -5 gpurun_out/r3e_mlp$sk.log; exit 1; }
   echo "skinny=$sk $(tail -1 gpurun_out/r3e_mlp$sk.log | cut -c1-260)"
 done
+for cfg in "PDE_OPTIM_NT=0" "PDE_OPTIM_BLOCKS=2048" "PDE_OPTIM_NT=0 PDE_OPTIM_BLOCKS=2048"; do
+  env $cfg timeout -k 10 200 python bench.py --model mlp --steps 50 --warmup 10 > gpurun_out/r3e_mlpopt.log 2>&1 || { tail -5 gpurun_out/r3e_mlpopt.log; exit 1; }
+  echo "[$cfg] $(tail -1 gpurun_out/r3e_mlpopt.log | cut -c1-200)"
+done
 for d in 1 0; do
   PDE_CONV_BN_DEFER=$d timeout -k 10 300 python -u -m pytest tests/test_models_gpu.py -x -q --timeout 200 \
     --timeout-method thread -k "resnet_blocks_backward" > gpurun_out/r3e_defer$d.log 2>&1
