@@ -157,6 +157,20 @@ struct DeferredReduce {
   Tensor ws;
 };
 std::vector<DeferredReduce> g_deferred;
+size_t g_deferred_bytes = 0;
+int gemm_flush_deferred();
+
+// Peak-memory bound for the deferred slabs: once the pending workspaces pass this many bytes (default
+// 1 GiB, PDE_DEFER_CAP_MB) the list is flushed early, so a deep network's backward keeps O(cap) of slabs
+// alive rather than one workspace per layer.  A full launch's worth of jobs flushes too.
+size_t deferred_cap_bytes() {
+  static const size_t cap = [] {
+    const char* e = std::getenv("PDE_DEFER_CAP_MB");
+    long mb = e ? std::atol(e) : 1024;
+    return static_cast<size_t>(mb > 0 ? mb : 1024) << 20;
+  }();
+  return cap;
+}
 
 // Launch what was collected (2 GEMMs: one paired launch; fewer: ordinary launches).  abort=true drops it.
 // defer=true: the second GEMM's slab reduction is deferred to gemm_flush_deferred (returns true if it was).
@@ -175,6 +189,9 @@ bool gemm_pair_end(bool abort, bool defer) {
       j.M = a.M; j.N = a.N; j.splits = sp1; j.epi = a.epi;
       j.oihw_ci = a.oihw_ci; j.oihw_rs = a.oihw_rs; j.oihw_cp = a.oihw_cp; j.bias_col = a.bias_col;
       g_deferred.push_back({j, q[1].ws});
+      g_deferred_bytes += q[1].ws.nbytes();
+      if (g_deferred_bytes > deferred_cap_bytes() || static_cast<int>(g_deferred.size()) >= pde::kMaxReduceJobs)
+        gemm_flush_deferred();
       return true;
     }
   } else {
@@ -187,6 +204,7 @@ bool gemm_pair_end(bool abort, bool defer) {
 int gemm_flush_deferred() {
   std::vector<DeferredReduce> d;
   d.swap(g_deferred);
+  g_deferred_bytes = 0;
   if (d.empty()) return 0;
   std::vector<pde::ReduceJob> jobs;
   jobs.reserve(d.size());

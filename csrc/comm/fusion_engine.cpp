@@ -5,6 +5,8 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <sstream>
 
@@ -57,6 +59,8 @@ FusionEngine::FusionEngine(int rank, int size, int64_t fusion_bytes, const std::
                            double cycle_ms)
     : rank_(rank), size_(size), fusion_bytes_(fusion_bytes), cycle_ms_(cycle_ms),
       t0_(std::chrono::steady_clock::now()) {
+  if (const char* e = std::getenv("PDE_HVD_IDLE_MS")) idle_ms_ = std::max(0.05, std::atof(e));
+  if (const char* e = std::getenv("HOROVOD_STALL_CHECK_TIME_SECONDS")) stall_warn_s_ = std::max(1.0, std::atof(e));
   if (!timeline_path.empty()) {
     trace_.open(timeline_path);
     trace_ << "[\n";
@@ -98,7 +102,11 @@ void FusionEngine::set_py_backend(py::object allreduce_fn, py::object broadcast_
 
 void FusionEngine::set_control(c10::intrusive_ptr<c10d::ProcessGroup> pg) {
   TORCH_CHECK(pg->getSize() == size_ && pg->getRank() == rank_, "fusion engine: control group rank/size mismatch");
-  control_ = std::move(pg);
+  {
+    std::lock_guard<std::mutex> g(mu_);  // the worker reads control_ under mu_ to decide lockstep cycling
+    control_ = std::move(pg);
+  }
+  cv_.notify_all();
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -389,13 +397,20 @@ void FusionEngine::loop() {
     {
       std::unique_lock<std::mutex> lk(mu_);
       auto has_work = [&] { return stop_requested_ || !unannounced_.empty() || !announced_.empty(); };
+      // Multi-rank engines cycle in lockstep whether or not this rank has work: a rank that announced a
+      // tensor blocks in the control-plane all-gather until every peer joins the cycle, so an idle peer
+      // (running eval, writing a checkpoint) must keep taking part -- Horovod's background loop does the
+      // same.  Idle cycles back off to idle_ms_ so an idle job costs one small all-gather per few ms.
+      const bool lockstep = size_ > 1 && control_ && error_.empty();
       if (!has_work()) {
-        if (inflight_.empty())
+        if (lockstep)
+          cv_.wait_for(lk, std::chrono::microseconds(static_cast<int64_t>(idle_ms_ * 1e3)), has_work);
+        else if (inflight_.empty())
           cv_.wait(lk, has_work);
         else
           cv_.wait_for(lk, std::chrono::milliseconds(5), has_work);
       }
-      if (!has_work()) {
+      if (!has_work() && !lockstep) {
         lk.unlock();
         check_inflight();
         continue;
@@ -407,7 +422,12 @@ void FusionEngine::loop() {
       }
     }
     // coalesce a burst of enqueues (backward hooks) into one cycle, as Horovod's cycle time does
-    if (cycle_ms_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(static_cast<int64_t>(cycle_ms_ * 1e3)));
+    bool local_work;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      local_work = !unannounced_.empty();
+    }
+    if (local_work && cycle_ms_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(static_cast<int64_t>(cycle_ms_ * 1e3)));
     {
       std::lock_guard<std::mutex> g(mu_);
       while (!unannounced_.empty()) {
@@ -419,7 +439,12 @@ void FusionEngine::loop() {
     std::vector<Request> ready;
     bool stop = stop_local;
     const double tn = now();
-    if (size_ == 1 || !control_) {
+    bool have_control;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      have_control = static_cast<bool>(control_);
+    }
+    if (size_ == 1 || !have_control) {
       ready = std::move(announce);
     } else {
       try {
@@ -447,6 +472,7 @@ void FusionEngine::loop() {
 }
 
 void FusionEngine::negotiate(std::vector<Request>& announce, std::vector<Request>& ready, bool& stop) {
+  const double tn = now();
   // 1. this rank's message: stop flag + (name, signature) records, in local enqueue order
   std::string msg(1, stop ? 'S' : '-');
   for (const auto& r : announce) {
@@ -501,6 +527,7 @@ void FusionEngine::negotiate(std::vector<Request>& announce, std::vector<Request
         e.signature = sig;
         e.count = 1;
         e.order = order_seq_++;
+        e.t_first = tn;
         table_.emplace(name, std::move(e));
       } else {
         if (it->second.signature != sig && it->second.error.empty())
@@ -511,8 +538,17 @@ void FusionEngine::negotiate(std::vector<Request>& announce, std::vector<Request
     }
   }
   std::vector<std::pair<int64_t, std::string>> complete;
-  for (const auto& kv : table_)
-    if (kv.second.count >= size_) complete.emplace_back(kv.second.order, kv.first);
+  for (auto& kv : table_) {
+    if (kv.second.count >= size_) {
+      complete.emplace_back(kv.second.order, kv.first);
+    } else if (!kv.second.warned && tn - kv.second.t_first > stall_warn_s_ * 1e6) {
+      // stall inspector: a tensor some ranks announced long ago and others never did is reported, not fatal
+      kv.second.warned = true;
+      if (rank_ == 0)
+        std::fprintf(stderr, "[hvd] stall: tensor '%s' announced by %d of %d ranks for over %.0f s\n", kv.first.c_str(),
+                     kv.second.count, size_, stall_warn_s_);
+    }
+  }
   std::sort(complete.begin(), complete.end());
   {
     std::lock_guard<std::mutex> g(mu_);

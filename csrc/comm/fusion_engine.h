@@ -88,6 +88,8 @@ struct NegEntry {
   int count = 0;
   int64_t order = 0;
   std::string error;
+  double t_first = 0;   // when the first rank announced it (stall inspector)
+  bool warned = false;  // stall warning printed once
 };
 
 class FusionEngine {
@@ -139,6 +141,8 @@ class FusionEngine {
   int rank_, size_;
   std::atomic<int64_t> fusion_bytes_;
   double cycle_ms_;
+  double idle_ms_ = 2.0;         // lockstep back-off between idle cycles (PDE_HVD_IDLE_MS)
+  double stall_warn_s_ = 60.0;   // stall inspector threshold (HOROVOD_STALL_CHECK_TIME_SECONDS)
   std::shared_ptr<RcclComm> comm_;
   c10::intrusive_ptr<c10d::ProcessGroup> control_;
   py::object py_allreduce_, py_broadcast_, py_allgather_;

@@ -30,7 +30,9 @@ from ..ops import functional as OF
 class CapturedStep:
     def __init__(self, step_fn, example_inputs, warmup: int = 3):
         self.step_fn = step_fn
-        self.static_inputs = [t.clone() for t in example_inputs]
+        # static inputs are leaves: an input that requires grad (a pipeline stage's activation) gets its
+        # gradient in .grad of the static buffer, not through a CloneBackward into the caller's tensor
+        self.static_inputs = [t.detach().clone().requires_grad_(t.requires_grad) for t in example_inputs]
         self.graph = None
         self.static_out = None
         self._warmup = warmup

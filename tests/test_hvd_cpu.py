@@ -134,6 +134,30 @@ def test_hvd_negotiation_world2():
     spawn(_negotiation_worker, 2)
 
 
+def _late_rank_worker(rank, world):
+    """A rank that announces a tensor long after its peer (eval, checkpoint on one rank) is a stall, not a
+    control-plane failure: the idle rank keeps joining the engine's negotiation cycles, so the announcing
+    rank's all-gather never waits out the (here 3 s) control-plane timeout."""
+    import time
+
+    os.environ["PDE_HVD_TIMEOUT"] = "3"
+    os.environ["HOROVOD_STALL_CHECK_TIME_SECONDS"] = "1"
+    from pytorch_distributed_examples_amd import hvd
+
+    hvd.init(device="cpu")
+    t = torch.full((8,), float(rank + 1))
+    if rank == 1:
+        time.sleep(5.0)  # longer than the control-plane timeout
+    hvd.allreduce_(t, name="late", op=hvd.Sum)
+    assert torch.allclose(t, torch.full((8,), 3.0))
+    assert torch.allclose(hvd.allreduce(torch.ones(2), name="after", op=hvd.Sum), torch.full((2,), 2.0))
+    hvd.shutdown()
+
+
+def test_hvd_late_rank_is_not_fatal_world2():
+    spawn(_late_rank_worker, 2)
+
+
 def _bpps_worker(rank, world):
     """backward_passes_per_step=2 with a step() after ONE pass (end of an epoch): the early reduction resets
     the pass counter, so the next window again accumulates 2 local passes before reducing."""
