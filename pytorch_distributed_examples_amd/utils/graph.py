@@ -54,9 +54,10 @@ class CapturedStep:
         return self
 
     def __call__(self, *inputs):
-        for dst, src in zip(self.static_inputs, inputs):
-            if dst.data_ptr() != src.data_ptr():
-                dst.copy_(src, non_blocking=True)
+        with torch.no_grad():  # (a static input may be a leaf that requires grad)
+            for dst, src in zip(self.static_inputs, inputs):
+                if dst.data_ptr() != src.data_ptr():
+                    dst.copy_(src, non_blocking=True)
         self.graph.replay()
         return self.static_out
 
