@@ -749,15 +749,19 @@ void optim_step(const Tensor& table, const Tensor& chunks, int64_t nchunks, int 
 // Returns y, save_mean, save_invstd, scale_shift ([2C] fp32: y = relu?(x*scale + shift + res)).
 std::vector<Tensor> bn_fwd(const Tensor& x, const optional<Tensor>& gamma, const optional<Tensor>& beta,
                            const optional<Tensor>& running_mean, const optional<Tensor>& running_var, double eps,
-                           double momentum, const optional<Tensor>& res, bool relu) {
+                           double momentum, const optional<Tensor>& res, bool relu, int64_t groups) {
   CHECK_IN(x); CHECK_BF16(x);
   const int C = x.size(-1);
   const int P = x.numel() / C;
+  const int G = static_cast<int>(groups);
   TORCH_CHECK(C % 8 == 0, "bn_fwd: C must be a multiple of 8");
+  TORCH_CHECK(G >= 1 && x.size(0) % G == 0, "bn_fwd: batch ", x.size(0), " is not a multiple of groups ", G);
   auto fo = x.options().dtype(at::kFloat);
   Tensor y = at::empty_like(x);
-  Tensor mean = at::empty({C}, fo), invstd = at::empty({C}, fo), ss = at::empty({2 * C}, fo);
-  Tensor ws = at::empty({static_cast<long>(pde::bn_workspace_blocks(P, C)) * 2 * C}, fo);
+  // grouped: per-group statistics [G][C], scale/shift [G][2C] (groups = micro-batches of one launch)
+  Tensor mean = at::empty({G * C}, fo), invstd = at::empty({G * C}, fo), ss = at::empty({G * 2 * C}, fo);
+  Tensor ws = at::empty({static_cast<long>(pde::bn_workspace_blocks(P, C, G)) * 2 * C}, fo);
+  Tensor gs = G > 1 ? at::empty({G * 2 * C}, fo) : Tensor();
   resolve_pending(res);
   PendingConv pc{};
   {
@@ -773,7 +777,7 @@ std::vector<Tensor> bn_fwd(const Tensor& x, const optional<Tensor>& gamma, const
                           static_cast<float>(momentum), f32(running_mean), f32(running_var), mean.data_ptr<float>(),
                           invstd.data_ptr<float>(), ss.data_ptr<float>(), ws.data_ptr<float>(), cu16(res), relu,
                           u16(y), cur_stream(), pc.ws.defined() ? pc.ws.data_ptr<float>() : nullptr,
-                          pc.ws.defined() ? pc.splits : 1),
+                          pc.ws.defined() ? pc.splits : 1, G, G > 1 ? gs.data_ptr<float>() : nullptr),
         "bn_fwd");
   return {y, mean, invstd, ss};
 }
@@ -796,25 +800,29 @@ Tensor bn_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, const
 std::vector<Tensor> bn_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const Tensor& mean,
                            const Tensor& invstd, const optional<Tensor>& gamma, bool relu, bool want_dres,
                            const optional<Tensor>& dg_out, const optional<Tensor>& db_out,
-                           const optional<Tensor>& scale_shift) {
+                           const optional<Tensor>& scale_shift, int64_t groups) {
   CHECK_IN(dy); CHECK_IN(x); CHECK_IN(y); CHECK_BF16(dy);
   resolve_pending(x);
   resolve_pending(y);
   const int C = x.size(-1);
   const int P = x.numel() / C;
+  const int G = static_cast<int>(groups);
+  TORCH_CHECK(G >= 1 && x.size(0) % G == 0 && mean.numel() == static_cast<long>(G) * C,
+              "bn_bwd: groups / statistics shape mismatch");
   auto fo = x.options().dtype(at::kFloat);
   Tensor dx = at::empty_like(x);
   const bool direct = dg_out.has_value() && dg_out->defined() && db_out.has_value() && db_out->defined();
   Tensor dg = direct ? grad_sink(dg_out, {C}, x) : at::empty({C}, fo);
   Tensor db = direct ? grad_sink(db_out, {C}, x) : at::empty({C}, fo);
-  Tensor coef = at::empty({3 * C}, fo);
-  Tensor ws = at::empty({static_cast<long>(pde::bn_workspace_blocks(P, C)) * 2 * C}, fo);
+  Tensor coef = at::empty({G * 3 * C}, fo);
+  Tensor ws = at::empty({static_cast<long>(pde::bn_workspace_blocks(P, C, G)) * 2 * C}, fo);
+  Tensor gs = G > 1 ? at::empty({G * 2 * C}, fo) : Tensor();
   Tensor dres;
   if (want_dres) dres = at::empty_like(x);
   check(pde::bn_bwd(u16(dy), u16(x), u16(y), mean.data_ptr<float>(), invstd.data_ptr<float>(), cf32(gamma), P, C,
                     relu, dg.data_ptr<float>(), db.data_ptr<float>(), direct ? 1 : 0, ws.data_ptr<float>(),
                     coef.data_ptr<float>(), u16(dx), want_dres ? u16(dres) : nullptr, cur_stream(),
-                    want_dres ? nullptr : cf32(scale_shift)),
+                    want_dres ? nullptr : cf32(scale_shift), G, G > 1 ? gs.data_ptr<float>() : nullptr),
         "bn_bwd");
   return {dx, dg, db, dres};
 }
@@ -1048,13 +1056,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mse_bwd", &mse_bwd);
   m.def("optim_table", &optim_table);
   m.def("optim_step", &optim_step);
-  m.def("bn_fwd", &bn_fwd);
+  m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
+        py::arg("running_var"), py::arg("eps"), py::arg("momentum"), py::arg("res"), py::arg("relu"),
+        py::arg("groups") = 1);
   // 1 if a one-launch BatchNorm wait timed out since the last reset (synchronises the device)
   m.def("bn_error", [](bool reset) { return pde::bn_error(reset ? 1 : 0); }, py::arg("reset") = true);
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("mean"), py::arg("invstd"),
         py::arg("gamma"), py::arg("relu"), py::arg("want_dres"), py::arg("dg_out") = py::none(),
-        py::arg("db_out") = py::none(), py::arg("scale_shift") = py::none());
+        py::arg("db_out") = py::none(), py::arg("scale_shift") = py::none(), py::arg("groups") = 1);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);

@@ -170,14 +170,18 @@ hipError_t multi_tensor_optim(int mode, const OptimEntry* dev_table, const Optim
 // ---------------------------------------------------------------------------------------------
 // BatchNorm / pooling / dropout / EmbeddingBag (norm_pool.hip).  Activations NHWC bf16, [P = N*H*W][C].
 // ---------------------------------------------------------------------------------------------
-int bn_workspace_blocks(int P, int C);  // ws needs bn_workspace_blocks * 2 * C floats
+// ws needs bn_workspace_blocks * 2 * C floats.  groups > 1: P rows = `groups` equal micro-batches, each
+// normalised with its own statistics (mean / invstd [groups][C], scale_shift [groups][2C], coef [groups][3C]);
+// gscratch: 2 * groups * C floats.
+int bn_workspace_blocks(int P, int C, int groups = 1);
 // slabs != nullptr (splits > 1): x is the UNREDUCED output of a split-K conv GEMM (GemmArgs::splits_out):
 // the BatchNorm sums the fp32 slabs [splits][P][C] in z order, rounds to bf16, WRITES x and normalizes it --
 // the GEMM's separate slab-reduction launch is gone.
 hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, const float* beta, float eps,
                         float momentum, float* running_mean, float* running_var, float* save_mean,
                         float* save_invstd, float* scale_shift, float* ws, const uint16_t* res, int relu,
-                        uint16_t* y, hipStream_t s, const float* slabs = nullptr, int splits = 1);
+                        uint16_t* y, hipStream_t s, const float* slabs = nullptr, int splits = 1, int groups = 1,
+                        float* gscratch = nullptr);
 // 1 when a one-launch BatchNorm wait timed out (a block of the grid was never resident); reset clears it
 int bn_error(int reset);
 hipError_t bn_apply(const uint16_t* x, int P, int C, const float* scale, const float* shift, const uint16_t* res,
@@ -187,7 +191,8 @@ hipError_t bn_apply(const uint16_t* x, int P, int C, const float* scale, const f
 // recomputed from x (y is not read by the one-launch kernel)
 hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
                   const float* gamma, int P, int C, int relu, float* dgamma, float* dbeta, int accum_params, float* ws,
-                  float* coef, uint16_t* dx, uint16_t* dres, hipStream_t s, const float* ss = nullptr);
+                  float* coef, uint16_t* dx, uint16_t* dres, hipStream_t s, const float* ss = nullptr, int groups = 1,
+                  float* gscratch = nullptr);
 hipError_t maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
                        int k, int st, int p, int relu, hipStream_t s);
 hipError_t maxpool_bwd(const uint16_t* dy, const uint16_t* y, const uint8_t* idx, uint16_t* dx, int N, int H, int W,

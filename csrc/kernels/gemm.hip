@@ -1348,7 +1348,14 @@ int kind_code_of(const GemmArgs& a) { return kind_code(is_kc(a.a), is_kc(a.b), a
 // (so the pair computes exactly what two separate launches would).
 bool pair_member_plan(const GemmArgs& a, int& tm, int& tn, int& kps, int& split, int& av, int& bv) {
   if (a.M <= 0 || a.N <= 0 || generic_only()) return false;
-  if (choose_tiles(a, split) != kTile64) return false;
+  if (choose_tiles(a, split) != kTile64) {
+    // a narrow (<= 32 rows or columns), short-K problem the lone launch would give a 32-wide tile: in a pair
+    // it takes 64x64 tiles without split -- half-empty tiles, but one launch fewer (the MLP's 10-wide last
+    // layer: its weight gradient joins the dgrad launch)
+    const long t64 = static_cast<long>(ceil_div(a.M, 64)) * ceil_div(a.N, 64);
+    if (!((a.M <= 32 || a.N <= 32) && t64 <= 64 && a.K <= 1024)) return false;
+    split = 1;
+  }
   const bool akc = is_kc(a.a), bkc = is_kc(a.b);
   if (!fast_ok(a, a.a, akc, a.M) || !fast_ok(a, a.b, bkc, a.N)) return false;
   tm = ceil_div(a.M, 64);

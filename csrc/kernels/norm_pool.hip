@@ -561,13 +561,37 @@ __device__ __forceinline__ void slab_row8(const float* __restrict__ slabs, long 
   }
 }
 
+// Grouped BatchNorm (blockIdx.z = group: the rows of G equal, contiguous micro-batches normalised with
+// their OWN statistics in one launch -- a pipeline stage running several micro-batches per launch keeps the
+// reference's per-micro-batch BatchNorm semantics, quirk Q17).  Quantities that combine the groups IN ORDER
+// (running statistics: G sequential momentum updates; dgamma / dbeta: sum over groups) are finished by the
+// last group's finalizer of each channel group: finalizer stores -> vmcnt(0) -> barrier -> lane-0 agent
+// release + ticket; the last arrival acquires, resets the ticket and combines.  Returns true on that block.
+__device__ __forceinline__ bool bn_group_last(int* gticket, int G, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const bool last = __hip_atomic_fetch_add(gticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(gticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    }
+    *s_flag = last ? 1 : 0;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
 __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
     uint16_t* x, int P, int C, int rpb, float* __restrict__ ws, int* __restrict__ tickets,
     uint32_t* __restrict__ flags, int* __restrict__ err, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float momentum, float* __restrict__ running_mean,
     float* __restrict__ running_var, float* __restrict__ save_mean, float* __restrict__ save_invstd,
     float* __restrict__ scale, float* __restrict__ shift, const uint16_t* __restrict__ res, int relu,
-    uint16_t* __restrict__ y, const float* __restrict__ slabs, int splits) {
+    uint16_t* __restrict__ y, const float* __restrict__ slabs, int splits, long slab_zs,
+    float* __restrict__ gvar, int* __restrict__ gtickets) {
   __shared__ float red[2][kBnRows][kBnCG + 1];
   __shared__ float tot1[kBnCG], tot2[kBnCG];
   __shared__ int s_last;
@@ -575,6 +599,23 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
   const int tid = threadIdx.x, tv = tid & 7, tr = tid >> 3;
   const int c0 = blockIdx.y * kBnCG + tv * 8;
   const bool cok = c0 < C;
+  // group z: rows [z P, (z + 1) P) of x / res / y / slabs, its own partials, tickets, flags and statistics
+  const int gz = blockIdx.z, G = gridDim.z;
+  const float* save_mean_all = save_mean;
+  {
+    const long xo = static_cast<long>(gz) * P * C;
+    x += xo;
+    y += xo;
+    if (res) res += xo;
+    if (slabs) slabs += xo;
+    ws += static_cast<long>(gz) * gridDim.x * 2 * C;
+    tickets += gz * gridDim.y;
+    flags += gz * gridDim.y;
+    save_mean += gz * C;
+    save_invstd += gz * C;
+    scale += gz * 2 * C;
+    shift += gz * 2 * C;
+  }
   bn_gen_start(flags + blockIdx.y, &s_gen);
   const int r1 = min(P, (blockIdx.x + 1) * rpb);
   float s1[8], s2[8], piv[8];
@@ -583,7 +624,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
   if (cok && slabs != nullptr) {
     // x = bf16(sum_z slab_z) in z order (== the GEMM's own reduction), written here, its statistics taken
     // from the rounded values; the pivot (row 0) is recomputed from the slabs by every block
-    const long zs = static_cast<long>(P) * C;
+    const long zs = slab_zs;
     slab_row8(slabs, zs, splits, c0, piv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) piv[j] = bf2f(f2bf(piv[j]));  // the ROUNDED row 0, as the finalize uses it
@@ -631,7 +672,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
       float pv;
       if (slabs != nullptr) {  // the pivot row of another block may not be visible yet: from the slabs
         float a = slabs[c];
-        for (int z = 1; z < splits; ++z) a += slabs[static_cast<long>(z) * P * C + c];
+        for (int z = 1; z < splits; ++z) a += slabs[z * slab_zs + c];
         pv = bf2f(f2bf(a));
       } else {
         pv = bf2f(x[c]);
@@ -646,12 +687,29 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
       shift[c] = b - mean * g * invstd;
       if (running_mean) {
         const float unbiased = P > 1 ? static_cast<float>(var * n / (n - 1.0)) : static_cast<float>(var);
-        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
-        running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+        if (G == 1) {
+          running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+          running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+        } else {
+          gvar[gz * C + c] = unbiased;
+        }
       }
     }
     bn_publish(flags + blockIdx.y, s_gen);
     __syncthreads();
+    // grouped: the last group's finalizer applies the G momentum updates in micro-batch order
+    if (G > 1 && running_mean != nullptr && bn_group_last(gtickets + blockIdx.y, G, &s_last)) {
+      if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
+        const int c = blockIdx.y * kBnCG + tid;
+        float rm = running_mean[c], rv = running_var[c];
+        for (int g = 0; g < G; ++g) {
+          rm = (1.f - momentum) * rm + momentum * save_mean_all[g * C + c];
+          rv = (1.f - momentum) * rv + momentum * gvar[g * C + c];
+        }
+        running_mean[c] = rm;
+        running_var[c] = rv;
+      }
+    }
   } else {
     bn_wait(flags + blockIdx.y, s_gen, err);
   }
@@ -726,7 +784,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
     float* __restrict__ ws, int* __restrict__ tickets, uint32_t* __restrict__ flags, int* __restrict__ err,
     const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta, int accum,
     float* __restrict__ coef, uint16_t* __restrict__ dx, uint16_t* __restrict__ dres,
-    const float* __restrict__ ss) {
+    const float* __restrict__ ss, float* __restrict__ gdgb, int* __restrict__ gtickets) {
   __shared__ float red[2][kBnRows][kBnCG + 1];
   __shared__ float tot1[kBnCG], tot2[kBnCG];
   __shared__ int s_last;
@@ -735,6 +793,22 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
   const int c0 = blockIdx.y * kBnCG + tv * 8;
   const bool cok = c0 < C;
   const bool from_x = relu && ss != nullptr;
+  const int gz = blockIdx.z, G = gridDim.z;  // group (see bn_group_last)
+  {
+    const long xo = static_cast<long>(gz) * P * C;
+    dy += xo;
+    x += xo;
+    if (y) y += xo;
+    dx += xo;
+    if (dres) dres += xo;
+    mean += gz * C;
+    invstd += gz * C;
+    if (ss) ss += gz * 2 * C;
+    ws += static_cast<long>(gz) * gridDim.x * 2 * C;
+    tickets += gz * gridDim.y;
+    flags += gz * gridDim.y;
+    coef += gz * 3 * C;
+  }
   bn_gen_start(flags + blockIdx.y, &s_gen);
   const int r0 = blockIdx.x * rpb + tr;
   const int r1 = min(P, (blockIdx.x + 1) * rpb);
@@ -809,8 +883,13 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
     if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
       const int c = blockIdx.y * kBnCG + tid;
       const float t1 = tot1[tid], t2 = tot2[tid];
-      if (dgamma) dgamma[c] = accum ? dgamma[c] + t2 : t2;
-      if (dbeta) dbeta[c] = accum ? dbeta[c] + t1 : t1;
+      if (G == 1) {
+        if (dgamma) dgamma[c] = accum ? dgamma[c] + t2 : t2;
+        if (dbeta) dbeta[c] = accum ? dbeta[c] + t1 : t1;
+      } else {
+        gdgb[gz * 2 * C + c] = t2;
+        gdgb[gz * 2 * C + C + c] = t1;
+      }
       const float a = (gamma ? gamma[c] : 1.f) * invstd[c];
       coef[c] = a;
       coef[C + c] = a * t1 / static_cast<float>(P);
@@ -818,6 +897,19 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
     }
     bn_publish(flags + blockIdx.y, s_gen);
     __syncthreads();
+    // grouped: dgamma / dbeta = sum over the groups in group order, by the last group's finalizer
+    if (G > 1 && bn_group_last(gtickets + blockIdx.y, G, &s_last)) {
+      if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
+        const int c = blockIdx.y * kBnCG + tid;
+        float t2 = 0.f, t1 = 0.f;
+        for (int g = 0; g < G; ++g) {
+          t2 += gdgb[g * 2 * C + c];
+          t1 += gdgb[g * 2 * C + C + c];
+        }
+        if (dgamma) dgamma[c] = accum ? dgamma[c] + t2 : t2;
+        if (dbeta) dbeta[c] = accum ? dbeta[c] + t1 : t1;
+      }
+    }
   } else {
     bn_wait(flags + blockIdx.y, s_gen, err);
   }
@@ -1191,12 +1283,12 @@ int bn_blocks(int P, int C, int& rows_per_block) {
 // made the finalizing tail 0.14 ms/step slower; 64 chunks measure level with the 3-pass form at 106 fewer
 // launches per step)
 // (the finalizing block reads chunks x 2 x 64 partials).
-int bn_fin_grid(int P, int C, int& rpb) {
+int bn_fin_grid(int P, int C, int& rpb, int groups = 1) {
   const int ncg = (C + kBnCG - 1) / kBnCG;
   static const int kChunks = std::getenv("PDE_BN_CHUNKS") ? std::atoi(std::getenv("PDE_BN_CHUNKS")) : 64;
   // r2m sweep at 512 threads per block: 256 blocks (one per CU, 8 waves) 3.83 -> 3.79 ms/step
   static const int kTarget = std::getenv("PDE_BN_BLOCKS") ? std::atoi(std::getenv("PDE_BN_BLOCKS")) : 256;
-  int nrb = std::max(1, std::min(kChunks, kTarget / ncg));
+  int nrb = std::max(1, std::min(kChunks, kTarget / (ncg * groups)));
   nrb = std::min(nrb, std::max(1, P / kBnRows));
   rpb = ceil_div(P, nrb);
   return ceil_div(P, rpb);
@@ -1262,34 +1354,50 @@ bool bn_one_launch(int blocks) {
 
 const long kBnApplyCap = std::getenv("PDE_BN_APPLY_CAP") ? std::atol(std::getenv("PDE_BN_APPLY_CAP")) : 2048;
 
-int bn_workspace_blocks(int P, int C) {
+int bn_workspace_blocks(int P, int C, int groups) {
   int rpb;
-  return std::max(bn_blocks(P, C, rpb), bn_fin_grid(P, C, rpb));
+  const int one = std::max(bn_blocks(P, C, rpb), bn_fin_grid(P, C, rpb));
+  if (groups <= 1 || P % groups != 0) return one;
+  const int Pg = P / groups;
+  return std::max({one, groups * bn_fin_grid(Pg, C, rpb, groups), bn_blocks(Pg, C, rpb), bn_fin_grid(Pg, C, rpb)});
 }
 
 hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, const float* beta, float eps,
                         float momentum, float* running_mean, float* running_var, float* save_mean,
                         float* save_invstd, float* scale_shift, float* ws, const uint16_t* res, int relu,
-                        uint16_t* y, hipStream_t s, const float* slabs, int splits) {
+                        uint16_t* y, hipStream_t s, const float* slabs, int splits, int groups, float* gscratch) {
   int rpb;
   const int ncg = ceil_div(C, kBnCG);
   int* err = nullptr;
-  const int nrb1 = bn_fin_grid(P, C, rpb);
+  if (groups < 1 || P % groups != 0) return hipErrorInvalidValue;
+  const int Pg = P / groups;  // rows per group (micro-batch)
+  const int nrb1 = bn_fin_grid(Pg, C, rpb, groups);
   if (splits <= 1) slabs = nullptr;
-  if (bn_one_launch(nrb1 * ncg) && bn_ticket_base(s, &err) != nullptr) {
-    int* tk = bn_tickets(ncg, s);
-    uint32_t* fl = bn_flags(ncg, s);  // generation flags of the channel groups
-    if (tk != nullptr && fl != nullptr) {
-      hipLaunchKernelGGL(k_bn_fwd_fused, dim3(nrb1, ncg), dim3(kBnThreads), 0, s, const_cast<uint16_t*>(x), P, C,
-                         rpb, ws, tk, fl, err,
-                         gamma, beta, eps, momentum, running_mean, running_var, save_mean, save_invstd, scale_shift,
-                         scale_shift + C, res, relu, y, slabs, splits);
+  if (bn_one_launch(nrb1 * ncg * groups) && bn_ticket_base(s, &err) != nullptr) {
+    int* tk = bn_tickets(ncg * groups, s);
+    uint32_t* fl = bn_flags(ncg * groups, s);  // generation flags of the (group, channel group)s
+    int* gt = groups > 1 ? bn_tickets(ncg, s) : nullptr;
+    if (tk != nullptr && fl != nullptr && (groups == 1 || (gt != nullptr && gscratch != nullptr))) {
+      hipLaunchKernelGGL(k_bn_fwd_fused, dim3(nrb1, ncg, groups), dim3(kBnThreads), 0, s, const_cast<uint16_t*>(x),
+                         Pg, C, rpb, ws, tk, fl, err, gamma, beta, eps, momentum, running_mean, running_var, save_mean,
+                         save_invstd, scale_shift, scale_shift + C, res, relu, y, slabs, splits,
+                         static_cast<long>(P) * C, gscratch, gt);
       return hipGetLastError();
     }
   }
   if (slabs != nullptr) {  // multi-launch BatchNorm: reduce the conv's slabs into x first
     const hipError_t e = gemm_reduce_slabs_bf16(const_cast<float*>(slabs), splits, P, C, const_cast<uint16_t*>(x), s);
     if (e != hipSuccess) return e;
+  }
+  if (groups > 1) {  // grouped, multi-launch: one BatchNorm per group in order (running stats sequential)
+    for (int g = 0; g < groups; ++g) {
+      const long xo = static_cast<long>(g) * Pg * C;
+      const hipError_t e = bn_fwd_train(x + xo, Pg, C, gamma, beta, eps, momentum, running_mean, running_var,
+                                        save_mean + g * C, save_invstd + g * C, scale_shift + 2 * g * C, ws,
+                                        res ? res + xo : nullptr, relu, y + xo, s, nullptr, 1, 1, nullptr);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
   }
   int* tk = bn_tickets(ncg, s);
   if (tk != nullptr) {
@@ -1330,24 +1438,39 @@ hipError_t bn_apply(const uint16_t* x, int P, int C, const float* scale, const f
 
 hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
                   const float* gamma, int P, int C, int relu, float* dgamma, float* dbeta, int accum_params, float* ws,
-                  float* coef, uint16_t* dx, uint16_t* dres, hipStream_t s, const float* ss) {
+                  float* coef, uint16_t* dx, uint16_t* dres, hipStream_t s, const float* ss, int groups,
+                  float* gscratch) {
   int rpb;
   const int ncg = ceil_div(C, kBnCG);
   int* err = nullptr;
-  const int nrb1 = bn_fin_grid(P, C, rpb);
-  if (bn_one_launch(nrb1 * ncg) && bn_ticket_base(s, &err) != nullptr) {
-    int* tk = bn_tickets(ncg, s);
-    uint32_t* fl = bn_flags(ncg, s);
-    if (tk != nullptr && fl != nullptr) {
+  if (groups < 1 || P % groups != 0) return hipErrorInvalidValue;
+  const int Pg = P / groups;
+  const int nrb1 = bn_fin_grid(Pg, C, rpb, groups);
+  if (bn_one_launch(nrb1 * ncg * groups) && bn_ticket_base(s, &err) != nullptr) {
+    int* tk = bn_tickets(ncg * groups, s);
+    uint32_t* fl = bn_flags(ncg * groups, s);
+    int* gt = groups > 1 ? bn_tickets(ncg, s) : nullptr;
+    if (tk != nullptr && fl != nullptr && (groups == 1 || (gt != nullptr && gscratch != nullptr))) {
+      const dim3 grid(nrb1, ncg, groups);
       // rows per thread of a chunk: small enough -> kept in registers for the apply pass
       if (ceil_div(rpb, kBnRows) <= 4)
-        hipLaunchKernelGGL(k_bn_bwd_fused<4>, dim3(nrb1, ncg), dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, P, C,
-                           rpb, relu, ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss);
+        hipLaunchKernelGGL(k_bn_bwd_fused<4>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
+                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt);
       else
-        hipLaunchKernelGGL(k_bn_bwd_fused<0>, dim3(nrb1, ncg), dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, P, C,
-                           rpb, relu, ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss);
+        hipLaunchKernelGGL(k_bn_bwd_fused<0>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
+                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt);
       return hipGetLastError();
     }
+  }
+  if (groups > 1) {  // grouped, multi-launch: group 0 writes / adds the parameter gradients, the rest add
+    for (int g = 0; g < groups; ++g) {
+      const long xo = static_cast<long>(g) * Pg * C;
+      const hipError_t e = bn_bwd(dy + xo, x + xo, y ? y + xo : nullptr, mean + g * C, invstd + g * C, gamma, Pg, C,
+                                  relu, dgamma, dbeta, g > 0 ? 1 : accum_params, ws, coef + 3 * g * C, dx + xo,
+                                  dres ? dres + xo : nullptr, s, ss ? ss + 2 * g * C : nullptr, 1, nullptr);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
   }
   int* tk = bn_tickets(ncg, s);
   if (tk != nullptr) {

@@ -134,11 +134,16 @@ class ResNetPipelineDP:
       micro-batch forwards/backwards, P2P sends/recvs, all-reduce, SGD -- records into ONE hipGraph);
     * ``split_size`` is the micro-batch size (reference quirk Q2), BatchNorm statistics are per micro-batch
       (Q17), each replica draws its own batch (seeded by pipeline index);
+    * ``mb_group`` micro-batches form one pipeline unit, run as one launch sequence with grouped BatchNorm
+      (per-micro-batch statistics, ``ops.functional.bn_groups``).  Default on the GPU: all of them (one unit
+      per step -- at m = 4..32 the stage kernels are latency-bound, so one m = 32 pass beats four pipelined
+      m = 8 passes: profiles/r3f_stage_bench.jsonl); ``PDE_PIPE_MB_GROUP`` / ``--mb-group`` override, 1 = the
+      reference's one-micro-batch units;
     * ``step()`` runs one full training step and returns the loss on the last stage (a zero elsewhere).
     """
 
     def __init__(self, ctx, batch: int = 32, split_size: int = 8, image: int = 128, schedule: str = "gpipe",
-                 lr: float = 0.05, tag: str = "hybrid", seed: int = 1234):
+                 lr: float = 0.05, tag: str = "hybrid", seed: int = 1234, mb_group: int | None = None):
         from ..data.synthetic import resnet_batch
         from ..models.resnet import ResNetShard1, ResNetShard2
         from ..ops.optim import FusedSGD
@@ -181,8 +186,18 @@ class ResNetPipelineDP:
             self.engine.ddp = self.ddp
         g = torch.Generator().manual_seed(seed + ctx.rank // self.stages)
         x, y = resnet_batch(batch, image, 1000, dev, g)
-        self.n_mb = batch // split_size
-        self.xs, self.ys = list(x.split(split_size)), list(y.split(split_size))
+        n_mb = batch // split_size
+        if mb_group is None:
+            env = os.environ.get("PDE_PIPE_MB_GROUP")
+            mb_group = int(env) if env else (n_mb if dev.type == "cuda" else 1)
+        mb_group = max(1, min(int(mb_group), n_mb))
+        while n_mb % mb_group:  # whole units only
+            mb_group -= 1
+        self.mb_group = mb_group
+        self.engine.bn_groups = mb_group
+        unit = split_size * mb_group
+        self.n_mb = n_mb // mb_group  # pipeline units per step
+        self.xs, self.ys = list(x.split(unit)), list(y.split(unit))
         self._zero = torch.zeros((), device=dev)
 
     @property
@@ -226,14 +241,15 @@ class ResNetPipelineDP:
 
 
 def run_resnet_hybrid(stages: int, dp: int, steps: int, warmup: int, batch: int, split_size: int,
-                      schedule: str = "gpipe", quiet: bool = False, image: int = 128, device: str | None = None):
+                      schedule: str = "gpipe", quiet: bool = False, image: int = 128, device: str | None = None,
+                      mb_group: int | None = None):
     from ..parallel import dist as pdist
 
     ctx = pdist.init_distributed(device=device)
     world = ctx.world_size
     assert world == stages * dp, f"world {world} != stages {stages} x dp {dp}"
     assert stages == 2, "ResNet-50 is split at layer2|layer3 (2 stages)"
-    pipe = ResNetPipelineDP(ctx, batch, split_size, image, schedule)
+    pipe = ResNetPipelineDP(ctx, batch, split_size, image, schedule, mb_group=mb_group)
     for _ in range(warmup):
         pipe.step()
     pdist.barrier(ctx)
@@ -267,6 +283,8 @@ def main(argv=None):
     ap.add_argument("--batch-size", type=int, default=32)
     ap.add_argument("--split-size", type=int, default=8)
     ap.add_argument("--schedule", default="gpipe", choices=["gpipe", "1f1b"])
+    ap.add_argument("--mb-group", type=int, default=None,
+                    help="micro-batches per pipeline unit (grouped BatchNorm); default: all on the GPU")
     ap.add_argument("--image", type=int, default=128)
     add_runtime_args(ap)
     args = ap.parse_args(argv)
@@ -277,7 +295,8 @@ def main(argv=None):
         world = int(os.environ.get("WORLD_SIZE", "1"))
         dp = args.dp or max(1, world // args.stages)
         run_resnet_hybrid(args.stages, dp, args.steps, args.warmup, args.batch_size, args.split_size,
-                          args.schedule, image=args.image, device="cpu" if args.device == "cpu" else None)
+                          args.schedule, image=args.image, device="cpu" if args.device == "cpu" else None,
+                          mb_group=args.mb_group)
         dist.destroy_process_group()
         return
     use_gpu = torch.cuda.is_available() and args.device != "cpu"

@@ -37,12 +37,13 @@ NUM_CLASSES = 1000
 class DistResNet50(RemotePipeline):
     """Same constructor/forward/parameter_rrefs surface as the reference's DistResNet50 (:142-184)."""
 
-    def __init__(self, split_size, workers, devices):
-        super().__init__(split_size, workers, [ResNetShard1, ResNetShard2], devices)
+    def __init__(self, split_size, workers, devices, mb_group=None):
+        # mb_group: micro-batches per pipeline unit with per-micro-batch (grouped) BatchNorm (RemotePipeline)
+        super().__init__(split_size, workers, [ResNetShard1, ResNetShard2], devices, mb_group=mb_group)
 
 
 def run_master(split_size, args, devices):
-    model = DistResNet50(split_size, ["worker1", "worker2"], devices)
+    model = DistResNet50(split_size, ["worker1", "worker2"], devices, mb_group=args.mb_group)
     loss_fn = nn.MSELoss()
     opt = DistributedOptimizer(optim.SGD, model.parameter_rrefs(), lr=0.05)
     one_hot_indices = torch.LongTensor(args.batch_size).random_(0, NUM_CLASSES).view(args.batch_size, 1)
@@ -101,6 +102,8 @@ def main(argv=None):
     ap.add_argument("--image-h", type=int, default=128)
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--mb-group", type=int, default=None,
+                    help="micro-batches per pipeline unit (grouped BatchNorm); default: all on GPUs, 1 on CPU")
     add_runtime_args(ap)
     args = ap.parse_args(argv)
     _cfg = rtconfig.apply(rtconfig.from_args(args))

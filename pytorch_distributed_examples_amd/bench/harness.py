@@ -74,6 +74,9 @@ def parse_args(argv=None):
     ap.add_argument("--batch", type=int, default=None, help="per-replica batch")
     ap.add_argument("--split-size", type=int, default=8, help="resnet50_pp: micro-batch size (reference: 4 or 8)")
     ap.add_argument("--schedule", default="gpipe", choices=["gpipe", "1f1b"], help="resnet50_pp schedule")
+    ap.add_argument("--mb-group", type=int, default=None,
+                    help="resnet50_pp: micro-batches per pipeline unit, run as one launch sequence with grouped "
+                         "(per-micro-batch) BatchNorm; default: all of them on the GPU (PDE_PIPE_MB_GROUP)")
     ap.add_argument("--image", type=int, default=None, help="override the image size (CPU plumbing tests)")
     ap.add_argument("--no-graph", action="store_true", help="run the step eagerly (no hipGraph capture)")
     ap.add_argument("--graph-steps", type=int, default=0,
@@ -208,6 +211,10 @@ def build_data_parallel(args, ctx, batch) -> Workload:
         def batch_fn(i):
             return batches[i % 2]
 
+    # resnet50_stage --mb-group G: the stage's batch is G micro-batches run as one unit (grouped BatchNorm)
+    bn_groups = (args.mb_group or 1) if args.model == "resnet50_stage" else 1
+    if batch % bn_groups:
+        raise SystemExit(f"--batch {batch} is not a multiple of --mb-group {bn_groups}")
     use_graph = not args.no_graph and on_gpu and (ctx.world_size == 1 or ctx.backend == "nccl")
     # GPU data plane for world > 1: our stream-ordered RCCL communicator (c10d's ProcessGroupNCCL aborts the
     # process when its work is captured into a hipGraph on ROCm -- parallel/rccl.py)
@@ -268,13 +275,13 @@ def build_data_parallel(args, ctx, batch) -> Workload:
         if x.requires_grad:
             x.grad = None  # a stage input: its gradient is produced fresh every step (sent upstream)
         if loss_fn is None:  # a pipeline stage without the loss: backward from the upstream gradient y
-            with t.phase("fwd"):
+            with t.phase("fwd"), OF.bn_groups(bn_groups):
                 out = ddp(x)
             with t.phase("bwd"):
                 out.backward(y)
             loss = None
         else:
-            with t.phase("fwd"):
+            with t.phase("fwd"), OF.bn_groups(bn_groups):
                 loss = loss_fn(ddp(x), y)
             with t.phase("bwd"):
                 loss.backward()
@@ -298,7 +305,7 @@ def build_data_parallel(args, ctx, batch) -> Workload:
         return one(x, y) if one is not None else train_step(x, y)
 
     routed = getattr(comm, "routed", None)
-    extra = {"stage": args.stage} if args.model == "resnet50_stage" else {}
+    extra = {"stage": args.stage, "mb_per_unit": bn_groups} if args.model == "resnet50_stage" else {}
     w = Workload(step, batch * ctx.world_size, f"dp{ctx.world_size}", **extra, hipgraph=one is not None,
                  fused_step=fused is not None or fmlp is not None, rccl_nranks=nranks,
                  steps_per_graph=group.steps if group is not None else (1 if one is not None else 0),
@@ -324,7 +331,8 @@ def build_pipeline(args, ctx, batch) -> Workload:
 
     on_gpu = ctx.device.type == "cuda"
     nranks = _data_plane_check(ctx, None)
-    pipe = ResNetPipelineDP(ctx, batch, args.split_size, args.image or 128, args.schedule, tag="bench")
+    pipe = ResNetPipelineDP(ctx, batch, args.split_size, args.image or 128, args.schedule, tag="bench",
+                            mb_group=args.mb_group)
     one = None
     if not args.no_graph and pipe.capturable:
         one, _ = _capture(pipe.step, [()], 1, ctx.rank)
@@ -334,7 +342,8 @@ def build_pipeline(args, ctx, batch) -> Workload:
 
     w = Workload(step, pipe.images_per_step, f"pp{pipe.stages}xdp{pipe.dp}", hipgraph=one is not None,
                  fused_step=False, rccl_nranks=nranks, steps_per_graph=1 if one is not None else 0,
-                 split_size=args.split_size, microbatches=pipe.n_mb, schedule=args.schedule)
+                 split_size=args.split_size, microbatches=batch // args.split_size, mb_per_unit=pipe.mb_group,
+                 pipeline_units=pipe.n_mb, schedule=args.schedule)
     w.loss_rank = pipe.stages - 1
     w.close = pipe.close
     w.check = pipe.check

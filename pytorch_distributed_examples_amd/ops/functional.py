@@ -17,7 +17,9 @@ small layout kernels and cached per (parameter version, optimiser generation).
 """
 from __future__ import annotations
 
+import contextlib
 import math
+import threading
 
 import torch
 import torch.nn.functional as F
@@ -460,13 +462,37 @@ def to_native_image(x: torch.Tensor) -> torch.Tensor:
 # ---------------------------------------------------------------------------------------------
 # BatchNorm2d (train: batch statistics; eval: running statistics), fused residual add + ReLU
 # ---------------------------------------------------------------------------------------------
+_BN_GROUPS = threading.local()
+
+
+@contextlib.contextmanager
+def bn_groups(groups: int):
+    """Training-mode BatchNorm inside this context normalises ``groups`` equal, contiguous slices of the
+    batch (micro-batches) with their OWN statistics, in one launch per layer; running statistics get the
+    ``groups`` momentum updates in slice order.  A pipeline stage runs several micro-batches per launch this
+    way and keeps the per-micro-batch BatchNorm semantics of the reference (``split_size``, quirk Q17):
+    identical results to ``groups`` separate forward passes, at the launch count of one."""
+    prev = getattr(_BN_GROUPS, "g", 1)
+    _BN_GROUPS.g = int(groups)
+    try:
+        yield
+    finally:
+        _BN_GROUPS.g = prev
+
+
+def current_bn_groups() -> int:
+    return getattr(_BN_GROUPS, "g", 1)
+
+
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, running_mean, running_var, residual, eps, momentum, relu, join=None):
+    def forward(ctx, x, gamma, beta, running_mean, running_var, residual, eps, momentum, relu, join=None,
+                groups=1):
         ctx.join = join
+        ctx.groups = groups
         y, mean, invstd, ss = _C().bn_fwd(x, gamma.detach() if gamma is not None else None,
                                           beta.detach() if beta is not None else None, running_mean,
-                                          running_var, eps, momentum, residual, relu)
+                                          running_var, eps, momentum, residual, relu, groups)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.beta = beta
@@ -483,21 +509,26 @@ class _BatchNormFn(torch.autograd.Function):
         dx, dg, db, dres = _C().bn_bwd(dy.contiguous(), x, y, mean, invstd,
                                        gamma.detach() if gamma is not None else None, ctx.relu, ctx.has_res,
                                        dg_sink if direct else None, db_sink if direct else None,
-                                       None if ctx.has_res else ss)
+                                       None if ctx.has_res else ss, ctx.groups)
         if direct:  # dgamma / dbeta were added into .grad by the finalize kernel
             dg = db = None
         if ctx.has_res and ctx.join is not None:  # the residual fork's conv adds it in its dgrad epilogue
             ctx.join.put(dres)
             dres = None
-        return dx, dg, db, None, None, (dres if ctx.has_res else None), None, None, None, None
+        return dx, dg, db, None, None, (dres if ctx.has_res else None), None, None, None, None, None
 
 
 def batch_norm(x, weight, bias, running_mean, running_var, training, momentum=0.1, eps=1e-5, residual=None,
                relu=False, residual_grad_to=None):
     """BatchNorm2d with optional fused residual add and ReLU:  relu?(bn(x) + residual).
     ``residual_grad_to``: a :class:`GradJoin` that receives the residual's gradient (GPU training only)."""
+    groups = current_bn_groups() if training else 1
     if not x.is_cuda:
-        y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+        if groups > 1:  # per-slice statistics, running stats updated slice by slice (in order)
+            y = torch.cat([F.batch_norm(xs, running_mean, running_var, weight, bias, True, momentum, eps)
+                           for xs in x.chunk(groups)])
+        else:
+            y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
         if residual is not None:
             y = y + residual
         return _emu(F.relu(y) if relu else y)
@@ -505,7 +536,7 @@ def batch_norm(x, weight, bias, running_mean, running_var, training, momentum=0.
     if training:
         return _BatchNormFn.apply(x, weight, bias, running_mean, running_var,
                                   residual.contiguous() if residual is not None else None, eps, momentum, relu,
-                                  residual_grad_to if residual is not None else None)
+                                  residual_grad_to if residual is not None else None, groups)
     invstd = torch.rsqrt(running_var + eps)
     scale = (weight * invstd if weight is not None else invstd).float().contiguous()
     shift = ((bias if bias is not None else 0) - running_mean * scale).float().contiguous()

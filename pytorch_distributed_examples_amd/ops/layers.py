@@ -93,10 +93,11 @@ class BatchNorm2d(nn.Module):
 
     def forward(self, x, residual=None, relu=False, residual_grad_to=None):
         if self.training:
+            n = OF.current_bn_groups()  # grouped BatchNorm: one tracked batch per micro-batch, as separately
             if x.is_cuda:
-                self._nbt_pending += 1
+                self._nbt_pending += n
             else:
-                self.num_batches_tracked.add_(1)
+                self.num_batches_tracked.add_(n)
         return OF.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
                              self.momentum, self.eps, residual, relu, residual_grad_to)
 

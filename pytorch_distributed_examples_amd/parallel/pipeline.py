@@ -14,7 +14,10 @@ stage-per-GPU engine:
   4x fewer bytes than the reference's fp32 tensors);
 * explicit schedules: ``gpipe`` (all forwards, then all backwards -- the reference's fill/drain) and
   ``1f1b`` (steady-state one-forward-one-backward; same bubble, bounded in-flight activations);
-* per-micro-batch BatchNorm statistics (quirk Q17 kept);
+* per-micro-batch BatchNorm statistics (quirk Q17 kept), also when several micro-batches run as one
+  pipeline unit (``bn_groups``): at micro-batch 4-8 every ResNet-50 kernel is latency-bound on MI355X
+  (stage 1: 1.11 ms at m = 8 vs 1.68 ms at m = 32, profiles/r3f_stage_bench.jsonl), so a stage runs G
+  micro-batches per launch sequence with grouped BatchNorm -- the reference's math at 1/G of the launches;
 * composes with data parallelism: ``dp_group`` all-reduces each stage's gradients across its replicas
   (hybrid "2-stage pipeline x 4-way DDP" of BASELINE config 4).
 
@@ -29,6 +32,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _native
+from ..ops import functional as OF
 from ..utils.log import NO_PHASES
 
 
@@ -231,6 +235,9 @@ class PipelineEngine:
         self._fwd_meta = None  # (shape, dtype) of activations received from prev
         self._bwd_meta = None
         self.timer = NO_PHASES  # utils.log.PhaseTimer: per-stage fwd / bwd / recv-wait times (bench)
+        # micro-batches per pipeline unit: each unit passed to train_step is `bn_groups` micro-batches run as
+        # ONE launch sequence with per-micro-batch BatchNorm statistics (ops.functional.bn_groups)
+        self.bn_groups = 1
         # a DistributedDataParallel(overlap=True) over this stage's replicas: its bucket all-reduces fire
         # during the LAST micro-batch's backward (earlier ones run under no_sync), overlapping the rest of it
         self.ddp = None
@@ -254,7 +261,7 @@ class PipelineEngine:
         else:
             with self.timer.phase("recv_wait"):
                 x = self._recv_act()
-        with self.timer.phase("fwd"):
+        with self.timer.phase("fwd"), OF.bn_groups(self.bn_groups):
             y = self.module(x)
             loss = self.loss_fn(y, targets[mb]) / n_mb if self.last else None
         if self.last:

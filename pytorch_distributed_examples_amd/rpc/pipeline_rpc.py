@@ -15,11 +15,13 @@ like the reference's hybrid example builds a trainer-only group next to the RPC 
 from __future__ import annotations
 
 import itertools
+import os
 
 import torch
 import torch.distributed as dist
 import torch.distributed.rpc as rpc
 
+from ..ops import functional as OF
 from ..parallel.pipeline import P2PChannel
 from . import core
 
@@ -46,7 +48,7 @@ def _make_stage_server(module_fn, args, kwargs, device, stage, num_stages):
 
 
 @rpc.functions.async_execution
-def _stage_forward(srv_rref, ctx_id, call_id, seq, x_cpu):
+def _stage_forward(srv_rref, ctx_id, call_id, seq, x_cpu, groups=1):
     srv = srv_rref.local_value()
     ch = srv.extra
 
@@ -58,7 +60,8 @@ def _stage_forward(srv_rref, ctx_id, call_id, seq, x_cpu):
             if ch["meta"] is None:
                 ch["meta"] = ch["prev"].recv_meta()
             x = ch["prev"].recv(*ch["meta"]).requires_grad_(True)
-        y = srv.module(x)
+        with OF.bn_groups(groups):  # a unit of `groups` micro-batches: per-micro-batch BatchNorm statistics
+            y = srv.module(x)
         srv.saved[(ctx_id, call_id)] = (x, y)
         if last:
             return y.detach().float().cpu()
@@ -97,8 +100,14 @@ class RemotePipeline:
     ``stage_fns[i]`` builds stage i on ``workers[i]`` (device ``devices[i]``); ``split_size`` is the
     micro-batch SIZE (the reference's ``split_size`` semantics, quirk Q2)."""
 
-    def __init__(self, split_size: int, workers, stage_fns, devices, stage_args=None):
+    def __init__(self, split_size: int, workers, stage_fns, devices, stage_args=None, mb_group: int | None = None):
         self.split_size = split_size
+        # micro-batches per pipeline unit (grouped BatchNorm keeps per-micro-batch statistics; see
+        # apps/hybrid_ps.ResNetPipelineDP): default all of them when the stages run on GPUs
+        if mb_group is None:
+            env = os.environ.get("PDE_PIPE_MB_GROUP")
+            mb_group = int(env) if env else (0 if any(torch.device(d).type == "cuda" for d in devices) else 1)
+        self.mb_group = mb_group  # 0: every micro-batch of the batch in one unit
         self.workers = list(workers)
         n = len(self.workers)
         stage_args = stage_args or [() for _ in range(n)]
@@ -115,9 +124,13 @@ class RemotePipeline:
     def forward(self, xs: torch.Tensor) -> torch.Tensor:
         ctx = core.current_context()
         outs = []
-        for x in xs.split(self.split_size, dim=0):
+        n_mb = -(-xs.shape[0] // self.split_size)
+        g = n_mb if self.mb_group <= 0 else min(self.mb_group, n_mb)
+        while n_mb % g or (g > 1 and xs.shape[0] % self.split_size):  # equal units (whole micro-batches)
+            g -= 1
+        for x in xs.split(self.split_size * g, dim=0):
             call = next(ctx.calls)
-            futs = [self._call(i, _stage_forward, ctx.id, call, x if i == 0 else None)
+            futs = [self._call(i, _stage_forward, ctx.id, call, x if i == 0 else None, g)
                     for i in range(len(self.stages))]
             outs.append((call, futs[-1]))
         results = []

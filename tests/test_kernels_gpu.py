@@ -184,6 +184,56 @@ def test_batchnorm(gpu, relu, res, n, c, h):
     assert OF._C().bn_error(True) == 0  # no one-launch BatchNorm wait timed out
 
 
+@pytest.mark.parametrize("groups,n,c,h,res", [(4, 8, 64, 8, False), (4, 32, 256, 4, True), (2, 8, 512, 16, False),
+                                                (8, 16, 2048, 4, True)])
+def test_batchnorm_groups(gpu, groups, n, c, h, res):
+    """Grouped BatchNorm (ops.functional.bn_groups): ONE launch per direction normalising `groups`
+    micro-batches with their own statistics must equal `groups` separate BatchNorm calls: outputs and input
+    gradients, running statistics after the `groups` in-order momentum updates, dgamma / dbeta
+    as the sum over the groups."""
+    torch.manual_seed(11)
+    x = ((torch.randn(n, h, h, c, device=gpu) * 2 + torch.arange(n, device=gpu).view(n, 1, 1, 1) * 0.3)
+         .bfloat16())
+    r = torch.randn(n, h, h, c, device=gpu).bfloat16() if res else None
+    gamma = torch.rand(c, device=gpu) + 0.5
+    beta = torch.randn(c, device=gpu)
+    gy = torch.randn(n, h, h, c, device=gpu).bfloat16()
+
+    def run(grouped):
+        rm, rv = torch.zeros(c, device=gpu), torch.ones(c, device=gpu)
+        g_, b_ = gamma.clone().requires_grad_(), beta.clone().requires_grad_()
+        xg = x.clone().requires_grad_()
+        rg = r.clone().requires_grad_() if res else None
+        if grouped:
+            with OF.bn_groups(groups):
+                y = OF.batch_norm(xg, g_, b_, rm, rv, True, 0.1, 1e-5, rg, True)
+            y.backward(gy)
+        else:
+            ys = []
+            for k, (xs, gs) in enumerate(zip(xg.chunk(groups), gy.chunk(groups))):
+                ys.append(OF.batch_norm(xs, g_, b_, rm, rv, True, 0.1, 1e-5, rg.chunk(groups)[k] if res else None,
+                                        True))
+            y = torch.cat(ys)
+            y.backward(gy)
+        return y.detach(), xg.grad, (rg.grad if res else None), g_.grad, b_.grad, rm, rv
+
+    a, b = run(True), run(False)
+    # (the grouped launch cuts each group into fewer row chunks than a lone call: fp32 partial sums in a
+    # different order, so bf16 outputs may differ by an ulp here and there)
+    assert rel_err(a[0].float(), b[0].float()) < 2e-3, "forward"
+    assert rel_err(a[1].float(), b[1].float()) < 2e-3, "dx"
+    if res:
+        assert rel_err(a[2].float(), b[2].float()) < 2e-3, "dres"
+    for k, name in ((3, "dgamma"), (4, "dbeta"), (5, "running_mean"), (6, "running_var")):
+        assert rel_err(a[k], b[k]) < 1e-4, name
+    # and it is not the ungrouped BatchNorm: statistics over the whole batch give a different output
+    with torch.no_grad():
+        whole = OF.batch_norm(x, gamma, beta, torch.zeros(c, device=gpu), torch.ones(c, device=gpu), True, 0.1,
+                              1e-5, r, True)
+    assert rel_err(whole.float(), a[0].float()) > 1e-2
+    assert OF._C().bn_error(True) == 0
+
+
 def test_batchnorm_one_launch_graph_replays(gpu):
     """The one-launch BatchNorm kernels (stats -> ticket finalize -> generation flag -> apply) captured in
     a hipGraph: every replay counts the channel groups' flags up and must reproduce the eager results bit

@@ -121,6 +121,42 @@ def test_resnet_shards_match_cpu(gpu):
         assert rel_err(p2.grad.cpu(), p1.grad) < (0.3 if "bn" in n else 0.15), n
 
 
+def test_resnet_blocks_grouped_bn_match_microbatches(gpu):
+    """A pipeline unit of 4 micro-batches with grouped BatchNorm (one launch sequence, per-micro-batch
+    statistics; conv -> BN split-K slab path included) against the same block run micro-batch by
+    micro-batch: outputs, input gradients and parameter gradients agree to bf16 noise."""
+    torch.manual_seed(3)
+    s1, s2 = ResNetShard1(), ResNetShard2()
+    blocks = [s1.seq[4][0], s1.seq[5][0], s2.seq[0][0], s2.seq[1][1]]
+    shapes = [(64, 32), (256, 32), (512, 16), (2048, 4)]
+    G, m = 4, 4
+    for blk, (c, hw) in zip(blocks, shapes):
+        x = torch.randn(G * m, hw, hw, c).to(torch.bfloat16).to(gpu)
+        gy = None
+        outs = []
+        for grouped in (True, False):
+            b = copy.deepcopy(blk).to(gpu)
+            xg = x.clone().requires_grad_()
+            if grouped:
+                with OF.bn_groups(G):
+                    y = b(xg)
+                gen = torch.Generator().manual_seed(c)
+                gy = torch.randn(y.shape, generator=gen).to(torch.bfloat16).to(gpu)
+                y.backward(gy)
+            else:
+                ys = [b(xs) for xs in xg.split(m)]
+                torch.cat(ys).backward(gy)
+                y = torch.cat(ys)
+            grads = torch.cat([p.grad.float().reshape(-1) for p in b.parameters()])
+            bufs = torch.cat([t.float().reshape(-1) for n, t in b.named_buffers() if "running" in n])
+            outs.append((y.detach().float(), xg.grad.float(), grads, bufs))
+        (ya, da, ga, ba), (yb, db, gb, bb) = outs
+        assert rel_err(ya, yb) < 1e-2, (c, rel_err(ya, yb))
+        assert rel_err(da, db) < 3e-2, (c, rel_err(da, db))
+        assert rel_err(ga, gb) < 3e-2, (c, rel_err(ga, gb))
+        assert rel_err(ba, bb) < 1e-3, (c, rel_err(ba, bb))
+
+
 def test_resnet_blocks_match_cpu(gpu):
     """Each bottleneck (with and without downsample / stride) on the same bf16 input: GPU NHWC vs CPU NCHW."""
     torch.manual_seed(0)

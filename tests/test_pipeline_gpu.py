@@ -85,12 +85,14 @@ r, dev = ctx.rank, ctx.device
 B, M, IMG, STEPS = 8, 2, 64, 3
 torch.manual_seed(0)
 pipe = ResNetPipelineDP(ctx, batch=B, split_size=M, image=IMG, schedule=schedule, lr=0.05)
+assert pipe.mb_group == int(os.environ["PDE_PIPE_MB_GROUP"]), pipe.mb_group
 assert pipe.capturable, "ring data plane + dp1: the whole step must be capturable"
 graph = CapturedStep(pipe.step, [], warmup=1).capture()   # one eager warm-up step (meta handshake), then capture
 losses = [float(graph().item()) for _ in range(STEPS)]
 pipe.check()
 flat = torch.cat([p.detach().float().reshape(-1) for p in pipe.module.parameters()]).cpu()
-# reference: the same two shards, same init, same batch, in ONE process (rank 0), same micro-batching
+# reference: the same two shards, same init, same batch, in ONE process (rank 0), same micro-batching (the
+# grouped-vs-separate BatchNorm equivalence itself: test_batchnorm_groups / test_resnet_pipeline_mb_groups_match)
 objs = [None, None]
 dist.all_gather_object(objs, (losses, flat))
 if r == 0:
@@ -108,8 +110,10 @@ if r == 0:
         for p in list(s1.parameters()) + list(s2.parameters()):
             p.grad = None
         tot = 0.0
-        for xm, ym in zip(x.split(M), y.split(M)):
-            loss = OF.mse_loss(s2(s1(xm)), ym) / (B // M)
+        G = pipe.mb_group  # same units, same grouped BatchNorm: identical numerics to the pipelined step
+        for xm, ym in zip(x.split(M * G), y.split(M * G)):
+            with OF.bn_groups(G):
+                loss = OF.mse_loss(s2(s1(xm)), ym) / (B // (M * G))
             loss.backward()
             tot += float(loss.item())
         opt.step()
@@ -155,9 +159,12 @@ def test_p2p_ring_rehearsal_one_gpu(gpu):
     _check(_torchrun(_RING, 2), "RING_OK", 2, "p2p_ring")
 
 
-@pytest.mark.parametrize("schedule", ["gpipe", "1f1b"])
-def test_resnet_pipeline_graph_rehearsal_one_gpu(gpu, schedule):
-    _check(_torchrun(_PIPE, 2, {"SCHEDULE": schedule}), "PIPE_OK", 2, f"pipe_{schedule}")
+@pytest.mark.parametrize("schedule,group", [("gpipe", "1"), ("1f1b", "1"), ("gpipe", "4"), ("1f1b", "2")])
+def test_resnet_pipeline_graph_rehearsal_one_gpu(gpu, schedule, group):
+    """group = micro-batches per pipeline unit (grouped BatchNorm, PDE_PIPE_MB_GROUP); the single-process
+    reference always runs one micro-batch at a time."""
+    _check(_torchrun(_PIPE, 2, {"SCHEDULE": schedule, "PDE_PIPE_MB_GROUP": group}), "PIPE_OK", 2,
+           f"pipe_{schedule}_g{group}")
 
 
 def test_resnet_rpc_pipeline_one_gpu(gpu):
