@@ -157,6 +157,9 @@ struct DeferredReduce {
   Tensor ws;
 };
 std::vector<DeferredReduce> g_deferred;
+// an optimiser segment waiting for the next paired GEMM launch (optim_attach)
+bool g_seg_pending = false;
+pde::OptimSeg g_seg{};
 size_t g_deferred_bytes = 0;
 int gemm_flush_deferred();
 
@@ -178,10 +181,14 @@ bool gemm_pair_end(bool abort, bool defer) {
   g_collect = false;
   std::vector<PendingGemm> q;
   q.swap(g_pending);
+  const bool has_seg = g_seg_pending;
+  const pde::OptimSeg seg = g_seg;
+  g_seg_pending = false;
   if (abort) return false;
   if (q.size() == 2) {
     int sp1 = 0;
-    check(pde::gemm_bf16_pair(q[0].args, q[1].args, cur_stream(), defer ? &sp1 : nullptr), "gemm_pair");
+    check(pde::gemm_bf16_pair(q[0].args, q[1].args, cur_stream(), defer ? &sp1 : nullptr, has_seg ? &seg : nullptr),
+          "gemm_pair");
     if (sp1 > 1) {
       const pde::GemmArgs& a = q[1].args;
       pde::ReduceJob j{};
@@ -196,6 +203,10 @@ bool gemm_pair_end(bool abort, bool defer) {
     }
   } else {
     for (auto& p : q) check(pde::gemm_bf16(p.args, cur_stream()), "gemm");
+    if (has_seg)
+      check(pde::multi_tensor_optim_range(seg.mode, seg.tab, seg.chunks, seg.c0, seg.c1, seg.hp, seg.step,
+                                          seg.publish, cur_stream()),
+            "optim segment");
   }
   return false;
 }
@@ -743,6 +754,44 @@ void optim_step(const Tensor& table, const Tensor& chunks, int64_t nchunks, int 
         "optim_step");
 }
 
+// Chunk range [c0, c1) of an optimiser table: its own launch (publish: the step's last segment advances the
+// device step counter), or -- optim_attach -- appended as extra blocks to the NEXT paired GEMM launch
+// (gemm_pair_end), so the HBM-bound update of one layer overlaps the latency-bound backward GEMMs of the next.
+pde::OptimSeg make_seg(const Tensor& table, const Tensor& chunks, int64_t c0, int64_t c1, int mode,
+                       const Tensor& hparams, Tensor& step, bool publish) {
+  CHECK_IN(table); CHECK_IN(chunks); CHECK_IN(hparams); CHECK_IN(step);
+  TORCH_CHECK(hparams.numel() >= pde::HP_COUNT, "hparams size");
+  TORCH_CHECK(step.scalar_type() == at::kInt && step.numel() >= 2, "step must be int32[2]");
+  TORCH_CHECK(0 <= c0 && c0 <= c1 && c1 * static_cast<long>(sizeof(pde::OptimChunk)) <= chunks.nbytes(),
+              "optimiser chunk range out of bounds");
+  pde::OptimSeg g{};
+  g.tab = reinterpret_cast<const pde::OptimEntry*>(table.data_ptr());
+  g.chunks = reinterpret_cast<const pde::OptimChunk*>(chunks.data_ptr());
+  g.hp = hparams.data_ptr<float>();
+  g.step = step.data_ptr<int>();
+  g.c0 = static_cast<int>(c0);
+  g.c1 = static_cast<int>(c1);
+  g.mode = mode;
+  g.publish = publish ? 1 : 0;
+  g.blocks = std::min(static_cast<int>(c1 - c0), 1024);
+  return g;
+}
+void optim_step_range(const Tensor& table, const Tensor& chunks, int64_t c0, int64_t c1, int mode,
+                      const Tensor& hparams, Tensor& step, bool publish) {
+  const pde::OptimSeg g = make_seg(table, chunks, c0, c1, mode, hparams, step, publish);
+  if (!g_deferred.empty()) gemm_flush_deferred();  // the gradients it reads must be final
+  check(pde::multi_tensor_optim_range(mode, g.tab, g.chunks, g.c0, g.c1, g.hp, g.step, g.publish, cur_stream()),
+        "optim_step_range");
+}
+void optim_attach(const Tensor& table, const Tensor& chunks, int64_t c0, int64_t c1, int mode, const Tensor& hparams,
+                  Tensor& step, bool publish) {
+  TORCH_CHECK(!g_seg_pending, "optim_attach: a segment is already waiting for a GEMM pair");
+  // its gradients must be final: deferred split-K reductions are flushed first
+  if (!g_deferred.empty()) gemm_flush_deferred();
+  g_seg = make_seg(table, chunks, c0, c1, mode, hparams, step, publish);
+  g_seg_pending = true;
+}
+
 // ------------------------------------------------------------------------------------------------
 // BatchNorm / pooling / dropout / EmbeddingBag
 // ------------------------------------------------------------------------------------------------
@@ -1056,6 +1105,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mse_bwd", &mse_bwd);
   m.def("optim_table", &optim_table);
   m.def("optim_step", &optim_step);
+  m.def("optim_step_range", &optim_step_range);
+  m.def("optim_chunk_elems", &pde::optim_chunk_elems);
+  m.def("optim_attach", &optim_attach);
   m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("eps"), py::arg("momentum"), py::arg("res"), py::arg("relu"),
         py::arg("groups") = 1);

@@ -77,7 +77,11 @@ hipError_t gemm_bf16(const GemmArgs& args, hipStream_t stream);
 // split-K slab reductions in one more; otherwise two ordinary gemm_bf16 launches (problem 0 first).
 // defer_split1 != nullptr: problem 1's split-K slab reduction is NOT launched; its split count is returned
 // there (0 / 1: nothing deferred) and the caller reduces it later with gemm_reduce_jobs.
-hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t stream, int* defer_split1 = nullptr);
+struct OptimSeg;
+// seg (optional): optimiser blocks appended to the launch (their own chunk range; run as a separate launch when
+// the two problems cannot be paired)
+hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t stream, int* defer_split1 = nullptr,
+                          const OptimSeg* seg = nullptr);
 bool gemm_pair_enabled();
 // A deferred split-K slab reduction (vector form: N % 4 == 0, 16-B aligned slabs) with the fp32 epilogue of
 // its GEMM (accumulate, OIHW remap, ones-column bias gradient).
@@ -162,6 +166,19 @@ struct OptimChunk {      // elements [start, start + count) of tensor `tensor`
 };
 enum HParam { HP_LR = 0, HP_BETA1, HP_BETA2, HP_EPS, HP_WD, HP_MOMENTUM, HP_GRAD_SCALE, HP_COUNT };
 int optim_chunk_elems();  // chunk size the host must cut tensors into
+// A range of optimiser chunks [c0, c1) run by `blocks` extra blocks appended to a GEMM pair launch
+// (gemm_bf16_pair) -- or by its own launch (multi_tensor_optim_range).  publish: this segment is the step's
+// last one (its last block stores the new device step count).
+struct OptimSeg {
+  const OptimEntry* tab;
+  const OptimChunk* chunks;
+  const float* hp;
+  int* step;
+  int c0, c1, mode, publish, blocks, pad;
+};
+int optim_segment_blocks(int nchunks);
+hipError_t multi_tensor_optim_range(int mode, const OptimEntry* dev_table, const OptimChunk* dev_chunks, int c_begin,
+                                    int c_end, const float* dev_hparams, int* dev_step, int publish, hipStream_t s);
 // mode 0 SGD, 1 Adam, 2 AdamW.  dev_hparams: float[HP_COUNT]; dev_step: int[2] = {steps taken so far,
 // arrival counter (0 between launches)}; the step is advanced on device by the update itself.
 hipError_t multi_tensor_optim(int mode, const OptimEntry* dev_table, const OptimChunk* dev_chunks, int nchunks,

@@ -31,11 +31,13 @@
 //   * Epilogue options: bias, ReLU, ReLU-mask (backward), fp32 / bf16 output, accumulate, and an OIHW
 //     remap that writes a conv weight gradient straight into the parameter's [Co][Ci][R][S] fp32 grad.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 
 #include "common.cuh"
 #include "pde_kernels.h"
+#include "optim_device.h"
 
 namespace pde {
 
@@ -860,11 +862,16 @@ struct PairDims {
 };
 template <bool AKC0, bool BKC0, int AK0, int BK0, bool AKC1, bool BKC1, int AK1, int BK1>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void gemm_pair_kernel(
-    GemmArgs a0, GemmArgs a1, PairDims d) {
+    GemmArgs a0, GemmArgs a1, PairDims d, OptimSeg seg) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM_BYTES_OF<64, 64>() / 2];
   const int t0 = d.tm[0] * d.tn[0];
   const int nb0 = t0 * d.nz[0];
   int b = blockIdx.x;
+  const int nbg = nb0 + d.tm[1] * d.tn[1] * d.nz[1];
+  if (b >= nbg) {  // appended optimiser blocks (another layer's update; never a tensor these GEMMs touch)
+    optdev::run_segment(seg, b - nbg);
+    return;
+  }
   if (b < nb0) {
     gemm_tile<64, 64, 32, 2, 2, AKC0, BKC0, AK0, BK0, PDE_FAST_STAGES>(a0, d.tm[0], d.tn[0], d.kps[0], d.av[0], d.bv[0], b % t0,
                                                          b / t0, d.nz[0], smem);
@@ -1000,12 +1007,17 @@ __global__ __launch_bounds__(kThreads) void gemm_skinny_kernel(GemmArgs args, in
 // A layer's skinny dgrad (problem 0) and its weight gradient on the 64x64 FAST tile (problem 1) in one launch.
 template <bool BKC0, bool AKC1, bool BKC1, int AK1, int BK1>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void gemm_pair_skinny_kernel(
-    GemmArgs a0, int tm0, int tn0, GemmArgs a1, PairDims d) {
+    GemmArgs a0, int tm0, int tn0, GemmArgs a1, PairDims d, OptimSeg seg) {
   constexpr int kS = skinny_smem_bytes<kSkinnyFM, kSkinnyFN, kSkinnyNW, BKC0>();
   constexpr int kT = SMEM_BYTES_OF<64, 64>();
   __shared__ __attribute__((aligned(16))) uint16_t smem[(kS > kT ? kS : kT) / 2];
   const int nb0 = tm0 * tn0;
   const int b = blockIdx.x;
+  const int nbg = nb0 + d.tm[1] * d.tn[1] * d.nz[1];
+  if (b >= nbg) {  // appended optimiser blocks
+    optdev::run_segment(seg, b - nbg);
+    return;
+  }
   if (b < nb0) {
     skinny_tile<kSkinnyFM, kSkinnyFN, kSkinnyNW, BKC0>(a0, tm0, tn0, b, smem);
   } else {
@@ -1223,6 +1235,18 @@ bool generic_only() {
   return g;
 }
 
+// PDE_GEMM_LOG=1: one stderr line per GEMM launch decision (shape, operand kinds, tile, grid, split) -- the
+// shape table behind the per-kernel traces (scripts/gemm_shape_table.py joins the two).
+bool gemm_log_on() {
+  static const bool on = std::getenv("PDE_GEMM_LOG") != nullptr && std::getenv("PDE_GEMM_LOG")[0] == '1';
+  return on;
+}
+void gemm_log(const char* what, const GemmArgs& a, int bm, int bn, int tiles, int split) {
+  if (!gemm_log_on()) return;
+  std::fprintf(stderr, "[gemm] %s M=%d N=%d K=%d akind=%d bkind=%d tile=%dx%d tiles=%d split=%d gflop=%.4f\n", what,
+               a.M, a.N, a.K, a.a.kind, a.b.kind, bm, bn, tiles, split, 2e-9 * a.M * a.N * static_cast<double>(a.K));
+}
+
 template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC>
 hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
   const int tm = ceil_div(a.M, BM), tn = ceil_div(a.N, BN);
@@ -1231,6 +1255,7 @@ hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
   splitk = ceil_div(a.K, kps);
   const int av = vec_ok(a.a, AKC), bv = vec_ok(a.b, BKC);
   dim3 grid(tm * tn, 1, splitk);
+  gemm_log("single", a, BM, BN, tm * tn, splitk);
   GemmArgs ka = a;
   const bool in_kernel = splitk > 1 && splitk <= kMaxInKernelSplits && a.splits_out == nullptr &&
                          static_cast<long>(splitk) * a.M * a.N * 4 < (1L << 31);  // buffer offsets
@@ -1368,12 +1393,13 @@ bool pair_member_plan(const GemmArgs& a, int& tm, int& tn, int& kps, int& split,
 }
 
 template <bool AKC1, bool BKC1, int AK1, int BK1>
-bool launch_pair_k0(int k0, dim3 grid, hipStream_t s, const GemmArgs& a0, const GemmArgs& a1, const PairDims& d) {
+bool launch_pair_k0(int k0, dim3 grid, hipStream_t s, const GemmArgs& a0, const GemmArgs& a1, const PairDims& d,
+                    const OptimSeg& seg) {
   switch (k0) {  // data-gradient kinds: dgrad gather / dense dy x {dgrad layout, forward copy read transposed}
 #define PDE_PAIR(AKC0, BKC0, AK0, BK0)                                                                          \
   case kind_code(AKC0, BKC0, AK0, BK0):                                                                         \
     hipLaunchKernelGGL((gemm_pair_kernel<AKC0, BKC0, AK0, BK0, AKC1, BKC1, AK1, BK1>), grid, dim3(kThreads), 0, s, \
-                       a0, a1, d);                                                                              \
+                       a0, a1, d, seg);                                                                         \
     return true;
     PDE_PAIR(true, true, 3, 0)
     PDE_PAIR(true, true, 0, 0)
@@ -1411,6 +1437,7 @@ void skinny_grid(const GemmArgs& a, int& tm, int& tn) {
 hipError_t launch_skinny(const GemmArgs& a, hipStream_t s) {
   int tm, tn;
   skinny_grid(a, tm, tn);
+  gemm_log("skinny", a, 16 * kSkinnyFM, 16 * kSkinnyFN, tm * tn, 1);
   if (is_kc(a.b))
     hipLaunchKernelGGL(gemm_skinny_kernel<true>, dim3(tm * tn), dim3(kThreads), 0, s, a, tm, tn);
   else
@@ -1418,17 +1445,20 @@ hipError_t launch_skinny(const GemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 // skinny problem 0 + 64x64 FAST-tile problem 1 (a weight gradient: dy^T x dense activation)
-bool launch_pair_skinny(const GemmArgs& a0, const GemmArgs& a1, const PairDims& d, hipStream_t s) {
+bool launch_pair_skinny(const GemmArgs& a0, const GemmArgs& a1, const PairDims& d, hipStream_t s,
+                        const OptimSeg& seg) {
   if (kind_code_of(a1) != kind_code(false, false, 0, 0)) return false;
   int tm0, tn0;
   skinny_grid(a0, tm0, tn0);
-  const dim3 grid(static_cast<unsigned>(tm0 * tn0 + d.tm[1] * d.tn[1] * d.nz[1]));
+  const dim3 grid(static_cast<unsigned>(tm0 * tn0 + d.tm[1] * d.tn[1] * d.nz[1] + seg.blocks));
+  gemm_log("pair-skinny.0", a0, 16 * kSkinnyFM, 16 * kSkinnyFN, tm0 * tn0, 1);
+  gemm_log("pair-skinny.1", a1, 64, 64, d.tm[1] * d.tn[1], d.nz[1]);
   if (is_kc(a0.b))
     hipLaunchKernelGGL((gemm_pair_skinny_kernel<true, false, false, 0, 0>), grid, dim3(kThreads), 0, s, a0, tm0, tn0,
-                       a1, d);
+                       a1, d, seg);
   else
     hipLaunchKernelGGL((gemm_pair_skinny_kernel<false, false, false, 0, 0>), grid, dim3(kThreads), 0, s, a0, tm0,
-                       tn0, a1, d);
+                       tn0, a1, d, seg);
   return true;
 }
 
@@ -1477,8 +1507,11 @@ bool gemm_pair_enabled() {
   return on;
 }
 
-hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s, int* defer_split1) {
+hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s, int* defer_split1,
+                          const OptimSeg* seg_in) {
   if (defer_split1 != nullptr) *defer_split1 = 0;
+  OptimSeg seg{};  // blocks = 0: no optimiser segment
+  if (seg_in != nullptr && seg_in->c1 > seg_in->c0 && seg_in->blocks > 0) seg = *seg_in;
   PairDims d{};
   int sp0 = 1, sp1 = 1;
   if (gemm_pair_enabled() && skinny_ok(a0) &&
@@ -1487,7 +1520,7 @@ hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s,
     GemmArgs g1 = a1;
     g1.tickets = nullptr;
     d.nz[1] = sp1;
-    if (static_cast<long>(d.tm[1]) * d.tn[1] * sp1 < (1L << 30) && launch_pair_skinny(a0, g1, d, s)) {
+    if (static_cast<long>(d.tm[1]) * d.tn[1] * sp1 < (1L << 30) && launch_pair_skinny(a0, g1, d, s, seg)) {
       if (defer_split1 != nullptr && sp1 > 1) {
         *defer_split1 = sp1;
       } else if (sp1 > 1) {
@@ -1505,22 +1538,31 @@ hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s,
   const int k0 = ok ? kind_code_of(a0) : -1, k1 = ok ? kind_code_of(a1) : -1;
   d.nz[0] = sp0;
   d.nz[1] = sp1;
-  const long blocks = static_cast<long>(d.tm[0]) * d.tn[0] * sp0 + static_cast<long>(d.tm[1]) * d.tn[1] * sp1;
+  const long blocks = static_cast<long>(d.tm[0]) * d.tn[0] * sp0 + static_cast<long>(d.tm[1]) * d.tn[1] * sp1 +
+                      seg.blocks;
   bool launched = false;
   if (ok && blocks < (1L << 31)) {
+    gemm_log("pair.0", a0, 64, 64, d.tm[0] * d.tn[0], sp0);
+    gemm_log("pair.1", a1, 64, 64, d.tm[1] * d.tn[1], sp1);
     GemmArgs g0 = a0, g1 = a1;
     g0.tickets = g1.tickets = nullptr;  // pair: split-K partials always go through the reduce launch
     const dim3 grid(static_cast<unsigned>(blocks));
     switch (k1) {  // weight-gradient kinds: dy^T x {im2col^T gather, dense activation}
-      case kind_code(false, false, 0, 2): launched = launch_pair_k0<false, false, 0, 2>(k0, grid, s, g0, g1, d); break;
-      case kind_code(false, false, 0, 0): launched = launch_pair_k0<false, false, 0, 0>(k0, grid, s, g0, g1, d); break;
+      case kind_code(false, false, 0, 2):
+        launched = launch_pair_k0<false, false, 0, 2>(k0, grid, s, g0, g1, d, seg);
+        break;
+      case kind_code(false, false, 0, 0):
+        launched = launch_pair_k0<false, false, 0, 0>(k0, grid, s, g0, g1, d, seg);
+        break;
       default: break;
     }
   }
-  if (!launched) {  // not a pairable configuration: two ordinary launches, problem 0 first
+  if (!launched) {  // not a pairable configuration: two ordinary launches, problem 0 first (+ the optimiser)
     hipError_t e = gemm_bf16(a0, s);
-    if (e != hipSuccess) return e;
-    return gemm_bf16(a1, s);
+    if (e == hipSuccess) e = gemm_bf16(a1, s);
+    if (e == hipSuccess && seg.blocks > 0)
+      e = multi_tensor_optim_range(seg.mode, seg.tab, seg.chunks, seg.c0, seg.c1, seg.hp, seg.step, seg.publish, s);
+    return e;
   }
   if (defer_split1 != nullptr && sp1 > 1) {  // problem 1's slabs are reduced later by gemm_reduce_jobs
     *defer_split1 = sp1;

@@ -15,193 +15,45 @@
 // step counter is int32[2] = {steps taken, arrival counter}: the last block to finish advances it.
 #include <cstdlib>
 
-#include "common.cuh"
-#include "pde_kernels.h"
+#include "optim_device.h"
 
 namespace pde {
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kGroups = 4;                       // 16-byte groups per thread per chunk
-constexpr int kChunk = kThreads * 4 * kGroups;   // elements per chunk (4096)
-
-struct Hyper {
-  float lr, b1, b2, eps, wd, mom, gscale, step_size, inv_sqrt_bc2;
-  int step;
-};
-
-template <int MODE>
-__device__ __forceinline__ void update(const Hyper& h, float& p, float g, float& m, float& v) {
-  g *= h.gscale;
-  if (MODE == 0) {  // SGD (+momentum, +L2)
-    if (h.wd != 0.f) g += h.wd * p;
-    if (h.mom != 0.f) {
-      m = (h.step == 1) ? g : h.mom * m + g;
-      g = m;
-    }
-    p -= h.lr * g;
-  } else {
-    if (MODE == 1) {
-      if (h.wd != 0.f) g += h.wd * p;
-    } else {
-      p *= 1.f - h.lr * h.wd;
-    }
-    m = h.b1 * m + (1.f - h.b1) * g;
-    v = h.b2 * v + (1.f - h.b2) * g * g;
-    p -= h.step_size * m / (sqrtf(v) * h.inv_sqrt_bc2 + h.eps);
-  }
-}
-
-// 16-B state accesses; NT: non-temporal (streaming) loads and stores -- every state byte is touched once per
-// step, so keeping it in L2 / MALL only evicts the GEMMs' operands (A/B: PDE_OPTIM_NT=0)
-template <bool NT>
-__device__ __forceinline__ f32x4 ld4(const float* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-  else return *reinterpret_cast<const f32x4*>(p);
-}
-template <bool NT>
-__device__ __forceinline__ void st4(float* p, const f32x4& v) {
-  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
-  else *reinterpret_cast<f32x4*>(p) = v;
-}
-
-// One chunk's state for one thread: kGroups x 16 B of every state tensor, loaded before any math.
-template <int MODE, bool NT>
-struct ChunkRegs {
-  float p[kGroups][4], g[kGroups][4], m[kGroups][4], v[kGroups][4];
-  int e0[kGroups], cnt[kGroups];
-  int tensor;
-
-  __device__ __forceinline__ void load(const OptimEntry* tab, const OptimChunk& ch, bool use_m) {
-    tensor = ch.tensor;
-    const OptimEntry& te = tab[ch.tensor];
-    const int end = ch.start + ch.count;
-#pragma unroll
-    for (int u = 0; u < kGroups; ++u) {
-      e0[u] = ch.start + (u * kThreads + threadIdx.x) * 4;
-      cnt[u] = e0[u] < end ? min(4, end - e0[u]) : 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) p[u][k] = g[u][k] = m[u][k] = v[u][k] = 0.f;
-      if (cnt[u] == 4 && te.vec) {
-        const f32x4 pv = ld4<NT>(te.param + e0[u]);
-        p[u][0] = pv[0]; p[u][1] = pv[1]; p[u][2] = pv[2]; p[u][3] = pv[3];
-        if (te.grad) {
-          const f32x4 gv = ld4<NT>(te.grad + e0[u]);
-          g[u][0] = gv[0]; g[u][1] = gv[1]; g[u][2] = gv[2]; g[u][3] = gv[3];
-        }
-        if (use_m) {
-          const f32x4 mv = ld4<NT>(te.exp_avg + e0[u]);
-          m[u][0] = mv[0]; m[u][1] = mv[1]; m[u][2] = mv[2]; m[u][3] = mv[3];
-        }
-        if (MODE != 0) {
-          const f32x4 vv = ld4<NT>(te.exp_avg_sq + e0[u]);
-          v[u][0] = vv[0]; v[u][1] = vv[1]; v[u][2] = vv[2]; v[u][3] = vv[3];
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (k < cnt[u]) {
-            p[u][k] = te.param[e0[u] + k];
-            if (te.grad) g[u][k] = te.grad[e0[u] + k];
-            if (use_m) m[u][k] = te.exp_avg[e0[u] + k];
-            if (MODE != 0) v[u][k] = te.exp_avg_sq[e0[u] + k];
-          }
-        }
-      }
-    }
-  }
-
-  __device__ __forceinline__ void finish(const Hyper& h, const OptimEntry* tab, bool use_m) {
-    const OptimEntry& te = tab[tensor];
-#pragma unroll
-    for (int u = 0; u < kGroups; ++u) {
-      if (cnt[u] == 0) continue;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) update<MODE>(h, p[u][k], g[u][k], m[u][k], v[u][k]);
-      const int i = e0[u];
-      if (cnt[u] == 4 && te.vec) {
-        st4<NT>(te.param + i, f32x4{p[u][0], p[u][1], p[u][2], p[u][3]});
-        if (use_m) st4<NT>(te.exp_avg + i, f32x4{m[u][0], m[u][1], m[u][2], m[u][3]});
-        if (MODE != 0) st4<NT>(te.exp_avg_sq + i, f32x4{v[u][0], v[u][1], v[u][2], v[u][3]});
-        if (te.bf16_copy)
-          *reinterpret_cast<u16x4*>(te.bf16_copy + i) = u16x4{f2bf(p[u][0]), f2bf(p[u][1]), f2bf(p[u][2]), f2bf(p[u][3])};
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (k < cnt[u]) {
-            te.param[i + k] = p[u][k];
-            if (use_m) te.exp_avg[i + k] = m[u][k];
-            if (MODE != 0) te.exp_avg_sq[i + k] = v[u][k];
-            if (te.bf16_copy) te.bf16_copy[i + k] = f2bf(p[u][k]);
-          }
-        }
-      }
-    }
-  }
-};
+using optdev::kOptChunk;
+using optdev::kOptThreads;
 
 template <int MODE, bool NT>
-__global__ __launch_bounds__(kThreads) void k_optim(const OptimEntry* __restrict__ tab,
-                                                    const OptimChunk* __restrict__ chunks, int nchunks,
-                                                    const float* __restrict__ hp, int* __restrict__ step_ptr) {
-  __shared__ int s_step;
-  if (threadIdx.x == 0) s_step = step_ptr[0] + 1;  // step being taken (1-based)
-  __syncthreads();
-  Hyper h;
-  h.lr = hp[HP_LR]; h.b1 = hp[HP_BETA1]; h.b2 = hp[HP_BETA2]; h.eps = hp[HP_EPS];
-  h.wd = hp[HP_WD]; h.mom = hp[HP_MOMENTUM]; h.gscale = hp[HP_GRAD_SCALE];
-  h.step = s_step;
-  if (MODE != 0) {
-    const float bc1 = 1.f - __powf(h.b1, static_cast<float>(h.step));
-    const float bc2 = 1.f - __powf(h.b2, static_cast<float>(h.step));
-    h.step_size = h.lr / bc1;
-    h.inv_sqrt_bc2 = rsqrtf(bc2);
-  }
-  const bool use_m = MODE != 0 || h.mom != 0.f;
-
-  // Grid-stride over chunks, software-pipelined: the next chunk's loads are issued before the current
-  // chunk's math and stores, so every block keeps a chunk of loads in flight while it writes.
-  ChunkRegs<MODE, NT> cur, nxt;
-  int c = blockIdx.x;
-  if (c < nchunks) cur.load(tab, chunks[c], use_m);
-  for (; c < nchunks; c += gridDim.x) {
-    const int cn = c + gridDim.x;
-    if (cn < nchunks) nxt.load(tab, chunks[cn], use_m);
-    cur.finish(h, tab, use_m);
-    cur = nxt;
-  }
-  // The last block to finish publishes the new step count.  Every block read the old count before its
-  // arrival (the value was consumed before the barrier above), and the next launch sees the store
-  // across the kernel boundary: a relaxed device-scope ticket is enough (no fence).
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int prev = atomicAdd(step_ptr + 1, 1);
-    if (prev == static_cast<int>(gridDim.x) - 1) {
-      step_ptr[0] = s_step;
-      step_ptr[1] = 0;
-    }
-  }
+__global__ __launch_bounds__(kOptThreads) void k_optim(const OptimEntry* __restrict__ tab,
+                                                       const OptimChunk* __restrict__ chunks, int c_begin, int c_end,
+                                                       const float* __restrict__ hp, int* __restrict__ step_ptr,
+                                                       int publish) {
+  optdev::run_chunks<MODE, NT>(tab, chunks, c_begin, c_end, hp, step_ptr, blockIdx.x, gridDim.x, publish != 0);
 }
 
 }  // namespace
 
-int optim_chunk_elems() { return kChunk; }
+int optim_chunk_elems() { return kOptChunk; }
 
-hipError_t multi_tensor_optim(int mode, const OptimEntry* dev_table, const OptimChunk* dev_chunks, int nchunks,
-                              const float* dev_hparams, int* dev_step, hipStream_t s) {
-  if (nchunks <= 0) return hipSuccess;
+int optim_segment_blocks(int nchunks) {
   // ~3 blocks per CU, each walking several chunks with the next one's loads in flight (pipelined loop)
   static const int kMaxBlocks = std::getenv("PDE_OPTIM_BLOCKS") ? std::atoi(std::getenv("PDE_OPTIM_BLOCKS")) : 768;
+  return nchunks < kMaxBlocks ? nchunks : kMaxBlocks;
+}
+
+hipError_t multi_tensor_optim_range(int mode, const OptimEntry* dev_table, const OptimChunk* dev_chunks, int c_begin,
+                                    int c_end, const float* dev_hparams, int* dev_step, int publish, hipStream_t s) {
+  if (c_end <= c_begin) return hipSuccess;
   static const bool nt = !(std::getenv("PDE_OPTIM_NT") && std::getenv("PDE_OPTIM_NT")[0] == '0');
-  dim3 grid(static_cast<unsigned>(nchunks < kMaxBlocks ? nchunks : kMaxBlocks));
+  dim3 grid(static_cast<unsigned>(optim_segment_blocks(c_end - c_begin)));
 #define PDE_OPT(M)                                                                                            \
   if (nt)                                                                                                     \
-    hipLaunchKernelGGL((k_optim<M, true>), grid, dim3(kThreads), 0, s, dev_table, dev_chunks, nchunks,       \
-                       dev_hparams, dev_step);                                                                \
+    hipLaunchKernelGGL((k_optim<M, true>), grid, dim3(kOptThreads), 0, s, dev_table, dev_chunks, c_begin,     \
+                       c_end, dev_hparams, dev_step, publish);                                               \
   else                                                                                                        \
-    hipLaunchKernelGGL((k_optim<M, false>), grid, dim3(kThreads), 0, s, dev_table, dev_chunks, nchunks,      \
-                       dev_hparams, dev_step);
+    hipLaunchKernelGGL((k_optim<M, false>), grid, dim3(kOptThreads), 0, s, dev_table, dev_chunks, c_begin,    \
+                       c_end, dev_hparams, dev_step, publish);
   if (mode == 0) {
     PDE_OPT(0)
   } else if (mode == 1) {
@@ -211,6 +63,11 @@ hipError_t multi_tensor_optim(int mode, const OptimEntry* dev_table, const Optim
   }
 #undef PDE_OPT
   return hipGetLastError();
+}
+
+hipError_t multi_tensor_optim(int mode, const OptimEntry* dev_table, const OptimChunk* dev_chunks, int nchunks,
+                              const float* dev_hparams, int* dev_step, hipStream_t s) {
+  return multi_tensor_optim_range(mode, dev_table, dev_chunks, 0, nchunks, dev_hparams, dev_step, 1, s);
 }
 
 }  // namespace pde

@@ -242,6 +242,9 @@ def build_data_parallel(args, ctx, batch) -> Workload:
 
             fmlp = FusedMLP(model)
         ddp = DistributedDataParallel(model, overlap=not use_graph and fmlp is None, comm=comm)
+    # world 1, fused MLP, PDE_MLP_FOLD_OPT=1: each layer's Adam update appended to the next backward GEMM launch
+    # (default: the separate multi-tensor launch after backward -- measured faster, profiles/README.md r3k)
+    fold_opt = fmlp is not None and ctx.world_size == 1 and os.environ.get("PDE_MLP_FOLD_OPT", "0") == "1"
     # world > 1 on the xGMI data plane: the fused CNN exchanges its gradients inside the slab reduction
     # (PDE_CNN_XCHG=0: all-reduce through the DDP communicator + a separate SGD launch instead)
     xgmi = getattr(comm, "xgmi", None) if fused is not None and os.environ.get("PDE_CNN_XCHG", "1") != "0" else None
@@ -263,6 +266,9 @@ def build_data_parallel(args, ctx, batch) -> Workload:
                 fused.sgd_step(opt, ddp.flat_grad)
             return loss
         if fmlp is not None:
+            if fold_opt:  # one process: the optimiser step rides on the backward launches (FusedMLP)
+                with t.phase("fwd_bwd_opt"):
+                    return fmlp.forward_backward(x, y, opt=opt)
             with t.phase("fwd_bwd"):
                 loss = fmlp.forward_backward(x, y)  # gradients written (not accumulated): no zeroing
             if ctx.world_size > 1:
@@ -308,6 +314,7 @@ def build_data_parallel(args, ctx, batch) -> Workload:
     extra = {"stage": args.stage, "mb_per_unit": bn_groups} if args.model == "resnet50_stage" else {}
     w = Workload(step, batch * ctx.world_size, f"dp{ctx.world_size}", **extra, hipgraph=one is not None,
                  fused_step=fused is not None or fmlp is not None, rccl_nranks=nranks,
+                 **({"optimizer": "adam folded into the backward launches"} if fold_opt else {}),
                  steps_per_graph=group.steps if group is not None else (1 if one is not None else 0),
                  allreduce=("xgmi-in-reduce-kernel" if xgmi is not None else
                             "xgmi-oneshot<=%dB+rccl" % comm.threshold) if routed is not None else
@@ -383,7 +390,8 @@ def _secondary_pipeline(ctx, timeout_s: float = 420.0):
             result.update(value=rec["value"], unit=rec["unit"], ms_per_step=rec["ms_per_step"], steps=rec["steps"],
                           warmup=rec["warmup"], vs_baseline=rec["vs_baseline"],
                           parallelism=rec["config"]["parallelism"], hipgraph=rec["config"]["hipgraph"],
-                          global_batch=rec["config"]["global_batch"], final_loss=rec["config"]["final_loss"])
+                          global_batch=rec["config"]["global_batch"], final_loss=rec["config"]["final_loss"],
+                          split_size=rec["config"].get("split_size"), mb_per_unit=rec["config"].get("mb_per_unit"))
     except subprocess.TimeoutExpired:
         result["error"] = f"timeout after {timeout_s:.0f} s"
     except Exception as exc:  # noqa: BLE001 - never let the secondary measurement cost the headline

@@ -69,10 +69,19 @@ class FusedMLP:
         return L.weight.grad, L.bias.grad
 
     @torch.no_grad()
-    def forward_backward(self, x: torch.Tensor, y: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
+    def forward_backward(self, x: torch.Tensor, y: torch.Tensor, accumulate: bool = False, opt=None) -> torch.Tensor:
         """Mean cross-entropy of the batch (device scalar); parameter gradients written (``accumulate``:
-        added) into each parameter's ``.grad``."""
+        added) into each parameter's ``.grad``.
+
+        ``opt`` (a fused optimiser, single process -- no gradient all-reduce between backward and update):
+        the optimiser step is folded into the backward: layer i+1's update runs as extra blocks of layer i's
+        paired dgrad + wgrad launch (its gradients are final by then, and no GEMM of that launch touches its
+        weights), layers 1 and 0 in one closing launch.  Replaces ``opt.step()``; same update math, same
+        kernels' device code."""
         C = _native.C()
+        params_of = [[L.weight, L.bias] for L in self.layers]
+        fuse_opt = (opt is not None and not streams.active_for(x) and
+                    opt.supports_segments([p for ps in params_of for p in ps]))
         B = x.shape[0]
         acts, logits, dys, dlog = self._buffers(B, x.device)
         C.cast_rows_ones(x.reshape(B, -1).float().contiguous(), acts[0])
@@ -94,8 +103,11 @@ class FusedMLP:
                 with streams.fork(dy, join_at_backward_end=False):
                     C.linear_wgrad_bias(dy, acts[i][:, :L.in_features + 1], gw, gb, accumulate)
             elif i > 0:
-                # dgrad + weight/bias gradient as ONE paired GEMM launch (dgrad tiles first)
+                # dgrad + weight/bias gradient as ONE paired GEMM launch (dgrad tiles first), carrying the update
+                # of layer i + 1 when the optimiser is folded in
                 wpad = OF._maintained(L.weight, "bf16_pad") if i == last else None
+                if fuse_opt and i < last:
+                    opt.attach_update(params_of[i + 1])
                 with OF.gemm_pair(defer_second=True, flush_by_caller=True):
                     if wpad is not None:  # K padded to 16: zero columns of d logits x zero rows of the weight
                         C.linear_dgrad_out(dlog, wpad, acts[i][:, :L.in_features], dys[i - 1])
@@ -111,6 +123,8 @@ class FusedMLP:
                 dy = dys[i - 1]
         # the deferred weight-gradient reductions: one batched launch (and the side stream, if used)
         streams.join(x.device)
+        if fuse_opt:  # the updates no backward launch could carry: layers 0 and 1 (1 only if it exists)
+            opt.step_range([p for ps in params_of[:min(2, last + 1)] for p in ps], last=True)
         return loss
 
     def launches_per_step(self) -> int:

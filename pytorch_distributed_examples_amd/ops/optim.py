@@ -115,6 +115,47 @@ class _FusedBase(torch.optim.Optimizer):
         OF.bump_weight_generation()
         return loss
 
+    # -- update segments: one layer's update appended to a later backward GEMM launch ------------
+    def _segment(self, subset):
+        """(table, chunks, c0, c1, mode, hp, step) of ``subset`` -- parameters contiguous in the (single, GPU)
+        param group's order -- for ``optim_attach`` / ``optim_step_range``."""
+        assert len(self.param_groups) == 1, "update segments: one parameter group"
+        group = self.param_groups[0]
+        params = [p for p in group["params"] if p.grad is not None]
+        st = self._group_dev(0, group, params)
+        chunk = _native.C().optim_chunk_elems()
+        starts, c = {}, 0
+        for p in params:
+            starts[id(p)] = c
+            c += -(-p.numel() // chunk)
+        ids = [id(p) for p in subset]
+        c0 = min(starts[i] for i in ids)
+        c1 = max(starts[id(p)] + -(-p.numel() // chunk) for p in subset)
+        assert c1 - c0 == sum(-(-p.numel() // chunk) for p in subset), "segment parameters must be contiguous"
+        return st["table"], st["chunks"], c0, c1, _MODES[self.KIND], st["hp"], st["step"]
+
+    def supports_segments(self, params) -> bool:
+        """True when :meth:`attach_update` / :meth:`step_range` can run this optimiser's update piecewise:
+        one GPU parameter group, no KxK conv layout copies to refresh."""
+        return (len(self.param_groups) == 1 and all(p.is_cuda for p in params) and
+                not any("kxk" in (OF.maintain_compute_copies(p) or {}) for p in params))
+
+    @torch.no_grad()
+    def attach_update(self, subset):
+        """Append the update of ``subset`` (whose gradients are final) to the NEXT paired backward GEMM launch
+        as extra blocks (``OF.gemm_pair``): the HBM-bound update overlaps the latency-bound GEMMs."""
+        t, ch, c0, c1, mode, hp, step = self._segment(subset)
+        _native.C().optim_attach(t, ch, c0, c1, mode, hp, step, False)
+
+    @torch.no_grad()
+    def step_range(self, subset, last: bool = True):
+        """The update of ``subset`` as its own launch; ``last``: the step's final segment (advances the device
+        step counter -- every parameter must have been updated by a segment of this step)."""
+        t, ch, c0, c1, mode, hp, step = self._segment(subset)
+        _native.C().optim_step_range(t, ch, c0, c1, mode, hp, step, last)
+        if last:
+            OF.bump_weight_generation()
+
     # -- CPU reference math (torch.optim semantics) ---------------------------------------------
     def _cpu_step(self, group, params):
         lr, (b1, b2), eps = group["lr"], group["betas"], group["eps"]

@@ -493,3 +493,42 @@ def test_fused_cnn_training_is_visible_to_eval(gpu):
     ref = fresh(x).float()
     assert (after - before).abs().max().item() > 1e-3  # the weights moved
     assert torch.allclose(after, ref, atol=2e-2, rtol=2e-2)
+
+
+def test_fused_mlp_folded_adam_matches_separate_step(gpu):
+    """FusedMLP.forward_backward(opt=...) folds each layer's Adam update into the next backward GEMM launch
+    (optimiser blocks appended to the paired dgrad + wgrad grid, layers 0-1 in a closing launch).  Same
+    device update code as the separate multi-tensor step: weights, Adam moments, bf16 compute copies and the
+    device step counter must match the unfused schedule after several steps."""
+    from pytorch_distributed_examples_amd.models.mlp import reference_mlp
+    from pytorch_distributed_examples_amd.models.mlp_fused import FusedMLP
+    from pytorch_distributed_examples_amd.ops.optim import FusedAdam
+
+    torch.manual_seed(0)
+    base = reference_mlp()
+    g = torch.Generator().manual_seed(1)
+    xs = [torch.randn(128, 1, 28, 28, generator=g).to(gpu) for _ in range(4)]
+    ys = [torch.randint(0, 10, (128,), generator=g).to(gpu) for _ in range(4)]
+    runs = []
+    for fold in (False, True):
+        net = copy.deepcopy(base).to(gpu)
+        opt = FusedAdam(net.parameters(), lr=1e-3)
+        f = FusedMLP(net)
+        losses = []
+        for x, y in zip(xs, ys):
+            if fold:
+                loss = f.forward_backward(x, y, opt=opt)
+            else:
+                loss = f.forward_backward(x, y)
+                opt.step()
+            losses.append(float(loss))
+        torch.cuda.synchronize()
+        st = opt.state_dict()
+        flat = torch.cat([p.detach().reshape(-1) for p in net.parameters()])
+        moments = torch.cat([opt.state[p]["exp_avg_sq"].reshape(-1) for p in net.parameters()])
+        copies = torch.cat([OF._bf16_weight(L.weight).float().reshape(-1) for L in f.layers])
+        runs.append((losses, flat, moments, copies, st["state"][0]["step"]))
+    (l0, f0, m0, c0, s0), (l1, f1, m1, c1, s1) = runs
+    assert s0 == s1 == 4, (s0, s1)
+    assert l0 == l1, (l0, l1)
+    assert torch.equal(f0, f1) and torch.equal(m0, m1) and torch.equal(c0, c1)
