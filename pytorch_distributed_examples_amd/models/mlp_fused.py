@@ -82,6 +82,9 @@ class FusedMLP:
         params_of = [[L.weight, L.bias] for L in self.layers]
         fuse_opt = (opt is not None and not streams.active_for(x) and
                     opt.supports_segments([p for ps in params_of for p in ps]))
+        if fuse_opt:
+            for L in self.layers:  # every gradient exists up front: ONE optimiser table for the whole step
+                self._grads(L)
         B = x.shape[0]
         acts, logits, dys, dlog = self._buffers(B, x.device)
         C.cast_rows_ones(x.reshape(B, -1).float().contiguous(), acts[0])

@@ -137,8 +137,12 @@ class _FusedBase(torch.optim.Optimizer):
     def supports_segments(self, params) -> bool:
         """True when :meth:`attach_update` / :meth:`step_range` can run this optimiser's update piecewise:
         one GPU parameter group, no KxK conv layout copies to refresh."""
+        # (inspects the maintained copies without re-allocating them: maintain_compute_copies would replace the
+        # copies the optimiser table writes)
         return (len(self.param_groups) == 1 and all(p.is_cuda for p in params) and
-                not any("kxk" in (OF.maintain_compute_copies(p) or {}) for p in params))
+                not any(getattr(p, "_pde_conv", False) and p.dim() == 4 and p.shape[2] * p.shape[3] > 1
+                        for p in params) and
+                not any("kxk" in p.__dict__.get("_pde_maint", {}) for p in params))
 
     @torch.no_grad()
     def attach_update(self, subset):
