@@ -96,6 +96,8 @@ struct CnnSmem {
                                            // 16 distinct 16-B bank groups (128-B rows: 4-8-way conflicts)
   alignas(16) uint16_t zero16[8];      // 16 zero bytes: the target of every out-of-range operand read
   uint16_t x[NI][NX];                  // images
+  uint16_t x1[NI][NX];                 // images shifted by one element (x1[i] = x[i + 1]): every pair of
+                                       // consecutive pixels is ONE aligned 4-byte LDS read from x or x1
   uint16_t r1[NI][NR1];                // relu(maxpool(conv1)), [ci][cell]
   uint16_t dr1[NI][NR1];               // grad at r1 (relu'-masked) == conv1-output grad at argmax taps
   // fp32 head
@@ -161,8 +163,13 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (n < B) v = *reinterpret_cast<const f32x4*>(images + static_cast<long>(n) * NX + off);
     uint16_t* dst = &S.x[im][off];
-    dst[0] = f2bf(v[0]); dst[1] = f2bf(v[1]); dst[2] = f2bf(v[2]); dst[3] = f2bf(v[3]);
+    const uint16_t b0 = f2bf(v[0]), b1 = f2bf(v[1]), b2 = f2bf(v[2]), b3 = f2bf(v[3]);
+    dst[0] = b0; dst[1] = b1; dst[2] = b2; dst[3] = b3;
+    uint16_t* d1 = &S.x1[im][off];
+    if (off > 0) d1[-1] = b0;
+    d1[0] = b1; d1[1] = b2; d1[2] = b3;
   }
+  if (t < NI) S.x1[t][NX - 1] = 0;
   {  // weight fragments, pre-laid-out in bf16 MFMA order by k_cnn_prep: straight 16-byte copies
     u16x8* dst = &S.w2f[0][0][0];
     for (int e = t; e < NFRAG; e += T) dst[e] = frag[e];
@@ -195,24 +202,32 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   __syncthreads();
   PDE_STAMP(1);
 
-  // ---- P1: conv1 (MFMA, M = (cell, tap), K = 25 -> 32, N = co) + maxpool2 + relu -------------------
+  // ---- P1: conv1 (MFMA, M = (cell, tap), K = (ky, kx6) 30 -> 32, N = co) + maxpool2 + relu ----------
+  // K runs over 6-wide kernel rows (kx = 5 has zero weight): every k pair (kx even) is two consecutive
+  // pixels, read as ONE aligned 4-byte LDS load -- from x when the window starts on an even column (dx = 0),
+  // from the shifted copy x1 otherwise: 4 gathers per fragment instead of 8.
   {
-    int koff[8];       // k = (ky,kx) offsets into the image; padding k (>= 25) reads offset 0, masked
-    uint16_t kmsk[8];
+    int koff[4];       // pair p: k = 8 lg + 2p = (ky, kx) offset into the image; pairs past k = 30 are zero
+    uint32_t kmsk[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = lg * 8 + j;
-      koff[j] = k < 25 ? (k / 5) * H0 + (k % 5) : 0;
-      kmsk[j] = k < 25 ? 0xFFFFu : 0u;
+    for (int p = 0; p < 4; ++p) {
+      const int k = lg * 8 + 2 * p;
+      koff[p] = k < KS * 6 ? (k / 6) * H0 + (k % 6) : 0;
+      kmsk[p] = k < KS * 6 ? 0xFFFFFFFFu : 0u;
     }
     const u16x8 bw = S.w1f[lane];
     const int tap = lr & 3, dy = tap >> 1, dx = tap & 1;
+    const uint16_t* xsrc = dx ? &S.x1[0][0] - 1 : &S.x[0][0];  // x1[i - 1] = x[i]: odd starts become even
     auto gather = [&](int tile, u16x8& a) {
       const int im = tile / MT1, c0 = (tile - im * MT1) * 4;
       const int cell = c0 + (lr >> 2), py = cell / P1, px = cell - py * P1;
-      const uint16_t* xb = S.x[im] + (2 * py + dy) * H0 + 2 * px + dx;
+      const uint16_t* xb = xsrc + im * NX + (2 * py + dy) * H0 + 2 * px + dx;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] = xb[koff[j]] & kmsk[j];
+      for (int p = 0; p < 4; ++p) {
+        const uint32_t v = *reinterpret_cast<const uint32_t*>(xb + koff[p]) & kmsk[p];
+        a[2 * p] = static_cast<uint16_t>(v);
+        a[2 * p + 1] = static_cast<uint16_t>(v >> 16);
+      }
     };
     static_assert((NI * MT1) % NW == 0, "every wave runs the same number of conv1 tiles");
     u16x8 an;
@@ -550,11 +565,13 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   {
     int nb[2];
     bool nv[2];
+    const uint16_t* xw[2];  // x for even kx, x1 - 1 for odd kx (aligned pairs either way)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int kidx = u * 16 + lr;
       nv[u] = kidx < 25;
       nb[u] = nv[u] ? (kidx / 5) * H0 + kidx % 5 : 0;
+      xw[u] = (nv[u] && ((kidx % 5) & 1)) ? &S.x1[0][0] - 1 : &S.x[0][0];
     }
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     const int co = lr;
@@ -576,12 +593,17 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        // 8 separate u16 reads (this file is built without unaligned-access mode, _build.HIP_FLAGS): merged
-        // into one 16-byte read at this 2-byte-aligned address the LDS would replay it as an unaligned access
-        const uint16_t* src = S.x[im] + nb[u] + y * H0 + x0;
+        // 8 consecutive pixels from offset nb + y H0 + x0 (x0 % 8 == 0): four aligned 4-byte reads of x (kx
+        // even) or of the shifted copy x1 (kx odd) -- never one 16-byte read at a 2-byte-aligned address,
+        // which the LDS would replay as an unaligned access
+        const uint16_t* src = xw[u] + im * NX + nb[u] + y * H0 + x0;
         u16x8 b;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) b[j] = nv[u] ? src[j] : 0;
+        for (int p = 0; p < 4; ++p) {
+          const uint32_t v = nv[u] ? *reinterpret_cast<const uint32_t*>(src + 2 * p) : 0u;
+          b[2 * p] = static_cast<uint16_t>(v);
+          b[2 * p + 1] = static_cast<uint16_t>(v >> 16);
+        }
         acc[u] = mfma(a, b, acc[u]);
       }
     }
@@ -639,11 +661,14 @@ __global__ __launch_bounds__(256) void k_cnn_prep(const float* __restrict__ para
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       f[j] = (g < NGD && ci < C1 && c0 + j < C2) ? f2bf(gW2[(c0 + j) * K2 + ci * 25 + tap]) : 0;
-  } else {  // conv1: B[k=(ky,kx)][n=co] = w1[co][k]
+  } else {  // conv1: B[k = (ky, kx6)][n = co] = w1[co][ky][kx] (kx = 5 and k >= 30: zero)
     const int l = e - KS2 * 2 * 64 - KSD * 64;
     const int co = l & 15, k0 = (l >> 4) * 8;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = (co < C1 && k0 + j < 25) ? f2bf(gW1[co * 25 + k0 + j]) : 0;
+    for (int j = 0; j < 8; ++j) {
+      const int k = k0 + j, ky = k / 6, kx = k - ky * 6;
+      f[j] = (co < C1 && k < KS * 6 && kx < KS) ? f2bf(gW1[co * 25 + ky * KS + kx]) : 0;
+    }
   }
   frag[e] = f;
 }
@@ -662,7 +687,8 @@ __device__ __forceinline__ void write_frag(uint16_t* __restrict__ f, int p, floa
     const int e2 = KS2 * 2 * 64 + (gd >> 2) * 64 + (((gd & 3) << 4) | ci);
     f[e2 * 8 + (co & 7)] = b;
   } else if (p >= O_W1 && p < O_W1 + W1N) {
-    const int co = p / (KS * KS), k = p - co * (KS * KS);
+    const int co = p / (KS * KS), k25 = p - co * (KS * KS);
+    const int k = (k25 / KS) * 6 + k25 % KS;                                     // (ky, kx6) order
     const int e = KS2 * 2 * 64 + KSD * 64 + (((k >> 3) << 4) | co);             // conv1 [lane]
     f[e * 8 + (k & 7)] = b;
   }
