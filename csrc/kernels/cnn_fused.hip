@@ -112,6 +112,7 @@ struct CnnSmem {
   float mc2[NI][C2];
   float logit[NI][F2], dlog[NI][F2];
   float valid[NI];
+  int label[NI];
   unsigned char a1[NI][NR1];
   unsigned char a2[NI][NIN];
 };
@@ -131,6 +132,16 @@ static_assert(F1 * FC1_KC <= T && NIN * DP2_JC <= T, "fc1 work split");
 static_assert(sizeof(float) * NI * F1 * FC1_KC <= sizeof(u16x8) * KS2 * 2 * 64, "fc1 partials alias w2f");
 static_assert(sizeof(float) * NI * NIN * DP2_JC <= sizeof(u16x8) * KS2 * 2 * 64, "dp2 partials alias w2f");
 static_assert(NT2 * NW == 16, "conv2 wgrad tiling");
+
+// Workgroup barrier for LDS hand-offs only: every wave's LDS accesses complete (lgkmcnt), then s_barrier --
+// outstanding GLOBAL loads and stores stay in flight (an LDS-scoped fence; __syncthreads would also wait
+// vmcnt(0)).  Waves of k_cnn_train only exchange data through LDS: the slab / activation stores drain under
+// the following phases and prefetched weights (w3, w6) arrive across barriers.
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ images, const int64_t* __restrict__ tgt,
                                                  int B, const float* __restrict__ params,
@@ -196,10 +207,13 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     const unsigned long long id = static_cast<unsigned long long>(n0 + im) * F1 + j;
     S.m1[im][j] = (!training || hash_u01(seed ^ 0x27d4eb2fULL, id) >= p_drop1) ? keep1 : 0.f;
   } else if (t >= 384 && t < 384 + NI) {
-    S.valid[t - 384] = (n0 + t - 384) < B ? 1.f : 0.f;
+    const int im = t - 384;
+    const bool ok = n0 + im < B;
+    S.valid[im] = ok ? 1.f : 0.f;
+    S.label[im] = ok ? static_cast<int>(tgt[n0 + im]) : 0;
   }
   float* slab = slabs + static_cast<long>(blockIdx.x) * NSLAB;
-  __syncthreads();
+  lds_sync();
   PDE_STAMP(1);
 
   // ---- P1: conv1 (MFMA, M = (cell, tap), K = (ky, kx6) 30 -> 32, N = co) + maxpool2 + relu ----------
@@ -254,8 +268,18 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       }
     }
   }
-  __syncthreads();
+  lds_sync();
   PDE_STAMP(2);
+
+  // fc1's weights for P3 (32 per thread, 8 x 16-B L2 loads) are requested now: their latency hides under
+  // conv2 (registers: 78 -> ~110 VGPRs, no spill at 4 waves per SIMD)
+  f32x4 w3[8];
+  if (t < F1 * FC1_KC) {
+    const int j = t / FC1_KC, kc = t - j * FC1_KC;
+    const f32x4* w4 = reinterpret_cast<const f32x4*>(gFC1W + j * NIN + kc * 4);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) w3[q] = w4[q * (FC1_KC)];
+  }
 
   // ---- P2: conv2 (MFMA, M = (cell, tap) 64/image = 4 M-tiles, K = (ci,ky,kx) 250 -> 256, N = co 20 -> 32)
   //          + dropout2d + maxpool2 + relu.  One (image, M-tile) per wave iteration, both N-tiles.
@@ -290,7 +314,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       }
     }
   }
-  __syncthreads();
+  lds_sync();
   PDE_STAMP(3);
 
   // ---- P3: fc1 + relu + dropout.  Thread (j, kc): 32 weights of row j (8 x 16-B L2 loads, all in flight
@@ -300,11 +324,9 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     if (t < F1 * FC1_KC) {
       const int j = t / FC1_KC, kc = t - j * FC1_KC;
       // chunk kc = inputs {40 q + 4 kc .. +3 : q = 0..7}: the 10 chunks of a wave read 10 consecutive
-      // float4s of r2 (conflict-free), and adjacent lanes load adjacent 16 B of the weight row
-      const f32x4* w4 = reinterpret_cast<const f32x4*>(gFC1W + j * NIN + kc * 4);
-      f32x4 w[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) w[q] = w4[q * (FC1_KC)];
+      // float4s of r2 (conflict-free), and adjacent lanes load adjacent 16 B of the weight row (w3, loaded
+      // before P2)
+      const f32x4* w = w3;
       float s4[NI] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int q = 0; q < 8; ++q)
@@ -316,7 +338,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
 #pragma unroll
       for (int im = 0; im < NI; ++im) part[(kc * NI + im) * F1 + j] = s4[im];
     }
-    __syncthreads();
+    lds_sync();
     if (t < NI * F1) {
       const int im = t / F1, j = t - im * F1;
       float s1 = S.fc1b[j];
@@ -327,43 +349,62 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       S.h1d[im][j] = h * S.m1[im][j];
     }
   }
-  __syncthreads();
+  lds_sync();
   PDE_STAMP(4);
+
+  // fc1 weight columns for P6's dp2 (thread (i, jc): up to 17 rows of column i), requested now so their L2
+  // latency hides under P4 / P5
+  // (unconditional loads from clamped addresses -- no divergent branch around them, so the compiler tracks
+  // them precisely; rows past the chunk / threads past NIN x DP2_JC load a valid element P6 never uses)
+  constexpr int JPER = (F1 + DP2_JC - 1) / DP2_JC;
+  float w6[JPER];
+  {
+    const int tc = min(t, NIN * DP2_JC - 1);
+    const int jc = tc / NIN, i = tc - jc * NIN;
+#pragma unroll
+    for (int u = 0; u < JPER; ++u) w6[u] = gFC1W[min(jc * JPER + u, F1 - 1) * NIN + i];
+  }
 
   // ---- P4: fc2 logits, then log_softmax + NLL + dlogits per image ---------------------------------
   if (t < NI * F2) {
     const int im = t / F2, v = t - im * F2;
     float s = S.fc2b[v];
-#pragma unroll 10
+    // (fully unrolled, like every loop between the w6 prefetch and P6: a loop header makes the compiler wait
+    // for ALL outstanding global loads, w6 included)
+#pragma unroll
     for (int j = 0; j < F1; ++j) s += S.fc2w[v * F1 + j] * S.h1d[im][j];
     S.logit[im][v] = s;
   }
-  __syncthreads();
+  lds_sync();
   PDE_STAMP(5);
   float loss_acc = 0.f;
   if (t < NI) {
     const int im = t;
     float m = S.logit[im][0];
+#pragma unroll
     for (int v = 1; v < F2; ++v) m = fmaxf(m, S.logit[im][v]);
     float se = 0.f;
+#pragma unroll
     for (int v = 0; v < F2; ++v) se += __expf(S.logit[im][v] - m);
     const float lse = m + __logf(se);
     const float val = S.valid[im];
-    const int y = val > 0.f ? static_cast<int>(tgt[n0 + im]) : 0;
+    const int y = S.label[im];  // (loaded in P0: a global load here would wait behind the w6 prefetch)
     loss_acc = val * (lse - S.logit[im][y]);
     const float inv_b = val / static_cast<float>(B);
+#pragma unroll
     for (int v = 0; v < F2; ++v) S.dlog[im][v] = (__expf(S.logit[im][v] - lse) - (v == y ? 1.f : 0.f)) * inv_b;
   }
-  __syncthreads();
+  lds_sync();
   PDE_STAMP(6);
 
   // ---- P5: fc2 backward; dh = relu'(h1) * mask * (W2^T dlog) ------------------------------------
-  for (int i = t; i < FC2N; i += T) {
-    const int v = i / F1, j = i - v * F1;
+  static_assert(FC2N <= T, "fc2 weight gradient: one element per thread");
+  if (t < FC2N) {
+    const int v = t / F1, j = t - v * F1;
     float s = 0.f;
 #pragma unroll
     for (int im = 0; im < NI; ++im) s += S.dlog[im][v] * S.h1d[im][j];
-    slab[S_FC2W + i] = s;
+    slab[S_FC2W + t] = s;
   }
   if (t < F2) {
     float s = 0.f;
@@ -378,7 +419,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     for (int v = 0; v < F2; ++v) s += S.fc2w[v * F1 + j] * S.dlog[im][v];
     S.dh[im][j] = (S.h1[im][j] > 0.f) ? s * S.m1[im][j] : 0.f;
   }
-  __syncthreads();
+  lds_sync();
   PDE_STAMP(7);
 
   // ---- P6: fc1 backward: dH / R2 columns for the batch-wide dW GEMM (k_cnn_reduce), db to the slab, and
@@ -402,11 +443,8 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   float* dpart = reinterpret_cast<float*>(&S.w2f[0][0][0]);  // [jc][im][i]
   if (t < NIN * DP2_JC) {  // thread (i, jc): sum over fc1 outputs j in chunk jc (column loads coalesced)
     const int jc = t / NIN, i = t - jc * NIN;
-    constexpr int JPER = (F1 + DP2_JC - 1) / DP2_JC;
     const int j0 = jc * JPER, j1 = min(F1, j0 + JPER);
-    float w[JPER];
-#pragma unroll
-    for (int u = 0; u < JPER; ++u) w[u] = j0 + u < j1 ? gFC1W[(j0 + u) * NIN + i] : 0.f;
+    const float* w = w6;  // loaded before P4
     float s4[NI] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < JPER; ++u)
@@ -416,7 +454,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
 #pragma unroll
     for (int im = 0; im < NI; ++im) dpart[(jc * NI + im) * NIN + i] = s4[im];
   }
-  __syncthreads();
+  lds_sync();
   for (int it = t; it < NI * NIN; it += T) {
     const int im = it / NIN, i = it - im * NIN, co = i / NC2;
     float s1 = 0.f;
@@ -424,7 +462,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     for (int jc = 0; jc < DP2_JC; ++jc) s1 += dpart[(jc * NI + im) * NIN + i];
     S.dp2[im][i] = (S.r2[im][i] > 0.f) ? s1 * S.mc2[im][co] : 0.f;
   }
-  __syncthreads();
+  lds_sync();
   // scatter dp2 to the argmax taps (both layouts; every tap of every window is written); conv2 bias
   // grad alongside
   for (int it = t; it < NI * NIN; it += T) {
@@ -447,7 +485,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       for (int c = 0; c < NC2; ++c) s += S.dp2[im][co * NC2 + c];
     slab[O_B2 + co] = s;
   }
-  __syncthreads();
+  lds_sync();
   PDE_STAMP(8);
 
   // ---- P7a: conv2 wgrad (MFMA): dW2[co][(ci,ky,kx)] = sum_(im,y,x) d2[co][y][x] * r1[ci][y+ky][x+kx].
@@ -556,7 +594,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       }
     }
   }
-  __syncthreads();
+  lds_sync();
   PDE_STAMP(10);
 
   // ---- P9: conv1 wgrad (MFMA): dW1[co][(ky,kx)] = sum_(im,y,x) dconv1[co][y][x] * x[y+ky][x+kx], with
@@ -607,11 +645,11 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
         acc[u] = mfma(a, b, acc[u]);
       }
     }
-    __syncthreads();  // w2f / w2d are dead after P7b: reuse them for the per-wave partials
+    lds_sync();  // w2f / w2d are dead after P7b: reuse them for the per-wave partials
     f32x4* part = reinterpret_cast<f32x4*>(&S.w2f[0][0][0]);
     part[(wid * 2 + 0) * 64 + lane] = acc[0];
     part[(wid * 2 + 1) * 64 + lane] = acc[1];
-    __syncthreads();
+    lds_sync();
     if (t < W1N) {
       const int c = t / 25, kidx = t - c * 25, u = kidx >> 4;
       const int l = (c >> 2) * 16 + (kidx & 15), r = c & 3;
