@@ -53,7 +53,11 @@ constexpr int KSW2 = NI * 8 * 8 / 32;           // 8 conv2-wgrad k-steps: K = (i
 constexpr int CG = 3;                                // co groups of 8 per tap
 constexpr int NGD = KS * KS * CG;                    // 75 (tap, co-group) pairs
 constexpr int KSD = (NGD + 3) / 4;                   // 19 k-steps (25 with one k-step per tap)
-constexpr int C2P = 40;  // 80-byte rows: a ds_read_b128 lane octet spans all 64 banks (conflict-free)
+#ifndef PDE_CNN_C2P
+#define PDE_CNN_C2P 40
+#endif
+constexpr int C2P = PDE_CNN_C2P;  // 80-byte rows: a ds_read_b128 lane octet spans all 64 banks (conflict-free)
+static_assert(C2P >= 24 && C2P % 8 == 0, "d2n rows: co padded to >= 24, 16-byte aligned");
 constexpr int D2R = O2 * O2 + 8;       // d2 plane row stride (u16): 144 B
 constexpr int MT1 = O1 * O1 / 16;      // 36 conv1 M-tiles per image (4 cells x 4 taps each)
 constexpr int MTD = NC1 * 1 / 16;      // 9 conv2-dgrad M-tiles per image (144 r1 positions)
