@@ -584,6 +584,9 @@ __device__ __forceinline__ bool bn_group_last(int* gticket, int G, int* s_flag) 
   return *s_flag != 0;
 }
 
+// RC > 0: a thread's rows of the chunk (<= RC of them) stay in registers from the statistics pass to the apply
+// pass, and the residual rows are requested before the finalize wait (micro-batch sized tensors).
+template <int RC>
 __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
     uint16_t* x, int P, int C, int rpb, float* __restrict__ ws, int* __restrict__ tickets,
     uint32_t* __restrict__ flags, int* __restrict__ err, const float* __restrict__ gamma,
@@ -618,10 +621,53 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
   }
   bn_gen_start(flags + blockIdx.y, &s_gen);
   const int r1 = min(P, (blockIdx.x + 1) * rpb);
+  const int r0 = blockIdx.x * rpb + tr;
   float s1[8], s2[8], piv[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = piv[j] = 0.f;
-  if (cok && slabs != nullptr) {
+  u16x8 cx[RC > 0 ? RC : 1], cq[RC > 0 ? RC : 1];  // RC: the thread's x rows / residual rows
+  if constexpr (RC > 0) {
+    if (cok && slabs != nullptr) {
+      slab_row8(slabs, slab_zs, splits, c0, piv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) piv[j] = bf2f(f2bf(piv[j]));
+#pragma unroll
+      for (int k = 0; k < RC; ++k) {
+        const int r = r0 + k * kBnRows;
+        if (r < r1) {
+          float v[8];
+          slab_row8(slabs, slab_zs, splits, static_cast<long>(r) * C + c0, v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            cx[k][j] = f2bf(v[j]);
+            const float d = bf2f(cx[k][j]) - piv[j];
+            s1[j] += d;
+            s2[j] += d * d;
+          }
+          *reinterpret_cast<u16x8*>(x + static_cast<long>(r) * C + c0) = cx[k];
+        }
+      }
+    } else if (cok) {
+      load8(x + c0, piv);
+#pragma unroll
+      for (int k = 0; k < RC; ++k) {  // every load in flight, then the sums
+        const int r = r0 + k * kBnRows;
+        if (r < r1) cx[k] = *reinterpret_cast<const u16x8*>(x + static_cast<long>(r) * C + c0);
+      }
+#pragma unroll
+      for (int k = 0; k < RC; ++k)
+        if (r0 + k * kBnRows < r1)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { const float d = bf2f(cx[k][j]) - piv[j]; s1[j] += d; s2[j] += d * d; }
+    }
+    if (cok && res != nullptr) {  // independent of the statistics: requested before the finalize wait
+#pragma unroll
+      for (int k = 0; k < RC; ++k) {
+        const int r = r0 + k * kBnRows;
+        if (r < r1) cq[k] = *reinterpret_cast<const u16x8*>(res + static_cast<long>(r) * C + c0);
+      }
+    }
+  } else if (cok && slabs != nullptr) {
     // x = bf16(sum_z slab_z) in z order (== the GEMM's own reduction), written here, its statistics taken
     // from the rounded values; the pivot (row 0) is recomputed from the slabs by every block
     const long zs = slab_zs;
@@ -717,7 +763,25 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
   float sc[8], sh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; }
-  int r = blockIdx.x * rpb + tr;
+  if constexpr (RC > 0) {
+#pragma unroll
+    for (int k = 0; k < RC; ++k) {
+      const int r = r0 + k * kBnRows;
+      if (r < r1) {
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float t = bf2f(cx[k][j]) * sc[j] + sh[j];
+          if (res) t += bf2f(cq[k][j]);
+          if (relu) t = fmaxf(t, 0.f);
+          o[j] = f2bf(t);
+        }
+        *reinterpret_cast<u16x8*>(y + static_cast<long>(r) * C + c0) = o;
+      }
+    }
+    return;
+  }
+  int r = r0;
   constexpr int U = 4;
   for (; r + (U - 1) * kBnRows < r1; r += U * kBnRows) {
     u16x8 u[U], q[U];
@@ -1378,10 +1442,18 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
     uint32_t* fl = bn_flags(ncg * groups, s);  // generation flags of the (group, channel group)s
     int* gt = groups > 1 ? bn_tickets(ncg, s) : nullptr;
     if (tk != nullptr && fl != nullptr && (groups == 1 || (gt != nullptr && gscratch != nullptr))) {
-      hipLaunchKernelGGL(k_bn_fwd_fused, dim3(nrb1, ncg, groups), dim3(kBnThreads), 0, s, const_cast<uint16_t*>(x),
-                         Pg, C, rpb, ws, tk, fl, err, gamma, beta, eps, momentum, running_mean, running_var, save_mean,
-                         save_invstd, scale_shift, scale_shift + C, res, relu, y, slabs, splits,
-                         static_cast<long>(P) * C, gscratch, gt);
+      // rows per thread of a chunk: few enough -> kept in registers for the apply pass (PDE_BN_FWD_RC=0: off)
+      static const bool rc_on = !(std::getenv("PDE_BN_FWD_RC") && std::getenv("PDE_BN_FWD_RC")[0] == '0');
+      if (rc_on && ceil_div(rpb, kBnRows) <= 4)
+        hipLaunchKernelGGL(k_bn_fwd_fused<4>, dim3(nrb1, ncg, groups), dim3(kBnThreads), 0, s,
+                           const_cast<uint16_t*>(x), Pg, C, rpb, ws, tk, fl, err, gamma, beta, eps, momentum,
+                           running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C, res,
+                           relu, y, slabs, splits, static_cast<long>(P) * C, gscratch, gt);
+      else
+        hipLaunchKernelGGL(k_bn_fwd_fused<0>, dim3(nrb1, ncg, groups), dim3(kBnThreads), 0, s,
+                           const_cast<uint16_t*>(x), Pg, C, rpb, ws, tk, fl, err, gamma, beta, eps, momentum,
+                           running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C, res,
+                           relu, y, slabs, splits, static_cast<long>(P) * C, gscratch, gt);
       return hipGetLastError();
     }
   }
