@@ -173,10 +173,23 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   const int n0 = blockIdx.x * NI;
 
   // ---- P0: images -> bf16, weights -> bf16 MFMA fragments, fp32 head weights, dropout masks ------
-  for (int i = t; i < NI * NX / 4; i += T) {
-    const int im = (i * 4) / NX, off = i * 4 - im * NX, n = n0 + im;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (n < B) v = *reinterpret_cast<const f32x4*>(images + static_cast<long>(n) * NX + off);
+  // every global load of the phase is issued first (unconditional, clamped addresses): the conv weight
+  // fragments (3 x 16 B per thread), then the image quad.  Only conv1's fragment (w1f) is stored to LDS now;
+  // conv2's forward / dgrad fragments stay in registers until the end of P1, so their latency is not on P0's
+  // critical path.
+  // (vmcnt retires loads in issue order: the loads P0 itself consumes -- images, the third fragment slot that
+  // holds w1f, the head parameters -- are issued before the two deferred fragment slots, at the end of P0)
+  static_assert(NI * NX / 4 <= T, "one image quad per thread");
+  const int qi = min(t, NI * NX / 4 - 1);
+  const int qim = (qi * 4) / NX, qoff = qi * 4 - qim * NX;
+  constexpr int FPER = (NFRAG + T - 1) / T;
+  static_assert(FPER == 3 && NFRAG - 64 >= 2 * T, "w1f (the last 64 fragments) lies in the third slot");
+  u16x8 fr[FPER];
+  fr[2] = frag[min(t + 2 * T, NFRAG - 1)];
+  f32x4 img = *reinterpret_cast<const f32x4*>(images + static_cast<long>(min(n0 + qim, B - 1)) * NX + qoff);
+  if (t < NI * NX / 4) {
+    const int im = qim, off = qoff, n = n0 + im;
+    const f32x4 v = n < B ? img : f32x4{0.f, 0.f, 0.f, 0.f};
     uint16_t* dst = &S.x[im][off];
     const uint16_t b0 = f2bf(v[0]), b1 = f2bf(v[1]), b2 = f2bf(v[2]), b3 = f2bf(v[3]);
     dst[0] = b0; dst[1] = b1; dst[2] = b2; dst[3] = b3;
@@ -185,10 +198,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     d1[0] = b1; d1[1] = b2; d1[2] = b3;
   }
   if (t < NI) S.x1[t][NX - 1] = 0;
-  {  // weight fragments, pre-laid-out in bf16 MFMA order by k_cnn_prep: straight 16-byte copies
-    u16x8* dst = &S.w2f[0][0][0];
-    for (int e = t; e < NFRAG; e += T) dst[e] = frag[e];
-  }
+  if (t + 2 * T < NFRAG) (&S.w2f[0][0][0])[t + 2 * T] = fr[2];  // the third slot: w2d tail and w1f (conv1)
   constexpr int PADG = (C2P - 16) / 8;  // co padding groups of 8 (co 16..C2P-1; 16..19 rewritten per step)
   for (int i = t; i < NI * O2 * O2 * PADG; i += T) {
     const int pos = i / PADG, h = i - pos * PADG;
@@ -217,6 +227,8 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     S.label[im] = ok ? static_cast<int>(tgt[n0 + im]) : 0;
   }
   float* slab = slabs + static_cast<long>(blockIdx.x) * NSLAB;
+  fr[0] = frag[t];  // conv2 fragment slots 0 / 1: stored to LDS at the end of P1
+  fr[1] = frag[t + T];
   lds_sync();
   PDE_STAMP(1);
 
@@ -271,6 +283,11 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
         S.r1n[im][c0 + lg][co] = 0;  // ci padding 10..15
       }
     }
+  }
+  {  // conv2 forward / dgrad fragments (loaded in P0): pre-laid-out bf16 MFMA order, straight 16-byte stores
+    u16x8* dst = &S.w2f[0][0][0];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) dst[t + u * T] = fr[u];
   }
   lds_sync();
   PDE_STAMP(2);
