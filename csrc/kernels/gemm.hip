@@ -1502,6 +1502,11 @@ hipError_t gemm_reduce_jobs(const ReduceJob* jobs, int n, hipStream_t s) {
   return hipGetLastError();
 }
 
+bool pair_balance_on() {  // opt-in (PDE_GEMM_PAIR_BALANCE=1): measured slower, r3s (more slab traffic)
+  static const bool on = std::getenv("PDE_GEMM_PAIR_BALANCE") && std::getenv("PDE_GEMM_PAIR_BALANCE")[0] == '1';
+  return on;
+}
+
 bool gemm_pair_enabled() {
   static const bool on = !(std::getenv("PDE_GEMM_PAIR") && std::getenv("PDE_GEMM_PAIR")[0] == '0');
   return on;
@@ -1535,6 +1540,27 @@ hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s,
                   pair_member_plan(a0, d.tm[0], d.tn[0], d.kps[0], sp0, d.av[0], d.bv[0]) &&
                   pair_member_plan(a1, d.tm[1], d.tn[1], d.kps[1], sp1, d.av[1], d.bv[1]) &&
                   (sp0 == 1 || reduce_vec_ok(a0)) && (sp1 == 1 || reduce_vec_ok(a1));
+  if (ok && pair_balance_on()) {
+    // a paired launch lasts as long as its longest K slice: while one member's slices are >= 2x the other's,
+    // split it further (within its workspace, <= 64 MB of slabs): e.g. layer4's 3x3 dgrad (36 K-tiles per
+    // slice at split 4) next to its weight gradient (16)
+    for (int it = 0; it < 4; ++it) {
+      const int kt0 = d.kps[0] / 32, kt1 = d.kps[1] / 32;
+      const int w = kt0 >= 2 * kt1 ? 0 : (kt1 >= 2 * kt0 ? 1 : -1);
+      if (w < 0) break;
+      const GemmArgs& a = w ? a1 : a0;
+      int& sp = w ? sp1 : sp0;
+      int nsp = sp * 2;
+      if (a.workspace == nullptr || nsp > a.splitk || static_cast<long>(nsp) * a.M * a.N * 4 > (64L << 20) ||
+          !reduce_vec_ok(a))
+        break;
+      const int kps = ceil_div(ceil_div(a.K, nsp), 32) * 32;
+      nsp = ceil_div(a.K, kps);
+      if (nsp <= sp) break;
+      sp = nsp;
+      d.kps[w] = kps;
+    }
+  }
   const int k0 = ok ? kind_code_of(a0) : -1, k1 = ok ? kind_code_of(a1) : -1;
   d.nz[0] = sp0;
   d.nz[1] = sp1;
