@@ -326,8 +326,23 @@ __device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], con
     const int q = tid >> 6, ch = tid & 63;
     float a1 = 0.f, a2 = 0.f;
     if (cbase + ch < C) {
-      // 8 chunks per trip with all 16 loads issued before the adds (the tail is latency-bound)
+      // KT chunks per trip with all 2 KT loads issued before the adds (the tail is latency-bound): up to 256
+      // chunks (kBnQ = 8 lanes per channel) in ONE round trip
+      constexpr int KT = 32;
       int b = q;
+      for (; b + (KT - 1) * kBnQ < nrb; b += KT * kBnQ) {
+        float u1[KT], u2[KT];
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+          u1[k] = ws[(static_cast<long>(b + kBnQ * k) * 2) * C + cbase + ch];
+          u2[k] = ws[(static_cast<long>(b + kBnQ * k) * 2 + 1) * C + cbase + ch];
+        }
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+          a1 += u1[k];
+          a2 += u2[k];
+        }
+      }
       for (; b + 7 * kBnQ < nrb; b += 8 * kBnQ) {
         float u1[8], u2[8];
 #pragma unroll
