@@ -1113,6 +1113,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("groups") = 1);
   // 1 if a one-launch BatchNorm wait timed out since the last reset (synchronises the device)
   m.def("bn_error", [](bool reset) { return pde::bn_error(reset ? 1 : 0); }, py::arg("reset") = true);
+  m.def("cnn_tail_error", [](bool reset) { return pde::cnn_tail_error(reset ? 1 : 0); }, py::arg("reset") = true);
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("mean"), py::arg("invstd"),
         py::arg("gamma"), py::arg("relu"), py::arg("want_dres"), py::arg("dg_out") = py::none(),

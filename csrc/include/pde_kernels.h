@@ -248,6 +248,8 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
                            const XgmiView* xv = nullptr, float xscale = 1.f);
 // params -= lr * gscale * grads (plain SGD) and the matching fragment-image refresh, one launch (used
 // after the gradient all-reduce when world > 1).
+// 1 when the single-process fused tail's grid barrier timed out (PDE_CNN_FUSED_TAIL); reset clears it
+int cnn_tail_error(int reset);
 hipError_t cnn_sgd_fused(float* params, const float* grads, const float* hp, void* frag, hipStream_t s,
                          int* step = nullptr);  // step: the optimiser's device step counter (+1 per call)
 

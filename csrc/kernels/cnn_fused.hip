@@ -147,13 +147,65 @@ __device__ __forceinline__ void lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// Single-process fused tail (cnn_train_fused with PDE_CNN_FUSED_TAIL): after P9 every workgroup of k_cnn_train
+// meets at a grid barrier and the first RED_BLOCKS of them run k_cnn_reduce's roles (slab columns, fc1
+// weight-gradient tiles, loss, SGD + fragment refresh) -- one launch per step instead of two, and no kernel
+// boundary between the slabs' producers and their reducers.  Requires every workgroup resident at once (one
+// 157 KB-LDS workgroup per CU: nwg <= CUs, checked on the host) and nothing else on the device: the barrier's
+// bounded spin (2 s) sets `err` instead of hanging if that is ever violated.
+struct CnnTail {
+  const float* gscale;
+  float* grads;
+  float* loss;
+  unsigned long long* rng;
+  float* params;
+  const float* hp;
+  uint16_t* frag;
+  int* step;
+  unsigned* bar;  // [0] arrival counter, [1] generation
+  int* err;
+  int accumulate, B, on, pad;
+};
+__device__ void cnn_fused_tail(const CnnTail& tl, int rb, f32x4* part, uint32_t* s_epoch, int* s_fail,
+                               const float* slabs, int nwg, const float* acts, const float* loss_part);
+
+// Grid barrier over co-resident workgroups: every wave's global stores complete, one agent-scope release +
+// arrival per workgroup; the last arrival resets the counter and bumps the generation; the others poll it
+// (bounded), then acquire.
+__device__ __forceinline__ void cnn_grid_barrier(unsigned* bar, unsigned n, int* err, unsigned* s_gen) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned g0 = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned old = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == n - 1) {
+      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+      __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    *s_gen = g0;
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ images, const int64_t* __restrict__ tgt,
                                                  int B, const float* __restrict__ params,
                                                  const u16x8* __restrict__ frag,
                                                  const unsigned long long* __restrict__ rng, float p_drop2,
                                                  float p_drop1, int training, float* __restrict__ slabs,
                                                  float* __restrict__ loss_part, float* __restrict__ acts,
-                                                 unsigned long long* __restrict__ stamps, int stop_after) {
+                                                 unsigned long long* __restrict__ stamps, int stop_after,
+                                                 CnnTail tail) {
   // optional phase timestamps (diagnostic only: stamps == nullptr in production launches); stop_after = k
   // ends the kernel after phase stamp k (diagnostic: hardware counters of a kernel prefix)
 #define PDE_STAMP(k)                                                                      \
@@ -698,6 +750,15 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     __syncthreads();
     PDE_STAMP(12);
   }
+  if (tail.on) {  // single process: the reduction roles in this launch (see CnnTail)
+    __shared__ uint32_t s_epoch;
+    __shared__ int s_fail;
+    __shared__ unsigned s_gen;
+    cnn_grid_barrier(tail.bar, gridDim.x, tail.err, &s_gen);
+    // (w2f / w2d are dead after P9: the roles' 8 KB of partials live there)
+    cnn_fused_tail(tail, blockIdx.x, reinterpret_cast<f32x4*>(&S.w2f[0][0][0]), &s_epoch, &s_fail, slabs,
+                   gridDim.x, acts, loss_part);
+  }
 }
 
 // The conv weights in bf16 MFMA B-fragment order (conv2 fwd [ks][ntile][lane], conv2 dgrad [tap][lane],
@@ -792,29 +853,32 @@ __device__ __forceinline__ void sgd_update(float* params, const float* hp, uint1
   write_frag(frag, p, w);
 }
 
-__global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ slabs, int nwg,
-                                                      const float* __restrict__ acts,
-                                                      const float* __restrict__ gscale, float* __restrict__ grads,
-                                                      int accumulate, const float* __restrict__ loss_part, int B,
-                                                      float* __restrict__ loss, unsigned long long* __restrict__ rng,
-                                                      float* __restrict__ params, const float* __restrict__ hp,
-                                                      uint16_t* __restrict__ frag, int* __restrict__ step,
-                                                      XgmiView xv, float xscale) {
-  __shared__ f32x4 part[RED_LANES][RED_COLS];  // slab: [lane][column]; fc1: [wave][lane] (same 8 KB)
-  __shared__ uint32_t s_epoch;
-  __shared__ int s_fail;
+// One reduction role (rb = role block: slab columns for rb < RED_SLAB_BLOCKS, else an fc1 weight-gradient
+// tile; role 0 also reduces the loss partials and advances the dropout RNG / SGD step counters), run by the
+// first RED_T threads of a block whose every thread calls it (block barriers inside).  Called by k_cnn_reduce
+// (one role per block) and, single process, by k_cnn_train's workgroups after a grid barrier.
+__device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s_epoch, int* s_fail,
+                                                const float* __restrict__ slabs, int nwg,
+                                                const float* __restrict__ acts, const float* __restrict__ gscale,
+                                                float* __restrict__ grads, int accumulate,
+                                                const float* __restrict__ loss_part, int B, float* __restrict__ loss,
+                                                unsigned long long* __restrict__ rng, float* __restrict__ params,
+                                                const float* __restrict__ hp, uint16_t* __restrict__ frag,
+                                                int* __restrict__ step, const XgmiView& xv, float xscale) {
+  const int tid = threadIdx.x;
+  const bool act = tid < RED_T;  // (k_cnn_train's threads past RED_T only join the barriers)
   const float gs = gscale ? gscale[0] : 1.f;
   // world > 1 with a peer view: this block's gradients go through the one-shot xGMI exchange (stage to my
   // slot, flags, read all ranks' values in rank order, x xscale) before the store + SGD update
   const bool xchg = xv.size > 1;
-  const uint32_t epoch = xchg ? xgmi_epoch(xv, blockIdx.x, &s_epoch) : 0u;
+  const uint32_t epoch = xchg ? xgmi_epoch(xv, rb, s_epoch) : 0u;
   float* xmine = xchg ? xgmi_slot(xv, xv.rank, epoch) : nullptr;
-  if (blockIdx.x < RED_SLAB_BLOCKS) {
-    const int col = threadIdx.x % RED_COLS, sl = threadIdx.x / RED_COLS;
-    const int c4 = blockIdx.x * RED_COLS + col;
+  if (rb < RED_SLAB_BLOCKS) {
+    const int col = tid % RED_COLS, sl = tid / RED_COLS;
+    const int c4 = rb * RED_COLS + col;
     const f32x4* s4 = reinterpret_cast<const f32x4*>(slabs);
     f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
-    if (c4 < NSLAB4) {
+    if (act && c4 < NSLAB4) {
       int b = sl;
       for (; b + 7 * RED_LANES < nwg; b += 8 * RED_LANES) {  // 8 independent loads in flight
         f32x4 v[8];
@@ -827,21 +891,21 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
       }
       for (; b < nwg; b += RED_LANES) a0 += s4[static_cast<long>(b) * NSLAB4 + c4];
     }
-    part[sl][col] = (a0 + a1) + (a2 + a3);
+    if (act) part[sl * RED_COLS + col] = (a0 + a1) + (a2 + a3);
     __syncthreads();
-    const bool owner = sl == 0 && c4 < NSLAB4;
+    const bool owner = act && sl == 0 && c4 < NSLAB4;
     const int p4 = c4 < O_FC1W / 4 ? c4 : c4 + FC1N / 4;  // slab column -> parameter float4
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (owner) {
-      v = part[0][col];
+      v = part[col];
 #pragma unroll 8
-      for (int k = 1; k < RED_LANES; ++k) v += part[k][col];
+      for (int k = 1; k < RED_LANES; ++k) v += part[k * RED_COLS + col];
       v *= gs;
       if (xchg) reinterpret_cast<f32x4*>(xmine)[p4] = v;
     }
     bool ok = true;
     if (xchg) {
-      ok = xgmi_publish_and_wait(xv, blockIdx.x, epoch, &s_fail);
+      ok = xgmi_publish_and_wait(xv, rb, epoch, s_fail);
       if (owner && ok) {
         f32x4 r4[kXgmiMaxRanks];
 #pragma unroll
@@ -853,7 +917,7 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
           if (r < xv.size) v += r4[r];
         v *= xscale;
       }
-      xgmi_finish(xv, blockIdx.x, epoch);
+      xgmi_finish(xv, rb, epoch);
     }
     if (owner && ok) {
       f32x4* g4 = reinterpret_cast<f32x4*>(grads) + p4;
@@ -865,12 +929,12 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
       }
     }
   } else {
-    const int fb = blockIdx.x - RED_SLAB_BLOCKS;
+    const int fb = rb - RED_SLAB_BLOCKS;
     const int j0 = (fb / FC1_IT) * 16, i0 = (fb % FC1_IT) * 16;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, lr = lane & 15, lg = lane >> 4;
+    const int lane = tid & 63, wid = tid >> 6, lr = lane & 15, lg = lane >> 4;
     const int Bk = nwg * NI;
     const int kper = ((Bk + 8 * 16 - 1) / (8 * 16)) * 16;  // this wave's K slice, a multiple of 16
-    const int k0 = wid * kper, k1 = min(Bk, k0 + kper);
+    const int k0 = wid * kper, k1 = act ? min(Bk, k0 + kper) : k0;
     const bool jv = j0 + lr < F1;
     const float* arow = acts + static_cast<long>(jv ? j0 + lr : 0) * Bk;
     const float* brow = acts + static_cast<long>(F1 + i0 + lr) * Bk;
@@ -893,8 +957,8 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
         acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][3], b[c][3], acc1, 0, 0, 0);
       }
     }
-    f32x4* wpart = &part[0][0];
-    wpart[wid * 64 + lane] = acc0 + acc1;
+    f32x4* wpart = part;
+    if (act) wpart[wid * 64 + lane] = acc0 + acc1;
     __syncthreads();
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     const int i = i0 + lr;
@@ -913,7 +977,7 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
     }
     bool ok = true;
     if (xchg) {
-      ok = xgmi_publish_and_wait(xv, blockIdx.x, epoch, &s_fail);
+      ok = xgmi_publish_and_wait(xv, rb, epoch, s_fail);
       if (wid == 0 && ok) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -930,7 +994,7 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
           v[r] = g * xscale;
         }
       }
-      xgmi_finish(xv, blockIdx.x, epoch);
+      xgmi_finish(xv, rb, epoch);
     }
     if (wid == 0 && ok) {
 #pragma unroll
@@ -946,8 +1010,8 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
       }
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x >= RED_T - 64) {  // last wave: loss
-    const int lane = threadIdx.x - (RED_T - 64);
+  if (rb == 0 && tid >= RED_T - 64 && tid < RED_T) {  // role 0's last active wave: loss
+    const int lane = tid - (RED_T - 64);
     float s = 0.f;
     for (int b = lane; b < nwg; b += 64) s += loss_part[b];
     s = wave_sum(s);
@@ -959,9 +1023,82 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
   }
 }
 
+__global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ slabs, int nwg,
+                                                      const float* __restrict__ acts,
+                                                      const float* __restrict__ gscale, float* __restrict__ grads,
+                                                      int accumulate, const float* __restrict__ loss_part, int B,
+                                                      float* __restrict__ loss, unsigned long long* __restrict__ rng,
+                                                      float* __restrict__ params, const float* __restrict__ hp,
+                                                      uint16_t* __restrict__ frag, int* __restrict__ step,
+                                                      XgmiView xv, float xscale) {
+  __shared__ f32x4 part[RED_LANES * RED_COLS];  // slab: [lane][column]; fc1: [wave][lane] (same 8 KB)
+  __shared__ uint32_t s_epoch;
+  __shared__ int s_fail;
+  cnn_reduce_role(blockIdx.x, part, &s_epoch, &s_fail, slabs, nwg, acts, gscale, grads, accumulate, loss_part, B,
+                  loss, rng, params, hp, frag, step, xv, xscale);
+}
+
+__device__ void cnn_fused_tail(const CnnTail& tl, int rb, f32x4* part, uint32_t* s_epoch, int* s_fail,
+                               const float* slabs, int nwg, const float* acts, const float* loss_part) {
+  if (rb >= RED_BLOCKS) return;  // block-uniform: workgroups past the roles are done
+  XgmiView one{};
+  one.size = 1;
+  cnn_reduce_role(rb, part, s_epoch, s_fail, slabs, nwg, acts, tl.gscale, tl.grads, tl.accumulate, loss_part, tl.B,
+                  tl.loss, tl.rng, tl.params, tl.hp, tl.frag, tl.step, one, 1.f);
+}
+
 }  // namespace
 
 int cnn_num_params() { return NPARAM; }
+// PDE_CNN_FUSED_TAIL=1: the single-process reduction inside k_cnn_train (CnnTail).  Off: measured SLOWER
+// (r3v: 0.054 vs 0.041 ms/step) -- the grid barrier's agent-scope release / acquire in every workgroup writes
+// back and invalidates the L2 of all 8 XCDs 256 times, where the kernel boundary does it once.
+bool cnn_fused_tail_enabled() {
+  const char* e = std::getenv("PDE_CNN_FUSED_TAIL");
+  return e != nullptr && e[0] == '1';
+}
+int cnn_device_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    hipDeviceProp_t prop{};
+    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+              ? prop.multiProcessorCount : -1;
+  }
+  return cus;
+}
+// The barrier's counter / generation words and error flag: one zeroed allocation per device, made outside any
+// graph capture (until then the two-launch form runs).
+bool cnn_barrier_words(hipStream_t s, unsigned** bar, int** err) {
+  static unsigned* base[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  if (base[dev] == nullptr) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return false;
+    void* p = nullptr;
+    if (hipMalloc(&p, 64) != hipSuccess) return false;
+    if (hipMemset(p, 0, 64) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(p);
+      return false;
+    }
+    base[dev] = static_cast<unsigned*>(p);
+  }
+  *bar = base[dev];
+  *err = reinterpret_cast<int*>(base[dev] + 4);
+  return true;
+}
+int cnn_tail_error(int reset) {
+  unsigned* bar = nullptr;
+  int* err = nullptr;
+  if (!cnn_barrier_words(nullptr, &bar, &err)) return 0;
+  int v = 0;
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&v, err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  if (reset && v != 0) (void)hipMemset(err, 0, sizeof(int));
+  return v;
+}
+
 size_t cnn_frag_bytes() { return sizeof(u16x8) * NFRAG; }
 size_t cnn_smem_bytes() { return sizeof(CnnSmem); }
 int cnn_images_per_workgroup() { return NI; }
@@ -996,12 +1133,22 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
   if (prep)
     hipLaunchKernelGGL(k_cnn_prep, dim3(ceil_div(NFRAG, 256)), dim3(256), 0, s, params, static_cast<u16x8*>(frag));
   if (reinterpret_cast<uintptr_t>(acts) & 15) return hipErrorInvalidValue;
+  CnnTail tail{};
+  unsigned* bar = nullptr;
+  int* berr = nullptr;
+  if (view.size == 1 && stamps == nullptr && stop_after < 0 && cnn_fused_tail_enabled() && nwg >= RED_BLOCKS &&
+      nwg <= cnn_device_cus() && cnn_barrier_words(s, &bar, &berr)) {
+    tail.gscale = gscale; tail.grads = grads; tail.loss = loss; tail.rng = rng; tail.params = params;
+    tail.hp = sgd_hp; tail.frag = static_cast<uint16_t*>(frag); tail.step = sgd_step; tail.bar = bar;
+    tail.err = berr; tail.accumulate = accumulate; tail.B = B; tail.on = 1;
+  }
   hipLaunchKernelGGL(k_cnn_train, dim3(nwg), dim3(T), sm, s, images, tgt, B, params,
                      static_cast<const u16x8*>(frag), rng, p_drop2, p_drop1, training, slabs, loss_part, acts, stamps,
-                     stop_after);
-  hipLaunchKernelGGL(k_cnn_reduce, dim3(RED_BLOCKS), dim3(RED_T), 0, s, slabs, nwg, acts, gscale, grads,
-                     accumulate, loss_part, B, loss, rng, params, sgd_hp, static_cast<uint16_t*>(frag), sgd_step,
-                     view, xscale);
+                     stop_after, tail);
+  if (!tail.on)
+    hipLaunchKernelGGL(k_cnn_reduce, dim3(RED_BLOCKS), dim3(RED_T), 0, s, slabs, nwg, acts, gscale, grads,
+                       accumulate, loss_part, B, loss, rng, params, sgd_hp, static_cast<uint16_t*>(frag), sgd_step,
+                       view, xscale);
   return hipGetLastError();
 }
 

@@ -534,3 +534,35 @@ def test_fused_mlp_folded_adam_matches_separate_step(gpu):
     # elements (scripts/diag_fold_opt.py: 1e-9 after one step), which later steps' gradients carry along
     assert all(abs(a - b) <= 1e-5 * abs(b) for a, b in zip(l0, l1)), (l0, l1)
     assert rel_err(f1, f0) < 1e-5 and rel_err(m1, m0) < 1e-3 and rel_err(c1, c0) < 1e-3
+
+
+def test_fused_cnn_single_launch_tail_matches_two_launches(gpu, monkeypatch):
+    """PDE_CNN_FUSED_TAIL=1 (single process): k_cnn_train runs the slab reduction, the fc1 weight-gradient tiles,
+    the loss and the SGD + fragment refresh itself after a grid barrier -- one launch per step.  Same reduction
+    code in the same order as k_cnn_reduce: losses, gradients, weights and the dropout stream (training mode)
+    must match the two-launch step bit for bit over several steps, and the barrier must never time out."""
+    from pytorch_distributed_examples_amd import _native
+    from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
+    from pytorch_distributed_examples_amd.ops.optim import FusedSGD
+
+    torch.manual_seed(0)
+    base = Net().to(gpu).train()
+    x = torch.randn(4, 1024, 1, 28, 28, device=gpu)
+    y = torch.randint(0, 10, (4, 1024), device=gpu)
+    runs = []
+    rng = OF._rng_counter(x.device)
+    rng0 = rng.clone()
+    for tail in ("0", "1"):
+        monkeypatch.setenv("PDE_CNN_FUSED_TAIL", tail)
+        rng.copy_(rng0)  # the same dropout stream for both runs
+        m = copy.deepcopy(base)
+        f = FusedCNN(m)
+        g = f.grad_buffer()
+        opt = FusedSGD(m.parameters(), lr=0.05)
+        losses = [f.forward_backward(x[i], y[i], grad_out=g, sgd=opt).item() for i in range(4)]
+        torch.cuda.synchronize()
+        runs.append((losses, g.clone(), f.flat.clone()))
+    assert _native.C().cnn_tail_error(True) == 0
+    (l0, g0, w0), (l1, g1, w1) = runs
+    assert l0 == l1, (l0, l1)
+    assert torch.equal(g0, g1) and torch.equal(w0, w1)
