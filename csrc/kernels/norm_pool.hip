@@ -291,12 +291,18 @@ __device__ __forceinline__ void st_sc1(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// lite: an agent-coherent load (sc1) of data another block stored with st_sc1, instead of a plain load behind an
+// agent acquire (buffer_inv sc1: the XCD's L1/L2 invalidated once per reading block)
+__device__ __forceinline__ float ld_coh(const float* p, int lite) {
+  return lite ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+}
+
 // Block-collective tail shared by both passes: partial (s1, s2)[64] -> ws, ticket, and on the last arrival
 // the per-channel totals over all row chunks in fixed order into tot1/tot2 (LDS).  Returns true on the block
 // that finalizes.
 __device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], const float (&s2)[8], float* ws, int C,
                                                        int* ticket, float (*red)[kBnRows][kBnCG + 1], float* tot1,
-                                                       float* tot2, int* s_last) {
+                                                       float* tot2, int* s_last, int lite = 0) {
   const int tid = threadIdx.x, tv = tid & 7, tr = tid >> 3;
   const int rb = blockIdx.x, nrb = gridDim.x, cbase = blockIdx.y * kBnCG;
 #pragma unroll
@@ -317,7 +323,7 @@ __device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], con
   __syncthreads();
   if (!*s_last) return false;
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (!lite) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
@@ -334,8 +340,8 @@ __device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], con
         float u1[KT], u2[KT];
 #pragma unroll
         for (int k = 0; k < KT; ++k) {
-          u1[k] = ws[(static_cast<long>(b + kBnQ * k) * 2) * C + cbase + ch];
-          u2[k] = ws[(static_cast<long>(b + kBnQ * k) * 2 + 1) * C + cbase + ch];
+          u1[k] = ld_coh(ws + (static_cast<long>(b + kBnQ * k) * 2) * C + cbase + ch, lite);
+          u2[k] = ld_coh(ws + (static_cast<long>(b + kBnQ * k) * 2 + 1) * C + cbase + ch, lite);
         }
 #pragma unroll
         for (int k = 0; k < KT; ++k) {
@@ -347,8 +353,8 @@ __device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], con
         float u1[8], u2[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          u1[k] = ws[(static_cast<long>(b + kBnQ * k) * 2) * C + cbase + ch];
-          u2[k] = ws[(static_cast<long>(b + kBnQ * k) * 2 + 1) * C + cbase + ch];
+          u1[k] = ld_coh(ws + (static_cast<long>(b + kBnQ * k) * 2) * C + cbase + ch, lite);
+          u2[k] = ld_coh(ws + (static_cast<long>(b + kBnQ * k) * 2 + 1) * C + cbase + ch, lite);
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -357,8 +363,8 @@ __device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], con
         }
       }
       for (; b < nrb; b += kBnQ) {
-        a1 += ws[(static_cast<long>(b) * 2) * C + cbase + ch];
-        a2 += ws[(static_cast<long>(b) * 2 + 1) * C + cbase + ch];
+        a1 += ld_coh(ws + (static_cast<long>(b) * 2) * C + cbase + ch, lite);
+        a2 += ld_coh(ws + (static_cast<long>(b) * 2 + 1) * C + cbase + ch, lite);
       }
     }
     red[0][q][ch] = a1;
@@ -532,18 +538,20 @@ __device__ __forceinline__ void bn_gen_start(const uint32_t* flag, uint32_t* s_g
 }
 
 // The finalizing block, after its threads stored the group's coefficients: publish generation gen + 1.
-__device__ __forceinline__ void bn_publish(uint32_t* flag, uint32_t gen) {
+// lite: the hand-off data was stored write-through (st_sc1) and is read with agent-coherent loads (ld_sc1), so
+// neither the L2 write-back (release) nor the L2 invalidate (acquire, one per waiting block) is issued.
+__device__ __forceinline__ void bn_publish(uint32_t* flag, uint32_t gen, int lite) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (!lite) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(flag, gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 // Every other block of the group: wait (bounded) for generation gen + 1, then acquire.
-__device__ __forceinline__ void bn_wait(const uint32_t* flag, uint32_t gen, int* err) {
+__device__ __forceinline__ void bn_wait(const uint32_t* flag, uint32_t gen, int* err, int lite) {
   if (threadIdx.x == 0) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
@@ -553,11 +561,12 @@ __device__ __forceinline__ void bn_wait(const uint32_t* flag, uint32_t gen, int*
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (!lite) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
 }
+
 
 // 8 consecutive channels of one row of the sum over z of fp32 slabs [splits][P*C] (z order).
 __device__ __forceinline__ void slab_row8(const float* __restrict__ slabs, long zs, int splits, long off,
@@ -609,7 +618,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
     float* __restrict__ running_var, float* __restrict__ save_mean, float* __restrict__ save_invstd,
     float* __restrict__ scale, float* __restrict__ shift, const uint16_t* __restrict__ res, int relu,
     uint16_t* __restrict__ y, const float* __restrict__ slabs, int splits, long slab_zs,
-    float* __restrict__ gvar, int* __restrict__ gtickets) {
+    float* __restrict__ gvar, int* __restrict__ gtickets, int lite) {
   __shared__ float red[2][kBnRows][kBnCG + 1];
   __shared__ float tot1[kBnCG], tot2[kBnCG];
   __shared__ int s_last;
@@ -723,7 +732,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
     }
   }
   // (bn_partials_and_ticket's first barrier also publishes s_gen to the block)
-  if (bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last)) {
+  if (bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last, lite)) {
     if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
       const int c = blockIdx.y * kBnCG + tid;
       const double n = static_cast<double>(P);
@@ -744,8 +753,8 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
       save_invstd[c] = invstd;
       const float g = gamma ? gamma[c] : 1.f;
       const float b = beta ? beta[c] : 0.f;
-      scale[c] = g * invstd;
-      shift[c] = b - mean * g * invstd;
+      st_sc1(scale + c, g * invstd);
+      st_sc1(shift + c, b - mean * g * invstd);
       if (running_mean) {
         const float unbiased = P > 1 ? static_cast<float>(var * n / (n - 1.0)) : static_cast<float>(var);
         if (G == 1) {
@@ -756,7 +765,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
         }
       }
     }
-    bn_publish(flags + blockIdx.y, s_gen);
+    bn_publish(flags + blockIdx.y, s_gen, lite);
     __syncthreads();
     // grouped: the last group's finalizer applies the G momentum updates in micro-batch order
     if (G > 1 && running_mean != nullptr && bn_group_last(gtickets + blockIdx.y, G, &s_last)) {
@@ -772,12 +781,12 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
       }
     }
   } else {
-    bn_wait(flags + blockIdx.y, s_gen, err);
+    bn_wait(flags + blockIdx.y, s_gen, err, lite);
   }
   if (!cok) return;
   float sc[8], sh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; }
+  for (int j = 0; j < 8; ++j) { sc[j] = ld_coh(scale + c0 + j, lite); sh[j] = ld_coh(shift + c0 + j, lite); }
   if constexpr (RC > 0) {
 #pragma unroll
     for (int k = 0; k < RC; ++k) {
@@ -863,7 +872,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
     float* __restrict__ ws, int* __restrict__ tickets, uint32_t* __restrict__ flags, int* __restrict__ err,
     const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta, int accum,
     float* __restrict__ coef, uint16_t* __restrict__ dx, uint16_t* __restrict__ dres,
-    const float* __restrict__ ss, float* __restrict__ gdgb, int* __restrict__ gtickets) {
+    const float* __restrict__ ss, float* __restrict__ gdgb, int* __restrict__ gtickets, int lite) {
   __shared__ float red[2][kBnRows][kBnCG + 1];
   __shared__ float tot1[kBnCG], tot2[kBnCG];
   __shared__ int s_last;
@@ -958,7 +967,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
       }
     }
   }
-  if (bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last)) {
+  if (bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last, lite)) {
     if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
       const int c = blockIdx.y * kBnCG + tid;
       const float t1 = tot1[tid], t2 = tot2[tid];
@@ -970,11 +979,11 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
         gdgb[gz * 2 * C + C + c] = t1;
       }
       const float a = (gamma ? gamma[c] : 1.f) * invstd[c];
-      coef[c] = a;
-      coef[C + c] = a * t1 / static_cast<float>(P);
-      coef[2 * C + c] = a * t2 / static_cast<float>(P);
+      st_sc1(coef + c, a);
+      st_sc1(coef + C + c, a * t1 / static_cast<float>(P));
+      st_sc1(coef + 2 * C + c, a * t2 / static_cast<float>(P));
     }
-    bn_publish(flags + blockIdx.y, s_gen);
+    bn_publish(flags + blockIdx.y, s_gen, lite);
     __syncthreads();
     // grouped: dgamma / dbeta = sum over the groups in group order, by the last group's finalizer
     if (G > 1 && bn_group_last(gtickets + blockIdx.y, G, &s_last)) {
@@ -990,12 +999,16 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
       }
     }
   } else {
-    bn_wait(flags + blockIdx.y, s_gen, err);
+    bn_wait(flags + blockIdx.y, s_gen, err, lite);
   }
   if (!cok) return;
   float ca[8], cb[8], cc[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { ca[j] = coef[c0 + j]; cb[j] = coef[C + c0 + j]; cc[j] = coef[2 * C + c0 + j]; }
+  for (int j = 0; j < 8; ++j) {
+    ca[j] = ld_coh(coef + c0 + j, lite);
+    cb[j] = ld_coh(coef + C + c0 + j, lite);
+    cc[j] = ld_coh(coef + 2 * C + c0 + j, lite);
+  }
   auto apply = [&](const u16x8& ud, const u16x8& ux, long off) {
     float d[8];
 #pragma unroll
@@ -1431,6 +1444,13 @@ bool bn_one_launch(int blocks) {
   return !off && blocks <= 2 * cus;
 }
 
+// flag hand-off without the agent-scope L2 write-back / invalidate (see bn_publish); r3w: ResNet-50
+// 3.875 -> 3.760 ms/step.  PDE_BN_LITE=0: the fenced hand-off.
+int bn_lite_sync() {
+  static const int on = !(std::getenv("PDE_BN_LITE") != nullptr && std::getenv("PDE_BN_LITE")[0] == '0');
+  return on;
+}
+
 const long kBnApplyCap = std::getenv("PDE_BN_APPLY_CAP") ? std::atol(std::getenv("PDE_BN_APPLY_CAP")) : 2048;
 
 int bn_workspace_blocks(int P, int C, int groups) {
@@ -1463,12 +1483,12 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
         hipLaunchKernelGGL(k_bn_fwd_fused<4>, dim3(nrb1, ncg, groups), dim3(kBnThreads), 0, s,
                            const_cast<uint16_t*>(x), Pg, C, rpb, ws, tk, fl, err, gamma, beta, eps, momentum,
                            running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C, res,
-                           relu, y, slabs, splits, static_cast<long>(P) * C, gscratch, gt);
+                           relu, y, slabs, splits, static_cast<long>(P) * C, gscratch, gt, bn_lite_sync());
       else
         hipLaunchKernelGGL(k_bn_fwd_fused<0>, dim3(nrb1, ncg, groups), dim3(kBnThreads), 0, s,
                            const_cast<uint16_t*>(x), Pg, C, rpb, ws, tk, fl, err, gamma, beta, eps, momentum,
                            running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C, res,
-                           relu, y, slabs, splits, static_cast<long>(P) * C, gscratch, gt);
+                           relu, y, slabs, splits, static_cast<long>(P) * C, gscratch, gt, bn_lite_sync());
       return hipGetLastError();
     }
   }
@@ -1542,10 +1562,10 @@ hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, cons
       // rows per thread of a chunk: small enough -> kept in registers for the apply pass
       if (ceil_div(rpb, kBnRows) <= 4)
         hipLaunchKernelGGL(k_bn_bwd_fused<4>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
-                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt);
+                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, bn_lite_sync());
       else
         hipLaunchKernelGGL(k_bn_bwd_fused<0>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
-                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt);
+                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, bn_lite_sync());
       return hipGetLastError();
     }
   }
