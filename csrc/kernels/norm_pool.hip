@@ -300,11 +300,11 @@ __device__ __forceinline__ float ld_coh(const float* p, int lite) {
 // Block-collective tail shared by both passes: partial (s1, s2)[64] -> ws, ticket, and on the last arrival
 // the per-channel totals over all row chunks in fixed order into tot1/tot2 (LDS).  Returns true on the block
 // that finalizes.
-__device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], const float (&s2)[8], float* ws, int C,
-                                                       int* ticket, float (*red)[kBnRows][kBnCG + 1], float* tot1,
-                                                       float* tot2, int* s_last, int lite = 0) {
+// (1) the block's partial (s1, s2)[64] -> ws (write-through), every storing wave drained, barrier.
+__device__ __forceinline__ void bn_store_partials(const float (&s1)[8], const float (&s2)[8], float* ws, int C,
+                                                  float (*red)[kBnRows][kBnCG + 1]) {
   const int tid = threadIdx.x, tv = tid & 7, tr = tid >> 3;
-  const int rb = blockIdx.x, nrb = gridDim.x, cbase = blockIdx.y * kBnCG;
+  const int rb = blockIdx.x, cbase = blockIdx.y * kBnCG;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     red[0][tr][tv * 8 + j] = s1[j];
@@ -319,14 +319,13 @@ __device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], con
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) *s_last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nrb - 1;
-  __syncthreads();
-  if (!*s_last) return false;
-  if (tid == 0) {
-    if (!lite) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
+}
+
+// (2) the per-channel totals over all gridDim.x row chunks in fixed order -> tot1/tot2 (LDS; written by the
+// first kBnCG threads, the caller synchronises).
+__device__ __forceinline__ void bn_load_totals(const float* ws, int C, float (*red)[kBnRows][kBnCG + 1], float* tot1,
+                                               float* tot2, int lite) {
+  const int tid = threadIdx.x, nrb = gridDim.x, cbase = blockIdx.y * kBnCG;
   // kBnQ lanes per (which, channel) over the row chunks, combined in lane order
   {
     const int q = tid >> 6, ch = tid & 63;
@@ -381,6 +380,24 @@ __device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], con
     tot1[tid] = v1;
     tot2[tid] = v2;
   }
+}
+
+// Block-collective tail shared by both passes: partials -> ws, ticket, and on the last arrival the per-channel
+// totals over all row chunks in fixed order into tot1/tot2 (LDS).  Returns true on the block that finalizes.
+__device__ __forceinline__ bool bn_partials_and_ticket(const float (&s1)[8], const float (&s2)[8], float* ws, int C,
+                                                       int* ticket, float (*red)[kBnRows][kBnCG + 1], float* tot1,
+                                                       float* tot2, int* s_last, int lite = 0) {
+  const int tid = threadIdx.x, nrb = gridDim.x;
+  bn_store_partials(s1, s2, ws, C, red);
+  if (tid == 0) *s_last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nrb - 1;
+  __syncthreads();
+  if (!*s_last) return false;
+  if (tid == 0) {
+    if (!lite) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  bn_load_totals(ws, C, red, tot1, tot2, lite);
   if (tid == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
   __syncthreads();
   return true;
@@ -585,6 +602,41 @@ __device__ __forceinline__ void slab_row8(const float* __restrict__ slabs, long 
   }
 }
 
+// All-finalize variant of the hand-off (allfin): the last arrival at the ticket publishes the generation flag at
+// once, and EVERY block then reads the chunk partials (agent-coherent loads) and derives the coefficients of its
+// channel group itself, in the same fixed order -- identical values in every block.  The serial chain per launch
+// is ticket -> flag -> partial loads instead of ticket -> partial loads -> coefficient stores (drained) -> flag ->
+// coefficient loads.  Returns true on the last arrival, which writes the launch's global outputs.
+__device__ __forceinline__ bool bn_partials_all(const float (&s1)[8], const float (&s2)[8], float* ws, int C,
+                                                int* ticket, uint32_t* flag, uint32_t gen, int* err,
+                                                float (*red)[kBnRows][kBnCG + 1], float* tot1, float* tot2,
+                                                int* s_last) {
+  const int tid = threadIdx.x, nrb = gridDim.x;
+  bn_store_partials(s1, s2, ws, C, red);
+  if (tid == 0) {
+    const bool last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nrb - 1;
+    if (last) {
+      __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+      __hip_atomic_store(flag, gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kBnWaitTicks) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    *s_last = last ? 1 : 0;
+  }
+  __syncthreads();
+  bn_load_totals(ws, C, red, tot1, tot2, 1);
+  __syncthreads();
+  return *s_last != 0;
+}
+
 // Grouped BatchNorm (blockIdx.z = group: the rows of G equal, contiguous micro-batches normalised with
 // their OWN statistics in one launch -- a pipeline stage running several micro-batches per launch keeps the
 // reference's per-micro-batch BatchNorm semantics, quirk Q17).  Quantities that combine the groups IN ORDER
@@ -620,7 +672,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
     uint16_t* __restrict__ y, const float* __restrict__ slabs, int splits, long slab_zs,
     float* __restrict__ gvar, int* __restrict__ gtickets, int lite) {
   __shared__ float red[2][kBnRows][kBnCG + 1];
-  __shared__ float tot1[kBnCG], tot2[kBnCG];
+  __shared__ float tot1[kBnCG], tot2[kBnCG], s_coef[2][kBnCG];
   __shared__ int s_last;
   __shared__ uint32_t s_gen;
   const int tid = threadIdx.x, tv = tid & 7, tr = tid >> 3;
@@ -732,7 +784,14 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
     }
   }
   // (bn_partials_and_ticket's first barrier also publishes s_gen to the block)
-  if (bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last, lite)) {
+  // lite bit 0: fence-free hand-off; bit 1: every block finalizes its channel group (bn_partials_all)
+  const bool allfin = (lite & 2) != 0;
+  lite &= 1;
+  const bool writer = allfin ? bn_partials_all(s1, s2, ws, C, tickets + blockIdx.y, flags + blockIdx.y, s_gen, err,
+                                               red, tot1, tot2, &s_last)
+                             : bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last,
+                                                      lite);
+  if (writer || allfin) {
     if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
       const int c = blockIdx.y * kBnCG + tid;
       const double n = static_cast<double>(P);
@@ -749,44 +808,55 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
       }
       const float mean = static_cast<float>(mean_s) + pv;
       const float invstd = rsqrtf(static_cast<float>(var) + eps);
-      save_mean[c] = mean;
-      save_invstd[c] = invstd;
       const float g = gamma ? gamma[c] : 1.f;
       const float b = beta ? beta[c] : 0.f;
-      st_sc1(scale + c, g * invstd);
-      st_sc1(shift + c, b - mean * g * invstd);
-      if (running_mean) {
-        const float unbiased = P > 1 ? static_cast<float>(var * n / (n - 1.0)) : static_cast<float>(var);
-        if (G == 1) {
-          running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
-          running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
-        } else {
-          gvar[gz * C + c] = unbiased;
+      const float a_sc = g * invstd, a_sh = b - mean * g * invstd;
+      s_coef[0][tid] = a_sc;
+      s_coef[1][tid] = a_sh;
+      if (writer) {  // the launch's global outputs: one block per (group, channel group)
+        save_mean[c] = mean;
+        save_invstd[c] = invstd;
+        st_sc1(scale + c, a_sc);
+        st_sc1(shift + c, a_sh);
+        if (running_mean) {
+          const float unbiased = P > 1 ? static_cast<float>(var * n / (n - 1.0)) : static_cast<float>(var);
+          if (G == 1) {
+            running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+            running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+          } else {
+            gvar[gz * C + c] = unbiased;
+          }
         }
       }
     }
-    bn_publish(flags + blockIdx.y, s_gen, lite);
-    __syncthreads();
-    // grouped: the last group's finalizer applies the G momentum updates in micro-batch order
-    if (G > 1 && running_mean != nullptr && bn_group_last(gtickets + blockIdx.y, G, &s_last)) {
-      if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
-        const int c = blockIdx.y * kBnCG + tid;
-        float rm = running_mean[c], rv = running_var[c];
-        for (int g = 0; g < G; ++g) {
-          rm = (1.f - momentum) * rm + momentum * save_mean_all[g * C + c];
-          rv = (1.f - momentum) * rv + momentum * gvar[g * C + c];
+    if (writer) {
+      if (!allfin) bn_publish(flags + blockIdx.y, s_gen, lite);
+      __syncthreads();
+      // grouped: the last group's finalizer applies the G momentum updates in micro-batch order
+      if (G > 1 && running_mean != nullptr && bn_group_last(gtickets + blockIdx.y, G, &s_last)) {
+        if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
+          const int c = blockIdx.y * kBnCG + tid;
+          float rm = running_mean[c], rv = running_var[c];
+          for (int g = 0; g < G; ++g) {
+            rm = (1.f - momentum) * rm + momentum * save_mean_all[g * C + c];
+            rv = (1.f - momentum) * rv + momentum * gvar[g * C + c];
+          }
+          running_mean[c] = rm;
+          running_var[c] = rv;
         }
-        running_mean[c] = rm;
-        running_var[c] = rv;
       }
     }
+    if (allfin) __syncthreads();  // s_coef
   } else {
     bn_wait(flags + blockIdx.y, s_gen, err, lite);
   }
   if (!cok) return;
   float sc[8], sh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { sc[j] = ld_coh(scale + c0 + j, lite); sh[j] = ld_coh(shift + c0 + j, lite); }
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = allfin ? s_coef[0][tv * 8 + j] : ld_coh(scale + c0 + j, lite);
+    sh[j] = allfin ? s_coef[1][tv * 8 + j] : ld_coh(shift + c0 + j, lite);
+  }
   if constexpr (RC > 0) {
 #pragma unroll
     for (int k = 0; k < RC; ++k) {
@@ -874,7 +944,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
     float* __restrict__ coef, uint16_t* __restrict__ dx, uint16_t* __restrict__ dres,
     const float* __restrict__ ss, float* __restrict__ gdgb, int* __restrict__ gtickets, int lite) {
   __shared__ float red[2][kBnRows][kBnCG + 1];
-  __shared__ float tot1[kBnCG], tot2[kBnCG];
+  __shared__ float tot1[kBnCG], tot2[kBnCG], s_coef[3][kBnCG];
   __shared__ int s_last;
   __shared__ uint32_t s_gen;
   const int tid = threadIdx.x, tv = tid & 7, tr = tid >> 3;
@@ -967,37 +1037,53 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
       }
     }
   }
-  if (bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last, lite)) {
+  // lite bit 0: fence-free hand-off; bit 1: every block finalizes its channel group (bn_partials_all)
+  const bool allfin = (lite & 2) != 0;
+  lite &= 1;
+  const bool writer = allfin ? bn_partials_all(s1, s2, ws, C, tickets + blockIdx.y, flags + blockIdx.y, s_gen, err,
+                                               red, tot1, tot2, &s_last)
+                             : bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last,
+                                                      lite);
+  if (writer || allfin) {
     if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
       const int c = blockIdx.y * kBnCG + tid;
       const float t1 = tot1[tid], t2 = tot2[tid];
-      if (G == 1) {
-        if (dgamma) dgamma[c] = accum ? dgamma[c] + t2 : t2;
-        if (dbeta) dbeta[c] = accum ? dbeta[c] + t1 : t1;
-      } else {
-        gdgb[gz * 2 * C + c] = t2;
-        gdgb[gz * 2 * C + C + c] = t1;
-      }
       const float a = (gamma ? gamma[c] : 1.f) * invstd[c];
-      st_sc1(coef + c, a);
-      st_sc1(coef + C + c, a * t1 / static_cast<float>(P));
-      st_sc1(coef + 2 * C + c, a * t2 / static_cast<float>(P));
-    }
-    bn_publish(flags + blockIdx.y, s_gen, lite);
-    __syncthreads();
-    // grouped: dgamma / dbeta = sum over the groups in group order, by the last group's finalizer
-    if (G > 1 && bn_group_last(gtickets + blockIdx.y, G, &s_last)) {
-      if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
-        const int c = blockIdx.y * kBnCG + tid;
-        float t2 = 0.f, t1 = 0.f;
-        for (int g = 0; g < G; ++g) {
-          t2 += gdgb[g * 2 * C + c];
-          t1 += gdgb[g * 2 * C + C + c];
+      const float a1 = a * t1 / static_cast<float>(P), a2 = a * t2 / static_cast<float>(P);
+      s_coef[0][tid] = a;
+      s_coef[1][tid] = a1;
+      s_coef[2][tid] = a2;
+      if (writer) {  // the launch's global outputs: one block per (group, channel group)
+        if (G == 1) {
+          if (dgamma) dgamma[c] = accum ? dgamma[c] + t2 : t2;
+          if (dbeta) dbeta[c] = accum ? dbeta[c] + t1 : t1;
+        } else {
+          gdgb[gz * 2 * C + c] = t2;
+          gdgb[gz * 2 * C + C + c] = t1;
         }
-        if (dgamma) dgamma[c] = accum ? dgamma[c] + t2 : t2;
-        if (dbeta) dbeta[c] = accum ? dbeta[c] + t1 : t1;
+        st_sc1(coef + c, a);
+        st_sc1(coef + C + c, a1);
+        st_sc1(coef + 2 * C + c, a2);
       }
     }
+    if (writer) {
+      if (!allfin) bn_publish(flags + blockIdx.y, s_gen, lite);
+      __syncthreads();
+      // grouped: dgamma / dbeta = sum over the groups in group order, by the last group's finalizer
+      if (G > 1 && bn_group_last(gtickets + blockIdx.y, G, &s_last)) {
+        if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
+          const int c = blockIdx.y * kBnCG + tid;
+          float t2 = 0.f, t1 = 0.f;
+          for (int g = 0; g < G; ++g) {
+            t2 += gdgb[g * 2 * C + c];
+            t1 += gdgb[g * 2 * C + C + c];
+          }
+          if (dgamma) dgamma[c] = accum ? dgamma[c] + t2 : t2;
+          if (dbeta) dbeta[c] = accum ? dbeta[c] + t1 : t1;
+        }
+      }
+    }
+    if (allfin) __syncthreads();  // s_coef
   } else {
     bn_wait(flags + blockIdx.y, s_gen, err, lite);
   }
@@ -1005,9 +1091,9 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
   float ca[8], cb[8], cc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    ca[j] = ld_coh(coef + c0 + j, lite);
-    cb[j] = ld_coh(coef + C + c0 + j, lite);
-    cc[j] = ld_coh(coef + 2 * C + c0 + j, lite);
+    ca[j] = allfin ? s_coef[0][tv * 8 + j] : ld_coh(coef + c0 + j, lite);
+    cb[j] = allfin ? s_coef[1][tv * 8 + j] : ld_coh(coef + C + c0 + j, lite);
+    cc[j] = allfin ? s_coef[2][tv * 8 + j] : ld_coh(coef + 2 * C + c0 + j, lite);
   }
   auto apply = [&](const u16x8& ud, const u16x8& ux, long off) {
     float d[8];
@@ -1446,9 +1532,12 @@ bool bn_one_launch(int blocks) {
 
 // flag hand-off without the agent-scope L2 write-back / invalidate (see bn_publish); r3w: ResNet-50
 // 3.875 -> 3.760 ms/step.  PDE_BN_LITE=0: the fenced hand-off.
+// Every block finalizes its channel group (bn_partials_all), r3y: 3.77 -> 3.50 ms/step; PDE_BN_ALLFIN=0: one
+// finalizing block per channel group publishing the coefficients.
 int bn_lite_sync() {
-  static const int on = !(std::getenv("PDE_BN_LITE") != nullptr && std::getenv("PDE_BN_LITE")[0] == '0');
-  return on;
+  static const int lite = !(std::getenv("PDE_BN_LITE") != nullptr && std::getenv("PDE_BN_LITE")[0] == '0');
+  static const int allfin = !(std::getenv("PDE_BN_ALLFIN") != nullptr && std::getenv("PDE_BN_ALLFIN")[0] == '0');
+  return lite ? (allfin ? 3 : 1) : 0;
 }
 
 const long kBnApplyCap = std::getenv("PDE_BN_APPLY_CAP") ? std::atol(std::getenv("PDE_BN_APPLY_CAP")) : 2048;
