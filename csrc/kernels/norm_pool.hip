@@ -637,6 +637,97 @@ __device__ __forceinline__ bool bn_partials_all(const float (&s1)[8], const floa
   return *s_last != 0;
 }
 
+// Tagged hand-off (mode bit 4): no ticket, no flag wait.  Every block stores its chunk partials as 64-bit words
+// {value, tag = epoch + 1} (one single-copy-atomic store each, no drain) into the (group, channel group)'s own
+// fixed region, and every block polls the region until all nrb x 2 x 64 words carry the tag -- the serial chain
+// is one store + one load round trip.  epoch = the region's header word, read at kernel start; block 0, having
+// seen every block's tagged partials (so every block has read the header), stores header = epoch + 1.  A region
+// and its header are only ever written by launches that hold that slot, so every stale tag in it is <= the
+// header: a tag equal to header + 1 is always this launch's.  Returns true on block 0 (the writer).
+constexpr int kBnTagChunks = 64;                         // row chunks per region (nrb cap of the tagged mode)
+constexpr int kBnTagWords = kBnTagChunks * 2 * kBnCG;    // 64-bit words per region
+
+__device__ __forceinline__ uint64_t bn_tag_pack(float v, uint32_t tag) {
+  return (static_cast<uint64_t>(tag) << 32) | __float_as_uint(v);
+}
+
+__device__ __forceinline__ bool bn_partials_tagged(const float (&s1)[8], const float (&s2)[8], uint64_t* parts, int C,
+                                                   uint32_t* hdr, const uint32_t* s_epoch, int* err,
+                                                   float (*red)[kBnRows][kBnCG + 1], float* tot1, float* tot2) {
+  const int tid = threadIdx.x, tv = tid & 7, tr = tid >> 3;
+  const int rb = blockIdx.x, nrb = gridDim.x, cbase = blockIdx.y * kBnCG;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][tr][tv * 8 + j] = s1[j];
+    red[1][tr][tv * 8 + j] = s2[j];
+  }
+  __syncthreads();  // also publishes the epoch (bn_gen_start) to the block
+  const uint32_t tag = *s_epoch + 1u;
+  if (tid < 2 * kBnCG) {
+    const int which = tid / kBnCG, ch = tid % kBnCG;
+    float v = 0.f;
+    for (int r = 0; r < kBnRows; ++r) v += red[which][r][ch];
+    __hip_atomic_store(parts + (rb * 2 + which) * kBnCG + ch, bn_tag_pack(v, tag), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();  // red is reused below
+  const int q = tid >> 6, ch = tid & 63;
+  float a1 = 0.f, a2 = 0.f;
+  if (cbase + ch < C) {
+    constexpr int KT = kBnTagChunks / kBnQ;  // every chunk of the lane in one trip
+    uint64_t u1[KT], u2[KT];
+    const uint64_t pad = bn_tag_pack(0.f, tag);
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      const int b = q + k * kBnQ;
+      u1[k] = b < nrb ? __hip_atomic_load(parts + (b * 2) * kBnCG + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : pad;
+      u2[k] = b < nrb ? __hip_atomic_load(parts + (b * 2 + 1) * kBnCG + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : pad;
+    }
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < KT; ++k) ok = ok && (u1[k] >> 32) == tag && (u2[k] >> 32) == tag;
+      if (ok) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kBnWaitTicks) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int k = 0; k < KT; ++k) {
+        const int b = q + k * kBnQ;
+        if ((u1[k] >> 32) != tag)
+          u1[k] = __hip_atomic_load(parts + (b * 2) * kBnCG + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((u2[k] >> 32) != tag)
+          u2[k] = __hip_atomic_load(parts + (b * 2 + 1) * kBnCG + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      a1 += __uint_as_float(static_cast<uint32_t>(u1[k]));
+      a2 += __uint_as_float(static_cast<uint32_t>(u2[k]));
+    }
+  }
+  red[0][q][ch] = a1;
+  red[1][q][ch] = a2;
+  __syncthreads();
+  if (tid < kBnCG) {
+    float v1 = red[0][0][tid], v2 = red[1][0][tid];
+#pragma unroll
+    for (int qq = 1; qq < kBnQ; ++qq) {
+      v1 += red[0][qq][tid];
+      v2 += red[1][qq][tid];
+    }
+    tot1[tid] = v1;
+    tot2[tid] = v2;
+  }
+  if (rb == 0 && tid == 0) __hip_atomic_store(hdr, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return rb == 0;
+}
+
 // Grouped BatchNorm (blockIdx.z = group: the rows of G equal, contiguous micro-batches normalised with
 // their OWN statistics in one launch -- a pipeline stage running several micro-batches per launch keeps the
 // reference's per-micro-batch BatchNorm semantics, quirk Q17).  Quantities that combine the groups IN ORDER
@@ -670,7 +761,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
     float* __restrict__ running_var, float* __restrict__ save_mean, float* __restrict__ save_invstd,
     float* __restrict__ scale, float* __restrict__ shift, const uint16_t* __restrict__ res, int relu,
     uint16_t* __restrict__ y, const float* __restrict__ slabs, int splits, long slab_zs,
-    float* __restrict__ gvar, int* __restrict__ gtickets, int lite) {
+    float* __restrict__ gvar, int* __restrict__ gtickets, int lite, uint64_t* __restrict__ parts) {
   __shared__ float red[2][kBnRows][kBnCG + 1];
   __shared__ float tot1[kBnCG], tot2[kBnCG], s_coef[2][kBnCG];
   __shared__ int s_last;
@@ -784,13 +875,16 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
     }
   }
   // (bn_partials_and_ticket's first barrier also publishes s_gen to the block)
-  // lite bit 0: fence-free hand-off; bit 1: every block finalizes its channel group (bn_partials_all)
-  const bool allfin = (lite & 2) != 0;
+  // lite bit 0: fence-free hand-off; bit 1: every block finalizes its channel group (bn_partials_all); bit 2:
+  // tagged partials (bn_partials_tagged, implies 1 and 2)
+  const bool tagged = (lite & 4) != 0, allfin = (lite & 2) != 0;
   lite &= 1;
-  const bool writer = allfin ? bn_partials_all(s1, s2, ws, C, tickets + blockIdx.y, flags + blockIdx.y, s_gen, err,
-                                               red, tot1, tot2, &s_last)
-                             : bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last,
-                                                      lite);
+  const bool writer =
+      tagged ? bn_partials_tagged(s1, s2, parts + static_cast<long>(gz * gridDim.y + blockIdx.y) * kBnTagWords, C,
+                                  flags + blockIdx.y, &s_gen, err, red, tot1, tot2)
+      : allfin ? bn_partials_all(s1, s2, ws, C, tickets + blockIdx.y, flags + blockIdx.y, s_gen, err, red, tot1, tot2,
+                                 &s_last)
+               : bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last, lite);
   if (writer || allfin) {
     if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
       const int c = blockIdx.y * kBnCG + tid;
@@ -942,7 +1036,8 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
     float* __restrict__ ws, int* __restrict__ tickets, uint32_t* __restrict__ flags, int* __restrict__ err,
     const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta, int accum,
     float* __restrict__ coef, uint16_t* __restrict__ dx, uint16_t* __restrict__ dres,
-    const float* __restrict__ ss, float* __restrict__ gdgb, int* __restrict__ gtickets, int lite) {
+    const float* __restrict__ ss, float* __restrict__ gdgb, int* __restrict__ gtickets, int lite,
+    uint64_t* __restrict__ parts) {
   __shared__ float red[2][kBnRows][kBnCG + 1];
   __shared__ float tot1[kBnCG], tot2[kBnCG], s_coef[3][kBnCG];
   __shared__ int s_last;
@@ -1037,13 +1132,16 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
       }
     }
   }
-  // lite bit 0: fence-free hand-off; bit 1: every block finalizes its channel group (bn_partials_all)
-  const bool allfin = (lite & 2) != 0;
+  // lite bit 0: fence-free hand-off; bit 1: every block finalizes its channel group (bn_partials_all); bit 2:
+  // tagged partials (bn_partials_tagged, implies 1 and 2)
+  const bool tagged = (lite & 4) != 0, allfin = (lite & 2) != 0;
   lite &= 1;
-  const bool writer = allfin ? bn_partials_all(s1, s2, ws, C, tickets + blockIdx.y, flags + blockIdx.y, s_gen, err,
-                                               red, tot1, tot2, &s_last)
-                             : bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last,
-                                                      lite);
+  const bool writer =
+      tagged ? bn_partials_tagged(s1, s2, parts + static_cast<long>(gz * gridDim.y + blockIdx.y) * kBnTagWords, C,
+                                  flags + blockIdx.y, &s_gen, err, red, tot1, tot2)
+      : allfin ? bn_partials_all(s1, s2, ws, C, tickets + blockIdx.y, flags + blockIdx.y, s_gen, err, red, tot1, tot2,
+                                 &s_last)
+               : bn_partials_and_ticket(s1, s2, ws, C, tickets + blockIdx.y, red, tot1, tot2, &s_last, lite);
   if (writer || allfin) {
     if (tid < kBnCG && blockIdx.y * kBnCG + tid < C) {
       const int c = blockIdx.y * kBnCG + tid;
@@ -1513,6 +1611,39 @@ int* bn_window(int n, hipStream_t s, int which) {
   nx += n;
   return t;
 }
+// Tagged hand-off regions (bn_partials_tagged): kBnTagSlots fixed (header, region) pairs, zeroed once, handed
+// out in a rolling window of n consecutive slots.  A slot's region is only written by launches holding that slot.
+constexpr int kBnTagSlots = 4096;  // x 64 KB
+uint64_t* bn_tag_slots(int n, hipStream_t s, uint32_t** hdr) {
+  static uint64_t* parts[64] = {};
+  static uint32_t* hdrs[64] = {};
+  static int next[64] = {};
+  int dev = 0;
+  if (n > kBnTagSlots || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (parts[dev] == nullptr) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+    const size_t pb = sizeof(uint64_t) * kBnTagWords * kBnTagSlots, hb = sizeof(uint32_t) * kBnTagSlots;
+    void* p = nullptr;
+    void* h = nullptr;
+    if (hipMalloc(&p, pb) != hipSuccess) return nullptr;
+    if (hipMalloc(&h, hb) != hipSuccess || hipMemset(p, 0, pb) != hipSuccess || hipMemset(h, 0, hb) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(p);
+      if (h != nullptr) (void)hipFree(h);
+      return nullptr;
+    }
+    parts[dev] = static_cast<uint64_t*>(p);
+    hdrs[dev] = static_cast<uint32_t*>(h);
+  }
+  int& nx = next[dev];
+  if (nx + n > kBnTagSlots) nx = 0;
+  *hdr = hdrs[dev] + nx;
+  uint64_t* r = parts[dev] + static_cast<long>(nx) * kBnTagWords;
+  nx += n;
+  return r;
+}
+
 int* bn_tickets(int n, hipStream_t s) { return bn_window(n, s, 0); }
 uint32_t* bn_flags(int n, hipStream_t s) { return reinterpret_cast<uint32_t*>(bn_window(n, s, 1)); }
 
@@ -1538,6 +1669,12 @@ int bn_lite_sync() {
   static const int lite = !(std::getenv("PDE_BN_LITE") != nullptr && std::getenv("PDE_BN_LITE")[0] == '0');
   static const int allfin = !(std::getenv("PDE_BN_ALLFIN") != nullptr && std::getenv("PDE_BN_ALLFIN")[0] == '0');
   return lite ? (allfin ? 3 : 1) : 0;
+}
+// Tagged partials (bn_partials_tagged) where the grid allows (<= kBnTagChunks row chunks), r3aa: ResNet-50
+// 3.52 -> 3.34 ms/step; PDE_BN_TAGGED=0: the ticket + flag hand-off.
+bool bn_tagged_on() {
+  static const bool on = !(std::getenv("PDE_BN_TAGGED") != nullptr && std::getenv("PDE_BN_TAGGED")[0] == '0');
+  return on;
 }
 
 const long kBnApplyCap = std::getenv("PDE_BN_APPLY_CAP") ? std::atol(std::getenv("PDE_BN_APPLY_CAP")) : 2048;
@@ -1565,6 +1702,16 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
     int* tk = bn_tickets(ncg * groups, s);
     uint32_t* fl = bn_flags(ncg * groups, s);  // generation flags of the (group, channel group)s
     int* gt = groups > 1 ? bn_tickets(ncg, s) : nullptr;
+    int mode = bn_lite_sync();
+    uint64_t* parts = nullptr;
+    if (mode == 3 && bn_tagged_on() && nrb1 <= kBnTagChunks) {
+      uint32_t* hdr = nullptr;
+      parts = bn_tag_slots(ncg * groups, s, &hdr);
+      if (parts != nullptr) {
+        fl = hdr;  // the slots' headers are the epochs
+        mode = 7;
+      }
+    }
     if (tk != nullptr && fl != nullptr && (groups == 1 || (gt != nullptr && gscratch != nullptr))) {
       // rows per thread of a chunk: few enough -> kept in registers for the apply pass (PDE_BN_FWD_RC=0: off)
       static const bool rc_on = !(std::getenv("PDE_BN_FWD_RC") && std::getenv("PDE_BN_FWD_RC")[0] == '0');
@@ -1572,12 +1719,12 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
         hipLaunchKernelGGL(k_bn_fwd_fused<4>, dim3(nrb1, ncg, groups), dim3(kBnThreads), 0, s,
                            const_cast<uint16_t*>(x), Pg, C, rpb, ws, tk, fl, err, gamma, beta, eps, momentum,
                            running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C, res,
-                           relu, y, slabs, splits, static_cast<long>(P) * C, gscratch, gt, bn_lite_sync());
+                           relu, y, slabs, splits, static_cast<long>(P) * C, gscratch, gt, mode, parts);
       else
         hipLaunchKernelGGL(k_bn_fwd_fused<0>, dim3(nrb1, ncg, groups), dim3(kBnThreads), 0, s,
                            const_cast<uint16_t*>(x), Pg, C, rpb, ws, tk, fl, err, gamma, beta, eps, momentum,
                            running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C, res,
-                           relu, y, slabs, splits, static_cast<long>(P) * C, gscratch, gt, bn_lite_sync());
+                           relu, y, slabs, splits, static_cast<long>(P) * C, gscratch, gt, mode, parts);
       return hipGetLastError();
     }
   }
@@ -1646,15 +1793,25 @@ hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, cons
     int* tk = bn_tickets(ncg * groups, s);
     uint32_t* fl = bn_flags(ncg * groups, s);
     int* gt = groups > 1 ? bn_tickets(ncg, s) : nullptr;
+    int mode = bn_lite_sync();
+    uint64_t* parts = nullptr;
+    if (mode == 3 && bn_tagged_on() && nrb1 <= kBnTagChunks) {
+      uint32_t* hdr = nullptr;
+      parts = bn_tag_slots(ncg * groups, s, &hdr);
+      if (parts != nullptr) {
+        fl = hdr;
+        mode = 7;
+      }
+    }
     if (tk != nullptr && fl != nullptr && (groups == 1 || (gt != nullptr && gscratch != nullptr))) {
       const dim3 grid(nrb1, ncg, groups);
       // rows per thread of a chunk: small enough -> kept in registers for the apply pass
       if (ceil_div(rpb, kBnRows) <= 4)
         hipLaunchKernelGGL(k_bn_bwd_fused<4>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
-                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, bn_lite_sync());
+                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, mode, parts);
       else
         hipLaunchKernelGGL(k_bn_bwd_fused<0>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
-                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, bn_lite_sync());
+                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, mode, parts);
       return hipGetLastError();
     }
   }
