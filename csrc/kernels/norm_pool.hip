@@ -1670,6 +1670,12 @@ int bn_lite_sync() {
   static const int allfin = !(std::getenv("PDE_BN_ALLFIN") != nullptr && std::getenv("PDE_BN_ALLFIN")[0] == '0');
   return lite ? (allfin ? 3 : 1) : 0;
 }
+// Chunks of 5..8 rows per thread also stay in registers between the passes (RC = 8), r3ac: ResNet-50
+// 3.337 -> 3.319 ms/step (3 of 3 pairs); PDE_BN_RC8=0: off.
+bool bn_rc8_on() {
+  static const bool on = !(std::getenv("PDE_BN_RC8") != nullptr && std::getenv("PDE_BN_RC8")[0] == '0');
+  return on;
+}
 // Tagged partials (bn_partials_tagged) where the grid allows (<= kBnTagChunks row chunks), r3aa: ResNet-50
 // 3.52 -> 3.34 ms/step; PDE_BN_TAGGED=0: the ticket + flag hand-off.
 bool bn_tagged_on() {
@@ -1717,6 +1723,11 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
       static const bool rc_on = !(std::getenv("PDE_BN_FWD_RC") && std::getenv("PDE_BN_FWD_RC")[0] == '0');
       if (rc_on && ceil_div(rpb, kBnRows) <= 4)
         hipLaunchKernelGGL(k_bn_fwd_fused<4>, dim3(nrb1, ncg, groups), dim3(kBnThreads), 0, s,
+                           const_cast<uint16_t*>(x), Pg, C, rpb, ws, tk, fl, err, gamma, beta, eps, momentum,
+                           running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C, res,
+                           relu, y, slabs, splits, static_cast<long>(P) * C, gscratch, gt, mode, parts);
+      else if (rc_on && bn_rc8_on() && ceil_div(rpb, kBnRows) <= 8)
+        hipLaunchKernelGGL(k_bn_fwd_fused<8>, dim3(nrb1, ncg, groups), dim3(kBnThreads), 0, s,
                            const_cast<uint16_t*>(x), Pg, C, rpb, ws, tk, fl, err, gamma, beta, eps, momentum,
                            running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C, res,
                            relu, y, slabs, splits, static_cast<long>(P) * C, gscratch, gt, mode, parts);
@@ -1808,6 +1819,9 @@ hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, cons
       // rows per thread of a chunk: small enough -> kept in registers for the apply pass
       if (ceil_div(rpb, kBnRows) <= 4)
         hipLaunchKernelGGL(k_bn_bwd_fused<4>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
+                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, mode, parts);
+      else if (bn_rc8_on() && ceil_div(rpb, kBnRows) <= 8)
+        hipLaunchKernelGGL(k_bn_bwd_fused<8>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
                            ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, mode, parts);
       else
         hipLaunchKernelGGL(k_bn_bwd_fused<0>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
