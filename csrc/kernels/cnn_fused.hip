@@ -847,8 +847,10 @@ constexpr int RED_BLOCKS = RED_SLAB_BLOCKS + FC1_JT * FC1_IT;
 static_assert(NIN % 16 == 0, "fc1 input tiles");
 static_assert(NI == 4, "activation columns are written as one float4 per row");
 
-__device__ __forceinline__ void sgd_update(float* params, const float* hp, uint16_t* frag, int p, float g) {
-  const float w = params[p] - hp[HP_LR] * (g * hp[HP_GRAD_SCALE]);
+// w0 = params[p] and the hyper-parameters loaded at the start of the role (off the reduction's dependent chain)
+__device__ __forceinline__ void sgd_update(float* params, float lr, float gsc, uint16_t* frag, int p, float w0,
+                                           float g) {
+  const float w = w0 - lr * (g * gsc);
   params[p] = w;
   write_frag(frag, p, w);
 }
@@ -871,6 +873,8 @@ __device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s
   // world > 1 with a peer view: this block's gradients go through the one-shot xGMI exchange (stage to my
   // slot, flags, read all ranks' values in rank order, x xscale) before the store + SGD update
   const bool xchg = xv.size > 1;
+  // SGD operands requested up front: they do not depend on the reduction
+  const float lrate = hp ? hp[HP_LR] : 0.f, gsc = hp ? hp[HP_GRAD_SCALE] : 0.f;
   const uint32_t epoch = xchg ? xgmi_epoch(xv, rb, s_epoch) : 0u;
   float* xmine = xchg ? xgmi_slot(xv, xv.rank, epoch) : nullptr;
   if (rb < RED_SLAB_BLOCKS) {
@@ -878,6 +882,11 @@ __device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s
     const int c4 = rb * RED_COLS + col;
     const f32x4* s4 = reinterpret_cast<const f32x4*>(slabs);
     f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+    const bool owner = act && sl == 0 && c4 < NSLAB4;
+    const int p4 = c4 < O_FC1W / 4 ? c4 : c4 + FC1N / 4;  // slab column -> parameter float4
+    f32x4 w0 = a0, g0 = a0;
+    if (owner && hp) w0 = reinterpret_cast<const f32x4*>(params)[p4];
+    if (owner && accumulate) g0 = reinterpret_cast<const f32x4*>(grads)[p4];
     if (act && c4 < NSLAB4) {
       int b = sl;
       for (; b + 7 * RED_LANES < nwg; b += 8 * RED_LANES) {  // 8 independent loads in flight
@@ -893,8 +902,6 @@ __device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s
     }
     if (act) part[sl * RED_COLS + col] = (a0 + a1) + (a2 + a3);
     __syncthreads();
-    const bool owner = act && sl == 0 && c4 < NSLAB4;
-    const int p4 = c4 < O_FC1W / 4 ? c4 : c4 + FC1N / 4;  // slab column -> parameter float4
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (owner) {
       v = part[col];
@@ -921,11 +928,11 @@ __device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s
     }
     if (owner && ok) {
       f32x4* g4 = reinterpret_cast<f32x4*>(grads) + p4;
-      if (accumulate) v += *g4;
+      if (accumulate) v += g0;
       *g4 = v;
       if (hp) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) sgd_update(params, hp, frag, p4 * 4 + j, v[j]);
+        for (int j = 0; j < 4; ++j) sgd_update(params, lrate, gsc, frag, p4 * 4 + j, w0[j], v[j]);
       }
     }
   } else {
@@ -936,6 +943,18 @@ __device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s
     const int kper = ((Bk + 8 * 16 - 1) / (8 * 16)) * 16;  // this wave's K slice, a multiple of 16
     const int k0 = wid * kper, k1 = act ? min(Bk, k0 + kper) : k0;
     const bool jv = j0 + lr < F1;
+    float w0[4] = {0.f, 0.f, 0.f, 0.f}, g0[4] = {0.f, 0.f, 0.f, 0.f};  // wave 0's outputs (j0 + 4 lg + r, i0 + lr)
+    if (wid == 0 && act) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = j0 + lg * 4 + r;
+        if (j < F1) {
+          const int p = O_FC1W + j * NIN + i0 + lr;
+          if (hp) w0[r] = params[p];
+          if (accumulate) g0[r] = grads[p];
+        }
+      }
+    }
     const float* arow = acts + static_cast<long>(jv ? j0 + lr : 0) * Bk;
     const float* brow = acts + static_cast<long>(F1 + i0 + lr) * Bk;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
@@ -1003,9 +1022,9 @@ __device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s
         if (j < F1) {
           const int p = O_FC1W + j * NIN + i;
           float g = v[r];
-          if (accumulate) g += grads[p];
+          if (accumulate) g += g0[r];
           grads[p] = g;
-          if (hp) sgd_update(params, hp, frag, p, g);
+          if (hp) sgd_update(params, lrate, gsc, frag, p, w0[r], g);
         }
       }
     }
