@@ -644,7 +644,7 @@ __device__ __forceinline__ bool bn_partials_all(const float (&s1)[8], const floa
 // seen every block's tagged partials (so every block has read the header), stores header = epoch + 1.  A region
 // and its header are only ever written by launches that hold that slot, so every stale tag in it is <= the
 // header: a tag equal to header + 1 is always this launch's.  Returns true on block 0 (the writer).
-constexpr int kBnTagChunks = 64;                         // row chunks per region (nrb cap of the tagged mode)
+constexpr int kBnTagChunks = 128;                        // row chunks per region (nrb cap of the tagged mode)
 constexpr int kBnTagWords = kBnTagChunks * 2 * kBnCG;    // 64-bit words per region
 
 __device__ __forceinline__ uint64_t bn_tag_pack(float v, uint32_t tag) {
@@ -674,40 +674,44 @@ __device__ __forceinline__ bool bn_partials_tagged(const float (&s1)[8], const f
   const int q = tid >> 6, ch = tid & 63;
   float a1 = 0.f, a2 = 0.f;
   if (cbase + ch < C) {
-    constexpr int KT = kBnTagChunks / kBnQ;  // every chunk of the lane in one trip
-    uint64_t u1[KT], u2[KT];
+    constexpr int KT = 64 / kBnQ;  // 64 chunks per trip (one trip up to 64 chunks)
     const uint64_t pad = bn_tag_pack(0.f, tag);
-#pragma unroll
-    for (int k = 0; k < KT; ++k) {
-      const int b = q + k * kBnQ;
-      u1[k] = b < nrb ? __hip_atomic_load(parts + (b * 2) * kBnCG + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : pad;
-      u2[k] = b < nrb ? __hip_atomic_load(parts + (b * 2 + 1) * kBnCG + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                      : pad;
-    }
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-      bool ok = true;
-#pragma unroll
-      for (int k = 0; k < KT; ++k) ok = ok && (u1[k] >> 32) == tag && (u2[k] >> 32) == tag;
-      if (ok) break;
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kBnWaitTicks) {
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
+    for (int b0 = q; b0 < nrb; b0 += KT * kBnQ) {
+      uint64_t u1[KT], u2[KT];
 #pragma unroll
       for (int k = 0; k < KT; ++k) {
-        const int b = q + k * kBnQ;
-        if ((u1[k] >> 32) != tag)
-          u1[k] = __hip_atomic_load(parts + (b * 2) * kBnCG + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((u2[k] >> 32) != tag)
-          u2[k] = __hip_atomic_load(parts + (b * 2 + 1) * kBnCG + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int b = b0 + k * kBnQ;
+        u1[k] = b < nrb ? __hip_atomic_load(parts + (b * 2) * kBnCG + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : pad;
+        u2[k] = b < nrb ? __hip_atomic_load(parts + (b * 2 + 1) * kBnCG + ch, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT)
+                        : pad;
       }
-    }
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        bool ok = true;
 #pragma unroll
-    for (int k = 0; k < KT; ++k) {
-      a1 += __uint_as_float(static_cast<uint32_t>(u1[k]));
-      a2 += __uint_as_float(static_cast<uint32_t>(u2[k]));
+        for (int k = 0; k < KT; ++k) ok = ok && (u1[k] >> 32) == tag && (u2[k] >> 32) == tag;
+        if (ok) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kBnWaitTicks) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+          const int b = b0 + k * kBnQ;
+          if ((u1[k] >> 32) != tag)
+            u1[k] = __hip_atomic_load(parts + (b * 2) * kBnCG + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((u2[k] >> 32) != tag)
+            u2[k] = __hip_atomic_load(parts + (b * 2 + 1) * kBnCG + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < KT; ++k) {
+        a1 += __uint_as_float(static_cast<uint32_t>(u1[k]));
+        a2 += __uint_as_float(static_cast<uint32_t>(u2[k]));
+      }
     }
   }
   red[0][q][ch] = a1;
@@ -1561,7 +1565,8 @@ int bn_blocks(int P, int C, int& rows_per_block) {
 // (the finalizing block reads chunks x 2 x 64 partials).
 int bn_fin_grid(int P, int C, int& rpb, int groups = 1) {
   const int ncg = (C + kBnCG - 1) / kBnCG;
-  static const int kChunks = std::getenv("PDE_BN_CHUNKS") ? std::atoi(std::getenv("PDE_BN_CHUNKS")) : 64;
+  // r3af (tagged hand-off): 64 -> 128 chunks, ResNet-50 3.328 -> 3.284 ms (the C <= 128 layers get 128-256 blocks)
+  static const int kChunks = std::getenv("PDE_BN_CHUNKS") ? std::atoi(std::getenv("PDE_BN_CHUNKS")) : 128;
   // r2m sweep at 512 threads per block: 256 blocks (one per CU, 8 waves) 3.83 -> 3.79 ms/step
   static const int kTarget = std::getenv("PDE_BN_BLOCKS") ? std::atoi(std::getenv("PDE_BN_BLOCKS")) : 256;
   int nrb = std::max(1, std::min(kChunks, kTarget / (ncg * groups)));
@@ -1613,7 +1618,7 @@ int* bn_window(int n, hipStream_t s, int which) {
 }
 // Tagged hand-off regions (bn_partials_tagged): kBnTagSlots fixed (header, region) pairs, zeroed once, handed
 // out in a rolling window of n consecutive slots.  A slot's region is only written by launches holding that slot.
-constexpr int kBnTagSlots = 4096;  // x 64 KB
+constexpr int kBnTagSlots = 2048;  // x 128 KB
 uint64_t* bn_tag_slots(int n, hipStream_t s, uint32_t** hdr) {
   static uint64_t* parts[64] = {};
   static uint32_t* hdrs[64] = {};
