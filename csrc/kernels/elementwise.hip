@@ -173,18 +173,25 @@ __device__ __forceinline__ void conv_w_layouts_tiled3x3(const ConvLayoutEntry& e
       tile[tap][col][cil] = v[u];
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < kCwTile * RS * kCwTile; q += blockDim.x) {  // fwd [co][tap][ci]
-      const int col = q / (RS * kCwTile), rem = q - col * (RS * kCwTile);
-      const int tap = rem / kCwTile, cil = rem - tap * kCwTile;
-      const int co = co0 + col, ci = ci0 + cil;
-      if (co < e.Cop && ci < e.Cp) e.fwd[(static_cast<long>(co) * RS + tap) * e.Cp + ci] = f2bf(tile[tap][col][cil]);
-    }
-    for (int q = threadIdx.x; q < kCwTile * RS * kCwTile; q += blockDim.x) {  // dgrad [ci][tap][co]
-      const int cil = q / (RS * kCwTile), rem = q - cil * (RS * kCwTile);
-      const int tap = rem / kCwTile, col = rem - tap * kCwTile;
+    // 4 consecutive channels per 8-byte store (Cp, Cop are multiples of 8: a group never straddles the edge)
+    constexpr int kQ4 = kCwTile * RS * kCwTile / 4;
+    for (int q = threadIdx.x; q < kQ4; q += blockDim.x) {  // fwd [co][tap][ci]
+      const int col = q / (RS * kCwTile / 4), rem = q - col * (RS * kCwTile / 4);
+      const int tap = rem / (kCwTile / 4), cil = (rem - tap * (kCwTile / 4)) * 4;
       const int co = co0 + col, ci = ci0 + cil;
       if (co < e.Cop && ci < e.Cp)
-        e.dgrad[(static_cast<long>(ci) * RS + tap) * e.Cop + co] = f2bf(tile[tap][col][cil]);
+        *reinterpret_cast<u16x4*>(e.fwd + (static_cast<long>(co) * RS + tap) * e.Cp + ci) =
+            u16x4{f2bf(tile[tap][col][cil]), f2bf(tile[tap][col][cil + 1]), f2bf(tile[tap][col][cil + 2]),
+                  f2bf(tile[tap][col][cil + 3])};
+    }
+    for (int q = threadIdx.x; q < kQ4; q += blockDim.x) {  // dgrad [ci][tap][co]
+      const int cil = q / (RS * kCwTile / 4), rem = q - cil * (RS * kCwTile / 4);
+      const int tap = rem / (kCwTile / 4), col = (rem - tap * (kCwTile / 4)) * 4;
+      const int co = co0 + col, ci = ci0 + cil;
+      if (co < e.Cop && ci < e.Cp)
+        *reinterpret_cast<u16x4*>(e.dgrad + (static_cast<long>(ci) * RS + tap) * e.Cop + co) =
+            u16x4{f2bf(tile[tap][col][cil]), f2bf(tile[tap][col + 1][cil]), f2bf(tile[tap][col + 2][cil]),
+                  f2bf(tile[tap][col + 3][cil])};
     }
     __syncthreads();
   }

@@ -478,8 +478,9 @@ def test_optimizer_maintained_compute_copies(gpu, kind):
     torch.manual_seed(4)
     conv = L.Conv2d(32, 48, 1, bias=False).to(gpu)
     conv3 = L.Conv2d(3, 20, 3, padding=1).to(gpu)  # KxK: layout copies refreshed after the update
+    conv3b = L.Conv2d(40, 72, 3, padding=1, bias=False).to(gpu)  # several 32 x 32 tiles, partial edge tiles
     fc = L.Linear(40, 12).to(gpu)
-    params = list(conv.parameters()) + list(conv3.parameters()) + list(fc.parameters())
+    params = list(conv.parameters()) + list(conv3.parameters()) + list(conv3b.parameters()) + list(fc.parameters())
     opt = (FusedSGD(params, lr=0.1, momentum=0.9) if kind == "sgd" else FusedAdam(params, lr=1e-2))
     for p in params:
         p.grad = torch.randn_like(p)
@@ -492,6 +493,9 @@ def test_optimizer_maintained_compute_copies(gpu, kind):
     w3 = conv3.weight.detach()
     assert torch.equal(OF._maintained(conv3.weight, "conv_fwd"), C.conv_w_fwd(w3, 8, 24))
     assert torch.equal(OF._maintained(conv3.weight, "conv_dgrad"), C.conv_w_dgrad(w3, 8, 24))
+    w3b = conv3b.weight.detach()
+    assert torch.equal(OF._maintained(conv3b.weight, "conv_fwd"), C.conv_w_fwd(w3b, 40, 72))
+    assert torch.equal(OF._maintained(conv3b.weight, "conv_dgrad"), C.conv_w_dgrad(w3b, 40, 72))
     sd3 = {k: torch.randn_like(v) for k, v in conv3.state_dict().items()}
     conv3.load_state_dict(sd3)
     assert torch.equal(OF._maintained(conv3.weight, "conv_dgrad"), C.conv_w_dgrad(sd3["weight"], 8, 24))
