@@ -91,10 +91,30 @@ __global__ void k_ce_fused(const void* x, int f32, const int64_t* __restrict__ t
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     const long base = static_cast<long>(b) * V;
     const int t = static_cast<int>(tgt[b]);
-    const float l = row_lse(x, f32, base, V);
-    acc += l - ld(x, f32, base + t);
     uint16_t* drow = dx + static_cast<long>(b) * ldx;  // (row pitch ldx >= V: columns past V are untouched)
-    for (int v = 0; v < V; ++v) drow[v] = f2bf((__expf(ld(x, f32, base + v) - l) - (v == t ? 1.f : 0.f)) * inv_b);
+    if (V <= 16) {  // the row in registers: one round of loads, the target logit selected, not re-read
+      float r[16];
+#pragma unroll
+      for (int v = 0; v < 16; ++v) r[v] = v < V ? ld(x, f32, base + v) : -INFINITY;
+      float m = r[0], xt = 0.f;
+#pragma unroll
+      for (int v = 1; v < 16; ++v) m = fmaxf(m, r[v]);
+      float sum = 0.f;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        sum += v < V ? __expf(r[v] - m) : 0.f;
+        xt = v == t ? r[v] : xt;
+      }
+      const float l = m + __logf(sum);
+      acc += l - xt;
+#pragma unroll
+      for (int v = 0; v < 16; ++v)
+        if (v < V) drow[v] = f2bf((__expf(r[v] - l) - (v == t ? 1.f : 0.f)) * inv_b);
+    } else {
+      const float l = row_lse(x, f32, base, V);
+      acc += l - ld(x, f32, base + t);
+      for (int v = 0; v < V; ++v) drow[v] = f2bf((__expf(ld(x, f32, base + v) - l) - (v == t ? 1.f : 0.f)) * inv_b);
+    }
   }
   const float tot = block_sum(acc, red);
   if (threadIdx.x == 0) loss[0] = tot * inv_b;
@@ -142,12 +162,28 @@ __global__ void k_log_softmax_bwd(const float* __restrict__ dy, const float* __r
 __global__ void __launch_bounds__(kLossThreads)
 k_mse_fwd(const void* p, int f32, const float* __restrict__ t, long n, float* __restrict__ loss) {
   __shared__ float red[16];
-  float acc = 0.f;
-  for (long i = threadIdx.x; i < n; i += blockDim.x) {
-    const float d = ld(p, f32, i) - t[i];
-    acc += d * d;
+  // 8 element pairs per thread in flight per trip (one block: the trip count, not bandwidth, sets the time)
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const long st = blockDim.x;
+  long i = threadIdx.x;
+  for (; i + 7 * st < n; i += 8 * st) {
+    float a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a[u] = ld(p, f32, i + u * st);
+      b[u] = t[i + u * st];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float d = a[u] - b[u];
+      acc[u & 3] += d * d;
+    }
   }
-  const float tot = block_sum(acc, red);
+  for (; i < n; i += st) {
+    const float d = ld(p, f32, i) - t[i];
+    acc[0] += d * d;
+  }
+  const float tot = block_sum((acc[0] + acc[1]) + (acc[2] + acc[3]), red);
   if (threadIdx.x == 0) loss[0] = tot / static_cast<float>(n);
 }
 
