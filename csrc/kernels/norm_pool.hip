@@ -1681,6 +1681,11 @@ bool bn_rc8_on() {
   static const bool on = !(std::getenv("PDE_BN_RC8") != nullptr && std::getenv("PDE_BN_RC8")[0] == '0');
   return on;
 }
+// PDE_BN_RC16=1: chunks of 9..16 rows per thread in registers too (the stem's BatchNorm at batch 32)
+bool bn_rc16_on() {
+  static const bool on = std::getenv("PDE_BN_RC16") != nullptr && std::getenv("PDE_BN_RC16")[0] == '1';
+  return on;
+}
 // Tagged partials (bn_partials_tagged) where the grid allows (<= kBnTagChunks row chunks), r3aa: ResNet-50
 // 3.52 -> 3.34 ms/step; PDE_BN_TAGGED=0: the ticket + flag hand-off.
 bool bn_tagged_on() {
@@ -1733,6 +1738,11 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
                            relu, y, slabs, splits, static_cast<long>(P) * C, gscratch, gt, mode, parts);
       else if (rc_on && bn_rc8_on() && ceil_div(rpb, kBnRows) <= 8)
         hipLaunchKernelGGL(k_bn_fwd_fused<8>, dim3(nrb1, ncg, groups), dim3(kBnThreads), 0, s,
+                           const_cast<uint16_t*>(x), Pg, C, rpb, ws, tk, fl, err, gamma, beta, eps, momentum,
+                           running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C, res,
+                           relu, y, slabs, splits, static_cast<long>(P) * C, gscratch, gt, mode, parts);
+      else if (rc_on && bn_rc16_on() && ceil_div(rpb, kBnRows) <= 16)
+        hipLaunchKernelGGL(k_bn_fwd_fused<16>, dim3(nrb1, ncg, groups), dim3(kBnThreads), 0, s,
                            const_cast<uint16_t*>(x), Pg, C, rpb, ws, tk, fl, err, gamma, beta, eps, momentum,
                            running_mean, running_var, save_mean, save_invstd, scale_shift, scale_shift + C, res,
                            relu, y, slabs, splits, static_cast<long>(P) * C, gscratch, gt, mode, parts);
@@ -1827,6 +1837,9 @@ hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, cons
                            ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, mode, parts);
       else if (bn_rc8_on() && ceil_div(rpb, kBnRows) <= 8)
         hipLaunchKernelGGL(k_bn_bwd_fused<8>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
+                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, mode, parts);
+      else if (bn_rc16_on() && ceil_div(rpb, kBnRows) <= 16)
+        hipLaunchKernelGGL(k_bn_bwd_fused<16>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
                            ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, mode, parts);
       else
         hipLaunchKernelGGL(k_bn_bwd_fused<0>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
