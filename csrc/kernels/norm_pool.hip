@@ -1681,7 +1681,8 @@ bool bn_rc8_on() {
   static const bool on = !(std::getenv("PDE_BN_RC8") != nullptr && std::getenv("PDE_BN_RC8")[0] == '0');
   return on;
 }
-// PDE_BN_RC16=1: chunks of 9..16 rows per thread in registers too (the stem's BatchNorm at batch 32)
+// PDE_BN_RC16=1: chunks of 9..16 rows per thread in registers too (the stem's BatchNorm at batch 32); r3al:
+// level or slightly slower (3.251 -> 3.260 ms), so off by default
 bool bn_rc16_on() {
   static const bool on = std::getenv("PDE_BN_RC16") != nullptr && std::getenv("PDE_BN_RC16")[0] == '1';
   return on;
