@@ -59,6 +59,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            },
            py::arg("parent"), py::arg("exclude"), py::arg("abort_parent") = false)
       .def_static("shrink_supported", &RcclComm::shrink_supported)
+      .def("split_from",
+           [](RcclComm& c, RcclComm& parent, int color, int key) {
+             py::gil_scoped_release nogil;
+             return c.split_from(parent, color, key);
+           },
+           py::arg("parent"), py::arg("color"), py::arg("key"))
       .def("destroy", [](RcclComm& c) { py::gil_scoped_release nogil; c.destroy(); })
       .def_property_readonly("valid", &RcclComm::valid)
       .def_property_readonly("rank", &RcclComm::rank)

@@ -167,6 +167,26 @@ int RcclComm::shrink_from(RcclComm& parent, const std::vector<int>& exclude, boo
   return 2;
 }
 
+bool RcclComm::split_from(RcclComm& parent, int color, int key) {
+  if (parent.comm_ == nullptr) throw std::runtime_error("pde rccl: split from an invalid communicator");
+  if (comm_ != nullptr) abort();
+  hip_check(hipSetDevice(parent.device_), "hipSetDevice");
+  if (stream_ == nullptr) {
+    int lo = 0, hi = 0;
+    hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priority range");
+    hip_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "comm stream");
+  }
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  ncclComm_t out = nullptr;
+  check(ncclCommSplit(parent.comm_, color < 0 ? NCCL_SPLIT_NOCOLOR : color, key, &out, &cfg), "ncclCommSplit");
+  comm_ = out;
+  device_ = parent.device_;
+  if (comm_ == nullptr) return false;
+  check(ncclCommUserRank(comm_, &rank_), "ncclCommUserRank");
+  check(ncclCommCount(comm_, &size_), "ncclCommCount");
+  return true;
+}
+
 void RcclComm::abort() {
   if (comm_ != nullptr) {
     ncclCommAbort(comm_);

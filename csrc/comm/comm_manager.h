@@ -39,6 +39,10 @@ class RcclComm {
   // communicator) -> returns 2.  The parent stays valid (destroy/abort it separately).
   int shrink_from(RcclComm& parent, const std::vector<int>& exclude, bool abort_parent);
   static bool shrink_supported();
+  // Planned membership change with every parent rank alive (elastic scale-down): ncclCommSplit over the
+  // parent, collective over ALL parent ranks.  color < 0 = leaving (NCCL_SPLIT_NOCOLOR: no communicator,
+  // returns false); `key` orders the ranks of the child.  No unique-id exchange, topology reused.
+  bool split_from(RcclComm& parent, int color, int key);
   void destroy();  // ncclCommDestroy after a clean finish
   bool valid() const { return comm_ != nullptr; }
   int rank() const { return rank_; }

@@ -55,7 +55,10 @@ __device__ __forceinline__ bool xgmi_publish_and_wait(const XgmiView& v, int b, 
     uint32_t* mine = reinterpret_cast<uint32_t*>(v.base[v.rank]) + b * kXgmiMaxRanks + tid;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (static_cast<int32_t>(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks) {
+      // fail fast once any wait of this instance timed out (the error word stays set until the host reads and
+      // resets it at a commit point): a dead peer costs ONE timeout, not one per queued call of a graph replay
+      if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks ||
+          __hip_atomic_load(v.state + kXgmiStateError, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
         *s_fail = 1;
         __hip_atomic_store(v.state + kXgmiStateError, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;

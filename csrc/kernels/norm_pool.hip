@@ -1563,12 +1563,14 @@ int bn_blocks(int P, int C, int& rows_per_block) {
 // made the finalizing tail 0.14 ms/step slower; 64 chunks measure level with the 3-pass form at 106 fewer
 // launches per step)
 // (the finalizing block reads chunks x 2 x 64 partials).
+int bn_resident_cap();
 int bn_fin_grid(int P, int C, int& rpb, int groups = 1) {
   const int ncg = (C + kBnCG - 1) / kBnCG;
   // r3af (tagged hand-off): 64 -> 128 chunks, ResNet-50 3.328 -> 3.284 ms (the C <= 128 layers get 128-256 blocks)
   static const int kChunks = std::getenv("PDE_BN_CHUNKS") ? std::atoi(std::getenv("PDE_BN_CHUNKS")) : 128;
   // r2m sweep at 512 threads per block: 256 blocks (one per CU, 8 waves) 3.83 -> 3.79 ms/step
-  static const int kTarget = std::getenv("PDE_BN_BLOCKS") ? std::atoi(std::getenv("PDE_BN_BLOCKS")) : 256;
+  static const int kTarget = std::min(bn_resident_cap(),
+                                      std::getenv("PDE_BN_BLOCKS") ? std::atoi(std::getenv("PDE_BN_BLOCKS")) : 256);
   int nrb = std::max(1, std::min(kChunks, kTarget / (ncg * groups)));
   nrb = std::min(nrb, std::max(1, P / kBnRows));
   rpb = ceil_div(P, nrb);
@@ -1653,17 +1655,42 @@ int* bn_tickets(int n, hipStream_t s) { return bn_window(n, s, 0); }
 uint32_t* bn_flags(int n, hipStream_t s) { return reinterpret_cast<uint32_t*>(bn_window(n, s, 1)); }
 
 // One-launch BatchNorm (k_bn_fwd_fused / k_bn_bwd_fused): on unless PDE_BN_FUSED=0, and only for grids the
-// chip holds at once (every block must be resident for the flag waits).
+// chip holds at once (every block must be resident for the flag waits).  The cap is measured, not assumed:
+// the smallest hipOccupancyMaxActiveBlocksPerMultiprocessor over every k_bn_*_fused<RC> instantiation (the
+// register-resident RC = 4 / 8 / 16 variants hold 169-256 VGPRs: ONE 512-thread block per CU) times the CU
+// count, minus PDE_BN_HEADROOM blocks (default 0) left for kernels that other streams keep spinning (ring
+// sends waiting for credit, an overlapped RCCL all-reduce).  A hand-off that still times out sets the error
+// word, which every sync point reads (ops.functional.check_device_errors) and raises on.
+int bn_resident_cap() {
+  static int cap = -1;
+  if (cap < 0) {
+    int dev = 0, cus = 1;
+    hipDeviceProp_t prop{};
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      cus = prop.multiProcessorCount;
+    int occ = 1 << 20;
+    auto q = [&occ](const void* fn) {
+      int n = 0;
+      occ = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBnThreads, 0) == hipSuccess)
+                ? std::min(occ, n) : std::min(occ, 1);
+    };
+    q(reinterpret_cast<const void*>(&k_bn_fwd_fused<0>));
+    q(reinterpret_cast<const void*>(&k_bn_fwd_fused<4>));
+    q(reinterpret_cast<const void*>(&k_bn_fwd_fused<8>));
+    q(reinterpret_cast<const void*>(&k_bn_fwd_fused<16>));
+    q(reinterpret_cast<const void*>(&k_bn_bwd_fused<0>));
+    q(reinterpret_cast<const void*>(&k_bn_bwd_fused<4>));
+    q(reinterpret_cast<const void*>(&k_bn_bwd_fused<8>));
+    q(reinterpret_cast<const void*>(&k_bn_bwd_fused<16>));
+    const int headroom = std::getenv("PDE_BN_HEADROOM") ? std::max(0, std::atoi(std::getenv("PDE_BN_HEADROOM"))) : 0;
+    cap = std::max(1, std::max(1, occ) * cus - headroom);
+  }
+  return cap;
+}
+
 bool bn_one_launch(int blocks) {
   static const bool off = std::getenv("PDE_BN_FUSED") != nullptr && std::getenv("PDE_BN_FUSED")[0] == '0';
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    hipDeviceProp_t prop{};
-    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-              ? prop.multiProcessorCount : 1;
-  }
-  return !off && blocks <= 2 * cus;
+  return !off && blocks <= bn_resident_cap();
 }
 
 // flag hand-off without the agent-scope L2 write-back / invalidate (see bn_publish); r3w: ResNet-50

@@ -85,6 +85,11 @@ def comm():
     return _load("_comm")
 
 
+def loaded(name: str = "_C") -> bool:
+    """Whether the extension was already loaded by this process (no import attempted)."""
+    return name in _mods
+
+
 def available(name: str = "_C") -> bool:
     try:
         _load(name)

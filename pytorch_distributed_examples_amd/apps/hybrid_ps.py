@@ -213,7 +213,7 @@ class ResNetPipelineDP:
         return all(ch is None or ch.mode != "host" for ch in (self.engine.prev, self.engine.next))
 
     def check(self):
-        """Raise if a stage channel timed out (synchronises the device)."""
+        """Raise if a stage channel or a one-launch BatchNorm hand-off timed out (synchronises the device)."""
         self.engine.check()
 
     def step(self, timer=None):
@@ -262,6 +262,7 @@ def run_resnet_hybrid(stages: int, dp: int, steps: int, warmup: int, batch: int,
     pdist.barrier(ctx)
     if ctx.device.type == "cuda":
         torch.cuda.synchronize()
+    pipe.check()  # ring waits and one-launch BatchNorm hand-offs of the run: raise on a timeout
     dt = pdist.max_over_ranks(time.perf_counter() - t0, ctx.device)
     img_s = pipe.images_per_step * steps / dt
     if not quiet and ctx.rank == stages - 1:

@@ -142,6 +142,7 @@ class Trainer:
             check = getattr(self.ddp.comm, "check", None)
             if check is not None:
                 check()
+            OF.check_device_errors(f"rank {self.global_rank} epoch {epoch}")
         dt = time.perf_counter() - t0
         img_s = pdist.sum_over_ranks(n / dt, self.ctx.device)
         if self.metrics is not None:
@@ -203,7 +204,13 @@ def main(argv=None):
     args.device = rtconfig.device_for(cfg, args.device)
 
     start = time.time()
-    if args.rewire:
+    if args.rewire and args.fused and args.model == "cnn":
+        # the fused whole-step CNN with the gradient exchange over xGMI inside its reduction kernel, one hipGraph
+        # per membership round (BASELINE config 2's data plane; CPU: the same protocol over autograd + gloo)
+        from ..elastic.rewire import run_elastic_fused
+
+        run_elastic_fused(args)
+    elif args.rewire:
         from ..elastic.rewire import run_elastic
 
         run_elastic(args)

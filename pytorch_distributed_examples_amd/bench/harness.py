@@ -68,6 +68,8 @@ def parse_args(argv=None):
                              "elastic_cnn"])
     ap.add_argument("--stage", type=int, default=1, choices=[1, 2], help="resnet50_stage: which pipeline stage")
     ap.add_argument("--scale-to", type=int, default=None, help="elastic_cnn: world size after the first round")
+    ap.add_argument("--fault-at", type=int, default=None,
+                    help="elastic_cnn: the last rank exits at this training step; the survivors re-wire in-process")
     ap.add_argument("--elastic-worker", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--hosts-file", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--report", default=None, help=argparse.SUPPRESS)
@@ -480,6 +482,10 @@ def main(argv=None):
     dt = time.perf_counter() - t0
     if hasattr(work, "check"):
         work.check()
+    if on_gpu:  # a one-launch BatchNorm hand-off that timed out invalidates the measurement: fail loudly
+        from ..ops.functional import check_device_errors
+
+        check_device_errors(f"rank {ctx.rank} after the timed region")
     dt = pdist.max_over_ranks(dt, ctx.device)
     final_loss = _report_loss(work, ctx, loss)
     phases = _measure_phases(work, ctx, args) if os.environ.get("PDE_BENCH_PHASES", "1") != "0" else None

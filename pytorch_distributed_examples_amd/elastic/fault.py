@@ -30,12 +30,19 @@ def _armed():
 
 
 def maybe_fault(step: int, rank: int) -> None:
+    maybe_fault_in(step, step + 1, rank)
+
+
+def maybe_fault_in(lo: int, hi: int, rank: int) -> None:
+    """Fault if the armed step lies in ``[lo, hi)`` -- for loops that advance several steps at once (a hipGraph
+    replay of G training steps): the fault fires after the replay that contains the armed step."""
     cfg = _armed()
     if cfg is None:
         return
     at, frank, mode = cfg
-    if step != at or rank != frank:
+    if not (lo <= at < hi) or rank != frank:
         return
+    step = at
     marker = os.environ.get("PDE_FAULT_ONCE")
     if marker:
         if os.path.exists(marker):

@@ -57,6 +57,10 @@ class RendezvousClient:
                     return self.round, self.rank, self.size
                 if self.store.check(["shutdown"]):
                     raise SystemExit(0)
+                if self.round >= 0 and self.store.check([f"round/{r}/members"]):
+                    # a member of an earlier round that the newest one drops: the driver removed this worker's
+                    # host (planned scale-down; the driver never re-adds a worker id) -> leave cleanly
+                    raise SystemExit(0)
             if time.time() - t0 > self.timeout_s:
                 raise TimeoutError(f"worker {self.wid}: no rendezvous round after {after} within {self.timeout_s}s")
             time.sleep(0.05)

@@ -32,6 +32,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _native
+from . import fault
 from .rendezvous import RendezvousClient
 
 
@@ -66,49 +67,101 @@ class _GpuWork:
         return True
 
 
+def _emulated() -> bool:
+    """``PDE_REWIRE_EMULATE=gloo``: on CPU, RoundComm's data-plane communicator is a gloo stand-in for RCCL
+    (:class:`..parallel.gloo_comm.GlooComm`) so the init / shrink / split protocol runs in the CPU tests."""
+    return os.environ.get("PDE_REWIRE_EMULATE", "") == "gloo"
+
+
 class RoundComm:
     """Communicator set of one rendezvous round (see the module docstring).
 
-    ``parent`` (the previous round's RoundComm, not yet torn down): when this round's members are a subset
-    of the parent's -- a shrink -- and the loaded RCCL exports ``ncclCommShrink``, the RCCL communicator is
-    shrunk from the parent's (the dead ranks excluded, in-flight work aborted first) instead of being built
-    from a fresh unique id; ``self.how`` records ``shrink`` / ``init``.  (torch's bundled RCCL 2.26 has no
-    ncclCommShrink: there a shrink re-initialises.)  ``use_rccl=False``: control plane only (the fused CNN
-    exchanges gradients over xGMI inside its reduction kernel)."""
+    How the round's RCCL communicator is built (``self.how``), agreed by every member over the round's gloo
+    group first so no member can take a different path:
+
+    * ``split`` -- a PLANNED scale-down (the driver dropped hosts; every old member alive): all members of the
+      previous round called :meth:`planned_split` at its last commit point (``ncclCommSplit``, the leavers
+      with ``NCCL_SPLIT_NOCOLOR``) and pass the child here as ``premade``: no unique-id exchange, topology
+      reused (ref: horovod/horovod_mnist_elastic.py:108 ``--min-np`` shrink);
+    * ``shrink`` -- after a FAILURE, when this round only drops members of ``parent``'s round (same order), the
+      parent's communicator is still valid on EVERY survivor and the loaded RCCL exports ``ncclCommShrink``
+      (torch's bundled RCCL 2.26 does not);
+    * ``init`` -- otherwise: a fresh communicator from a new unique id (growth, or a shrink RCCL cannot do).
+
+    ``use_rccl=False``: control plane only (the fused CNN exchanges gradients over xGMI inside its reduction
+    kernel).  ``timing`` holds the seconds spent on the control group and on the data-plane communicator."""
 
     def __init__(self, rdzv: RendezvousClient, rank: int, size: int, device: torch.device,
                  timeout_s: float = 120.0, grace_s: float = 2.0, parent: "RoundComm | None" = None,
-                 use_rccl: bool = True):
+                 use_rccl: bool = True, premade=None):
         self.rdzv, self.rank, self.size, self.device = rdzv, rank, size, device
         self.timeout_s, self.grace_s = timeout_s, grace_s
         self.members = rdzv.members()
         self.how = "none"
+        self.timing = {}
+        t0 = time.perf_counter()
         store = rdzv.pg_store()
         dist.init_process_group("gloo", store=store, rank=rank, world_size=size,
                                 timeout=datetime.timedelta(seconds=timeout_s))
+        t1 = time.perf_counter()
+        self.timing["control_group_s"] = t1 - t0
         self.rccl = None
-        if use_rccl and device.type == "cuda" and size > 1:
-            C = _native.comm()
-            excl = self._shrink_plan(parent)
-            if excl is not None and C.RcclComm.shrink_supported():
-                self.rccl = C.RcclComm()
-                self.rccl.shrink_from(parent.rccl, excl, True)
-                self.how = "shrink"
-            else:
-                if rank == 0:
-                    store.set("rccl_uid", C.rccl_unique_id())
-                uid = store.get("rccl_uid")
-                self.rccl = C.RcclComm()
-                self.rccl.init(uid, rank, size, device.index, True)
-                self.how = "init"
+        self.emulated = device.type == "cpu" and _emulated()
+        if use_rccl and size > 1 and (device.type == "cuda" or self.emulated):
+            self._build_data_plane(store, parent, premade)
+        elif premade is not None:
+            premade[1].abort()  # a one-rank round needs no data plane
         if parent is not None:
             parent.release()
+        self.timing["data_plane_s"] = time.perf_counter() - t1
         self.supports_avg = self.rccl is not None
         self._steps = []  # end-of-step events not yet checked on the host (GPU data plane)
 
+    def _comm_cls(self):
+        if self.emulated:
+            from ..parallel.gloo_comm import GlooComm
+
+            return GlooComm
+        return _native.comm().RcclComm
+
+    def _build_data_plane(self, store, parent, premade):
+        Comm = self._comm_cls()
+        excl = self._shrink_plan(parent)
+        code = 0
+        if premade is not None and premade[0] == self.members and premade[1].valid:
+            code = 2
+        elif excl is not None and Comm.shrink_supported():
+            code = 1
+        t = torch.tensor([float(code), -float(code)])
+        try:
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        except RuntimeError as exc:
+            raise PeerFailure(str(exc)) from exc
+        lo, hi = int(t[0].item()), int(-t[1].item())
+        if lo == 2:
+            self.rccl, self.how = premade[1], "split"
+            return
+        if premade is not None:
+            premade[1].abort()
+        if lo == 1 and hi == 1:
+            self.rccl = Comm()
+            self.rccl.shrink_from(parent.rccl, excl, True)
+            self.how = "shrink"
+            return
+        self.rccl = Comm()
+        if self.emulated:
+            self.rccl.init(store, "emu_rccl", self.rank, self.size, self.timeout_s)
+        else:
+            if self.rank == 0:
+                store.set("rccl_uid", _native.comm().rccl_unique_id())
+            uid = store.get("rccl_uid")
+            self.rccl.init(uid, self.rank, self.size, self.device.index, True)
+        self.how = "init"
+
     def _shrink_plan(self, parent):
-        """Parent ranks to exclude when this round only drops members of the parent's round, else None."""
-        if parent is None or parent.rccl is None or not parent.members or not self.members:
+        """Parent ranks to exclude when this round only drops members of the parent's round and the parent's
+        communicator is still valid HERE, else None (a PeerFailure usually aborted it already)."""
+        if parent is None or parent.rccl is None or not parent.rccl.valid or not parent.members or not self.members:
             return None
         if not set(self.members) < set(parent.members):
             return None
@@ -116,6 +169,35 @@ class RoundComm:
         if survivors != self.members:  # the shrunk communicator keeps the parent's rank order
             return None
         return [i for i, m in enumerate(parent.members) if m not in self.members]
+
+    def planned_split(self):
+        """Collective over THIS round (every member alive, at a commit point that raised MembershipChanged):
+        when the driver's newest round keeps a subset of this round's members in the same order, split the
+        RCCL communicator for it (``ncclCommSplit``; leavers pass NOCOLOR).  Returns ``("leave", None)`` for a
+        worker the newest round no longer contains, ``("split", (members, child))`` for a survivor of a split,
+        else ``("none", None)`` (growth or reordering: the next round initialises)."""
+        rdzv = self.rdzv
+        newest = None
+        if self.rank == 0:
+            deadline = time.time() + 30.0
+            while rdzv._current_round() <= rdzv.round and time.time() < deadline:
+                time.sleep(0.02)
+            newest = rdzv._current_round()
+        newest = self.broadcast_object(newest) if self.size > 1 else newest
+        members = rdzv.members(newest) if newest is not None and newest > rdzv.round else []
+        leaving = bool(members) and rdzv.wid not in members
+        subset = bool(members) and set(members) < set(self.members) and \
+            [m for m in self.members if m in members] == members
+        if not subset or self.rccl is None or not self.rccl.valid:
+            return ("leave", None) if leaving else ("none", None)
+        child = self._comm_cls()()
+        try:
+            made = child.split_from(self.rccl, -1 if leaving else 0, 0 if leaving else members.index(rdzv.wid))
+        except RuntimeError as exc:
+            raise PeerFailure(str(exc)) from exc
+        if leaving or not made:
+            return "leave", None
+        return "split", (members, child)
 
     def release(self):
         """Drop the RCCL communicator of a round whose successor was built (shrunk from it or not)."""
@@ -125,6 +207,8 @@ class RoundComm:
 
     # -- data plane ------------------------------------------------------------------------------
     def allreduce_async(self, t: torch.Tensor, avg: bool = False):
+        if self.rccl is not None and self.emulated:
+            return _CpuWork(self.rccl.allreduce_async(t, avg))
         if self.rccl is not None:
             self.rccl.allreduce_(t, 1 if avg else 0)
             ev = torch.cuda.Event()
@@ -133,6 +217,11 @@ class RoundComm:
         return _CpuWork(dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True))
 
     def broadcast_(self, t: torch.Tensor, src: int):
+        if self.rccl is not None and self.emulated:
+            try:
+                return self.rccl.broadcast_(t, src)
+            except RuntimeError as exc:
+                raise PeerFailure(str(exc)) from exc
         if self.rccl is not None:
             self.rccl.broadcast_(t, src)
             ev = torch.cuda.Event()
@@ -154,7 +243,7 @@ class RoundComm:
         """Mark the end of a training step.  The host checks the step ``lag`` steps back (its collectives
         finished, or a failure surfaces as :class:`PeerFailure`), so it never stalls on the step it just
         enqueued -- one liveness wait per step instead of one host sync per bucket."""
-        if self.rccl is None:
+        if self.rccl is None or self.emulated:
             return
         ev = torch.cuda.Event()
         ev.record()
@@ -213,7 +302,7 @@ class RoundComm:
     def close(self, abort: bool = False, keep_rccl: bool = False):
         """End of the round.  ``keep_rccl``: leave the RCCL communicator alive as the next round's shrink
         parent (released by that round); the gloo control group is always torn down."""
-        if self.rccl is not None and not abort:
+        if self.rccl is not None and not abort and not self.emulated:
             try:
                 self.drain()
             except PeerFailure:
@@ -277,11 +366,22 @@ class Commit:
         self.position.update(self._pos)
 
 
+def _as_peer_failure(fn):
+    """Run a data-/control-plane call of the round; its RuntimeError (an xGMI exchange that timed out on a dead
+    peer, a gloo collective or store wait whose peer vanished) becomes :class:`PeerFailure`, which the re-wire
+    loop survives -- never a raw error that would take the survivors down with the dead peer."""
+    try:
+        return fn()
+    except PeerFailure:
+        raise
+    except RuntimeError as exc:
+        raise PeerFailure(str(exc)) from exc
+
+
 def run_elastic(args):
     """``mnist_ddp_elastic.py --rewire``: the Trainer loop of apps/mnist_ddp.py with in-process re-wire."""
     from ..apps.mnist_ddp import load_train_objs
     from ..data.loader import ShardedLoader
-    from ..elastic import fault
     from ..elastic.snapshot import save_snapshot
     from ..parallel import dist as pdist
     from ..parallel.ddp import DistributedDataParallel
@@ -310,10 +410,11 @@ def run_elastic(args):
     ddp = None
     pid = os.getpid()
     parent = None  # previous round's communicator set, kept as a possible shrink parent
+    premade = None  # (members, communicator) split off the previous round for a planned scale-down
     while True:
         rnd, rank, size = rdzv.join()
-        comm = RoundComm(rdzv, rank, size, dev, parent=parent)
-        parent = None
+        comm = RoundComm(rdzv, rank, size, dev, parent=parent, premade=premade)
+        parent = premade = None
         log = RankLogger(rank)
         log.print(f"[rewire] round {rnd}: rank {rank} of {size} (pid {pid}, rccl {comm.how})", all_ranks=True)
         try:
@@ -368,15 +469,22 @@ def run_elastic(args):
         except PeerFailure as exc:
             log.print(f"[rewire] round {rnd}: peer failure ({str(exc).splitlines()[0][:120]}); restoring commit "
                       f"epoch {commit._pos['epoch']} seen {commit._pos['seen']}", all_ranks=True)
-            keep = comm.rccl is not None and comm.rccl.shrink_supported()
+            # a communicator the failure already aborted cannot be a shrink parent (RoundComm re-checks
+            # validity on every survivor and agrees before anyone calls ncclCommShrink)
+            keep = comm.rccl is not None and comm.rccl.valid and comm.rccl.shrink_supported()
             comm.close(abort=not keep, keep_rccl=keep)  # a shrink (ABORT flag) tears its work down
             parent = comm if keep else None
             commit.restore()
         except MembershipChanged:
             log.print(f"[rewire] round {rnd}: membership changed, re-joining", all_ranks=True)
-            keep = comm.rccl is not None and comm.rccl.shrink_supported()
-            comm.close(keep_rccl=keep)
-            parent = comm if keep else None
+            try:  # every member is alive here: a scale-down splits the communicator instead of re-initialising
+                how, premade = comm.planned_split()
+            except PeerFailure:
+                how, premade = "none", None
+            comm.close()
+            if how == "leave":
+                log.print(f"[rewire] round {rnd}: leaving the job (planned scale-down, pid {pid})", all_ranks=True)
+                break
     pdist.shutdown()
 
 
@@ -454,12 +562,20 @@ def run_elastic_fused(args, report=None):
     changed_at = None
     pid = os.getpid()
     while True:
+        t_join = _time.perf_counter()
         rnd, rank, size = rdzv.join()
+        t_joined = _time.perf_counter()
         comm = RoundComm(rdzv, rank, size, dev, use_rccl=False)
         log = RankLogger(rank)
         xa = None
+        # re-wire breakdown (seconds): rendezvous = membership change seen -> this round joined (includes the
+        # driver noticing and publishing it); control = the round's gloo group; broadcast = rank 0's weights
+        # and position; map = xGMI IPC handle exchange + peer mapping; capture = hipGraph recapture
+        parts = {"rendezvous_s": t_joined - (changed_at if changed_at is not None else t_join),
+                 "control_s": comm.timing.get("control_group_s", 0.0)}
         try:
             # everybody adopts rank 0's weights and position (one 87 KB broadcast over the control plane)
+            tb = _time.perf_counter()
             if size > 1:
                 if on_gpu:
                     comm.broadcast_(fused.flat, 0)
@@ -469,9 +585,14 @@ def run_elastic_fused(args, report=None):
             state = comm.broadcast_object(dict(pos) if rank == 0 else None) if size > 1 else dict(pos)
             pos.clear()
             pos.update(state)
+            sync()
+            parts["broadcast_s"] = _time.perf_counter() - tb
+            tm = _time.perf_counter()
             if on_gpu:
                 fused.invalidate()
-                xa = XgmiAllreduce(dev, key=f"rewire/{rnd}") if size > 1 else None
+                xa = _as_peer_failure(lambda: XgmiAllreduce(dev, key=f"rewire/{rnd}")) if size > 1 else None
+                parts["map_s"] = _time.perf_counter() - tm
+                tc = _time.perf_counter()
 
                 def train_step(x, y):
                     return fused.forward_backward(x, y, grad_out=grads, sgd=opt, xgmi=xa)
@@ -482,6 +603,8 @@ def run_elastic_fused(args, report=None):
                 from ..parallel.ddp import DistributedDataParallel
 
                 ddp = DistributedDataParallel(model, comm=comm, overlap=False)
+                parts["map_s"] = _time.perf_counter() - tm
+                tc = _time.perf_counter()
 
                 class _Eager:  # CapturedSteps' replay() surface over eager steps
                     def replay(self):
@@ -496,11 +619,13 @@ def run_elastic_fused(args, report=None):
 
                 graph = _Eager()
             sync()
+            parts["capture_s"] = _time.perf_counter() - tc
             rewire_s = _time.perf_counter() - changed_at if changed_at is not None else None
             changed_at = None
             plane = f"fused CNN + xGMI exchange, {G} steps per graph" if on_gpu else "CPU autograd + gloo DDP"
             log.print(f"[rewire] round {rnd}: rank {rank} of {size} (pid {pid}), {plane}" +
-                      (f", re-wired in {rewire_s:.3f}s" if rewire_s is not None else ""), all_ranks=True)
+                      (f", re-wired in {rewire_s:.3f}s (" + ", ".join(f"{k[:-2]} {v:.3f}" for k, v in parts.items())
+                       + ")" if rewire_s is not None else ""), all_ranks=True)
             commit.save()
             # timed window of this round (the bench reads it through `report`)
             warm, timed = int(getattr(args, "round_warmup", 2)), int(getattr(args, "round_replays", 10))
@@ -514,20 +639,19 @@ def run_elastic_fused(args, report=None):
             sync()
             dt = _time.perf_counter() - t0
             if xa is not None:
-                xa.check()
-            t = torch.tensor([dt])
-            if size > 1:
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            img_s = batch * size * G * timed / float(t.item())
+                _as_peer_failure(xa.check)
+            t = torch.tensor([dt] + [rewire_s if rewire_s is not None else -1.0] + list(parts.values()))
+            if size > 1:  # the slowest member's window and re-wire (one MAX over the control plane)
+                _as_peer_failure(lambda: dist.all_reduce(t, op=dist.ReduceOp.MAX))
+            img_s = batch * size * G * timed / float(t[0].item())
             pos["step"] += G * (warm + timed)
-            rw = torch.tensor([rewire_s if rewire_s is not None else -1.0])
-            if size > 1:
-                dist.all_reduce(rw, op=dist.ReduceOp.MAX)  # the slowest member's re-wire
             stop = False
             if report is not None:
-                stop = bool(report(rnd, rank, size, {
-                    "images_per_s": img_s, "ms_per_step": float(t.item()) / (G * timed) * 1e3,
-                    "rewire_s": float(rw.item()) if rw.item() >= 0 else None, "loss": float(loss.item())}))
+                info = {"images_per_s": img_s, "ms_per_step": float(t[0].item()) / (G * timed) * 1e3,
+                        "rewire_s": float(t[1].item()) if t[1].item() >= 0 else None, "loss": float(loss.item())}
+                if t[1].item() >= 0:
+                    info["rewire_parts"] = {k: round(float(v), 4) for k, v in zip(parts, t[2:].tolist())}
+                stop = bool(report(rnd, rank, size, info))
             # keep training; commit points every `commit_every` replays check liveness and membership
             since = 0
             while not stop:
@@ -536,15 +660,13 @@ def run_elastic_fused(args, report=None):
                 if not total_steps and pos["step"] >= args.total_epochs * steps_per_epoch:
                     break
                 graph.replay()
+                fault.maybe_fault_in(pos["step"], pos["step"] + G, rank)  # PDE_FAULT_*: a step of this replay
                 pos["step"] += G
                 since += 1
                 if since % commit_every == 0:
                     sync()
                     if xa is not None:
-                        try:
-                            xa.check()
-                        except RuntimeError as exc:
-                            raise PeerFailure(str(exc)) from exc
+                        _as_peer_failure(xa.check)
                     commit.save()
                     if comm.agree(rdzv.hosts_updated()):
                         raise MembershipChanged()

@@ -80,6 +80,7 @@ class Driver:
         self.blacklist: dict[str, float] = {}
         self.counter = 0
         self.free_devices = list(range(args.num_devices)) if args.num_devices > 0 else []
+        self.leaving: dict[str, float] = {}  # worker id -> deadline of a planned departure
 
     # ---------------------------------------------------------------------------------------------
     def log(self, msg):
@@ -166,6 +167,13 @@ class Driver:
                       flush=True)
                 if w.wid in self.order:
                     changed = True
+            for wid, dl in list(self.leaving.items()):
+                if self.workers[wid].proc.poll() is not None:
+                    del self.leaving[wid]
+                elif time.time() > dl:
+                    self.log(f"{wid} did not leave within {self.args.leave_grace}s: terminating")
+                    self.workers[wid].proc.send_signal(signal.SIGTERM)
+                    del self.leaving[wid]
             members = [wid for wid in self.order if self.workers[wid].proc.poll() is None]
             if all(w.finished for w in self.workers.values()):
                 ok = all(w.proc.returncode == 0 for w in self.workers.values() if w.wid in self.order) or \
@@ -181,8 +189,11 @@ class Driver:
                 allowed_hosts = {h for h, _ in slots}
                 for wid in list(members):
                     if self.workers[wid].host not in allowed_hosts and self.args.host_discovery_script:
-                        self.log(f"host of {wid} removed by discovery: terminating")
-                        self.workers[wid].proc.send_signal(signal.SIGTERM)
+                        # a PLANNED scale-down: the worker sees the new round at its next commit point, takes
+                        # part in the communicator split (rewire.RoundComm.planned_split) and exits 0;
+                        # terminated only if it has not left within --leave-grace seconds
+                        self.log(f"host of {wid} removed by discovery: asking it to leave")
+                        self.leaving[wid] = time.time() + self.args.leave_grace
                         members.remove(wid)
                         changed = True
                 if any(self.workers[wid].finished and self.workers[wid].proc.returncode == 0
@@ -223,6 +234,9 @@ def main(argv=None):
     ap.add_argument("--discovery-interval", type=float, default=1.0)
     ap.add_argument("--start-timeout", type=float, default=600.0)
     ap.add_argument("--elastic-timeout", type=float, default=600.0)
+    ap.add_argument("--leave-grace", type=float, default=60.0,
+                    help="seconds a worker whose host discovery dropped may take to leave by itself (it joins the "
+                         "communicator split at its next commit point) before it is terminated")
     ap.add_argument("--num-devices", type=int, default=-1, help="GPUs on this node (default: autodetect)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("command", nargs=argparse.REMAINDER)

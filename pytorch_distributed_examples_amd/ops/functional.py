@@ -98,6 +98,25 @@ def _C():
     return _native.C()
 
 
+class DeviceHandoffError(RuntimeError):
+    """A one-launch BatchNorm's cross-block hand-off timed out on the device (norm_pool.hip error word):
+    the normalisation of that step used incomplete statistics, so the replica's state is not trustworthy."""
+
+
+def check_device_errors(where: str = "") -> None:
+    """Read (and reset) the one-launch BatchNorm error word at a sync point; raise :class:`DeviceHandoffError`
+    if any flag / tagged-partial wait timed out since the last check.  Synchronises the device (call it only
+    where the host already waits: end of a timed region, epoch end, pipeline ``check()``).  No-op without a
+    GPU or before the native library was loaded."""
+    if not torch.cuda.is_available() or not _native.loaded("_C"):
+        return
+    v = _native.C().bn_error(True)
+    if v != 0:
+        raise DeviceHandoffError(f"one-launch BatchNorm hand-off {'failed' if v < 0 else 'timed out'} "
+                                 f"(error word {v}){' at ' + where if where else ''}: statistics of the step are "
+                                 "incomplete; the grid was not co-resident (PDE_BN_FUSED=0 disables the one-launch path)")
+
+
 # ---------------------------------------------------------------------------------------------
 # GEMM pairing
 # ---------------------------------------------------------------------------------------------

@@ -340,9 +340,12 @@ class PipelineEngine:
         return self._fwd_meta
 
     def check(self):
+        """Raise if a ring wait or a one-launch BatchNorm hand-off of this stage timed out (syncs the device)."""
         for ch in (self.prev, self.next):
             if ch is not None:
                 ch.check()
+        if self.device.type == "cuda":
+            OF.check_device_errors(f"pipeline stage {self.stage}")
 
     def close(self):
         for ch in (self.prev, self.next):

@@ -183,6 +183,13 @@ def _remote_step(server_rref, key, ctx_id):
         srv.optimizers[key].step()
         for p in params:
             p.grad = None
+        if torch.device(srv.device).type == "cuda":
+            # the stage's one-launch BatchNorm hand-offs of this step: the master's opt.step() raises on a
+            # timeout instead of the stage training on with incomplete statistics (syncs the stage's device;
+            # the master waits for this step anyway before the next batch's forward)
+            from ..ops.functional import check_device_errors
+
+            check_device_errors(f"stage server {rpc.get_worker_info().name}")
         return True
 
     return srv.submit(run).wait()

@@ -102,3 +102,27 @@ def test_bench_elastic_scale_up_cpu():
             rnd = int(ln.split()[2].rstrip(":"))
             pids.setdefault(rnd, set()).add(int(re.match(r"\d+", ln.split("(pid ")[1]).group(0)))
     assert pids[0] <= pids[1] and len(pids[1]) == 4, pids
+
+
+def test_bench_elastic_survives_killed_worker_cpu():
+    """BASELINE config 2 failure rehearsal (horovod/horovod_mnist_elastic.py:55,104-106 semantics): rank 1 exits
+    mid-run (``--fault-at``); the survivor turns the failed collective into PeerFailure, restores its commit,
+    re-joins at world 1 in the SAME process and times the new round, reporting the re-wire latency and its
+    parts (rendezvous / control group / broadcast / map / capture)."""
+    rc, out = run_cmd(["python", os.path.join(REPO, "bench.py"), "--model", "elastic_cnn", "--gpus", "2",
+                       "--scale-to", "1", "--fault-at", "20", "--device", "cpu", "--batch", "32", "--steps", "4",
+                       "--warmup", "2", "--graph-steps", "2"], timeout=600)
+    assert rc == 0, out[-4000:]
+    rounds = [json.loads(ln) for ln in out.splitlines() if ln.startswith('{"event": "round"')]
+    final = [json.loads(ln) for ln in out.splitlines() if ln.startswith('{"metric"')]
+    assert "[fault-injector] rank 1 step 20" in out and "peer failure" in out, out[-4000:]
+    assert [r["world"] for r in rounds] == [2, 1] and len(final) == 1, out[-4000:]
+    assert rounds[1]["rewire_s"] > 0 and set(rounds[1]["rewire_parts"]) == {
+        "rendezvous_s", "control_s", "broadcast_s", "map_s", "capture_s"}, rounds[1]
+    assert "worker killed" in final[0]["config"]["parallelism"]
+    pids = {}
+    for ln in out.splitlines():
+        if ln.startswith("[rewire] round ") and "(pid " in ln:
+            rnd = int(ln.split()[2].rstrip(":"))
+            pids.setdefault(rnd, set()).add(int(re.match(r"\d+", ln.split("(pid ")[1]).group(0)))
+    assert pids[1] < pids[0], pids  # the survivor kept its process

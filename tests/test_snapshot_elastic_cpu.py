@@ -108,14 +108,20 @@ def test_round_shrink_plan():
     that left); growth, reordering or no parent falls back to a fresh init."""
     from pytorch_distributed_examples_amd.elastic.rewire import RoundComm
 
-    class P:  # a previous round: members in rank order, a live communicator
-        def __init__(self, members):
-            self.members, self.rccl = members, object()
+    class Live:
+        valid = True
 
-    def plan(parent_members, members):
+    class Dead:  # aborted when the failure surfaced (RoundComm.wait_event) -- ADVICE r3
+        valid = False
+
+    class P:  # a previous round: members in rank order, a live communicator
+        def __init__(self, members, comm=Live):
+            self.members, self.rccl = members, comm()
+
+    def plan(parent_members, members, comm=Live):
         rc = RoundComm.__new__(RoundComm)
         rc.members = members
-        return rc._shrink_plan(P(parent_members) if parent_members is not None else None)
+        return rc._shrink_plan(P(parent_members, comm) if parent_members is not None else None)
 
     assert plan(["a", "b", "c", "d"], ["a", "c", "d"]) == [1]
     assert plan(["a", "b", "c", "d"], ["b", "c"]) == [0, 3]
@@ -123,3 +129,88 @@ def test_round_shrink_plan():
     assert plan(["a", "b", "c"], ["a", "b", "c"]) is None           # no change
     assert plan(["a", "b", "c"], ["c", "a"]) is None                # reordered ranks
     assert plan(None, ["a"]) is None
+    assert plan(["a", "b", "c", "d"], ["a", "c", "d"], Dead) is None  # an aborted parent cannot be shrunk
+
+
+def test_rewire_planned_scale_down_splits_communicator(tmp_path):
+    """A planned scale-down (host discovery drops hostC of 3): every member of the old round takes part in the
+    communicator split at its next commit point (ncclCommSplit, leaver with NOCOLOR -- here on the gloo
+    stand-in, PDE_REWIRE_EMULATE=gloo), the leaver exits 0 by itself, and the survivors' round reports
+    ``rccl split`` (no fresh unique id) and finishes at world 2."""
+    from dist_utils import run_cmd
+
+    snap = tmp_path / "s.pt"
+    disc = tmp_path / "discover.sh"  # hostC disappears once the first epoch's snapshot exists
+    disc.write_text(f"#!/bin/bash\necho hostA:1\necho hostB:1\nif [ ! -f {snap} ]; then echo hostC:1; fi\n")
+    disc.chmod(0o755)
+    rc, out = run_cmd(HVDRUN + ["--min-np", "1", "--max-np", "3", "--host-discovery-script", str(disc), "--verbose",
+                                "--leave-grace", "120", SCRIPT, "3", "1", "--rewire", "--device", "cpu",
+                                "--train_size", "12288", "--test_size", "384", "--snapshot_path", str(snap)],
+                      env={"PDE_REWIRE_EMULATE": "gloo"})
+    assert rc == 0, out[-4000:]
+    assert re.search(r"\[rewire\] round 0: rank 2 of 3 \(pid \d+, rccl init\)", out), out[-4000:]
+    assert "leaving the job (planned scale-down" in out, out[-4000:]
+    assert "did not leave within" not in out, out[-4000:]
+    assert re.search(r"\[rewire\] round 1: rank 0 of 2 \(pid \d+, rccl split\)", out), out[-4000:]
+    assert re.search(r"\[rewire\] round 1: rank 1 of 2 \(pid \d+, rccl split\)", out), out[-4000:]
+    fin = re.findall(r"\[rewire\] finished 3 epochs in round (\d+) \(world (\d)", out)
+    assert len(fin) == 2 and all(w == "2" for _, w in fin), out[-4000:]
+
+
+def _agreement_worker(rank, world, port, valid, supported, result_dir):
+    """Rank of a 2-member round whose parent round had 3 members (the third died)."""
+    import datetime
+
+    import torch.distributed as dist
+
+    from pytorch_distributed_examples_amd.elastic import rewire
+    from pytorch_distributed_examples_amd.parallel.gloo_comm import GlooComm
+
+    os.environ["PDE_REWIRE_EMULATE"] = "gloo"
+    store = dist.TCPStore("127.0.0.1", port, world, rank == 0, timeout=datetime.timedelta(seconds=60))
+
+    class Rdzv:  # the round's view of the driver's store
+        wid, round = ["a", "b"][rank], 1
+
+        def members(self, rnd=None):
+            return ["a", "b"]
+
+        def pg_store(self):
+            return dist.PrefixStore("pg/1", store)
+
+    class Parent:  # previous round: a, b, c -- a live (or already aborted) communicator
+        members = ["a", "b", "c"]
+
+        def __init__(self):
+            self.rccl = GlooComm()
+            self.rccl.init(store, "parent", rank, 2)  # the survivors' part of the old communicator
+            if not valid[rank]:
+                self.rccl.abort()  # e.g. RoundComm.wait_event aborted it when the failure surfaced there
+
+        def release(self):
+            self.rccl.abort()
+
+    GlooComm.shrink_supported = staticmethod(lambda: supported)
+    rc = rewire.RoundComm(Rdzv(), rank, world, torch.device("cpu"), parent=Parent())
+    t = torch.full((4,), float(rank + 1))
+    rc.allreduce_async(t).wait()
+    with open(os.path.join(result_dir, f"r{rank}"), "w") as f:
+        f.write(f"{rc.how} {t[0].item()}")
+    rc.close()
+
+
+def test_rewire_shrink_needs_every_survivor():
+    """a survivor whose communicator the failure already aborted cannot shrink; the survivors AGREE
+    (one MIN all-reduce over the round's gloo group) before anyone calls ncclCommShrink, so either all shrink
+    or all re-initialise -- never a split where some hang in the collective shrink and others init."""
+    import tempfile
+
+    from dist_utils import free_port, spawn
+
+    for valid, supported, want in (((True, True), True, "shrink"), ((True, False), True, "init"),
+                                   ((True, True), False, "init")):
+        d = tempfile.mkdtemp()
+        spawn(_agreement_worker, world=2, args=(free_port(), valid, supported, d))
+        got = [open(os.path.join(d, f"r{r}")).read().split() for r in range(2)]
+        assert [g[0] for g in got] == [want, want], (valid, supported, got)
+        assert all(float(g[1]) == 3.0 for g in got), got  # the data plane works either way
