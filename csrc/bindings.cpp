@@ -1088,6 +1088,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum", &colsum, py::arg("x"), py::arg("ncols") = -1, py::arg("out") = py::none(),
         py::arg("accumulate") = false);
   m.def("relu_bwd", &relu_bwd);
+  m.def("time_stamp",
+        [](Tensor& stamps, int slot) {
+          TORCH_CHECK(stamps.is_cuda() && stamps.scalar_type() == at::kLong && slot >= 0 && slot < stamps.numel(),
+                      "time_stamp: int64 GPU tensor and a slot inside it");
+          check(pde::time_stamp(reinterpret_cast<unsigned long long*>(stamps.data_ptr()), slot, cur_stream()),
+                "time_stamp");
+        },
+        py::arg("stamps"), py::arg("slot"));
+  m.def("wall_clock_hz", []() {
+    int dev = 0, khz = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+    return static_cast<double>(khz) * 1e3;
+  });
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_fused", &ce_fused, py::arg("x"), py::arg("tgt"), py::arg("dx_out") = py::none());
   m.def("linear_fwd_out", &linear_fwd_out);

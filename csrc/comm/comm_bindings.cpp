@@ -196,6 +196,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def(py::init<int, int, int64_t, const std::string&, double>(), py::arg("rank"), py::arg("size"),
            py::arg("fusion_bytes"), py::arg("timeline_path") = "", py::arg("cycle_ms") = 0.5)
       .def("set_rccl", &FusionEngine::set_rccl)
+      .def("set_xgmi", &FusionEngine::set_xgmi, py::arg("xgmi"), py::arg("threshold_bytes"))
+      .def("allreduce_inline", &FusionEngine::allreduce_inline, py::arg("tensors"), py::arg("op"),
+           py::arg("prescale") = 1.0, py::arg("postscale") = 1.0, py::arg("compress") = false)
+      .def("cached", &FusionEngine::cached)
       .def("set_py_backend", &FusionEngine::set_py_backend)
       .def("set_control", &FusionEngine::set_control, py::arg("process_group"))
       .def("set_timeout", &FusionEngine::set_timeout)

@@ -61,6 +61,7 @@ FusionEngine::FusionEngine(int rank, int size, int64_t fusion_bytes, const std::
       t0_(std::chrono::steady_clock::now()) {
   if (const char* e = std::getenv("PDE_HVD_IDLE_MS")) idle_ms_ = std::max(0.05, std::atof(e));
   if (const char* e = std::getenv("HOROVOD_STALL_CHECK_TIME_SECONDS")) stall_warn_s_ = std::max(1.0, std::atof(e));
+  if (const char* e = std::getenv("HOROVOD_CACHE_CAPACITY")) cache_capacity_ = std::max<int64_t>(0, std::atoll(e));
   if (!timeline_path.empty()) {
     trace_.open(timeline_path);
     trace_ << "[\n";
@@ -91,7 +92,13 @@ void FusionEngine::trace(const std::string& name, const std::string& phase, doub
 
 void FusionEngine::set_rccl(std::shared_ptr<RcclComm> comm) {
   comm_ = std::move(comm);
-  gpu_backend_ = comm_ != nullptr;
+  gpu_backend_ = comm_ != nullptr || xgmi_ != nullptr;
+}
+
+void FusionEngine::set_xgmi(std::shared_ptr<XgmiAllreduce> xgmi, int64_t threshold_bytes) {
+  xgmi_ = std::move(xgmi);
+  xgmi_threshold_ = xgmi_ ? std::min<int64_t>(threshold_bytes, xgmi_->max_bytes()) : 0;
+  gpu_backend_ = comm_ != nullptr || xgmi_ != nullptr;
 }
 
 void FusionEngine::set_py_backend(py::object allreduce_fn, py::object broadcast_fn, py::object allgather_fn) {
@@ -123,6 +130,8 @@ int64_t FusionEngine::enqueue(Request&& r) {
     throw std::runtime_error("Horovod has been shut down");
   }
   const bool dup = announced_.count(r.name) > 0 ||
+                   std::any_of(cached_pending_.begin(), cached_pending_.end(),
+                               [&](const std::pair<const int, Request>& q) { return q.second.name == r.name; }) ||
                    std::any_of(unannounced_.begin(), unannounced_.end(),
                                [&](const Request& q) { return q.name == r.name; });
   if (dup) {
@@ -311,6 +320,7 @@ void FusionEngine::shutdown(bool abort) {
   }
   for (auto& f : inflight_) (void)hipEventDestroy(f.done);
   inflight_.clear();
+  // (own_stream_ is deliberately not destroyed: tensors were recordStream()-ed on it; see RcclComm's dtor)
   if (trace_.is_open()) {
     std::lock_guard<std::mutex> g(trace_mu_);
     trace_ << "\n]\n";
@@ -329,6 +339,15 @@ py::dict FusionEngine::stats() {
   d["fusion_bytes"] = fusion_bytes_.load();
   d["backend"] = gpu_backend_ ? "rccl" : "python";
   d["negotiated"] = control_ ? true : false;
+  d["xgmi_batches"] = n_xgmi_batches_;
+  d["rccl_batches"] = n_rccl_batches_;
+  d["inplace_batches"] = n_inplace_batches_;    // adjacent views of one buffer: no pack / unpack
+  d["inline_calls"] = n_inline_calls_;          // graph-mode calls (caller's stream, no negotiation)
+  d["string_gathers"] = n_string_gathers_;    // cycles that all-gathered name/signature strings (2 gathers each)
+  d["bit_allreduces"] = n_bit_allreduces_;    // cycles negotiated by the cached bit vector alone
+  d["cache_hits"] = n_cache_hits_;
+  d["cache_evictions"] = n_cache_evictions_;
+  d["cache_entries"] = static_cast<int64_t>(cache_.size());
   d["error"] = error_;
   return d;
 }
@@ -341,8 +360,11 @@ void FusionEngine::fail_all_locked(const std::string& err) {
     if (r.ready) (void)hipEventDestroy(r.ready);
   for (auto& kv : announced_)
     if (kv.second.ready) (void)hipEventDestroy(kv.second.ready);
+  for (auto& kv : cached_pending_)
+    if (kv.second.ready) (void)hipEventDestroy(kv.second.ready);
   unannounced_.clear();
   announced_.clear();
+  cached_pending_.clear();
   table_.clear();
   for (auto& kv : handles_) {
     if (!kv.second.done) {
@@ -396,7 +418,9 @@ void FusionEngine::loop() {
     std::vector<Request> announce;
     {
       std::unique_lock<std::mutex> lk(mu_);
-      auto has_work = [&] { return stop_requested_ || !unannounced_.empty() || !announced_.empty(); };
+      auto has_work = [&] {
+        return stop_requested_ || !unannounced_.empty() || !announced_.empty() || !cached_pending_.empty();
+      };
       // Multi-rank engines cycle in lockstep whether or not this rank has work: a rank that announced a
       // tensor blocks in the control-plane all-gather until every peer joins the cycle, so an idle peer
       // (running eval, writing a checkpoint) must keep taking part -- Horovod's background loop does the
@@ -473,9 +497,59 @@ void FusionEngine::loop() {
 
 void FusionEngine::negotiate(std::vector<Request>& announce, std::vector<Request>& ready, bool& stop) {
   const double tn = now();
+  // 0. response cache: requests whose (name, signature) negotiated before ride on their cache id's word
+  std::vector<Request> uncached;
+  int nbits = 0;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& r : announce) {
+      auto c = cache_.find(r.name);
+      if (c != cache_.end() && c->second.signature == r.signature()) {
+        ++n_cache_hits_;
+        cached_pending_.emplace(c->second.id, std::move(r));
+      } else {
+        uncached.push_back(std::move(r));
+      }
+    }
+    nbits = cache_ids_;
+  }
+  announce.clear();
+  auto i32 = at::TensorOptions().dtype(at::kInt);
+  at::Tensor bits = at::zeros({nbits + 2}, i32);
+  int32_t* bw = bits.data_ptr<int32_t>();
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (const auto& kv : cached_pending_) bw[kv.first] = 1;
+  }
+  bw[nbits] = stop ? -1 : 0;
+  bw[nbits + 1] = uncached.empty() ? 0 : -1;
+  {
+    std::vector<at::Tensor> v{bits};
+    c10d::AllreduceOptions o;
+    o.reduceOp = c10d::ReduceOp::MIN;
+    control_->allreduce(v, o)->wait();
+  }
+  bool any_stop = bw[nbits] < 0;
+  const bool any_uncached = bw[nbits + 1] < 0;
+  {  // cached tensors every rank announced: ready, in cache-id order (identical on every rank)
+    std::lock_guard<std::mutex> g(mu_);
+    for (int id = 0; id < nbits; ++id) {
+      if (bw[id] != 1) continue;
+      auto it = cached_pending_.find(id);
+      if (it == cached_pending_.end()) continue;  // cannot happen: the AND includes this rank's word
+      ready.push_back(std::move(it->second));
+      cached_pending_.erase(it);
+    }
+  }
+  if (!any_uncached) {
+    ++n_bit_allreduces_;
+    stop = any_stop;
+    return;
+  }
+  ++n_string_gathers_;
   // 1. this rank's message: stop flag + (name, signature) records, in local enqueue order
   std::string msg(1, stop ? 'S' : '-');
-  for (const auto& r : announce) {
+  for (const auto& r : uncached) {
     msg += r.name;
     msg += kFieldSep;
     msg += r.signature();
@@ -483,12 +557,12 @@ void FusionEngine::negotiate(std::vector<Request>& announce, std::vector<Request
   }
   {
     std::lock_guard<std::mutex> g(mu_);
-    for (auto& r : announce) {
+    for (auto& r : uncached) {
       std::string name = r.name;
       announced_.emplace(std::move(name), std::move(r));
     }
   }
-  announce.clear();
+  uncached.clear();
   // 2. all-gather the lengths, then the padded payloads, over the gloo control group
   auto i64 = at::TensorOptions().dtype(at::kLong);
   std::vector<at::Tensor> len_in{at::full({1}, static_cast<int64_t>(msg.size()), i64)};
@@ -509,7 +583,6 @@ void FusionEngine::negotiate(std::vector<Request>& announce, std::vector<Request
   for (int i = 0; i < size_; ++i) pay_out[0].push_back(at::empty({L}, u8));
   control_->allgather(pay_out, pay_in)->wait();
   // 3. the decentralised coordinator: every rank applies the same rule to the same table
-  bool any_stop = false;
   for (int r = 0; r < size_; ++r) {
     const char* p = reinterpret_cast<const char*>(pay_out[0][r].data_ptr());
     std::string m(p, static_cast<size_t>(lens[r]));
@@ -521,6 +594,20 @@ void FusionEngine::negotiate(std::vector<Request>& announce, std::vector<Request
       if (fs == std::string::npos || rs == std::string::npos || fs > rs) break;
       std::string name = m.substr(pos, fs - pos), sig = m.substr(fs + 1, rs - fs - 1);
       pos = rs + 1;
+      {  // a cached name announced through the strings (its signature changed on some rank): evict it on
+         // every rank; this rank's pending cached request for it is re-announced through the strings
+        std::lock_guard<std::mutex> g(mu_);
+        auto c = cache_.find(name);
+        if (c != cache_.end()) {
+          auto p = cached_pending_.find(c->second.id);
+          if (p != cached_pending_.end()) {
+            unannounced_.push_front(std::move(p->second));
+            cached_pending_.erase(p);
+          }
+          cache_.erase(c);
+          ++n_cache_evictions_;
+        }
+      }
       auto it = table_.find(name);
       if (it == table_.end()) {
         NegEntry e;
@@ -561,6 +648,9 @@ void FusionEngine::negotiate(std::vector<Request>& announce, std::vector<Request
         announced_.erase(it);
         ready.push_back(std::move(r));
       }
+      // cache ids in completion order: the same assignment on every rank
+      if (te->second.error.empty() && static_cast<int64_t>(cache_.size()) < cache_capacity_)
+        cache_[c.second] = CacheEntry{cache_ids_++, te->second.signature};
       table_.erase(te);
     }
   }
@@ -605,8 +695,9 @@ std::vector<Batch> FusionEngine::make_batches(std::vector<Request>& ready) {
 
 void FusionEngine::finish(Batch& b, const std::string& err, bool gpu_done) {
   hipEvent_t watch = nullptr;
+  hipStream_t cs = gpu_done ? engine_stream() : nullptr;
   if (gpu_done && hipEventCreateWithFlags(&watch, hipEventDisableTiming) == hipSuccess)
-    (void)hipEventRecord(watch, comm_->stream());
+    (void)hipEventRecord(watch, cs);
   std::lock_guard<std::mutex> g(mu_);
   ++n_batches_;
   n_bytes_ += b.bytes;
@@ -623,7 +714,7 @@ void FusionEngine::finish(Batch& b, const std::string& err, bool gpu_done) {
         // each handle owns an event (the waiter destroys it)
         hipEvent_t e2 = nullptr;
         if (hipEventCreateWithFlags(&e2, hipEventDisableTiming) == hipSuccess) {
-          (void)hipEventRecord(e2, comm_->stream());
+          (void)hipEventRecord(e2, cs);
           st.finished = e2;
         }
       }
@@ -648,12 +739,15 @@ void FusionEngine::execute(Batch& b) {
   const double t_start = now();
   try {
     if (gpu) {
-      TORCH_CHECK(comm_ && comm_->valid(), "RCCL communicator is not valid (aborted?)");
-      hip_ok(hipSetDevice(comm_->device()), "set device");
-      if (r0.type == ReqType::ALLREDUCE)
-        run_allreduce_gpu(b);
-      else
+      hip_ok(hipSetDevice(r0.tensor.device().index()), "set device");
+      if (r0.type == ReqType::ALLREDUCE) {
+        run_allreduce_gpu(b, engine_stream());
+      } else if (comm_) {
+        TORCH_CHECK(comm_->valid(), "RCCL communicator is not valid (aborted?)");
         run_single_gpu(b.reqs.front());
+      } else {
+        single_gpu_via_host(b.reqs.front());
+      }
     } else {
       if (r0.type == ReqType::ALLREDUCE)
         run_allreduce_cpu(b);
@@ -677,23 +771,108 @@ void FusionEngine::execute(Batch& b) {
   if (!err.empty() && gpu) set_error(err);  // a failed RCCL call leaves the communicator unusable
 }
 
-void FusionEngine::run_allreduce_gpu(Batch& b) {
-  hipStream_t s = comm_->stream();
-  const int dev = comm_->device();
+hipStream_t FusionEngine::engine_stream() {
+  if (comm_) return comm_->stream();
+  if (own_stream_ == nullptr) {
+    int lo = 0, hi = 0;
+    hip_ok(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priority range");
+    hip_ok(hipStreamCreateWithPriority(&own_stream_, hipStreamNonBlocking, hi), "engine stream");
+  }
+  return own_stream_;
+}
+
+// The batch's tensors are consecutive, in-place views of one buffer (a fused model's flat gradients):
+// reduce the span in place -- no pack, no unpack.
+static bool adjacent_inplace(const Batch& b) {
+  const Request& r0 = b.reqs.front();
+  const char* p = static_cast<const char*>(r0.tensor.data_ptr());
+  for (const auto& r : b.reqs) {
+    if (r.tensor.data_ptr() != r.output.data_ptr() || r.tensor.scalar_type() != r0.tensor.scalar_type() ||
+        static_cast<const char*>(r.tensor.data_ptr()) != p)
+      return false;
+    p += r.tensor.numel() * r.tensor.element_size();
+  }
+  return true;
+}
+
+void FusionEngine::run_allreduce_gpu(Batch& b, hipStream_t s) {
+  const int dev = b.reqs.front().tensor.device().index();
   for (auto& r : b.reqs)
     if (r.ready) hip_ok(hipStreamWaitEvent(s, r.ready, 0), "wait producer");
   Request& r0 = b.reqs.front();
   const int dt = dtype_code(r0.tensor);
-  if (b.reqs.size() == 1 && !r0.compress && r0.prescale == 1.0 && r0.postscale == 1.0) {
-    comm_->allreduce(r0.tensor.data_ptr(), r0.output.data_ptr(), r0.tensor.numel(), dt, r0.op, s);
-    record_on(r0.tensor, s, dev);
-    record_on(r0.output, s, dev);
+  int64_t total = 0;
+  for (auto& r : b.reqs) total += r.tensor.numel();
+  const bool span = adjacent_inplace(b);
+  // one-shot xGMI exchange for latency-bound fp32 batches (Sum / Average; pre/post scale folded in)
+  if (xgmi_ && dt == 0 && (r0.op == 0 || r0.op == 1) && total * 4 <= xgmi_threshold_) {
+    const float scale = static_cast<float>(r0.prescale * r0.postscale * (r0.op == 1 ? 1.0 / size_ : 1.0));
+    ++n_xgmi_batches_;
+    if (span) {
+      ++n_inplace_batches_;
+      float* p = static_cast<float*>(r0.tensor.data_ptr());
+      xgmi_->allreduce(p, p, total, scale, s, r0.compress);
+    } else {
+      if (!fused_.defined() || fused_.device() != r0.tensor.device() || fused_.numel() < total * 4) {
+        if (fused_.defined()) hip_ok(hipStreamSynchronize(s), "sync before regrow");
+        fused_ = at::empty({total * 4 + (1 << 20)}, r0.tensor.options().dtype(at::kByte));
+      }
+      PackTable tab;
+      int64_t off = 0;
+      size_t i = 0;
+      while (i < b.reqs.size()) {  // pack in chunks of kMaxPackSegs tensors
+        tab.count = 0;
+        const int64_t off0 = off;
+        const size_t first = i;
+        for (; i < b.reqs.size() && tab.count < kMaxPackSegs; ++i) {
+          PackSeg& sg = tab.seg[tab.count++];
+          sg.n = b.reqs[i].tensor.numel();
+          sg.offset = off;
+          sg.dtype = 0;
+          sg.ptr = b.reqs[i].tensor.data_ptr();
+          off += sg.n;
+        }
+        (void)off0;
+        (void)first;
+        hip_ok(fusion_pack(tab, fused_.data_ptr(), 0, 1.0f, s), "pack");
+      }
+      float* f = static_cast<float*>(fused_.data_ptr());
+      xgmi_->allreduce(f, f, total, scale, s, r0.compress);
+      off = 0;
+      i = 0;
+      while (i < b.reqs.size()) {
+        tab.count = 0;
+        for (; i < b.reqs.size() && tab.count < kMaxPackSegs; ++i) {
+          PackSeg& sg = tab.seg[tab.count++];
+          sg.n = b.reqs[i].tensor.numel();
+          sg.offset = off;
+          sg.dtype = 0;
+          sg.ptr = b.reqs[i].output.data_ptr();
+          off += sg.n;
+        }
+        hip_ok(fusion_unpack(tab, fused_.data_ptr(), 0, 1.0f, s), "unpack");
+      }
+    }
+    for (auto& r : b.reqs) {
+      record_on(r.tensor, s, dev);
+      record_on(r.output, s, dev);
+    }
+    return;
+  }
+  TORCH_CHECK(comm_ && comm_->valid(), "RCCL communicator is not valid (aborted?) and the batch (",
+              total * r0.tensor.element_size(), " B) exceeds the xGMI one-shot threshold");
+  ++n_rccl_batches_;
+  if ((b.reqs.size() == 1 || span) && !r0.compress && r0.prescale == 1.0 && r0.postscale == 1.0) {
+    if (span && b.reqs.size() > 1) ++n_inplace_batches_;
+    comm_->allreduce(r0.tensor.data_ptr(), r0.output.data_ptr(), total, dt, r0.op, s);
+    for (auto& r : b.reqs) {
+      record_on(r.tensor, s, dev);
+      record_on(r.output, s, dev);
+    }
     return;
   }
   TORCH_CHECK(dt == 0 || dt == 1, "fusion engine: fused batches support fp32/bf16 tensors");
   const int wire = (r0.compress || dt == 1) ? 1 : 0;
-  int64_t total = 0;
-  for (auto& r : b.reqs) total += r.tensor.numel();
   const int64_t need = total * (wire == 1 ? 2 : 4);
   if (!fused_.defined() || fused_.device() != r0.tensor.device() || fused_.numel() < need) {
     if (fused_.defined()) hip_ok(hipStreamSynchronize(s), "sync before regrow");
@@ -731,6 +910,50 @@ void FusionEngine::run_allreduce_gpu(Batch& b) {
     record_on(r.tensor, s, dev);
     record_on(r.output, s, dev);
   }
+}
+
+void FusionEngine::single_gpu_via_host(Request& r) {
+  // no RCCL communicator (ranks rehearsing on one GPU): broadcast / allgather through the CPU backend
+  if (r.ready) hip_ok(hipEventSynchronize(r.ready), "wait producer");
+  at::Tensor h = r.tensor.to(at::kCPU);
+  py::gil_scoped_acquire g;
+  if (r.type == ReqType::BROADCAST) {
+    py_broadcast_(h, r.root);
+    r.tensor.copy_(h);
+  } else {
+    at::Tensor out = at::empty(r.output.sizes(), h.options());
+    py_allgather_(h, out);
+    r.output.copy_(out);
+  }
+  hip_ok(hipDeviceSynchronize(), "host-staged collective");
+}
+
+void FusionEngine::allreduce_inline(const std::vector<at::Tensor>& tensors, int op, double prescale,
+                                    double postscale, bool compress) {
+  TORCH_CHECK(!tensors.empty(), "allreduce_inline: no tensors");
+  TORCH_CHECK(tensors.front().is_cuda() && gpu_backend_, "allreduce_inline: GPU tensors and a GPU data plane");
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!error_.empty()) throw std::runtime_error("HorovodInternalError: " + error_);
+    ++n_inline_calls_;
+  }
+  if (size_ == 1) return;
+  std::vector<Request> reqs;
+  for (const auto& t : tensors) {
+    TORCH_CHECK(t.is_contiguous(), "allreduce_inline: contiguous tensors");
+    Request r;
+    r.type = ReqType::ALLREDUCE;
+    r.tensor = t;
+    r.output = t;
+    r.op = op;
+    r.prescale = prescale;
+    r.postscale = postscale;
+    r.compress = compress && t.scalar_type() == at::kFloat;
+    reqs.push_back(std::move(r));
+  }
+  hipStream_t s = at::hip::getCurrentHIPStream(tensors.front().device().index()).stream();
+  std::vector<Batch> batches = make_batches(reqs);
+  for (auto& b : batches) run_allreduce_gpu(b, s);
 }
 
 void FusionEngine::run_single_gpu(Request& r) {

@@ -13,6 +13,23 @@
 //    different orders still cut identical fusion batches.  A signature mismatch fails that request on
 //    every rank ("mismatched ...") instead of mis-reducing.  A shutdown request from any rank ends the
 //    engine on all ranks at the end of that cycle.  World size 1 skips the collective.
+//  * Response cache (Horovod's): a (name, signature) that completed negotiation once gets a cache id, the
+//    same on every rank (ids are assigned in the deterministic completion order).  From then on a cycle is
+//    ONE small MIN all-reduce of an int32 vector [one 0/1 word per cache id, -stop, -has_uncached]: the
+//    per-id minimum is the AND of "announced by this rank" (ready everywhere), the two negated flags are
+//    MAXes.  The name/signature all-gathers run only in cycles where some rank announced an uncached
+//    request (first step, a new tensor, a changed shape); a cached name that reappears there is evicted on
+//    every rank and pending cached requests for it are re-announced through the string path, so a
+//    signature change is still reported as a mismatch.  HOROVOD_CACHE_CAPACITY=0 turns the cache off.
+//  * Data plane on GPUs: fused batches up to `xgmi_threshold` bytes (fp32, Sum/Average) take the one-shot
+//    xGMI peer all-reduce (every rank reads all peers' staged batch over its direct links: one kernel, no
+//    ring hops) when an XgmiAllreduce is attached; larger ones RCCL.  A batch whose tensors are adjacent views
+//    of one buffer (the flat gradient buffer of a fused model) is reduced in place, without pack / unpack.
+//    Broadcast / allgather of GPU tensors without an RCCL communicator (several ranks rehearsing on one GPU)
+//    stage through the host over the CPU backend.
+//  * Graph mode (`allreduce_inline`): once the response cache holds a fixed tensor set, the optimizer may
+//    skip the engine thread and enqueue the SAME batches on the caller's stream -- stream-ordered, no host
+//    wait, hipGraph-capturable.  Every rank must call it with the same tensors in the same order (SPMD).
 //  * Ready allreduces are fused into batches of up to `fusion_bytes` (same dtype/op/scaling/compression).
 //    GPU backend: wait producer events on the engine's high-priority comm stream -> ONE pack kernel
 //    (pre-scale, optional fp32->bf16 wire compression) -> RCCL all-reduce (ncclAvg for Average) -> ONE
@@ -43,6 +60,7 @@
 #include <vector>
 
 #include "comm_manager.h"
+#include "xgmi_allreduce.h"
 
 namespace pde {
 
@@ -98,6 +116,15 @@ class FusionEngine {
   ~FusionEngine();
 
   void set_rccl(std::shared_ptr<RcclComm> comm);
+  void set_xgmi(std::shared_ptr<XgmiAllreduce> xgmi, int64_t threshold_bytes);
+  // graph mode: all-reduce `tensors` (in place) as the engine would batch them, on the caller's CURRENT
+  // stream, without negotiation -- the caller guarantees every rank makes the same call (cached tensor set)
+  void allreduce_inline(const std::vector<at::Tensor>& tensors, int op, double prescale, double postscale,
+                        bool compress);
+  bool cached(const std::string& name) {
+    std::lock_guard<std::mutex> g(mu_);
+    return cache_.count(name) > 0;
+  }
   void set_py_backend(py::object allreduce_fn, py::object broadcast_fn, py::object allgather_fn);
   void set_control(c10::intrusive_ptr<c10d::ProcessGroup> pg);
   void set_timeout(double seconds) { timeout_s_ = seconds; }
@@ -126,7 +153,9 @@ class FusionEngine {
   void loop();
   void negotiate(std::vector<Request>& announce, std::vector<Request>& ready, bool& stop);
   void execute(Batch& b);
-  void run_allreduce_gpu(Batch& b);
+  void run_allreduce_gpu(Batch& b, hipStream_t s);
+  void single_gpu_via_host(Request& r);
+  hipStream_t engine_stream();  // the RCCL communicator's stream, else one of the engine's own
   void run_allreduce_cpu(Batch& b);
   void run_single_gpu(Request& r);
   void run_single_cpu(Request& r);
@@ -144,6 +173,9 @@ class FusionEngine {
   double idle_ms_ = 2.0;         // lockstep back-off between idle cycles (PDE_HVD_IDLE_MS)
   double stall_warn_s_ = 60.0;   // stall inspector threshold (HOROVOD_STALL_CHECK_TIME_SECONDS)
   std::shared_ptr<RcclComm> comm_;
+  std::shared_ptr<XgmiAllreduce> xgmi_;
+  int64_t xgmi_threshold_ = 0;
+  hipStream_t own_stream_ = nullptr;
   c10::intrusive_ptr<c10d::ProcessGroup> control_;
   py::object py_allreduce_, py_broadcast_, py_allgather_;
   bool gpu_backend_ = false;
@@ -156,6 +188,15 @@ class FusionEngine {
   std::map<std::string, Request> announced_;   // announced by this rank, not yet globally ready
   std::map<std::string, NegEntry> table_;      // negotiation state (same on every rank)
   int64_t order_seq_ = 0;
+  // response cache: name -> (id, signature); ids are never reused (an evicted id's word stays 0)
+  struct CacheEntry {
+    int id;
+    std::string signature;
+  };
+  std::map<std::string, CacheEntry> cache_;
+  std::map<int, Request> cached_pending_;  // announced through the cache, not yet ready everywhere
+  int cache_ids_ = 0;
+  int64_t cache_capacity_ = 1 << 16;
   std::map<int64_t, HandleState> handles_;
   int64_t next_handle_ = 1;
   bool stop_requested_ = false;
@@ -167,6 +208,8 @@ class FusionEngine {
 
   // stats
   int64_t n_requests_ = 0, n_batches_ = 0, n_bytes_ = 0, n_fused_requests_ = 0, n_cycles_ = 0;
+  int64_t n_xgmi_batches_ = 0, n_rccl_batches_ = 0, n_inline_calls_ = 0, n_inplace_batches_ = 0;
+  int64_t n_string_gathers_ = 0, n_bit_allreduces_ = 0, n_cache_hits_ = 0, n_cache_evictions_ = 0;
 
   std::mutex trace_mu_;
   std::ofstream trace_;

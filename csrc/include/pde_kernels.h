@@ -99,6 +99,8 @@ hipError_t gemm_reduce_jobs(const ReduceJob* jobs, int n, hipStream_t stream);
 // Elementwise / layout (elementwise.hip)
 // ---------------------------------------------------------------------------------------------
 hipError_t cast_f32_bf16(const float* in, uint16_t* out, long n, hipStream_t s);
+// stamps[slot] = the 100 MHz wall clock when this node runs (phase attribution inside captured graphs)
+hipError_t time_stamp(unsigned long long* stamps, int slot, hipStream_t s);
 // in [rows][cols] fp32 -> out [rows][ldo] bf16, plus out[r][cols] = 1 when ones != 0 (the ones column a
 // linear wgrad GEMM turns into the bias gradient)
 hipError_t cast_rows_bf16(const float* in, int rows, int cols, uint16_t* out, int ldo, int ones, hipStream_t s);

@@ -422,4 +422,15 @@ hipError_t relu_bwd_bf16(const uint16_t* dy, const uint16_t* y, uint16_t* dx, lo
   return hipGetLastError();
 }
 
+// One wall-clock timestamp (100 MHz constant clock) into stamps[slot]: a graph node at a phase boundary of a
+// captured training step (bench phase attribution, utils/log.GraphPhaseTimer).
+__global__ void k_time_stamp(unsigned long long* stamps, int slot) {
+  if (threadIdx.x == 0) stamps[slot] = wall_clock64();
+}
+
+hipError_t time_stamp(unsigned long long* stamps, int slot, hipStream_t s) {
+  hipLaunchKernelGGL(k_time_stamp, dim3(1), dim3(64), 0, s, stamps, slot);
+  return hipGetLastError();
+}
+
 }  // namespace pde

@@ -13,6 +13,12 @@ Workloads (``--model``), one process per GPU, synthetic data resident in HBM, ra
   [m,16,16,512] bf16 activation with MSE; each step is forward, backward against an upstream gradient
   (stage 1) / the loss (stage 2, input gradient included: it goes upstream), SGD -- what one stage GPU does
   per micro-batch, minus the P2P transfers.
+* ``hvd_cnn`` -- BASELINE config 1's CNN through the HOROVOD path (horovod/mnist_horovod.py:47-67):
+  ``hvd.DistributedOptimizer(FusedSGD)`` + ``hvd.broadcast_parameters``; the first step negotiates every
+  gradient through the C++ fusion engine (filling its response cache), then the optimizer switches to graph
+  mode (the cached batches enqueued stream-ordered: one in-place one-shot xGMI all-reduce of the fused
+  model's flat gradient buffer) and the whole step records into a hipGraph.  World 1: Horovod's all-reduce is
+  the identity, so the step is the fused kernel with the SGD update in its reduction (2 launches).
 * ``resnet50_pp`` -- BASELINE configs 3 and 4: the 2-stage ResNet-50 of rpc/model_parallel_ResNet50.py
   (stem+layer1+layer2 | layer3+layer4+fc, :85-139), batch 32 split into micro-batches of ``--split-size``
   (the reference's ``split_size`` semantics, :171, quirk Q2), one stage per GPU, activations and their
@@ -43,6 +49,7 @@ from ..utils.log import NO_PHASES, PhaseTimer
 # BASELINE.json names one metric for the whole suite; ``config`` says which of its workloads this run measured.
 METRIC = "images/sec (whole node) MNIST DDP + ResNet50 RPC-MP at 1/2/4/8 MI355X"
 BASELINE_CONFIG = {"cnn": "1: MNIST CNN DDP bf16, RCCL allreduce over xGMI",
+                   "hvd_cnn": "1 via the Horovod API (horovod/mnist_horovod.py DistributedOptimizer)",
                    "mlp": "0/1 workload of mnist_ddp_elastic.py (5x1024 MLP DDP)",
                    "resnet50": "ResNet-50 128px data parallel (no BASELINE config; kernel reference point)",
                    "resnet50_stage": "one stage of configs 3/4 at micro-batch size (per-stage kernel time)",
@@ -52,8 +59,8 @@ BASELINE_CONFIG = {"cnn": "1: MNIST CNN DDP bf16, RCCL allreduce over xGMI",
 # Only same-workload, same-world comparisons are reported.
 REFERENCE_IMG_S = {("mlp", 1): 7452.0, ("mlp", 2): 2630.0, ("mlp", 4): 4620.0,
                    ("resnet50_pp", 2): 18.0}
-DEFAULT_BATCH = {"cnn": 1024, "mlp": 128, "resnet50": 32, "resnet50_stage": 8, "resnet50_pp": 32}
-MODEL_NAMES = {"cnn": "mnist_cnn_Net", "mlp": "mnist_mlp_5x1024", "resnet50": "resnet50_128px",
+DEFAULT_BATCH = {"cnn": 1024, "hvd_cnn": 1024, "mlp": 128, "resnet50": 32, "resnet50_stage": 8, "resnet50_pp": 32}
+MODEL_NAMES = {"cnn": "mnist_cnn_Net", "hvd_cnn": "mnist_cnn_Net", "mlp": "mnist_mlp_5x1024", "resnet50": "resnet50_128px",
                "resnet50_stage": "resnet50_128px_stage", "resnet50_pp": "resnet50_128px_2stage"}
 
 
@@ -64,8 +71,8 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", default="cnn",
-                    choices=["cnn", "mlp", "resnet50", "resnet50_stage", "resnet50_pp", "resnet50_hybrid",
-                             "elastic_cnn"])
+                    choices=["cnn", "hvd_cnn", "mlp", "resnet50", "resnet50_stage", "resnet50_pp",
+                             "resnet50_hybrid", "elastic_cnn"])
     ap.add_argument("--stage", type=int, default=1, choices=[1, 2], help="resnet50_stage: which pipeline stage")
     ap.add_argument("--scale-to", type=int, default=None, help="elastic_cnn: world size after the first round")
     ap.add_argument("--fault-at", type=int, default=None,
@@ -330,6 +337,89 @@ def build_data_parallel(args, ctx, batch) -> Workload:
         return train_step(x, y, timer)
 
     w.phase_step = phase_step
+    w.phase_inputs = lambda: list(batch_fn(0))
+    w.phase_call = lambda timer, x, y: train_step(x, y, timer)
+    return w
+
+
+def build_hvd_cnn(args, ctx, batch) -> Workload:
+    """The reference's Horovod script (horovod/mnist_horovod.py:28-67) on the MI355X runtime; see the module
+    docstring.  CPU: the autograd Net through the same optimizer wrapper, eager."""
+    from .. import hvd
+    from ..data.synthetic import SyntheticMNIST
+    from ..models.cnn import Net
+    from ..ops import functional as OF
+    from ..ops.optim import FusedSGD
+
+    dev = ctx.device
+    on_gpu = dev.type == "cuda"
+    hvd.init(device="cpu" if not on_gpu else None)
+    torch.manual_seed(0)
+    model = Net().to(dev)
+    data = SyntheticMNIST(max(8 * batch, 16384), device=dev, seed=hvd.rank())
+    fused = grads = None
+    if on_gpu:
+        from ..models.cnn_fused import FusedCNN
+
+        fused = FusedCNN(model)
+        grads = fused.grad_buffer()  # p.grad = views of one flat buffer: the engine reduces it in place
+    opt = hvd.DistributedOptimizer(FusedSGD(model.parameters(), lr=0.01), named_parameters=model.named_parameters())
+    hvd.broadcast_parameters(model.state_dict(), root_rank=0)
+    if fused is not None:
+        fused.invalidate()
+    world = hvd.size()
+
+    def train_step(x, y):
+        if fused is None:
+            opt.zero_grad()
+            loss = OF.nll_loss(model(x), y)
+            loss.backward()
+            opt.step()
+            return loss
+        if world == 1:  # all-reduce = identity: the SGD update rides in the reduction kernel
+            opt.synchronize()
+            return fused.forward_backward(x, y, grad_out=grads, sgd=opt)
+        loss = fused.forward_backward(x, y, grad_out=grads)
+        opt.synchronize()  # engine (first step) / stream-ordered cached batches (graph mode)
+        with opt.skip_synchronize():
+            fused.sgd_step(opt, grads)  # opt.step(), fused with the conv-weight fragment refresh
+        return loss
+
+    def batch_fn(i):
+        return data.batch(i, batch)
+
+    one = group = None
+    if on_gpu:
+        train_step(*batch_fn(0))  # negotiated through the engine: every gradient enters the response cache
+        torch.cuda.synchronize()
+        opt.enable_graph_mode()
+        if not args.no_graph:
+            one, group = _capture(train_step, [batch_fn(j) for j in range(max(1, args.graph_steps))],
+                                  args.graph_steps, ctx.rank)
+
+    def step(i):
+        x, y = batch_fn(i)
+        return one(x, y) if one is not None else train_step(x, y)
+
+    st = hvd.engine_stats()
+    w = Workload(step, batch * world, f"dp{world}", hipgraph=one is not None, fused_step=fused is not None,
+                 steps_per_graph=group.steps if group is not None else (1 if one is not None else 0),
+                 api="horovod DistributedOptimizer + broadcast_parameters",
+                 allreduce=("none (world 1)" if world == 1 else
+                            f"fusion engine: {'xgmi-oneshot' if st.get('xgmi_batches') else st.get('backend')}"
+                            f"{' graph mode' if on_gpu else ''}"))
+    w.group = group
+
+    def check():
+        s2 = hvd.engine_stats()
+        w.info["engine"] = {k: s2[k] for k in ("requests", "batches", "string_gathers", "bit_allreduces",
+                                               "cache_hits", "cache_entries", "xgmi_batches", "rccl_batches",
+                                               "inplace_batches", "inline_calls") if k in s2}
+        if s2.get("error"):
+            raise RuntimeError(f"hvd engine error: {s2['error']}")
+
+    w.check = check
+    w.close = hvd.shutdown
     return w
 
 
@@ -357,6 +447,8 @@ def build_pipeline(args, ctx, batch) -> Workload:
     w.close = pipe.close
     w.check = pipe.check
     w.phase_step = lambda i, timer: pipe.step(timer)
+    w.phase_inputs = lambda: []
+    w.phase_call = lambda timer: pipe.step(timer)
     w.per_stage = True
     return w
 
@@ -426,28 +518,65 @@ def _report_loss(work, ctx, loss):
 PHASE_STEPS = 3
 
 
+def _graph_phases(work, ctx, args):
+    """Phases of the CAPTURED step: the workload's step with a :class:`GraphPhaseTimer` recorded into a fresh
+    single-step hipGraph (every rank captures in lockstep: pipeline stages exchange inside it), replayed
+    PHASE_STEPS times after the timed region."""
+    from ..utils.graph import CapturedStep
+    from ..utils.log import GraphPhaseTimer
+
+    timer = GraphPhaseTimer(ctx.device)
+    inputs = work.phase_inputs()
+
+    def fn(*xs):  # events only in the captured step, not in the capture's eager warm-up
+        return work.phase_call(timer if torch.cuda.is_current_stream_capturing() else NO_PHASES, *xs)
+
+    one = CapturedStep(fn, inputs, warmup=1).capture()
+    for _ in range(PHASE_STEPS):
+        one(*inputs)
+        torch.cuda.synchronize()
+        timer.replayed()
+    return timer.summary()
+
+
 def _measure_phases(work, ctx, args):
-    """Per-phase device milliseconds per step, from PHASE_STEPS eager steps run AFTER the
-    timed region (a captured hipGraph has no host-visible phase boundaries; eager steps add host launch
-    gaps between phases, which these device-time spans exclude).  Data parallel: rank 0's phases.  Pipeline:
-    one entry per stage of the first pipeline (fwd / bwd compute, recv_wait = time the stage's stream spends
-    in receive kernels waiting for its neighbour, comm = stage all-reduce, opt)."""
+    """Per-phase device milliseconds per step.  GPU runs with a captured step: timing events
+    inside a captured copy of the benchmarked step (:func:`_graph_phases`), so the phases sum to the step's
+    device time.  Otherwise (CPU, eager runs, or a capture failure): PHASE_STEPS eager steps after the timed
+    region.  Data parallel: rank 0's phases.  Pipeline: one entry per stage of the first pipeline (fwd / bwd
+    compute, recv_wait = time the stage's stream spends in receive kernels waiting for its neighbour, comm =
+    stage all-reduce, opt)."""
     if not hasattr(work, "phase_step"):
         return None
-    timer = PhaseTimer(ctx.device)
-    try:
-        for k in range(PHASE_STEPS):
-            work.phase_step(args.warmup + args.steps + k, timer)
-            timer.steps += 1
-        local = timer.summary()
-    except Exception as exc:  # noqa: BLE001 - diagnostics never cost the headline line
-        local = {"error": repr(exc)[:200]}
+    method = f"hipEvents, {PHASE_STEPS} eager steps after the timed region"
+    local = None
+    if ctx.device.type == "cuda" and work.info.get("hipgraph") and hasattr(work, "phase_call"):
+        try:
+            local = _graph_phases(work, ctx, args)
+            method = (f"wall-clock stamp nodes at the phase boundaries of a captured single-step hipGraph, "
+                      f"{PHASE_STEPS} replays")
+        except Exception as exc:  # noqa: BLE001 - diagnostics never cost the headline line
+            torch.cuda.synchronize()
+            from .. import _native
+
+            _native.C().clear_last_error()
+            local = None
+            method += f" (graph attribution failed: {repr(exc)[:120]})"
+    if local is None:
+        timer = PhaseTimer(ctx.device)
+        try:
+            for k in range(PHASE_STEPS):
+                work.phase_step(args.warmup + args.steps + k, timer)
+                timer.steps += 1
+            local = timer.summary()
+        except Exception as exc:  # noqa: BLE001 - diagnostics never cost the headline line
+            local = {"error": repr(exc)[:200]}
     if getattr(work, "per_stage", False) and ctx.world_size > 1:
         allp = [None] * ctx.world_size
         dist.all_gather_object(allp, local)
         stages = [dict(stage=s, **allp[s]) for s in range(min(2, ctx.world_size))]
-        return {"method": f"hipEvents, {PHASE_STEPS} eager steps after the timed region", "stages": stages}
-    return {"method": f"hipEvents, {PHASE_STEPS} eager steps after the timed region", "rank0_ms": local}
+        return {"method": method, "stages": stages}
+    return {"method": method, "rank0_ms": local}
 
 
 def main(argv=None):
@@ -471,7 +600,12 @@ def main(argv=None):
         if on_gpu:
             torch.cuda.synchronize()
 
-    work = build_pipeline(args, ctx, batch) if args.model == "resnet50_pp" else build_data_parallel(args, ctx, batch)
+    if args.model == "resnet50_pp":
+        work = build_pipeline(args, ctx, batch)
+    elif args.model == "hvd_cnn":
+        work = build_hvd_cnn(args, ctx, batch)
+    else:
+        work = build_data_parallel(args, ctx, batch)
     run_steps(work, 0, args.warmup)
     pdist.barrier(ctx)
     sync()
@@ -501,7 +635,7 @@ def main(argv=None):
         name = MODEL_NAMES[args.model] + (str(args.stage) if args.model == "resnet50_stage" else "")
         cfg = {"model": name, "baseline_config": BASELINE_CONFIG[args.model],
                "global_batch": work.images_per_step, "seq_len": None,
-               "image": "1x28x28" if args.model in ("cnn", "mlp") else f"3x{args.image or 128}x{args.image or 128}",
+               "image": "1x28x28" if args.model in ("cnn", "hvd_cnn", "mlp") else f"3x{args.image or 128}x{args.image or 128}",
                "parallelism": work.parallelism, "final_loss": round(final_loss, 4)}
         cfg.update(work.info)
         if phases is not None:

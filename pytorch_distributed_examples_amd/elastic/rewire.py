@@ -91,6 +91,8 @@ class RoundComm:
     ``use_rccl=False``: control plane only (the fused CNN exchanges gradients over xGMI inside its reduction
     kernel).  ``timing`` holds the seconds spent on the control group and on the data-plane communicator."""
 
+    emulated = False  # gloo stand-in for RCCL (PDE_REWIRE_EMULATE=gloo, CPU only)
+
     def __init__(self, rdzv: RendezvousClient, rank: int, size: int, device: torch.device,
                  timeout_s: float = 120.0, grace_s: float = 2.0, parent: "RoundComm | None" = None,
                  use_rccl: bool = True, premade=None):

@@ -21,6 +21,9 @@ where one exists):
     PDE_HVD_TIMEOUT            seconds before a stuck collective / control cycle is declared failed (300)
     PDE_HVD_BLOCKING_WAIT      1: synchronize() polls GPU completion on the host with liveness checks
                                (default on under the elastic driver, so failures raise from synchronize)
+    HOROVOD_CACHE_CAPACITY     response-cache entries (0: negotiate every request by name)
+    PDE_HVD_DATA_PLANE         auto (RCCL + one-shot xGMI for fused batches <= PDE_XGMI_THRESHOLD bytes) |
+                               rccl | xgmi (no RCCL: ranks rehearsing on ONE GPU, where RCCL refuses to run)
 """
 from __future__ import annotations
 
@@ -63,6 +66,7 @@ class _Ctx:
         self.device = torch.device("cpu")
         self.engine = None
         self.comm = None
+        self.xgmi = None
         self.group = None
         self.engine_group = None
         self.owns_pg = False
@@ -153,14 +157,24 @@ def init(comm=None, device: str | None = None):
     blocking = os.environ.get("PDE_HVD_BLOCKING_WAIT")
     eng.set_blocking_wait(blocking == "1" if blocking is not None else rendezvous.elastic_env())
     if use_gpu:
-        key = f"pde/hvd/rccl_uid/{_ctx.generation}"
-        if _ctx.rank == 0:
-            store.set(key, C.rccl_unique_id())
-        uid = store.get(key)
-        comm = C.RcclComm()
-        comm.init(uid, _ctx.rank, _ctx.size, _ctx.device.index, True)
-        eng.set_rccl(comm)
-        _ctx.comm = comm
+        plane = os.environ.get("PDE_HVD_DATA_PLANE", "auto")
+        # several ranks on one device (a one-GPU rehearsal): RCCL refuses duplicate devices -> xGMI only
+        shared = _ctx.size > 1 and torch.cuda.device_count() < _ctx.local_size
+        if plane == "rccl" or (plane == "auto" and not shared):
+            key = f"pde/hvd/rccl_uid/{_ctx.generation}"
+            if _ctx.rank == 0:
+                store.set(key, C.rccl_unique_id())
+            uid = store.get(key)
+            comm = C.RcclComm()
+            comm.init(uid, _ctx.rank, _ctx.size, _ctx.device.index, True)
+            eng.set_rccl(comm)
+            _ctx.comm = comm
+        if _ctx.size > 1 and plane in ("auto", "xgmi"):
+            # latency-bound fused batches (the CNN's 87 KB of gradients) take the one-shot peer exchange
+            from ..parallel.xgmi_allreduce import DEFAULT_THRESHOLD, XgmiAllreduce
+
+            _ctx.xgmi = XgmiAllreduce(_ctx.device, key=f"hvd/{_ctx.generation}")
+            eng.set_xgmi(_ctx.xgmi.impl, DEFAULT_THRESHOLD if plane == "auto" else _ctx.xgmi.max_bytes)
     _ctx.engine = eng
     _ctx.names = {}
     _ctx.initialized = True
@@ -184,8 +198,14 @@ def shutdown(abort: bool = False):
                 _ctx.comm.destroy()
             except Exception:  # noqa: BLE001
                 _ctx.comm.abort()
+    if _ctx.xgmi is not None:
+        try:
+            _ctx.xgmi.close()
+        except Exception:  # noqa: BLE001 - a dead peer's mapping may refuse a clean close
+            pass
     _ctx.engine = None
     _ctx.comm = None
+    _ctx.xgmi = None
     _ctx.engine_group = None
     try:
         if dist.is_initialized() and _ctx.owns_pg:
@@ -448,6 +468,23 @@ def allgather_object(obj, name=None):
     out = [None] * _ctx.size
     dist.all_gather_object(out, obj, group=_ctx.group)
     return out
+
+
+def allreduce_inline_(tensors, op=ReduceOp.Average, prescale_factor=1.0, postscale_factor=1.0,
+                      compression_bf16=False):
+    """Graph mode: all-reduce ``tensors`` in place on the CURRENT stream, batched exactly as the engine would,
+    without the negotiation cycle (stream-ordered, no host wait, hipGraph-capturable).  Every rank must make the
+    same call with the same tensors in the same order -- what a cached (already negotiated) tensor set
+    guarantees; :meth:`DistributedOptimizer.enable_graph_mode` checks that first."""
+    _need()
+    _ctx.engine.allreduce_inline(list(tensors), int(op), float(prescale_factor), float(postscale_factor),
+                                 bool(compression_bf16))
+
+
+def is_cached(name: str) -> bool:
+    """Whether ``name`` is in the engine's response cache (negotiated with the same signature before)."""
+    _need()
+    return bool(_ctx.engine.cached(name))
 
 
 def engine_stats() -> dict:

@@ -10,6 +10,10 @@ Used by the reference at horovod/mnist_horovod.py:53 and horovod/horovod_mnist_e
   :mod:`..ops.optim`.
 * ``op=Average`` uses RCCL's in-collective average (no extra kernel); ``gradient_predivide_factor``
   splits the averaging into a pre-scale in the pack kernel and a post-scale in the unpack kernel.
+* Graph mode (:meth:`enable_graph_mode`, MI355X addition): once the engine's response cache holds every
+  parameter (one step negotiated through the engine), ``synchronize()`` enqueues the same fused batches on
+  the caller's stream -- no engine thread, no host wait -- so the whole training step records into a hipGraph.
+  SPMD: every rank must reach ``synchronize()`` each step (as with a captured DDP step).
 * ``Compression.fp16`` sends fp32 gradients as bf16 on the wire (CDNA4's native 16-bit training format;
   same bytes as fp16, fp32 exponent range); ``Compression.bf16`` is the explicit name.
 """
@@ -79,6 +83,7 @@ class _DistributedOptimizerMixin:
         self._counts = {p: 0 for _, p in named}
         self._synchronized = False
         self._should_sync = True
+        self._graph = False
         self._hooks = []
         if core.size() > 1:
             for _, p in named:
@@ -87,6 +92,8 @@ class _DistributedOptimizerMixin:
 
     def _make_hook(self):
         def hook(p):
+            if self._graph:  # graph mode: reduced in synchronize(), stream-ordered
+                return
             if p in self._handles and self._handles[p] is not None:
                 # the gradient was already handed to the engine (in-place all-reduce in flight): another
                 # local pass would race with it and mix reduced and unreduced values
@@ -117,10 +124,34 @@ class _DistributedOptimizerMixin:
         return core.allreduce_async_(g, name=name, op=op, prescale_factor=pre, postscale_factor=post,
                                      compression_bf16=self._compression.wire_bf16)
 
+    def enable_graph_mode(self):
+        """Reduce gradients stream-ordered (hipGraph-capturable) from now on.  Needs every parameter's
+        all-reduce in the response cache, i.e. at least one step synchronized through the engine."""
+        if core.size() > 1:
+            missing = [n for n in self._param_names.values() if not core.is_cached(n)]
+            if missing:
+                raise RuntimeError(f"graph mode needs a negotiated step first; not cached: {missing[:4]}")
+        self._graph = True
+        return self
+
+    def _graph_synchronize(self):
+        op, pre, post = self._op, 1.0, 1.0
+        if self._predivide != 1.0 and op == core.ReduceOp.Average:
+            op, pre, post = core.ReduceOp.Sum, 1.0 / self._predivide, self._predivide / core.size()
+        grads = [p.grad for p in self._param_names if p.grad is not None]
+        if grads and grads[0].is_cuda:
+            streams.join(grads[0].device)
+        core.allreduce_inline_(grads, op, pre, post, self._compression.wire_bf16)
+        for p in self._param_names:
+            self._counts[p] = 0
+        self._synchronized = True
+
     def synchronize(self):
         if core.size() == 1:
             self._synchronized = True
             return
+        if self._graph:
+            return self._graph_synchronize()
         # parameters whose gradient was produced but whose hook count did not reach bpps, or that got no
         # gradient at all this step, are reduced now (same order on every rank: registration order)
         for p in self._param_names:

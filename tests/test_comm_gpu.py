@@ -2,6 +2,7 @@
 the fusion engine's GPU path (pack kernel -> RCCL all-reduce -> unpack, csrc/comm/pack.hip) and the
 Horovod-compatible API on top of it, world size 1 (multi-rank behaviour is covered on gloo by
 tests/test_hvd_cpu.py; the driver's 8-GPU bench exercises RCCL across ranks)."""
+import os
 import pytest
 import torch
 
@@ -192,3 +193,56 @@ def test_rccl_abort_and_reinit_rounds(gpu):
             rc.rccl = None
         else:
             rc.rccl.destroy()  # (RoundComm.close would also tear down the round's gloo group)
+
+
+def _clean_env():
+    """The parent's env minus the rendezvous variables earlier in-process tests exported."""
+    drop = ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE")
+    return {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC_")}
+
+
+def _bench_json(out):
+    import json
+
+    lines = [ln for ln in out.splitlines() if ln.startswith('{"metric"')]
+    assert lines, out[-3000:]
+    return json.loads(lines[-1])
+
+
+def test_hvd_cnn_bench_world1_graph(gpu):
+    """``bench.py --model hvd_cnn`` at world 1: the Horovod optimizer wrapper around the fused CNN, captured."""
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--model", "hvd_cnn", "--steps", "20",
+                          "--warmup", "5"], capture_output=True, text=True, timeout=300, env=_clean_env())
+    assert res.returncode == 0, res.stderr[-3000:]
+    rec = _bench_json(res.stdout)
+    assert rec["config"]["hipgraph"] and rec["config"]["fused_step"] and rec["value"] > 1e6, rec
+
+
+def test_hvd_cnn_world2_one_gpu_rehearsal(gpu):
+    """Two Horovod ranks sharing the card (RCCL refuses that; the engine's xGMI one-shot data plane does
+    not): the first step negotiates through the fusion engine, then graph mode reduces the flat gradient
+    buffer in place, stream-ordered, inside the captured step -- no string negotiation in steady state."""
+    import subprocess
+    import sys
+
+    from dist_utils import free_port
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(_clean_env(), PDE_BACKEND="gloo", PYTHONPATH=repo)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(repo, "bench.py"), "--gpus", "2", "--model",
+           "hvd_cnn", "--steps", "20", "--warmup", "5"]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert res.returncode == 0, (res.stdout[-2000:], res.stderr[-3000:])
+    rec = _bench_json(res.stdout)
+    eng = rec["config"]["engine"]
+    assert rec["n_gpus"] == 2 and rec["config"]["hipgraph"], rec
+    assert eng["xgmi_batches"] >= 1 and eng["inplace_batches"] >= 1 and eng["inline_calls"] >= 20, eng
+    assert eng["string_gathers"] <= 3, eng  # broadcast_parameters + the first step only
+    os.makedirs(os.path.join(repo, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(repo, "gpurun_out", "hvd_world2_rehearsal.json"), "w") as f:
+        f.write(res.stdout.strip().splitlines()[-1] + "\n")
