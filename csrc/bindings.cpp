@@ -419,6 +419,130 @@ Tensor conv_fwd(const Tensor& x, const Tensor& wf, const optional<Tensor>& bias,
   return y;
 }
 
+// ---- BatchNorm folded into the convolutions around it (pde_kernels.h BnStatsOut / BnFoldIn) ----
+// conv_fwd_bn(x, wf, ...): the forward convolution of a Bottleneck with
+//   stats_out (int64 [G, 2, Co] zero-initialised sums): its epilogue emits the statistics of the BatchNorm that
+//     normalises its output (the producer side);
+//   fold_sums / fold_ticket / gamma / beta / running stats: its A operand x is the RAW output of the previous
+//     conv and the BatchNorm (+ ReLU) between the two is applied in the A loader (the consumer side).  Returns
+//     {y, act, save_mean, save_invstd, scale_shift} -- act = relu(bn(x)) materialised for the backward.
+// bn_fold_plan(...) answers, from the shapes alone, whether both sides can run folded (plan before the first
+// launch, outside graph capture: it may allocate the split-K arrival tickets).
+pde::GemmArgs conv_shape_args(int N, int H, int W, int C, int Co, int R, int S, int stride, int pad, const void* xp,
+                              const void* wp, void* yp) {
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  pde::GemmArgs a{};
+  a.M = N * Ho * Wo; a.N = Co; a.K = R * S * C;
+  a.a.ptr = xp;
+  if (is_pointwise(R, S, stride, pad)) {
+    a.a.kind = 0; a.a.ld_r = C; a.a.ld_k = 1;
+  } else {
+    a.a.kind = 1; a.a.g = pde::ConvGeom{N, H, W, C, R, S, stride, pad, Ho, Wo};
+  }
+  a.b.ptr = wp; a.b.kind = 0; a.b.ld_r = a.K; a.b.ld_k = 1;
+  a.out = yp; a.ldo = Co;
+  a.epi = 0;
+  return a;
+}
+
+bool bn_fold_plan(int N, int H, int W, int C, int Co1, int R1, int S1, int stride1, int pad1, int Co2, int R2, int S2,
+                  int stride2, int pad2, int groups) {
+  void* fake = reinterpret_cast<void*>(static_cast<uintptr_t>(1) << 20);  // any 16-B aligned address
+  // producer: conv(x [N,H,W,C]) -> a [N,H1,W1,Co1] with statistics
+  pde::GemmArgs p = conv_shape_args(N, H, W, C, Co1, R1, S1, stride1, pad1, fake, fake, fake);
+  p.splitk = split_cap(p);
+  p.workspace = p.splitk > 1 ? static_cast<float*>(fake) : nullptr;
+  if (groups < 1 || p.M % groups != 0) return false;
+  p.bn_out.sums = static_cast<long long*>(fake);
+  p.bn_out.C = Co1; p.bn_out.G = groups; p.bn_out.rows_per_group = p.M / groups;
+  if (!pde::gemm_bn_stats_ok(p, cur_stream())) return false;
+  // consumer: conv(relu(bn(a))) with the BatchNorm in its A loader
+  const int H1 = (H + 2 * pad1 - R1) / stride1 + 1, W1 = (W + 2 * pad1 - S1) / stride1 + 1;
+  pde::GemmArgs c = conv_shape_args(N, H1, W1, Co1, Co2, R2, S2, stride2, pad2, fake, fake, fake);
+  c.splitk = split_cap(c);
+  c.workspace = c.splitk > 1 ? static_cast<float*>(fake) : nullptr;
+  c.bn_in.ss = static_cast<const float*>(fake);
+  c.bn_in.C = Co1; c.bn_in.G = groups; c.bn_in.rows_per_group = (N * H1 * W1) / groups;
+  c.bn_in.center = is_pointwise(R2, S2, stride2, pad2) ? 0 : 1;
+  return (N * H1 * W1) % groups == 0 && pde::gemm_bn_fold_ok(c);
+}
+
+// Returns {y, save_mean, save_invstd, scale_shift, act}: the last three-plus-one are defined when the conv
+// produces statistics (stats_sums: the NEXT BatchNorm's finalize) / consumes a folded BatchNorm (fold_ss).
+std::vector<Tensor> conv_fwd_bn(const Tensor& x, const Tensor& wf, int R, int S, int stride, int pad, int64_t groups,
+                                const optional<Tensor>& stats_sums, const optional<Tensor>& stats_ticket,
+                                const optional<Tensor>& gamma, const optional<Tensor>& beta,
+                                const optional<Tensor>& running_mean, const optional<Tensor>& running_var, double eps,
+                                double momentum, const optional<Tensor>& fold_ss, bool relu, bool defer) {
+  CHECK_IN(x); CHECK_IN(wf); CHECK_BF16(x); CHECK_BF16(wf);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 8 == 0, "conv_fwd_bn: input channels must be padded to a multiple of 8");
+  const int Co = wf.size(0);
+  TORCH_CHECK(wf.size(1) == R * S * C, "conv_fwd_bn: weight must be [Co, R*S*C]");
+  const int G = static_cast<int>(groups);
+  const int Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  Tensor y = at::empty({N, Ho, Wo, Co}, x.options());
+  pde::GemmArgs a = conv_shape_args(N, H, W, C, Co, R, S, stride, pad, x.data_ptr(), wf.data_ptr(), y.data_ptr());
+  auto fo = x.options().dtype(at::kFloat);
+  std::vector<Tensor> out{y, Tensor(), Tensor(), Tensor(), Tensor()};
+  const bool fold = fold_ss.has_value() && fold_ss->defined();
+  const bool stats = stats_sums.has_value() && stats_sums->defined();
+  static const int dbg = std::getenv("PDE_BN_FOLD_DEBUG") ? std::atoi(std::getenv("PDE_BN_FOLD_DEBUG")) : 0;
+  a.bn_in.debug = dbg;
+  a.bn_out.debug = dbg;
+  if (!fold) resolve_pending(x);
+  if (fold) {
+    TORCH_CHECK(fold_ss->scalar_type() == at::kFloat && fold_ss->numel() == static_cast<long>(G) * 2 * C,
+                "conv_fwd_bn: folded scale / shift must be fp32 [G, 2, C]");
+    TORCH_CHECK((N * H * W) % G == 0, "conv_fwd_bn: rows not divisible by groups");
+    Tensor act = at::empty_like(x);
+    pde::BnFoldIn& f = a.bn_in;
+    f.ss = fold_ss->data_ptr<float>();
+    f.act = u16(act);
+    f.C = C; f.G = G; f.rows_per_group = (N * H * W) / G;
+    f.relu = relu ? 1 : 0;
+    f.center = is_pointwise(R, S, stride, pad) ? 0 : 1;
+    out[4] = act;
+  }
+  if (stats) {
+    TORCH_CHECK(stats_ticket.has_value() && stats_ticket->defined(), "conv_fwd_bn: statistics need their ticket");
+    TORCH_CHECK(stats_sums->scalar_type() == at::kLong &&
+                    stats_sums->numel() == static_cast<long>(pde::kBnShards) * G * 2 * Co,
+                "conv_fwd_bn: statistics sums must be int64 [bn_fold_shards, G, 2, Co]");
+    TORCH_CHECK(a.M % G == 0, "conv_fwd_bn: output rows not divisible by groups");
+    Tensor mean = at::empty({G * Co}, fo), invstd = at::empty({G * Co}, fo), ss = at::empty({G * 2 * Co}, fo);
+    pde::BnStatsOut& f = a.bn_out;
+    f.sums = static_cast<long long*>(stats_sums->data_ptr());
+    f.ticket = stats_ticket->data_ptr<int>();
+    f.C = Co; f.G = G; f.rows_per_group = a.M / G;
+    f.gamma = cf32(gamma); f.beta = cf32(beta);
+    f.running_mean = f32(running_mean); f.running_var = f32(running_var);
+    f.save_mean = mean.data_ptr<float>(); f.save_invstd = invstd.data_ptr<float>(); f.ss = ss.data_ptr<float>();
+    f.eps = static_cast<float>(eps); f.momentum = static_cast<float>(momentum);
+    out[1] = mean; out[2] = invstd; out[3] = ss;
+  }
+  const int max_split = split_cap(a);
+  Tensor ws;
+  if (max_split > 1) {
+    ws = at::empty({static_cast<long>(max_split) * a.M * a.N}, fo);
+    a.workspace = ws.data_ptr<float>();
+    a.splitk = max_split;
+  } else {
+    a.workspace = nullptr;
+    a.splitk = 1;
+  }
+  if (stats) TORCH_CHECK(pde::gemm_bn_stats_ok(a, cur_stream()), "conv_fwd_bn: statistics epilogue not possible");
+  if (fold) TORCH_CHECK(pde::gemm_bn_fold_ok(a), "conv_fwd_bn: folded BatchNorm not possible for this shape");
+  int used = 1;
+  if (defer && !stats) a.splits_out = &used;  // the one-launch BatchNorm after this conv reduces the slabs
+  check(pde::gemm_bf16(a, cur_stream()), "conv_fwd_bn");
+  if (used > 1) {
+    std::lock_guard<std::mutex> lk(g_pending_mu);
+    g_pending_conv[y.data_ptr()] = PendingConv{ws, used, a.M, a.N};
+  }
+  return out;
+}
+
 // dx[N,H,W,Ci] from dy[N,Ho,Wo,Co] and wd = [Ci, R*S*Co]; or, for a 1x1 / stride-1 conv with
 // w_fwd_layout, from the forward copy wd = [Co, Ci] read transposed (no separate dgrad layout).
 // aux: with add_aux, a bf16 [N*H*W, Ci] gradient added in the epilogue (the other branch of a residual
@@ -1069,6 +1193,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("wf"), py::arg("bias"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("relu"), py::arg("out_f32"), py::arg("defer") = false);
   m.def("pending_conv_count", &pending_conv_count);
+  m.def("bn_fold_shards", []() { return pde::kBnShards; });
+  m.def("bn_fold_plan", &bn_fold_plan, py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co1"),
+        py::arg("R1"), py::arg("S1"), py::arg("stride1"), py::arg("pad1"), py::arg("Co2"), py::arg("R2"),
+        py::arg("S2"), py::arg("stride2"), py::arg("pad2"), py::arg("groups"));
+  m.def("conv_fwd_bn", &conv_fwd_bn, py::arg("x"), py::arg("wf"), py::arg("R"), py::arg("S"), py::arg("stride"),
+        py::arg("pad"), py::arg("groups"), py::arg("stats_sums"), py::arg("stats_ticket"), py::arg("gamma"),
+        py::arg("beta"), py::arg("running_mean"), py::arg("running_var"), py::arg("eps"), py::arg("momentum"),
+        py::arg("fold_ss"), py::arg("relu"), py::arg("defer") = false);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wd"), py::arg("H"), py::arg("W"), py::arg("R"),
         py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("aux") = py::none(), py::arg("w_fwd_layout") = false,
         py::arg("add_aux") = false);

@@ -50,6 +50,46 @@ struct Operand {
   ConvGeom g;          // gather geometry
 };
 
+// BatchNorm folded into the convolutions around it (forward, training mode; VERDICT r3 ask 1).
+//   producer (the conv whose output x the BatchNorm normalises): its epilogue adds per-tile column sums of the
+//     stored bf16 outputs into `sums` -- fixed point (S1 = sum x * 2^32, S2 = sum x^2 * 2^20, int64 atomics:
+//     exact, so the statistics do not depend on arrival order), SHARDED by row tile (kBnShards copies, tile tm
+//     adds into shard tm % kBnShards: hundreds of row tiles adding into the same 2C words would serialise at
+//     the memory side).  Every block then arrives on `ticket`; the LAST one reads-and-zeroes the shards
+//     (atomic exchange), derives mean / invstd / scale / shift per (group, channel), writes them and the
+//     running statistics (group order), and resets the ticket -- the BatchNorm's whole finalize, once;
+//   consumer (the next conv): every block copies its group's scale / shift [2][C] into LDS (overlapping its
+//     first operand loads) and its A loader applies relu(x * scale + shift) to every in-range element while
+//     staging the tile (padding taps stay zero).  Blocks of the first N-tile also write the activation `act`
+//     (the backward's operand): a 1x1 consumer every A element, a 3x3 stride-1 consumer the centre tap.
+constexpr int kBnShards = 16;
+struct BnStatsOut {
+  long long* sums;        // [kBnShards][G][2][C] zero-initialised; nullptr: off
+  int* ticket;            // zero-initialised arrival counter
+  int nblocks;            // blocks of the producing launch (set by the launcher)
+  int C;                  // real channels (the output may be padded)
+  int G, rows_per_group;  // micro-batch groups; rows per group (a multiple of the 64-row tile)
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  float* save_mean;       // [G][C]
+  float* save_invstd;     // [G][C]
+  float* ss;              // [G][2][C]: scale, shift (the consumer's coefficients, the backward's ReLU mask)
+  float eps, momentum;
+  int debug;              // PDE_BN_FOLD_DEBUG cost attribution (timing only, results invalid): 1 skip the
+                          // finalize tail, 2 skip the statistics epilogue
+};
+constexpr int kBnFoldMaxC = 512;  // 4 KB of scale / shift: 4 blocks of 36 KB still fit a CU
+struct BnFoldIn {
+  const float* ss;        // [G][2][C] from the producer's finalize; nullptr: off
+  uint16_t* act;          // [rows][C] bf16 activation written by the first N-tile's blocks
+  int C, G, rows_per_group;
+  int relu;
+  int center;             // 1: 3x3 stride-1 pad-1 gather, act from the centre tap; 0: 1x1 (every element)
+  int debug;              // PDE_BN_FOLD_DEBUG & 4: skip the A transform (timing only)
+};
+
 struct GemmArgs {
   int M, N, K;
   Operand a, b;
@@ -67,7 +107,15 @@ struct GemmArgs {
   int* splits_out;                 // != nullptr: a split-K GEMM leaves its slabs UNREDUCED for a consumer that
                                    //   sums them itself (the one-launch BatchNorm); the split count used is stored
                                    //   here (1: the output was written directly)
+  BnStatsOut bn_out;               // producer side of a folded BatchNorm (bn_out.sums != nullptr)
+  BnFoldIn bn_in;                  // consumer side (bn_in.ss != nullptr): A = relu(x * scale + shift)
 };
+// Whether gemm_bf16 would run `a` on a path whose epilogue emits BatchNorm statistics (bn_out): the 64x64
+// FAST tile, bf16 output without epilogue ops, and no split-K (or one reduced inside the launch).
+bool gemm_bn_stats_ok(const GemmArgs& a, hipStream_t s);
+// Whether gemm_bf16 can apply a folded BatchNorm in `a`'s A loader (bn_in): the 64x64 FAST tile with a dense
+// (1x1) or 3x3 stride-1 gathered A, K-contiguous dense B, rows_per_group a multiple of 64, C <= kBnFoldMaxC.
+bool gemm_bn_fold_ok(const GemmArgs& a);
 // Sum `splits` fp32 slabs [splits][M][N] in z order into bf16 out[M][N] (the plain split-K reduction of a
 // GEMM with no epilogue) -- the fallback when a deferred conv output is read by something else.
 hipError_t gemm_reduce_slabs_bf16(float* ws, int splits, int M, int N, uint16_t* out, hipStream_t s);

@@ -44,6 +44,10 @@ namespace pde {
 namespace {
 
 constexpr int kThreads = 256;
+// Minimum waves per SIMD the 64x64 tiles are compiled for (-DPDE_GEMM_WPE=N to sweep): 4 caps them at 128 VGPRs
+#ifndef PDE_GEMM_WPE
+#define PDE_GEMM_WPE 4
+#endif
 // K-tiles in flight in the FAST loaders' register ring (-DPDE_FAST_STAGES=N to sweep)
 #ifndef PDE_FAST_STAGES
 #define PDE_FAST_STAGES 4
@@ -300,6 +304,57 @@ struct KcLoader {
       }
     }
   }
+
+  // Folded BatchNorm (consumer side, FAST kinds 0 / 1): what load() just issued for each slot, for the
+  // transforming store of the same ring stage -- mc = channel of the slot's 8 elements (-1: a zero slot:
+  // out of range or a padding tap, which must stay zero), mr = activation row the slot's transformed values
+  // belong to (-1: not written: a non-centre tap of a 3x3 gather).
+  __device__ __forceinline__ void meta(const Operand& op, int rows, int K, int row0, int center, int (&mc)[kPer],
+                                       int (&mr)[kPer]) const {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      const int r = row0 + v / (BK / 8);
+      bool ok = v < kVecs && k0[i] < K && r < rows;
+      int ch = k0[i];
+      bool wr = ok;
+      if constexpr (KIND == 1) {
+        const ConvGeom& g = op.g;
+        const int iy = by[i] + kh[i], ix = bx[i] + kw[i];
+        ok = ok && nb[i] >= 0 && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+        ch = c[i];
+        wr = ok && center && kh[i] == 1 && kw[i] == 1;
+      }
+      mc[i] = ok ? ch : -1;
+      mr[i] = wr ? r : -1;
+    }
+  }
+
+  // store() with relu(x * scale[c] + shift[c]) applied to every live slot (ss: LDS [2][C] scale, shift);
+  // `write`: also store the transformed 16 B to act[mr][mc] (the first N-tile's blocks)
+  __device__ __forceinline__ void store_bn(uint16_t* lds, u16x8 (&regs)[kPer], const int (&mc)[kPer],
+                                           const int (&mr)[kPer], const float* ss, int C, int relu, bool write,
+                                           uint16_t* act) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      if (v < kVecs && mc[i] >= 0) {
+        const f32x4* sc = reinterpret_cast<const f32x4*>(ss + mc[i]);
+        const f32x4* sh = reinterpret_cast<const f32x4*>(ss + C + mc[i]);
+        const f32x4 s0 = sc[0], s1 = sc[1], h0 = sh[0], h1 = sh[1];
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float t = bf2f(regs[i][j]) * (j < 4 ? s0[j] : s1[j - 4]) + (j < 4 ? h0[j] : h1[j - 4]);
+          if (relu) t = fmaxf(t, 0.f);
+          o[j] = f2bf(t);
+        }
+        regs[i] = o;
+        if (write && mr[i] >= 0) *reinterpret_cast<u16x8*>(act + static_cast<long>(mr[i]) * C + mc[i]) = o;
+      }
+    }
+    store(lds, regs);
+  }
 };
 
 // Row-contiguous operand (kinds 0 and 2): each slot loads 8 consecutive ROW elements at one k.
@@ -469,6 +524,115 @@ constexpr int kSub = PDE_GEMM_SUB;
 template <int BM, int BN>
 constexpr int SMEM_BYTES_OF() { return 2 * kSub * (BM + BN) * 32 * 2; }  // gemm_kernel's LDS (BK = 32, bf16)
 
+// ---- BatchNorm folded into the convolutions (pde_kernels.h BnStatsOut / BnFoldIn) --------------------
+constexpr double kBnS1 = 4294967296.0;  // fixed-point scale of sum x   (2^32)
+constexpr double kBnS2 = 1048576.0;     // fixed-point scale of sum x^2 (2^20)
+
+// Producer epilogue: per-column sums of the tile's stored bf16 outputs (st: [BM][BN] in LDS), combined in a
+// fixed order inside the block and added to the group's fixed-point sums (exact int64 atomics).  red: LDS
+// scratch of 2 * (kThreads / BN) * BN floats.  Block-collective.
+template <int BM, int BN>
+__device__ __forceinline__ void tile_bn_stats(const GemmArgs& a, const uint16_t* st, int m0, int n0, float* red) {
+  constexpr int RG = kThreads / BN, RPG = BM / RG;
+  static_assert(RG * BN == kThreads && RPG * RG == BM, "stats tiling");
+  if (a.bn_out.debug & 2) return;
+  const int nl = threadIdx.x % BN, rg = threadIdx.x / BN;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll 4
+  for (int r = 0; r < RPG; ++r) {
+    const int ml = rg * RPG + r;
+    if (m0 + ml < a.M) {
+      const float v = bf2f(st[ml * BN + nl]);
+      s1 += v;
+      s2 += v * v;
+    }
+  }
+  red[rg * BN + nl] = s1;
+  red[(RG + rg) * BN + nl] = s2;
+  __syncthreads();
+  const int n = n0 + threadIdx.x;
+  if (threadIdx.x < BN && n < a.bn_out.C) {
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < RG; ++q) {
+      t1 += red[q * BN + threadIdx.x];
+      t2 += red[(RG + q) * BN + threadIdx.x];
+    }
+    const int shard = (m0 / BM) % kBnShards;
+    long long* sg = a.bn_out.sums +
+                    (static_cast<long>(shard) * a.bn_out.G + m0 / a.bn_out.rows_per_group) * 2 * a.bn_out.C;
+    atomicAdd(reinterpret_cast<unsigned long long*>(sg + n),
+              static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(t1) * kBnS1)));
+    atomicAdd(reinterpret_cast<unsigned long long*>(sg + a.bn_out.C + n),
+              static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(t2) * kBnS2)));
+  }
+}
+
+// Producer, after the block's tile is done (every block, whatever its split-K role): arrival on the launch's
+// ticket behind its statistics atomics; the LAST block reads and zeroes the shards and finalizes the
+// BatchNorm for every (group, channel), in group
+// order for the running statistics, then resets the ticket.  Block-collective; `flag`: one LDS int.
+__device__ __forceinline__ void bn_stats_finalize(const GemmArgs& a, int* flag) {
+  const BnStatsOut& f = a.bn_out;
+  if (f.debug & 1) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's statistics atomics are performed
+  __syncthreads();
+  if (threadIdx.x == 0)
+    flag[0] = __hip_atomic_fetch_add(f.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == f.nblocks - 1;
+  __syncthreads();
+  if (!flag[0]) return;
+  const double n = static_cast<double>(f.rows_per_group);
+  for (int c = threadIdx.x; c < f.C; c += kThreads) {
+    const float gm = f.gamma ? f.gamma[c] : 1.f, bt = f.beta ? f.beta[c] : 0.f;
+    float rm = f.running_mean ? f.running_mean[c] : 0.f, rv = f.running_var ? f.running_var[c] : 1.f;
+    for (int g = 0; g < f.G; ++g) {
+      // exact integer sums (two's complement wraps consistently).  Agent-scope loads: the adds were performed
+      // at the memory side and no block of this launch cached these lines, so every load reads them; all
+      // 2 x kBnShards loads of a (group, channel) are in flight at once, then the shards are zeroed for the
+      // next step (plain stores, written back at the kernel boundary before the next producer's adds)
+      long long s1 = 0, s2 = 0;
+#pragma unroll
+      for (int sh = 0; sh < kBnShards; ++sh) {
+        long long* sg = f.sums + (static_cast<long>(sh) * f.G + g) * 2 * f.C;
+        s1 += __hip_atomic_load(sg + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s2 += __hip_atomic_load(sg + f.C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+#pragma unroll
+      for (int sh = 0; sh < kBnShards; ++sh) {
+        long long* sg = f.sums + (static_cast<long>(sh) * f.G + g) * 2 * f.C;
+        sg[c] = 0;
+        sg[f.C + c] = 0;
+      }
+      const double mean_d = static_cast<double>(s1) / kBnS1 / n;
+      double var = static_cast<double>(s2) / kBnS2 / n - mean_d * mean_d;
+      if (var < 0.0) var = 0.0;
+      const float mean = static_cast<float>(mean_d);
+      const float invstd = rsqrtf(static_cast<float>(var) + f.eps);
+      const float vu = f.rows_per_group > 1 ? static_cast<float>(var * n / (n - 1.0)) : static_cast<float>(var);
+      f.save_mean[g * f.C + c] = mean;
+      f.save_invstd[g * f.C + c] = invstd;
+      f.ss[static_cast<long>(g) * 2 * f.C + c] = gm * invstd;
+      f.ss[static_cast<long>(g) * 2 * f.C + f.C + c] = bt - mean * gm * invstd;
+      rm = (1.f - f.momentum) * rm + f.momentum * mean;
+      rv = (1.f - f.momentum) * rv + f.momentum * vu;
+    }
+    if (f.running_mean) {
+      f.running_mean[c] = rm;
+      f.running_var[c] = rv;
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(f.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Consumer: the block's group's scale / shift into LDS ss[0..C) / ss[C..2C).  Block-collective.
+__device__ __forceinline__ void bn_fold_prologue(const GemmArgs& a, int m0, float* ss) {
+  const BnFoldIn& f = a.bn_in;
+  const float* src = f.ss + static_cast<long>(m0 / f.rows_per_group) * 2 * f.C;
+  for (int i = threadIdx.x * 4; i < 2 * f.C; i += kThreads * 4)
+    *reinterpret_cast<f32x4*>(ss + i) = *reinterpret_cast<const f32x4*>(src + i);
+  __syncthreads();
+}
+
 template <int BM, int BN, int FM, int FN, int WTM, int WTN>
 __device__ __forceinline__ void write_slab_and_reduce(const GemmArgs& args, const f32x4 (&acc)[FM][FN],
                                                       uint16_t* smem, int m0, int n0, int kz, int wm, int wn,
@@ -547,10 +711,21 @@ __device__ __forceinline__ void write_slab_and_reduce(const GemmArgs& args, cons
       for (int z = 1; z < kMaxInKernelSplits; ++z)
         if (z < splits) v[i] += *reinterpret_cast<const f32x4*>(&u[z]);
     }
+    const bool stats = out_vec && args.bn_out.sums != nullptr;
+    uint16_t* st = smem;  // [BM][BN] bf16 staging for the BatchNorm statistics
+    if (stats) __syncthreads();  // every thread has read `last` (aliases st) before anyone stages
 #pragma unroll
     for (int i = 0; i < QI; ++i) {
       const int q = threadIdx.x + i * kThreads;
       const int m = m0 + q / (BN / 4), n = n0 + (q % (BN / 4)) * 4;
+      if (stats) {  // rows / columns past the tile's extent stage zeros (skipped by the statistics)
+        u16x4 z = u16x4{0, 0, 0, 0};
+        if (m < args.M && n < args.N) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) z[j] = f2bf(apply_epi(v[i][j], args.epi, m, n + j, args));
+        }
+        *reinterpret_cast<u16x4*>(st + (q / (BN / 4)) * BN + (q % (BN / 4)) * 4) = z;
+      }
       if (m >= args.M || n >= args.N) continue;
       if (out_vec) {
         u16x4 o;
@@ -573,15 +748,22 @@ __device__ __forceinline__ void write_slab_and_reduce(const GemmArgs& args, cons
       store_out(apply_epi(v, args.epi, m, n, args), args.epi, m, n, args);
     }
   }
+  if (vec && out_vec && args.bn_out.sums != nullptr) {
+    __syncthreads();
+    tile_bn_stats<BM, BN>(args, smem, m0, n0, reinterpret_cast<float*>(smem + BM * BN));
+  }
   if (threadIdx.x == 0) __hip_atomic_store(args.tickets + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // One output tile (and K slice kz of nz) of a GEMM: the body of gemm_kernel, also run by gemm_pair_kernel for
 // either of its two problems.  `orig` is the block's tile slot within its problem, `smem` the block's LDS
 // (SMEM_BYTES_OF<BM, BN>() bytes).
-template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC, int AKIND, int BKIND, int STAGES>
+template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC, int AKIND, int BKIND, int STAGES,
+          bool BNF = false>
 __device__ __forceinline__ void gemm_tile(const GemmArgs& args, int tiles_m, int tiles_n, int k_per_split, int a_vec,
-                                          int b_vec, const int orig, const int kz, const int nz, uint16_t* smem) {
+                                          int b_vec, const int orig, const int kz, const int nz, uint16_t* smem,
+                                          float* bn_ss = nullptr) {
+  static_assert(!BNF || (AKC && (AKIND == 0 || AKIND == 1)), "folded BatchNorm: FAST K-contiguous dense / im2col A");
   static_assert(WM * WN == 4, "4 waves per block");
   static_assert(BK == 32, "swz_chunk assumes 4 16-byte K-chunks (64 B) per LDS row");
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -617,6 +799,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args, int tiles_m, int
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int wm = wid / WN, wn = wid % WN;
+  const bool bn_write = BNF && tn == 0;  // the first N-tile's blocks materialise the activation
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -639,8 +822,25 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args, int tiles_m, int
   // MFMAs of tile t.  Reduction bound for the loaders is kend (zero fill past the split's end).
   constexpr int S = STAGES;
   u16x8 ra[S][LA::kPer], rb[S][LB::kPer];
+  // folded BatchNorm: per ring stage, the channel / activation row of each A slot (KcLoader::meta)
+  [[maybe_unused]] int mca[BNF ? S : 1][LA::kPer], mra[BNF ? S : 1][LA::kPer];
+  const int bn_center = BNF ? args.bn_in.center : 0;
+  auto a_meta = [&](int u) {
+    if constexpr (BNF) la.meta(args.a, args.M, kend, m0, bn_center, mca[u], mra[u]);
+  };
+  auto a_store = [&](uint16_t* dst, int u) {
+    if constexpr (BNF) {
+      if (args.bn_in.debug & 4)
+        la.store(dst, ra[u]);
+      else
+        la.store_bn(dst, ra[u], mca[u], mra[u], bn_ss, args.bn_in.C, args.bn_in.relu, bn_write, args.bn_in.act);
+    } else {
+      la.store(dst, ra[u]);
+    }
+  };
   if (nk > 0) {
     la.load(args.a, args.M, kend, m0, avec, ra[0]);
+    a_meta(0);
     lb.load(args.b, args.N, kend, n0, bvec, rb[0]);
 #pragma unroll
     for (int u = 1; u < S; ++u) {
@@ -648,16 +848,21 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args, int tiles_m, int
         la.advance(args.a);
         lb.advance(args.b);
         la.load(args.a, args.M, kend, m0, avec, ra[u]);
+        a_meta(u);
         lb.load(args.b, args.N, kend, n0, bvec, rb[u]);
       }
     }
+    // folded BatchNorm: the coefficients' L2 round trip overlaps the ring loads just issued
+    if constexpr (BNF) bn_fold_prologue(args, m0, bn_ss);
 #pragma unroll
     for (int q = 0; q < KSUB; ++q) {
       if (q < nk) {
-        la.store(smem + q * SUBT, ra[q]);
+        a_store(smem + q * SUBT, q);
         lb.store(smem + q * SUBT + LDS_A, rb[q]);
       }
     }
+  } else if constexpr (BNF) {
+    bn_fold_prologue(args, m0, bn_ss);  // (block-collective: every block takes part)
   }
   __syncthreads();
 
@@ -700,6 +905,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args, int tiles_m, int
           la.advance(args.a);
           lb.advance(args.b);
           la.load(args.a, args.M, kend, m0, avec, ra[u + q]);
+          a_meta(u + q);
           lb.load(args.b, args.N, kend, n0, bvec, rb[u + q]);
         }
       }
@@ -712,7 +918,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args, int tiles_m, int
 #pragma unroll
         for (int q = 0; q < KSUB; ++q) {
           if (t + KSUB + q < nk) {
-            la.store(nxt + q * SUBT, ra[(u + KSUB + q) % S]);
+            a_store(nxt + q * SUBT, (u + KSUB + q) % S);
             lb.store(nxt + q * SUBT + LDS_A, rb[(u + KSUB + q) % S]);
           }
         }
@@ -758,6 +964,10 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args, int tiles_m, int
         if (m < args.M && n < args.N)
           *reinterpret_cast<u16x8*>(out + static_cast<long>(m) * args.ldo + n) =
               *reinterpret_cast<const u16x8*>(st + ml * BN + nl);
+      }
+      if constexpr (BM * BN * 2 + 2 * BN * (kThreads / BN) * 4 <= SMEM_BYTES && kThreads % BN == 0) {
+        if (args.bn_out.sums != nullptr)  // producer of a folded BatchNorm: its statistics from the staged tile
+          tile_bn_stats<BM, BN>(args, st, m0, n0, reinterpret_cast<float*>(st + BM * BN));
       }
       return;
     }
@@ -843,12 +1053,25 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args, int tiles_m, int
   }
 }
 
-template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC, int AKIND, int BKIND, int STAGES>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu((BM * BN >= 128 * 128) ? 1 : 4))) void gemm_kernel(GemmArgs args, int tiles_m, int tiles_n,
+template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC, int AKIND, int BKIND, int STAGES,
+          bool BNF = false>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu((BM * BN >= 128 * 128) ? 1 : PDE_GEMM_WPE))) void gemm_kernel(GemmArgs args, int tiles_m, int tiles_n,
                                                         int k_per_split, int a_vec, int b_vec) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM_BYTES_OF<BM, BN>() / 2];
-  gemm_tile<BM, BN, BK, WM, WN, AKC, BKC, AKIND, BKIND, STAGES>(args, tiles_m, tiles_n, k_per_split, a_vec, b_vec,
-                                                                blockIdx.x, blockIdx.z, gridDim.z, smem);
+  float* bn_ss = nullptr;
+  if constexpr (BNF) {
+    __shared__ __attribute__((aligned(16))) float ss[2 * kBnFoldMaxC + 4];
+    bn_ss = ss;
+  }
+  gemm_tile<BM, BN, BK, WM, WN, AKC, BKC, AKIND, BKIND, STAGES, BNF>(args, tiles_m, tiles_n, k_per_split, a_vec,
+                                                                     b_vec, blockIdx.x, blockIdx.z, gridDim.z, smem,
+                                                                     bn_ss);
+  if constexpr (BM == 64 && BN == 64 && AKC && BKC && (AKIND == 0 || AKIND == 1)) {
+    if (args.bn_out.sums != nullptr) {  // producer of a folded BatchNorm: the last block finalizes it
+      __syncthreads();                  // (LDS is free: every epilogue path ended its LDS use)
+      bn_stats_finalize(args, reinterpret_cast<int*>(smem));
+    }
+  }
 }
 
 // Two independent GEMMs in ONE launch (a layer's data gradient and weight gradient): blocks [0, nb0) run
@@ -861,7 +1084,7 @@ struct PairDims {
   int tm[2], tn[2], kps[2], av[2], bv[2], nz[2];
 };
 template <bool AKC0, bool BKC0, int AK0, int BK0, bool AKC1, bool BKC1, int AK1, int BK1>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void gemm_pair_kernel(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PDE_GEMM_WPE))) void gemm_pair_kernel(
     GemmArgs a0, GemmArgs a1, PairDims d, OptimSeg seg) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM_BYTES_OF<64, 64>() / 2];
   const int t0 = d.tm[0] * d.tn[0];
@@ -1126,12 +1349,13 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_jobs(ReduceJobs t) {
 // (0.39 vs 0.33 ms/step) and ResNet-50 (5.89 vs 5.80 ms/step): the tile's reducer is one workgroup reading
 // up to 8 slabs after the whole K range finished, a serial tail the 1.5-2 us launch boundary does not cost.
 constexpr int kTicketSlots = 1 << 22;
-int* split_tickets(int tiles, hipStream_t s) {
+// force: a producer of BatchNorm statistics needs the in-launch combine (its last arriver emits them)
+int* split_tickets(int tiles, hipStream_t s, bool force = false) {
   static int* base[64] = {};
   static int next[64] = {};
   static bool enabled = std::getenv("PDE_GEMM_INKERNEL_SPLITK") != nullptr &&
                         std::getenv("PDE_GEMM_INKERNEL_SPLITK")[0] == '1';
-  if (!enabled || tiles > kTicketSlots) return nullptr;
+  if ((!enabled && !force) || tiles > kTicketSlots) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   if (base[dev] == nullptr) {
@@ -1259,8 +1483,23 @@ hipError_t launch_cfg(const GemmArgs& a, hipStream_t s, int splitk) {
   GemmArgs ka = a;
   const bool in_kernel = splitk > 1 && splitk <= kMaxInKernelSplits && a.splits_out == nullptr &&
                          static_cast<long>(splitk) * a.M * a.N * 4 < (1L << 31);  // buffer offsets
-  ka.tickets = in_kernel ? split_tickets(tm * tn, s) : nullptr;
+  const bool stats = a.bn_out.sums != nullptr;
+  ka.tickets = in_kernel ? split_tickets(tm * tn, s, stats) : nullptr;
+  if (stats && splitk > 1 && ka.tickets == nullptr) return hipErrorInvalidValue;  // gemm_bn_stats_ok said no
+  if (stats) ka.bn_out.nblocks = tm * tn * splitk;
   if (a.splits_out != nullptr) *a.splits_out = splitk;  // the consumer reduces the slabs (no reduce launch)
+  if constexpr (BM == 64 && BN == 64 && AKC && BKC) {
+    if (a.bn_in.ss != nullptr) {  // folded BatchNorm in the A loader (gemm_bn_fold_ok checked the shape)
+      if (a.a.kind == 0)
+        hipLaunchKernelGGL((gemm_kernel<64, 64, 32, 2, 2, true, true, 0, 0, kFastStages, true>), grid, dim3(kThreads),
+                           0, s, ka, tm, tn, kps, av, bv);
+      else
+        hipLaunchKernelGGL((gemm_kernel<64, 64, 32, 2, 2, true, true, 1, 0, kFastStages, true>), grid, dim3(kThreads),
+                           0, s, ka, tm, tn, kps, av, bv);
+      if (splitk > 1 && ka.tickets == nullptr && a.splits_out == nullptr) launch_reduce(a, splitk, s);
+      return hipGetLastError();
+    }
+  }
   // FAST: both operands loaded branch-free through buffer descriptors (gathers always; dense operands when
   // every 16-B group is whole and aligned, extents < 2 GB) with compile-time operand kinds -- then the loads
   // are counted and a register ring of kFastStages K-tiles stays in flight.  The generic loaders' divergent scalar fallbacks make the
@@ -1365,6 +1604,45 @@ bool is_kc(const Operand& o) {
   return o.ld_k == 1;
 }
 
+// Host mirrors of the dispatch decisions the folded BatchNorm depends on (see pde_kernels.h).
+bool skinny_ok(const GemmArgs& a);
+bool bn_stats_ok_impl(const GemmArgs& a, hipStream_t s) {
+  if (a.M <= 0 || a.N <= 0 || generic_only() || a.bn_out.C <= 0 || a.bn_out.rows_per_group <= 0) return false;
+  if (a.epi != 0 || a.splits_out != nullptr || a.N % 8 != 0 || a.ldo % 8 != 0 || a.bn_out.C > a.N ||
+      (reinterpret_cast<uintptr_t>(a.out) & 15) != 0)
+    return false;
+  if (a.bn_out.rows_per_group % 64 != 0 || a.M % a.bn_out.rows_per_group != 0) return false;
+  if (skinny_ok(a) || !is_kc(a.a) || !is_kc(a.b)) return false;
+  int split = 1;
+  if (choose_tiles(a, split, true) != kTile64) return false;
+  if (!fast_ok(a, a.a, true, a.M) || !fast_ok(a, a.b, true, a.N)) return false;
+  if (split > 1) {  // the in-launch combine: its last arriver emits the statistics
+    if (split > kMaxInKernelSplits || static_cast<long>(split) * a.M * a.N * 4 >= (1L << 31)) return false;
+    if (split_tickets(1, s, true) == nullptr) return false;  // allocated (outside a capture) or not
+  }
+  return true;
+}
+
+bool bn_fold_ok_impl(const GemmArgs& a) {
+  const BnFoldIn& f = a.bn_in;
+  if (a.M <= 0 || a.N <= 0 || generic_only() || f.C <= 0 || f.C > kBnFoldMaxC || f.C % 8 != 0) return false;
+  if (f.rows_per_group <= 0 || f.rows_per_group % 64 != 0 || f.G * f.rows_per_group != a.M) return false;
+  if (skinny_ok(a) || !is_kc(a.a) || !is_kc(a.b) || a.b.kind != 0) return false;
+  if (a.a.kind == 0) {
+    if (a.K != f.C) return false;  // A = x [rows][C]: K index == channel
+  } else if (a.a.kind == 1) {
+    const ConvGeom& g = a.a.g;
+    if (g.C != f.C) return false;
+    if (f.center && !(g.R == 3 && g.S == 3 && g.stride == 1 && g.pad == 1 && g.Ho == g.H && g.Wo == g.W))
+      return false;
+  } else {
+    return false;
+  }
+  int split = 1;
+  if (choose_tiles(a, split, true) != kTile64) return false;
+  return fast_ok(a, a.a, true, a.M) && fast_ok(a, a.b, true, a.N);
+}
+
 // ---- GEMM pairs ------------------------------------------------------------------------------------
 constexpr int kind_code(bool akc, bool bkc, int ak, int bk) { return (akc ? 1 : 0) | (bkc ? 2 : 0) | (ak << 2) | (bk << 4); }
 int kind_code_of(const GemmArgs& a) { return kind_code(is_kc(a.a), is_kc(a.b), a.a.kind, a.b.kind); }
@@ -1463,6 +1741,9 @@ bool launch_pair_skinny(const GemmArgs& a0, const GemmArgs& a1, const PairDims& 
 }
 
 }  // namespace
+
+bool gemm_bn_stats_ok(const GemmArgs& a, hipStream_t s) { return bn_stats_ok_impl(a, s); }
+bool gemm_bn_fold_ok(const GemmArgs& a) { return bn_fold_ok_impl(a); }
 
 hipError_t gemm_bf16(const GemmArgs& a, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0) return hipSuccess;

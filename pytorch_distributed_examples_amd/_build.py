@@ -45,7 +45,7 @@ EXTENSIONS = {
 HIP_FLAGS = {
     "kernels/cnn_fused.hip": ["-Xclang", "-target-feature", "-Xclang", "-unaligned-access-mode"],
 }
-for _knob in ("PDE_FAST_STAGES", "PDE_GEMM_SUB"):  # GEMM ring depth / K-tiles per barrier sweeps (gemm.hip)
+for _knob in ("PDE_FAST_STAGES", "PDE_GEMM_SUB", "PDE_GEMM_WPE"):  # GEMM ring depth / K-tiles per barrier sweeps (gemm.hip)
     if os.environ.get(_knob):
         HIP_FLAGS.setdefault("kernels/gemm.hip", []).append(f"-D{_knob}={int(os.environ[_knob])}")
 if os.environ.get("PDE_CNN_C2P"):  # fused-CNN d2n row pitch sweep (cnn_fused.hip)

@@ -22,6 +22,13 @@ from ..ops import layers as L
 EXPANSION = 4
 
 
+class _ShapeOnly:
+    """A stand-in carrying only ``.shape`` for shape-only planning (ops.functional.bn_fold_plan)."""
+
+    def __init__(self, shape):
+        self.shape = shape
+
+
 class Bottleneck(nn.Module):
     expansion = EXPANSION
 
@@ -37,20 +44,48 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
         self.stride = stride
 
+    def _fold_plan(self, x):
+        """(bn1 folded into conv2, bn2 folded into conv3) for this input shape / micro-batch grouping."""
+        key = (tuple(x.shape), OF.current_bn_groups())
+        plans = self.__dict__.setdefault("_pde_fold_plan", {})
+        if key not in plans:
+            c, w = self.conv1, self.conv2
+            f1 = w.stride == 1 and OF.bn_fold_plan(x, c.in_channels, c.out_channels, 1, 1, 0, w.out_channels, 3, 1, 1)
+            # the bn2 plan needs conv2's input shape only (= conv1's output: 1x1, stride 1)
+            f2 = OF.bn_fold_plan(_ShapeOnly((x.shape[0], x.shape[1], x.shape[2], OF.pad8(w.in_channels))),
+                                 w.in_channels, w.out_channels, 3, w.stride, 1, self.conv3.out_channels, 1, 1, 0)
+            plans[key] = (f1, f2)
+        return plans[key]
+
     def forward(self, x):
         identity = x
         # on the GPU x's two gradients (residual / downsample branch and conv1 branch) meet in conv1's dgrad
         # epilogue instead of an autograd add (ops.functional.GradJoin)
         join = OF.GradJoin() if (x.is_cuda and torch.is_grad_enabled() and x.requires_grad) else None
         t = self.training  # training-mode BatchNorm reduces a split-K conv's slabs itself (bn_follows)
-        out = self.bn1(self.conv1(x, grad_join=join, bn_follows=t), relu=True)
-        out = self.bn2(self.conv2(out, bn_follows=t), relu=True)
+        f1 = f2 = False
+        if t and x.is_cuda and OF.bn_fold_enabled():
+            # BatchNorm folded into the convolutions: the producer conv's epilogue emits the statistics, the
+            # consumer conv applies bn + ReLU in its A loader (no BatchNorm launch in between)
+            f1, f2 = self._fold_plan(x)
+        g = OF.current_bn_groups()
+        st2 = OF.BnFoldStats(self.bn2, g) if f2 else None
+        if f1:
+            st1 = OF.BnFoldStats(self.bn1, g)
+            a1 = self.conv1(x, grad_join=join, bn_stats=st1)
+            a2 = OF.bn_relu_conv(a1, st1, self.conv2, stats_out=st2, bn_follows=t)
+        else:
+            out = self.bn1(self.conv1(x, grad_join=join, bn_follows=t), relu=True)
+            a2 = self.conv2(out, bn_follows=t, bn_stats=st2)
+        if f2:
+            out = OF.bn_relu_conv(a2, st2, self.conv3, bn_follows=t)
+        else:
+            out = self.conv3(self.bn2(a2, relu=True), bn_follows=t)
         if self.downsample is not None:
             conv, bn = self.downsample[0], self.downsample[1]
             identity = bn(conv(x, grad_to=join, bn_follows=t))
-        # relu(bn3(conv3(out)) + identity) in one fused kernel
-        return self.bn3(self.conv3(out, bn_follows=t), residual=identity, relu=True,
-                        residual_grad_to=join if self.downsample is None else None)
+        # relu(bn3(conv3(.)) + identity) in one fused kernel
+        return self.bn3(out, residual=identity, relu=True, residual_grad_to=join if self.downsample is None else None)
 
 
 class _StemReLU(nn.Module):

@@ -335,19 +335,40 @@ def linear(x, weight, bias=None, relu=False, out_f32=False, consumer_masks=False
 # ---------------------------------------------------------------------------------------------
 # NHWC implicit-GEMM convolution
 # ---------------------------------------------------------------------------------------------
+def _conv_fwd_weight(x, weight):
+    """The forward implicit-GEMM copy of a conv weight ([Cop, R*S*Cp] bf16) for input ``x``."""
+    co, ci, r, s = weight.shape
+    cp = x.shape[3]
+    cop = pad8(co)
+    wf = _maintained(weight, "conv_fwd") if cp == pad8(ci) else None
+    if wf is None:
+        wf = _cached(weight, ("conv_fwd", cp, cop), lambda: _C().conv_w_fwd(weight.detach().contiguous(), cp, cop))
+    return wf
+
+
+class _ConvBwdCtx:
+    """What :func:`_conv_backward` needs of a conv's autograd context (shared by the plain conv and the
+    conv with a BatchNorm folded into its input)."""
+    __slots__ = ("join", "grad_to", "geom", "relu", "has_bias", "bias", "needs_input_grad")
+
+
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, relu, join=None, grad_to=None, defer=False):
+    def forward(ctx, x, weight, bias, stride, pad, relu, join=None, grad_to=None, defer=False, stats=None):
         ctx.join = join
         ctx.grad_to = grad_to
         co, ci, r, s = weight.shape
         cp = x.shape[3]
         cop = pad8(co)
-        wf = _maintained(weight, "conv_fwd") if cp == pad8(ci) else None
-        if wf is None:
-            wf = _cached(weight, ("conv_fwd", cp, cop), lambda: _C().conv_w_fwd(weight.detach().contiguous(), cp, cop))
-        # defer: a split-K GEMM leaves its slabs for the BatchNorm that follows (it reduces them itself)
-        y = _C().conv_fwd(x, wf, bias.detach() if bias is not None else None, r, s, stride, pad, relu, False, defer)
+        wf = _conv_fwd_weight(x, weight)
+        if stats is not None:
+            # producer of a folded BatchNorm: the epilogue emits the output's statistics and the launch's last
+            # block finalizes that BatchNorm (mean / invstd / scale-shift / running statistics) into `stats`
+            y = stats.produce(x, wf, r, s, stride, pad)
+        else:
+            # defer: a split-K GEMM leaves its slabs for the BatchNorm that follows (it reduces them itself)
+            y = _C().conv_fwd(x, wf, bias.detach() if bias is not None else None, r, s, stride, pad, relu, False,
+                              defer)
         ctx.geom = (co, ci, r, s, stride, pad, cp, cop, x.shape[1], x.shape[2])
         ctx.relu = relu
         ctx.has_bias = bias is not None
@@ -358,6 +379,14 @@ class _Conv2dFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, weight, y = ctx.saved_tensors
+        dx, dw, db = _conv_backward(ctx, dy, x, weight, y)
+        return dx, dw, db, None, None, None, None, None, None, None
+
+
+def _conv_backward(ctx, dy, x, weight, y=None):
+    """dx, dw, db of a conv (dgrad + wgrad as one paired launch, or wgrad on the side stream); ``ctx`` carries
+    join / grad_to / geom / relu / has_bias / bias / needs_input_grad (x, weight, bias)."""
+    if True:
         co, ci, r, s, stride, pad, cp, cop, h, w = ctx.geom
         dy = dy.contiguous()
         if ctx.relu:
@@ -407,9 +436,9 @@ class _Conv2dFn(torch.autograd.Function):
                 db = _C().colsum(dy, co, bsink, bsink is not None)
                 if bsink is not None:
                     db = None
-            return dx, None, db, None, None, None, None, None, None
+            return dx, None, db
         if side:
-            return dx, None, None, None, None, None, None, None, None
+            return dx, None, None
         if ctx.needs_input_grad[1]:
             # OIHW epilogue: the GEMM writes the parameter's layout (and adds into .grad when it exists)
             dw = _C().conv_wgrad(dy, x, r, s, stride, pad, co, ci, wsink, wsink is not None)
@@ -419,7 +448,7 @@ class _Conv2dFn(torch.autograd.Function):
             db = _C().colsum(dy, co, bsink, bsink is not None)
             if bsink is not None:
                 db = None
-        return dx, dw, db, None, None, None, None, None, None
+        return dx, dw, db
 
 
 class GradJoin:
@@ -452,7 +481,8 @@ class GradJoin:
         return g
 
 
-def conv2d(x, weight, bias=None, stride=1, padding=0, relu=False, grad_join=None, grad_to=None, bn_follows=False):
+def conv2d(x, weight, bias=None, stride=1, padding=0, relu=False, grad_join=None, grad_to=None, bn_follows=False,
+           bn_stats=None):
     """2-D convolution.  GPU: ``x`` is NHWC bf16 with C padded to a multiple of 8; output NHWC with
     Cout padded to a multiple of 8 (padded channels are exactly zero).  CPU: NCHW fp32 F.conv2d.
     ``grad_join`` (this conv's dgrad adds the join's gradient) / ``grad_to`` (this conv's input gradient
@@ -463,7 +493,8 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, relu=False, grad_join=None
         y = F.conv2d(_emu(x), _emu(weight), bias, stride=stride, padding=padding)
         return _emu(F.relu(y) if relu else y)
     defer = bool(bn_follows) and bias is None and not relu and _DEFER_CONV[0]
-    return _Conv2dFn.apply(x.contiguous(), weight, bias, int(stride), int(padding), relu, grad_join, grad_to, defer)
+    return _Conv2dFn.apply(x.contiguous(), weight, bias, int(stride), int(padding), relu, grad_join, grad_to, defer,
+                           bn_stats)
 
 
 import os as _os
@@ -560,6 +591,124 @@ def batch_norm(x, weight, bias, running_mean, running_var, training, momentum=0.
     scale = (weight * invstd if weight is not None else invstd).float().contiguous()
     shift = ((bias if bias is not None else 0) - running_mean * scale).float().contiguous()
     return _C().bn_apply(x, scale, shift, residual.contiguous() if residual is not None else None, relu)
+
+
+# ---------------------------------------------------------------------------------------------
+# BatchNorm folded into the convolutions around it (training, GPU; csrc/kernels/gemm.hip BnFoldIn / BnStatsOut)
+# ---------------------------------------------------------------------------------------------
+# Opt-in (PDE_BN_FOLD=1). Measured on MI355X (profiles/r4h_bnfold_ab_bench.jsonl, README "BatchNorm fold"):
+# ResNet-50 bs32 step 3.55 ms folded vs 3.29 ms unfolded -- the producer's last-block finalize tail (~7.5 us)
+# and the consumer's A transform (~3.8 us) cost more than the BatchNorm launches they remove (~0.03 ms total).
+_BN_FOLD = [_os.environ.get("PDE_BN_FOLD", "0") == "1"]
+
+
+def bn_fold_enabled() -> bool:
+    return _BN_FOLD[0]
+
+
+def bn_fold_buffers(bn, groups: int):
+    """The persistent (self-cleaning) statistics buffer [shards, G, 2, C] int64 + arrival ticket of BatchNorm
+    ``bn``: the producer conv's epilogue adds into it, the producer launch's last block reads-and-zeroes it."""
+    bufs = bn.__dict__.setdefault("_pde_fold", {})
+    if groups not in bufs:
+        dev = bn.weight.device
+        shards = _C().bn_fold_shards()  # row-tile shards of the sums (contention, see pde_kernels.h)
+        bufs[groups] = (torch.zeros(shards * groups * 2 * bn.num_features, dtype=torch.long, device=dev),
+                        torch.zeros(1, dtype=torch.int32, device=dev))
+    return bufs[groups]
+
+
+class BnFoldStats:
+    """One training-mode BatchNorm2d ``bn`` folded into the convs around it, for one forward: the producer conv
+    (``conv2d(..., bn_stats=this)``) emits and finalizes its statistics -- :meth:`produce` keeps the saved mean /
+    invstd / scale-shift -- and :func:`bn_relu_conv` applies it in the consumer conv's A loader."""
+
+    def __init__(self, bn, groups: int):
+        self.bn, self.groups = bn, groups
+        self.sums, self.ticket = bn_fold_buffers(bn, groups)
+        self.mean = self.invstd = self.ss = None
+
+    def produce(self, x, wf, r, s, stride, pad):
+        bn = self.bn
+        y, self.mean, self.invstd, self.ss, _ = _C().conv_fwd_bn(
+            x, wf, r, s, stride, pad, self.groups, self.sums, self.ticket, bn.weight.detach(), bn.bias.detach(),
+            bn.running_mean, bn.running_var, bn.eps, bn.momentum, None, False, False)
+        bn._nbt_pending += self.groups
+        return y
+
+
+class _BnConvFn(torch.autograd.Function):
+    """conv(relu(bn(a))) with the BatchNorm (+ ReLU) applied in the conv's A loader from the scale / shift the
+    producer of ``a`` finalized; the activation is written once by the conv (the backward's operand).
+    Backward: the conv's dgrad / wgrad against that activation, then the BatchNorm backward (ReLU mask from
+    ``a`` and the saved scale / shift)."""
+
+    @staticmethod
+    def forward(ctx, a, gamma, beta, weight, st, relu, stride, pad, stats_out=None, defer=False):
+        co, ci, r, s = weight.shape
+        cp = a.shape[3]
+        wf = _conv_fwd_weight(a, weight)
+        if stats_out is not None:  # this conv also produces the NEXT BatchNorm's statistics
+            y = stats_out.produce_folded(a, wf, r, s, stride, pad, st.ss, relu)
+            act = stats_out.act
+        else:
+            y, _, _, _, act = _C().conv_fwd_bn(a, wf, r, s, stride, pad, st.groups, None, None, None, None, None,
+                                               None, 0.0, 0.0, st.ss, relu, defer)
+        ctx.geom = (co, ci, r, s, stride, pad, cp, pad8(co), a.shape[1], a.shape[2])
+        ctx.relu, ctx.groups = relu, st.groups
+        ctx.beta = beta
+        ctx.save_for_backward(a, act, st.mean, st.invstd, gamma, st.ss, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        a, act, mean, invstd, gamma, ss, weight = ctx.saved_tensors
+        cx = _ConvBwdCtx()
+        cx.join = cx.grad_to = None
+        cx.geom, cx.relu, cx.has_bias, cx.bias = ctx.geom, False, False, None
+        cx.needs_input_grad = (True, ctx.needs_input_grad[3], False)
+        dact, dw, _ = _conv_backward(cx, dy, act, weight)
+        beta = ctx.beta
+        dg_sink, db_sink = _grad_sink(gamma), _grad_sink(beta)
+        direct = dg_sink is not None and db_sink is not None
+        da, dg, db, _ = _C().bn_bwd(dact, a, act, mean, invstd, gamma.detach(), ctx.relu, False,
+                                    dg_sink if direct else None, db_sink if direct else None, ss, ctx.groups)
+        if direct:
+            dg = db = None
+        return da, dg, db, dw, None, None, None, None, None, None
+
+
+def _produce_folded(self, a, wf, r, s, stride, pad, fold_ss, relu):
+    """BnFoldStats.produce for a conv that itself consumes a folded BatchNorm (both sides in one launch)."""
+    bn = self.bn
+    y, self.mean, self.invstd, self.ss, self.act = _C().conv_fwd_bn(
+        a, wf, r, s, stride, pad, self.groups, self.sums, self.ticket, bn.weight.detach(), bn.bias.detach(),
+        bn.running_mean, bn.running_var, bn.eps, bn.momentum, fold_ss, relu, False)
+    bn._nbt_pending += self.groups
+    return y
+
+
+BnFoldStats.produce_folded = _produce_folded
+
+
+def bn_relu_conv(a, st: BnFoldStats, conv, relu=True, stats_out: BnFoldStats | None = None, bn_follows=False):
+    """``conv(relu(st.bn(a)))`` for the BatchNorm whose statistics the producer of ``a`` emitted
+    (``conv2d(..., bn_stats=st)``) and a bias-free Conv2d ``conv`` (a 1x1, or a 3x3 of stride 1).
+    ``stats_out``: this conv's epilogue also emits (and finalizes) the NEXT BatchNorm."""
+    assert st.ss is not None, "the producer conv of this BatchNorm has not run"
+    bn = st.bn
+    defer = bool(bn_follows) and stats_out is None and _DEFER_CONV[0]
+    return _BnConvFn.apply(a.contiguous(), bn.weight, bn.bias, conv.weight, st, relu, int(conv.stride),
+                           int(conv.padding), stats_out, defer)
+
+
+def bn_fold_plan(x, cin, co1, k1, s1, p1, co2, k2, s2, p2) -> bool:
+    """Whether conv1 (k1 x k1 / s1 / p1, cin -> co1) can emit the BatchNorm statistics of its output AND conv2
+    (k2 / s2 / p2, co1 -> co2) can apply that BatchNorm in its A loader, for input ``x`` (NHWC) and the current
+    micro-batch grouping (shape-only; cached by the caller)."""
+    n, h, w = x.shape[0], x.shape[1], x.shape[2]
+    return bool(_C().bn_fold_plan(n, h, w, x.shape[3], pad8(co1), k1, k1, s1, p1, pad8(co2), k2, k2, s2, p2,
+                                  current_bn_groups()))
 
 
 # ---------------------------------------------------------------------------------------------
