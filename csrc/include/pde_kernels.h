@@ -109,6 +109,7 @@ struct GemmArgs {
                                    //   here (1: the output was written directly)
   BnStatsOut bn_out;               // producer side of a folded BatchNorm (bn_out.sums != nullptr)
   BnFoldIn bn_in;                  // consumer side (bn_in.ss != nullptr): A = relu(x * scale + shift)
+  int wt;                          // vector output / slab stores write-through (set by gemm_bf16*: PDE_GEMM_WT)
 };
 // Whether gemm_bf16 would run `a` on a path whose epilogue emits BatchNorm statistics (bn_out): the 64x64
 // FAST tile, bf16 output without epilogue ops, and no split-K (or one reduced inside the launch).

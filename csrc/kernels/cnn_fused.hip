@@ -198,6 +198,23 @@ __device__ __forceinline__ void cnn_grid_barrier(unsigned* bar, unsigned n, int*
   __syncthreads();
 }
 
+// Stores of the per-workgroup outputs the reduction launch reads (slabs, activation columns, loss partials):
+// SM 0 plain, 1 non-temporal, 2 write-through (sc1: the bytes leave the XCD's L2 under the remaining phases
+// instead of at the kernel boundary).  Vector stores only.
+template <int SM>
+__device__ __forceinline__ void out_st(float* p, float v) {
+  if constexpr (SM == 1) __builtin_nontemporal_store(v, p);
+  else if constexpr (SM == 2) asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  else *p = v;
+}
+template <int SM>
+__device__ __forceinline__ void out_st4(float* p, f32x4 v) {
+  if constexpr (SM == 1) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+  else if constexpr (SM == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  else *reinterpret_cast<f32x4*>(p) = v;
+}
+
+template <int SM>
 __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ images, const int64_t* __restrict__ tgt,
                                                  int B, const float* __restrict__ params,
                                                  const u16x8* __restrict__ frag,
@@ -205,7 +222,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
                                                  float p_drop1, int training, float* __restrict__ slabs,
                                                  float* __restrict__ loss_part, float* __restrict__ acts,
                                                  unsigned long long* __restrict__ stamps, int stop_after,
-                                                 CnnTail tail) {
+                                                 CnnTail tail, int xmap) {
   // optional phase timestamps (diagnostic only: stamps == nullptr in production launches); stop_after = k
   // ends the kernel after phase stamp k (diagnostic: hardware counters of a kernel prefix)
 #define PDE_STAMP(k)                                                                      \
@@ -222,7 +239,10 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   const float* gW2 = params + O_W2;
   const float* gFC1W = params + O_FC1W;
   const float* gFC1B = params + O_FC1B;
-  const int n0 = blockIdx.x * NI;
+  // xmap: workgroups that share an XCD (blockIdx % 8 under the observed round-robin placement) take
+  // consecutive images, so the 8 workgroups writing one 128-B line of an activation row sit behind one L2
+  const int lwg = xmap ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  const int n0 = lwg * NI;
 
   // ---- P0: images -> bf16, weights -> bf16 MFMA fragments, fp32 head weights, dropout masks ------
   // every global load of the phase is issued first (unconditional, clamped addresses): the conv weight
@@ -477,13 +497,13 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     float s = 0.f;
 #pragma unroll
     for (int im = 0; im < NI; ++im) s += S.dlog[im][v] * S.h1d[im][j];
-    slab[S_FC2W + t] = s;
+    out_st<SM>(&slab[S_FC2W + t], s);
   }
   if (t < F2) {
     float s = 0.f;
 #pragma unroll
     for (int im = 0; im < NI; ++im) s += S.dlog[im][t];
-    slab[S_FC2B + t] = s;
+    out_st<SM>(&slab[S_FC2B + t], s);
   }
   if (t >= 256 && t < 256 + NI * F1) {
     const int u = t - 256, im = u / F1, j = u - im * F1;
@@ -504,14 +524,14 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       f32x4 v;
 #pragma unroll
       for (int im = 0; im < NI; ++im) v[im] = row < F1 ? S.dh[im][row] : S.r2[im][row - F1];
-      *reinterpret_cast<f32x4*>(acts + static_cast<long>(row) * Bk + n0) = v;
+      out_st4<SM>(acts + static_cast<long>(row) * Bk + n0, v);
     }
   }
   if (t < F1) {
     float s = 0.f;
 #pragma unroll
     for (int im = 0; im < NI; ++im) s += S.dh[im][t];
-    slab[S_FC1B + t] = s;
+    out_st<SM>(&slab[S_FC1B + t], s);
   }
   float* dpart = reinterpret_cast<float*>(&S.w2f[0][0][0]);  // [jc][im][i]
   if (t < NIN * DP2_JC) {  // thread (i, jc): sum over fc1 outputs j in chunk jc (column loads coalesced)
@@ -556,7 +576,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     float s = 0.f;
     for (int im = 0; im < NI; ++im)
       for (int c = 0; c < NC2; ++c) s += S.dp2[im][co * NC2 + c];
-    slab[O_B2 + co] = s;
+    out_st<SM>(&slab[O_B2 + co], s);
   }
   lds_sync();
   PDE_STAMP(8);
@@ -604,7 +624,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int co = mt * 16 + lg * 4 + r;
-          if (co < C2 && kidx < K2) slab[O_W2 + co * K2 + kidx] = acc[mt][u][r];
+          if (co < C2 && kidx < K2) out_st<SM>(&slab[O_W2 + co * K2 + kidx], acc[mt][u][r]);
         }
       }
   }
@@ -729,13 +749,13 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       float s = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) s += part[(w * 2 + u) * 64 + l][r];
-      slab[O_W1 + t] = s;
+      out_st<SM>(&slab[O_W1 + t], s);
     } else if (t >= 256 && t < 256 + C1) {
       const int c = t - 256;
       float s = 0.f;
       for (int im = 0; im < NI; ++im)
         for (int q = 0; q < NC1; ++q) s += bf2f(S.dr1[im][c * NC1 + q]);
-      slab[O_B1 + c] = s;
+      out_st<SM>(&slab[O_B1 + c], s);
     }
   }
   PDE_STAMP(11);
@@ -743,7 +763,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   // loss partial: threads 0..NI-1 of wave 0 hold it
   if (wid == 0) {
     const float l = wave_sum(loss_acc);
-    if (lane == 0) loss_part[blockIdx.x] = l;
+    if (lane == 0) out_st<SM>(&loss_part[blockIdx.x], l);
   }
   if (stamps != nullptr) {  // diagnostic: every wave's stores drained, then the workgroup's last stamp
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1049,11 +1069,11 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
                                                       float* __restrict__ loss, unsigned long long* __restrict__ rng,
                                                       float* __restrict__ params, const float* __restrict__ hp,
                                                       uint16_t* __restrict__ frag, int* __restrict__ step,
-                                                      XgmiView xv, float xscale) {
+                                                      XgmiView xv, float xscale, int rb0) {
   __shared__ f32x4 part[RED_LANES * RED_COLS];  // slab: [lane][column]; fc1: [wave][lane] (same 8 KB)
   __shared__ uint32_t s_epoch;
   __shared__ int s_fail;
-  cnn_reduce_role(blockIdx.x, part, &s_epoch, &s_fail, slabs, nwg, acts, gscale, grads, accumulate, loss_part, B,
+  cnn_reduce_role(rb0 + blockIdx.x, part, &s_epoch, &s_fail, slabs, nwg, acts, gscale, grads, accumulate, loss_part, B,
                   loss, rng, params, hp, frag, step, xv, xscale);
 }
 
@@ -1142,11 +1162,19 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
     view = *xv;
   }
   const size_t sm = sizeof(CnnSmem);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cnn_train), hipFuncAttributeMaxDynamicSharedMemorySize,
+  // PDE_CNN_STORE: store flavour of the slabs / activations (out_st).  Write-through (2) is the default: the
+  // 7.5 MB the reduction launch reads no longer sit dirty in the XCD L2s at the kernel boundary (r4k: 0.0408 ->
+  // 0.0381 ms/step; non-temporal 0.0390).  PDE_CNN_XMAP=1: XCD-grouped images (r4k: level, off)
+  static const int smode = std::getenv("PDE_CNN_STORE") ? std::atoi(std::getenv("PDE_CNN_STORE")) : 2;
+  static const int xmap_env = std::getenv("PDE_CNN_XMAP") ? std::atoi(std::getenv("PDE_CNN_XMAP")) : 0;
+  const int xmap = xmap_env != 0 && nwg % 8 == 0 ? 1 : 0;
+  auto train = smode == 1 ? &k_cnn_train<1> : smode == 2 ? &k_cnn_train<2> : &k_cnn_train<0>;
+  static bool attr[3] = {false, false, false};
+  const int si = smode == 1 || smode == 2 ? smode : 0;
+  if (!attr[si]) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(train), hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(sm));
-    attr = true;
+    attr[si] = true;
   }
   if (reinterpret_cast<uintptr_t>(frag) & 15) return hipErrorInvalidValue;
   if (prep)
@@ -1161,13 +1189,20 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
     tail.hp = sgd_hp; tail.frag = static_cast<uint16_t*>(frag); tail.step = sgd_step; tail.bar = bar;
     tail.err = berr; tail.accumulate = accumulate; tail.B = B; tail.on = 1;
   }
-  hipLaunchKernelGGL(k_cnn_train, dim3(nwg), dim3(T), sm, s, images, tgt, B, params,
-                     static_cast<const u16x8*>(frag), rng, p_drop2, p_drop1, training, slabs, loss_part, acts, stamps,
-                     stop_after, tail);
-  if (!tail.on)
-    hipLaunchKernelGGL(k_cnn_reduce, dim3(RED_BLOCKS), dim3(RED_T), 0, s, slabs, nwg, acts, gscale, grads,
+  // PDE_CNN_DIAG (timing diagnostics only, results invalid): 1 no reduce launch, 2 no train launch, 4 reduce
+  // slab-column roles only, 8 reduce fc1-tile roles only
+  static const int diag = std::getenv("PDE_CNN_DIAG") ? std::atoi(std::getenv("PDE_CNN_DIAG")) : 0;
+  if (!(diag & 2))
+    hipLaunchKernelGGL(train, dim3(nwg), dim3(T), sm, s, images, tgt, B, params,
+                       static_cast<const u16x8*>(frag), rng, p_drop2, p_drop1, training, slabs, loss_part, acts,
+                       stamps, stop_after, tail, xmap);
+  if (!tail.on && !(diag & 1)) {
+    const int rb0 = (diag & 8) ? RED_SLAB_BLOCKS : 0;
+    const int nrb = (diag & 4) ? RED_SLAB_BLOCKS : (diag & 8) ? RED_BLOCKS - RED_SLAB_BLOCKS : RED_BLOCKS;
+    hipLaunchKernelGGL(k_cnn_reduce, dim3(nrb), dim3(RED_T), 0, s, slabs, nwg, acts, gscale, grads,
                        accumulate, loss_part, B, loss, rng, params, sgd_hp, static_cast<uint16_t*>(frag), sgd_step,
-                       view, xscale);
+                       view, xscale, rb0);
+  }
   return hipGetLastError();
 }
 

@@ -731,7 +731,8 @@ __device__ __forceinline__ void write_slab_and_reduce(const GemmArgs& args, cons
         u16x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = f2bf(apply_epi(v[i][j], args.epi, m, n + j, args));
-        *reinterpret_cast<u16x4*>(static_cast<uint16_t*>(args.out) + static_cast<long>(m) * args.ldo + n) = o;
+        st_vec(reinterpret_cast<u16x4*>(static_cast<uint16_t*>(args.out) + static_cast<long>(m) * args.ldo + n), o,
+               args.wt != 0);
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) store_out(apply_epi(v[i][j], args.epi, m, n + j, args), args.epi, m, n + j, args);
@@ -962,8 +963,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args, int tiles_m, int
         const int ml = q / (BN / 8), nl = (q % (BN / 8)) * 8;
         const int m = m0 + ml, n = n0 + nl;
         if (m < args.M && n < args.N)
-          *reinterpret_cast<u16x8*>(out + static_cast<long>(m) * args.ldo + n) =
-              *reinterpret_cast<const u16x8*>(st + ml * BN + nl);
+          st_vec(reinterpret_cast<u16x8*>(out + static_cast<long>(m) * args.ldo + n),
+                 *reinterpret_cast<const u16x8*>(st + ml * BN + nl), args.wt != 0);
       }
       if constexpr (BM * BN * 2 + 2 * BN * (kThreads / BN) * 4 <= SMEM_BYTES && kThreads % BN == 0) {
         if (args.bn_out.sums != nullptr)  // producer of a folded BatchNorm: its statistics from the staged tile
@@ -1001,7 +1002,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args, int tiles_m, int
           for (int j = 0; j < 4; ++j) o[j] = apply_epi(v[j], args.epi, m, n + j, args);
           f32x4* dst = reinterpret_cast<f32x4*>(out + static_cast<long>(m) * args.ldo + n);
           if (args.epi & EPI_ACCUM) o += *dst;
-          *dst = o;
+          st_vec(dst, o, args.wt != 0);
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
@@ -1025,8 +1026,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& args, int tiles_m, int
         const int ml = q / (BN / 4), nl = (q % (BN / 4)) * 4;
         const int m = m0 + ml, n = n0 + nl;
         if (m < args.M && n < args.N)
-          *reinterpret_cast<f32x4*>(ws + (static_cast<long>(kz) * args.M + m) * args.N + n) =
-              *reinterpret_cast<const f32x4*>(st + ml * BN + nl);
+          st_vec(reinterpret_cast<f32x4*>(ws + (static_cast<long>(kz) * args.M + m) * args.N + n),
+                 *reinterpret_cast<const f32x4*>(st + ml * BN + nl), args.wt != 0);
       }
       return;
     }
@@ -1745,8 +1746,17 @@ bool launch_pair_skinny(const GemmArgs& a0, const GemmArgs& a1, const PairDims& 
 bool gemm_bn_stats_ok(const GemmArgs& a, hipStream_t s) { return bn_stats_ok_impl(a, s); }
 bool gemm_bn_fold_ok(const GemmArgs& a) { return bn_fold_ok_impl(a); }
 
-hipError_t gemm_bf16(const GemmArgs& a, hipStream_t s) {
-  if (a.M <= 0 || a.N <= 0) return hipSuccess;
+// Vector epilogue / slab stores write-through (GemmArgs::wt); PDE_GEMM_WT=0 plain.  r4l: ResNet-50 3.317 -> 3.248
+// ms/step, MLP level
+int gemm_wt() {
+  static const int on = std::getenv("PDE_GEMM_WT") ? std::atoi(std::getenv("PDE_GEMM_WT")) : 1;
+  return on;
+}
+
+hipError_t gemm_bf16(const GemmArgs& a_in, hipStream_t s) {
+  if (a_in.M <= 0 || a_in.N <= 0) return hipSuccess;
+  GemmArgs a = a_in;
+  a.wt = gemm_wt();
   if (skinny_ok(a)) return launch_skinny(a, s);
   const bool akc = is_kc(a.a), bkc = is_kc(a.b);
   if (akc && bkc) return dispatch_tiles<true, true>(a, s);
@@ -1793,8 +1803,10 @@ bool gemm_pair_enabled() {
   return on;
 }
 
-hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s, int* defer_split1,
+hipError_t gemm_bf16_pair(const GemmArgs& a0_in, const GemmArgs& a1_in, hipStream_t s, int* defer_split1,
                           const OptimSeg* seg_in) {
+  GemmArgs a0 = a0_in, a1 = a1_in;
+  a0.wt = a1.wt = gemm_wt();
   if (defer_split1 != nullptr) *defer_split1 = 0;
   OptimSeg seg{};  // blocks = 0: no optimiser segment
   if (seg_in != nullptr && seg_in->c1 > seg_in->c0 && seg_in->blocks > 0) seg = *seg_in;

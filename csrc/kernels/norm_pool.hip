@@ -880,8 +880,8 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
   }
   // (bn_partials_and_ticket's first barrier also publishes s_gen to the block)
   // lite bit 0: fence-free hand-off; bit 1: every block finalizes its channel group (bn_partials_all); bit 2:
-  // tagged partials (bn_partials_tagged, implies 1 and 2)
-  const bool tagged = (lite & 4) != 0, allfin = (lite & 2) != 0;
+  // tagged partials (bn_partials_tagged, implies 1 and 2); bit 3: write-through outputs (st_vec)
+  const bool tagged = (lite & 4) != 0, allfin = (lite & 2) != 0, wt = (lite & 8) != 0;
   lite &= 1;
   const bool writer =
       tagged ? bn_partials_tagged(s1, s2, parts + static_cast<long>(gz * gridDim.y + blockIdx.y) * kBnTagWords, C,
@@ -968,7 +968,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
           if (relu) t = fmaxf(t, 0.f);
           o[j] = f2bf(t);
         }
-        *reinterpret_cast<u16x8*>(y + static_cast<long>(r) * C + c0) = o;
+        st_vec(reinterpret_cast<u16x8*>(y + static_cast<long>(r) * C + c0), o, wt);
       }
     }
     return;
@@ -993,7 +993,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
         if (relu) t = fmaxf(t, 0.f);
         o[j] = f2bf(t);
       }
-      *reinterpret_cast<u16x8*>(y + static_cast<long>(r + kBnRows * k) * C + c0) = o;
+      st_vec(reinterpret_cast<u16x8*>(y + static_cast<long>(r + kBnRows * k) * C + c0), o, wt);
     }
   }
   for (; r < r1; r += kBnRows) {
@@ -1009,7 +1009,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_fwd_fused(
       if (relu) t = fmaxf(t, 0.f);
       o[j] = f2bf(t);
     }
-    *reinterpret_cast<u16x8*>(y + off) = o;
+    st_vec(reinterpret_cast<u16x8*>(y + off), o, wt);
   }
 }
 
@@ -1137,8 +1137,8 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
     }
   }
   // lite bit 0: fence-free hand-off; bit 1: every block finalizes its channel group (bn_partials_all); bit 2:
-  // tagged partials (bn_partials_tagged, implies 1 and 2)
-  const bool tagged = (lite & 4) != 0, allfin = (lite & 2) != 0;
+  // tagged partials (bn_partials_tagged, implies 1 and 2); bit 3: write-through outputs (st_vec)
+  const bool tagged = (lite & 4) != 0, allfin = (lite & 2) != 0, wt = (lite & 8) != 0;
   lite &= 1;
   const bool writer =
       tagged ? bn_partials_tagged(s1, s2, parts + static_cast<long>(gz * gridDim.y + blockIdx.y) * kBnTagWords, C,
@@ -1209,8 +1209,8 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
       o[j] = f2bf(ca[j] * d[j] - cb[j] - cc[j] * xh);
       orr[j] = f2bf(d[j]);
     }
-    *reinterpret_cast<u16x8*>(dx + off) = o;
-    if (dres) *reinterpret_cast<u16x8*>(dres + off) = orr;
+    st_vec(reinterpret_cast<u16x8*>(dx + off), o, wt);
+    if (dres) st_vec(reinterpret_cast<u16x8*>(dres + off), orr, wt);
   };
   if constexpr (RC > 0) {
 #pragma unroll
@@ -1700,7 +1700,10 @@ bool bn_one_launch(int blocks) {
 int bn_lite_sync() {
   static const int lite = !(std::getenv("PDE_BN_LITE") != nullptr && std::getenv("PDE_BN_LITE")[0] == '0');
   static const int allfin = !(std::getenv("PDE_BN_ALLFIN") != nullptr && std::getenv("PDE_BN_ALLFIN")[0] == '0');
-  return lite ? (allfin ? 3 : 1) : 0;
+  // bit 3 (PDE_BN_WT=1): the normalised outputs / data gradients stored write-through -- r4m: level (3.256 ms
+  // both ways), so off
+  static const int wt = std::getenv("PDE_BN_WT") != nullptr && std::getenv("PDE_BN_WT")[0] == '1';
+  return (lite ? (allfin ? 3 : 1) : 0) | (wt ? 8 : 0);
 }
 // Chunks of 5..8 rows per thread also stay in registers between the passes (RC = 8), r3ac: ResNet-50
 // 3.337 -> 3.319 ms/step (3 of 3 pairs); PDE_BN_RC8=0: off.
@@ -1748,12 +1751,12 @@ hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, con
     int* gt = groups > 1 ? bn_tickets(ncg, s) : nullptr;
     int mode = bn_lite_sync();
     uint64_t* parts = nullptr;
-    if (mode == 3 && bn_tagged_on() && nrb1 <= kBnTagChunks) {
+    if ((mode & 7) == 3 && bn_tagged_on() && nrb1 <= kBnTagChunks) {
       uint32_t* hdr = nullptr;
       parts = bn_tag_slots(ncg * groups, s, &hdr);
       if (parts != nullptr) {
         fl = hdr;  // the slots' headers are the epochs
-        mode = 7;
+        mode = 7 | (mode & 8);
       }
     }
     if (tk != nullptr && fl != nullptr && (groups == 1 || (gt != nullptr && gscratch != nullptr))) {
@@ -1849,12 +1852,12 @@ hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, cons
     int* gt = groups > 1 ? bn_tickets(ncg, s) : nullptr;
     int mode = bn_lite_sync();
     uint64_t* parts = nullptr;
-    if (mode == 3 && bn_tagged_on() && nrb1 <= kBnTagChunks) {
+    if ((mode & 7) == 3 && bn_tagged_on() && nrb1 <= kBnTagChunks) {
       uint32_t* hdr = nullptr;
       parts = bn_tag_slots(ncg * groups, s, &hdr);
       if (parts != nullptr) {
         fl = hdr;
-        mode = 7;
+        mode = 7 | (mode & 8);
       }
     }
     if (tk != nullptr && fl != nullptr && (groups == 1 || (gt != nullptr && gscratch != nullptr))) {

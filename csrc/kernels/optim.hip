@@ -24,7 +24,7 @@ namespace {
 using optdev::kOptChunk;
 using optdev::kOptThreads;
 
-template <int MODE, bool NT>
+template <int MODE, int NT>
 __global__ __launch_bounds__(kOptThreads) void k_optim(const OptimEntry* __restrict__ tab,
                                                        const OptimChunk* __restrict__ chunks, int c_begin, int c_end,
                                                        const float* __restrict__ hp, int* __restrict__ step_ptr,
@@ -45,15 +45,19 @@ int optim_segment_blocks(int nchunks) {
 hipError_t multi_tensor_optim_range(int mode, const OptimEntry* dev_table, const OptimChunk* dev_chunks, int c_begin,
                                     int c_end, const float* dev_hparams, int* dev_step, int publish, hipStream_t s) {
   if (c_end <= c_begin) return hipSuccess;
-  static const bool nt = !(std::getenv("PDE_OPTIM_NT") && std::getenv("PDE_OPTIM_NT")[0] == '0');
+  // PDE_OPTIM_NT: 0 plain, 1 non-temporal loads + stores, 2 non-temporal loads + write-through stores (ld4/st4)
+  static const int nt = std::getenv("PDE_OPTIM_NT") ? std::atoi(std::getenv("PDE_OPTIM_NT")) : 1;
   dim3 grid(static_cast<unsigned>(optim_segment_blocks(c_end - c_begin)));
 #define PDE_OPT(M)                                                                                            \
-  if (nt)                                                                                                     \
-    hipLaunchKernelGGL((k_optim<M, true>), grid, dim3(kOptThreads), 0, s, dev_table, dev_chunks, c_begin,     \
-                       c_end, dev_hparams, dev_step, publish);                                               \
+  if (nt == 2)                                                                                                \
+    hipLaunchKernelGGL((k_optim<M, 2>), grid, dim3(kOptThreads), 0, s, dev_table, dev_chunks, c_begin, c_end, \
+                       dev_hparams, dev_step, publish);                                                      \
+  else if (nt == 1)                                                                                           \
+    hipLaunchKernelGGL((k_optim<M, 1>), grid, dim3(kOptThreads), 0, s, dev_table, dev_chunks, c_begin, c_end, \
+                       dev_hparams, dev_step, publish);                                                      \
   else                                                                                                        \
-    hipLaunchKernelGGL((k_optim<M, false>), grid, dim3(kOptThreads), 0, s, dev_table, dev_chunks, c_begin,    \
-                       c_end, dev_hparams, dev_step, publish);
+    hipLaunchKernelGGL((k_optim<M, 0>), grid, dim3(kOptThreads), 0, s, dev_table, dev_chunks, c_begin, c_end, \
+                       dev_hparams, dev_step, publish);
   if (mode == 0) {
     PDE_OPT(0)
   } else if (mode == 1) {

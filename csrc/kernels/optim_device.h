@@ -41,21 +41,24 @@ __device__ __forceinline__ void update(const Hyper& h, float& p, float g, float&
   }
 }
 
-// 16-B state accesses; NT: non-temporal (streaming) loads and stores -- every state byte is touched once per
-// step, so keeping it in L2 / MALL only evicts the GEMMs' operands (A/B: PDE_OPTIM_NT=0)
-template <bool NT>
+// 16-B state accesses.  NT 1: non-temporal (streaming) loads and stores -- every state byte is touched once
+// per step, so keeping it in L2 / MALL only evicts the GEMMs' operands; NT 2: non-temporal loads, write-through
+// (sc1) stores -- the updated state leaves L2 during the update instead of at the kernel boundary, ahead of the
+// next step's first GEMM; NT 0: plain (A/B: PDE_OPTIM_NT)
+template <int NT>
 __device__ __forceinline__ f32x4 ld4(const float* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  if constexpr (NT != 0) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
   else return *reinterpret_cast<const f32x4*>(p);
 }
-template <bool NT>
+template <int NT>
 __device__ __forceinline__ void st4(float* p, const f32x4& v) {
-  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+  if constexpr (NT == 2) st_vec(reinterpret_cast<f32x4*>(p), v, true);
+  else if constexpr (NT == 1) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
   else *reinterpret_cast<f32x4*>(p) = v;
 }
 
 // One chunk's state for one thread: kOptGroups x 16 B of every state tensor, loaded before any math.
-template <int MODE, bool NT>
+template <int MODE, int NT>
 struct ChunkRegs {
   float p[kOptGroups][4], g[kOptGroups][4], m[kOptGroups][4], v[kOptGroups][4];
   int e0[kOptGroups], cnt[kOptGroups];
@@ -113,7 +116,8 @@ struct ChunkRegs {
         if (use_m) st4<NT>(te.exp_avg + i, f32x4{m[u][0], m[u][1], m[u][2], m[u][3]});
         if (MODE != 0) st4<NT>(te.exp_avg_sq + i, f32x4{v[u][0], v[u][1], v[u][2], v[u][3]});
         if (te.bf16_copy)
-          *reinterpret_cast<u16x4*>(te.bf16_copy + i) = u16x4{f2bf(p[u][0]), f2bf(p[u][1]), f2bf(p[u][2]), f2bf(p[u][3])};
+          st_vec(reinterpret_cast<u16x4*>(te.bf16_copy + i),
+                 u16x4{f2bf(p[u][0]), f2bf(p[u][1]), f2bf(p[u][2]), f2bf(p[u][3])}, NT == 2);
       } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -135,7 +139,7 @@ struct ChunkRegs {
 // publish: the last of the `nblocks` blocks to finish stores the new step count (the final segment of a step).
 // PIPE = false (the segments appended to GEMM launches: about one chunk per block, and the GEMM tiles' VGPR
 // budget): one chunk's registers live at a time.
-template <int MODE, bool NT, bool PIPE = true>
+template <int MODE, int NT, bool PIPE = true>
 __device__ __forceinline__ void run_chunks(const OptimEntry* __restrict__ tab, const OptimChunk* __restrict__ chunks,
                                            int c_begin, int c_end, const float* __restrict__ hp,
                                            int* __restrict__ step_ptr, int block, int nblocks, bool publish) {
@@ -187,11 +191,11 @@ __device__ __forceinline__ void run_chunks(const OptimEntry* __restrict__ tab, c
 // Runtime mode dispatch (NT loads / stores: every state byte is touched once per step).
 __device__ __forceinline__ void run_segment(const OptimSeg& s, int block) {
   if (s.mode == 0)
-    run_chunks<0, true, false>(s.tab, s.chunks, s.c0, s.c1, s.hp, s.step, block, s.blocks, s.publish != 0);
+    run_chunks<0, 1, false>(s.tab, s.chunks, s.c0, s.c1, s.hp, s.step, block, s.blocks, s.publish != 0);
   else if (s.mode == 1)
-    run_chunks<1, true, false>(s.tab, s.chunks, s.c0, s.c1, s.hp, s.step, block, s.blocks, s.publish != 0);
+    run_chunks<1, 1, false>(s.tab, s.chunks, s.c0, s.c1, s.hp, s.step, block, s.blocks, s.publish != 0);
   else
-    run_chunks<2, true, false>(s.tab, s.chunks, s.c0, s.c1, s.hp, s.step, block, s.blocks, s.publish != 0);
+    run_chunks<2, 1, false>(s.tab, s.chunks, s.c0, s.c1, s.hp, s.step, block, s.blocks, s.publish != 0);
 }
 
 }  // namespace optdev

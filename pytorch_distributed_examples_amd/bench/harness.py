@@ -160,6 +160,7 @@ def build_data_parallel(args, ctx, batch) -> Workload:
 
     dev = ctx.device
     on_gpu = dev.type == "cuda"
+    torch.manual_seed(0)  # reproducible random init (the same weights on every rank before the broadcast)
     if args.model in ("cnn", "mlp"):
         from ..data.synthetic import SyntheticMNIST
 
@@ -423,6 +424,12 @@ def build_hvd_cnn(args, ctx, batch) -> Workload:
     return w
 
 
+# Why the default GPU pipeline unit is the whole step (scripts/pipeline_units.py, profiles/r4g_pipeline_units.md):
+# stage kernels are latency-bound at the reference's micro-batch, so fewer, larger units win despite no overlap.
+UNIT_CHOICE = ("measured best of --mb-group 1/2/4 (predicted 2-GPU img/s 3942 / 5344 / 5976, "
+               "profiles/r4g_pipeline_units.md); with one unit per step the two stages do not overlap")
+
+
 def build_pipeline(args, ctx, batch) -> Workload:
     """ResNet-50 split in 2 stages (one GPU each) x world/2 data-parallel replicas of each stage
     (:class:`..apps.hybrid_ps.ResNetPipelineDP`); the whole pipelined step is one hipGraph per rank."""
@@ -442,7 +449,8 @@ def build_pipeline(args, ctx, batch) -> Workload:
     w = Workload(step, pipe.images_per_step, f"pp{pipe.stages}xdp{pipe.dp}", hipgraph=one is not None,
                  fused_step=False, rccl_nranks=nranks, steps_per_graph=1 if one is not None else 0,
                  split_size=args.split_size, microbatches=batch // args.split_size, mb_per_unit=pipe.mb_group,
-                 pipeline_units=pipe.n_mb, schedule=args.schedule)
+                 pipeline_units=pipe.n_mb, schedule=args.schedule, cross_stage_overlap=pipe.n_mb > 1,
+                 unit_choice=UNIT_CHOICE)
     w.loss_rank = pipe.stages - 1
     w.close = pipe.close
     w.check = pipe.check
@@ -485,7 +493,9 @@ def _secondary_pipeline(ctx, timeout_s: float = 420.0):
                           warmup=rec["warmup"], vs_baseline=rec["vs_baseline"],
                           parallelism=rec["config"]["parallelism"], hipgraph=rec["config"]["hipgraph"],
                           global_batch=rec["config"]["global_batch"], final_loss=rec["config"]["final_loss"],
-                          split_size=rec["config"].get("split_size"), mb_per_unit=rec["config"].get("mb_per_unit"))
+                          split_size=rec["config"].get("split_size"), mb_per_unit=rec["config"].get("mb_per_unit"),
+                          cross_stage_overlap=rec["config"].get("cross_stage_overlap"),
+                          unit_choice=rec["config"].get("unit_choice"))
     except subprocess.TimeoutExpired:
         result["error"] = f"timeout after {timeout_s:.0f} s"
     except Exception as exc:  # noqa: BLE001 - never let the secondary measurement cost the headline

@@ -96,10 +96,17 @@ class DistributedDataParallel(nn.Module):
         # param_order="forward" lays the flat gradient out in registration order instead, so a fused
         # whole-model kernel that produces all gradients at once can write it directly.
         order = list(reversed(self._params)) if param_order == "reverse" else list(self._params)
-        sizes = [p.numel() * (2 if grad_dtype == torch.bfloat16 else 4) for p in order]
+        # Every gradient view starts on a 256-byte boundary (64 fp32), so the kernels that read or write it (the
+        # fused optimiser, GEMM epilogues) take their 16-byte vector paths: one odd-sized tensor early in the
+        # layout (a 10-wide bias) would otherwise misalign every view after it -- the MLP's Adam ran its scalar
+        # path on all 5M parameters (r4n: 52 us).  The "forward" layout stays dense: it IS the fused CNN kernel's
+        # flat parameter order.  Padding elements are never written (zero) and ride along in the all-reduce.
+        align = 64 if param_order == "reverse" else 1
+        padded = [-(-p.numel() // align) * align for p in order]
+        sizes = [n * (2 if grad_dtype == torch.bfloat16 else 4) for n in padded]
         cap = int(bucket_cap_mb * 2 ** 20) if bucket_cap_mb else None
         plan = xgmi.plan_buckets(sizes, self.world, cap)
-        total = sum(p.numel() for p in order)
+        total = sum(padded)
         self.flat_grad = torch.zeros(total, dtype=torch.float32, device=dev)
         self._views = {}
         self._bucket_of = {}
@@ -112,7 +119,7 @@ class DistributedDataParallel(nn.Module):
                 n = p.numel()
                 self._views[p] = self.flat_grad[off:off + n].view_as(p)
                 self._bucket_of[p] = bi
-                off += n
+                off += padded[i]
             self._bucket_ranges.append((start, off))
         self._bucket_sizes = [len(idxs) for idxs in plan]
         for p in self._params:

@@ -81,7 +81,12 @@ def test_folded_bottleneck_matches_fp32_reference(gpu):
     g = copy.deepcopy(blk).to(gpu)  # (before the reference forward updates blk's running statistics)
     with OF.emulate_bf16_on_cpu():
         ref = blk(x)
-    out = g(x.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(gpu))
+    prev = OF._BN_FOLD[0]
+    OF._BN_FOLD[0] = True  # the fold is opt-in (PDE_BN_FOLD=1)
+    try:
+        out = g(x.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(gpu))
+    finally:
+        OF._BN_FOLD[0] = prev
     assert any(any(v) for v in g._pde_fold_plan.values()), g._pde_fold_plan
     assert rel_err(out.float().permute(0, 3, 1, 2).cpu(), ref) < 3e-2
     for n in ("bn1", "bn2"):
