@@ -40,6 +40,14 @@ constexpr int NW = T / 64;
 constexpr int NI = 4;             // images per workgroup
 constexpr int C1 = 10, C2 = 20, KS = 5, H0 = 28, O1 = 24, P1 = 12, O2 = 8, P2 = 4, F1 = 50, F2 = 10;
 constexpr int NX = H0 * H0, NC1 = P1 * P1, NR1 = C1 * NC1, NC2 = P2 * P2, NIN = C2 * NC2;  // 784 144 1440 16 320
+// LDS channel pitches of the [ci][cell] planes (r1 / dr1 in u16, a1 in bytes): 144 cells padded so that the
+// channels a wave touches at once fall in different banks (ds_*_b32 banks are (a / 4) mod 32; at a 288-byte
+// pitch channels 0, 4, 8 share one: P1's stores and P9's reads ran 3-6 LDS cycles per instruction, r4s)
+constexpr int RP16 = 146, RP8 = 148;
+// LDS row pitch of the images x / x1 (28 pixels + 8 zero columns): with x1 9 banks after x, P1's pixel-pair
+// gathers take 2.75 LDS cycles per instruction instead of 4 (r4t model; columns 28.. are read by the zero-weight
+// kx = 5 taps only)
+constexpr int XP = 36, NXP = H0 * XP;
 constexpr int W1N = C1 * KS * KS, W2N = C2 * C1 * KS * KS, FC1N = F1 * NIN, FC2N = F2 * F1;
 constexpr int K2 = C1 * KS * KS;       // 250: conv2 reduction (ci,ky,kx) in the weight's own order
 // conv2 fwd: K ordered (tap, ci) with ci padded to 16 over a channel-last copy of r1, so a lane's 8
@@ -99,11 +107,13 @@ struct CnnSmem {
   alignas(16) uint16_t d2[NI][C2][D2R];    // rows padded to 144 B: the 16 co rows of a wgrad A fragment hit
                                            // 16 distinct 16-B bank groups (128-B rows: 4-8-way conflicts)
   alignas(16) uint16_t zero16[8];      // 16 zero bytes: the target of every out-of-range operand read
-  uint16_t x[NI][NX];                  // images
-  uint16_t x1[NI][NX];                 // images shifted by one element (x1[i] = x[i + 1]): every pair of
+  uint16_t x[NI][NXP];                 // images, rows of XP (columns 28.. zero)
+  uint16_t xpad[18];                   // x1 starts 9 banks after x: P1 / P9 pixel-pair reads of x and x1 by
+                                       // the same instruction no longer collide (8064-byte arrays)
+  uint16_t x1[NI][NXP];                 // images shifted by one element (x1[i] = x[i + 1]): every pair of
                                        // consecutive pixels is ONE aligned 4-byte LDS read from x or x1
-  uint16_t r1[NI][NR1];                // relu(maxpool(conv1)), [ci][cell]
-  uint16_t dr1[NI][NR1];               // grad at r1 (relu'-masked) == conv1-output grad at argmax taps
+  uint16_t r1[NI][C1 * RP16];          // relu(maxpool(conv1)), [ci][cell] (pitch RP16)
+  uint16_t dr1[NI][C1 * RP16];               // grad at r1 (relu'-masked) == conv1-output grad at argmax taps
   // fp32 head
   alignas(16) float b1[C1];
   alignas(16) float b2[C2];
@@ -117,7 +127,7 @@ struct CnnSmem {
   float logit[NI][F2], dlog[NI][F2];
   float valid[NI];
   int label[NI];
-  unsigned char a1[NI][NR1];
+  unsigned char a1[NI][C1 * RP8];
   unsigned char a2[NI][NIN];
 };
 static_assert(sizeof(CnnSmem) <= 160 * 1024, "LDS budget");
@@ -214,7 +224,10 @@ __device__ __forceinline__ void out_st4(float* p, f32x4 v) {
   else *reinterpret_cast<f32x4*>(p) = v;
 }
 
-template <int SM>
+// BREG: P7b's B operand (the conv2 data-gradient fragments, identical for every wave) is loaded from the
+// fragment image into registers at the start of P7a instead of being staged in LDS -- a quarter of P7b's LDS
+// traffic moves to the vector-memory path (L1 / L2 hits), which runs beside the LDS.
+template <int SM, bool BREG>
 __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ images, const int64_t* __restrict__ tgt,
                                                  int B, const float* __restrict__ params,
                                                  const u16x8* __restrict__ frag,
@@ -241,36 +254,43 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   const float* gFC1B = params + O_FC1B;
   // xmap: workgroups that share an XCD (blockIdx % 8 under the observed round-robin placement) take
   // consecutive images, so the 8 workgroups writing one 128-B line of an activation row sit behind one L2
-  const int lwg = xmap ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  const int lwg = (xmap & 1) ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   const int n0 = lwg * NI;
 
   // ---- P0: images -> bf16, weights -> bf16 MFMA fragments, fp32 head weights, dropout masks ------
-  // every global load of the phase is issued first (unconditional, clamped addresses): the conv weight
-  // fragments (3 x 16 B per thread), then the image quad.  Only conv1's fragment (w1f) is stored to LDS now;
-  // conv2's forward / dgrad fragments stay in registers until the end of P1, so their latency is not on P0's
-  // critical path.
-  // (vmcnt retires loads in issue order: the loads P0 itself consumes -- images, the third fragment slot that
-  // holds w1f, the head parameters -- are issued before the two deferred fragment slots, at the end of P0)
+  // every global load of the phase is issued first (unconditional, clamped addresses): conv1's fragment (w1f),
+  // then the image quad.  Only w1f is stored to LDS now; conv2's forward fragments (w2f) are requested at the
+  // end of P0 and stored at the end of P1, its data-gradient fragments (w2d) are requested in P4 and stored at
+  // the end of P6 -- their latency is on no phase's critical path, and the burst of fragment reads every
+  // workgroup makes at the start is 28 KB instead of 47 KB.
+  // (vmcnt retires loads in issue order: the loads P0 itself consumes -- w1f, images, the head parameters --
+  // are issued before the deferred fragment loads)
   static_assert(NI * NX / 4 <= T, "one image quad per thread");
   const int qi = min(t, NI * NX / 4 - 1);
   const int qim = (qi * 4) / NX, qoff = qi * 4 - qim * NX;
-  constexpr int FPER = (NFRAG + T - 1) / T;
-  static_assert(FPER == 3 && NFRAG - 64 >= 2 * T, "w1f (the last 64 fragments) lies in the third slot");
-  u16x8 fr[FPER];
-  fr[2] = frag[min(t + 2 * T, NFRAG - 1)];
+  constexpr int NF2F = KS2 * 2 * 64, NF2D = KSD * 64;  // fragment image: [w2f | w2d | w1f]
+  static_assert(NF2F <= 2 * T && NF2D <= 2 * T && NF2F + NF2D + 64 == NFRAG, "fragment slots");
+  u16x8 fr[2];
+  const u16x8 fw1 = frag[NF2F + NF2D + (t & 63)];
   f32x4 img = *reinterpret_cast<const f32x4*>(images + static_cast<long>(min(n0 + qim, B - 1)) * NX + qoff);
   if (t < NI * NX / 4) {
     const int im = qim, off = qoff, n = n0 + im;
     const f32x4 v = n < B ? img : f32x4{0.f, 0.f, 0.f, 0.f};
-    uint16_t* dst = &S.x[im][off];
+    const int row = off / H0, col = off - row * H0;  // a quad never crosses a row (H0 % 4 == 0)
+    uint16_t* dst = &S.x[im][row * XP + col];
     const uint16_t b0 = f2bf(v[0]), b1 = f2bf(v[1]), b2 = f2bf(v[2]), b3 = f2bf(v[3]);
     dst[0] = b0; dst[1] = b1; dst[2] = b2; dst[3] = b3;
-    uint16_t* d1 = &S.x1[im][off];
-    if (off > 0) d1[-1] = b0;
+    uint16_t* d1 = &S.x1[im][row * XP + col];
+    if (col > 0) d1[-1] = b0;
     d1[0] = b1; d1[1] = b2; d1[2] = b3;
   }
-  if (t < NI) S.x1[t][NX - 1] = 0;
-  if (t + 2 * T < NFRAG) (&S.w2f[0][0][0])[t + 2 * T] = fr[2];  // the third slot: w2d tail and w1f (conv1)
+  static_assert(H0 % 4 == 0 && XP >= H0 + 6, "image quads within a row; kx = 5 reads stay in the row");
+  for (int i = t; i < NI * H0 * (XP - H0 + 1); i += T) {  // zero columns: x 28.., x1 27..
+    const int r = i / (XP - H0 + 1), c = i - r * (XP - H0 + 1);
+    if (c > 0) (&S.x[0][0])[r * XP + H0 - 1 + c] = 0;
+    (&S.x1[0][0])[r * XP + H0 - 1 + c] = 0;
+  }
+  if (t < 64) S.w1f[t] = fw1;
   constexpr int PADG = (C2P - 16) / 8;  // co padding groups of 8 (co 16..C2P-1; 16..19 rewritten per step)
   for (int i = t; i < NI * O2 * O2 * PADG; i += T) {
     const int pos = i / PADG, h = i - pos * PADG;
@@ -299,8 +319,8 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     S.label[im] = ok ? static_cast<int>(tgt[n0 + im]) : 0;
   }
   float* slab = slabs + static_cast<long>(blockIdx.x) * NSLAB;
-  fr[0] = frag[t];  // conv2 fragment slots 0 / 1: stored to LDS at the end of P1
-  fr[1] = frag[t + T];
+  fr[0] = frag[t];  // conv2 forward fragments: stored to LDS at the end of P1
+  fr[1] = frag[min(t + T, NF2F - 1)];
   lds_sync();
   PDE_STAMP(1);
 
@@ -314,7 +334,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int k = lg * 8 + 2 * p;
-      koff[p] = k < KS * 6 ? (k / 6) * H0 + (k % 6) : 0;
+      koff[p] = k < KS * 6 ? (k / 6) * XP + (k % 6) : 0;
       kmsk[p] = k < KS * 6 ? 0xFFFFFFFFu : 0u;
     }
     const u16x8 bw = S.w1f[lane];
@@ -323,7 +343,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     auto gather = [&](int tile, u16x8& a) {
       const int im = tile / MT1, c0 = (tile - im * MT1) * 4;
       const int cell = c0 + (lr >> 2), py = cell / P1, px = cell - py * P1;
-      const uint16_t* xb = xsrc + im * NX + (2 * py + dy) * H0 + 2 * px + dx;
+      const uint16_t* xb = xsrc + im * NXP + (2 * py + dy) * XP + 2 * px + dx;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const uint32_t v = *reinterpret_cast<const uint32_t*>(xb + koff[p]) & kmsk[p];
@@ -332,13 +352,21 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       }
     };
     static_assert((NI * MT1) % NW == 0, "every wave runs the same number of conv1 tiles");
-    u16x8 an;
-    gather(wid, an);
-    for (int tile = wid; tile < NI * MT1; tile += NW) {
-      const u16x8 a = an;
-      if (tile + NW < NI * MT1) gather(tile + NW, an);  // next tile's gathers overlap this tile's MFMA + epilogue
+    constexpr int NT1 = NI * MT1 / NW;  // 9 tiles per wave
+    // all of the wave's gathers first, then its MFMAs, then the epilogues: no tile waits on another's LDS
+    // round trip (a one-tile-ahead pipeline measured 3.0 us for this loop, r4p)
+    u16x8 ag[NT1];
+#pragma unroll
+    for (int u = 0; u < NT1; ++u) gather(wid + u * NW, ag[u]);
+    f32x4 accs[NT1];
+#pragma unroll
+    for (int u = 0; u < NT1; ++u) accs[u] = mfma(ag[u], bw, f32x4{0.f, 0.f, 0.f, 0.f});
+    const float bias1 = lr < C1 ? S.b1[lr] : 0.f;
+#pragma unroll
+    for (int u = 0; u < NT1; ++u) {
+      const int tile = wid + u * NW;
       const int im = tile / MT1, c0 = (tile - im * MT1) * 4;
-      const f32x4 acc = mfma(a, bw, f32x4{0.f, 0.f, 0.f, 0.f});
+      const f32x4 acc = accs[u];
       const int co = lr;  // rows (lg*4 + r) = taps r of cell c0 + lg
       if (co < C1) {
         int am = 0;
@@ -346,20 +374,23 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
         if (acc[1] > m) { m = acc[1]; am = 1; }
         if (acc[2] > m) { m = acc[2]; am = 2; }
         if (acc[3] > m) { m = acc[3]; am = 3; }
-        const int q = co * NC1 + c0 + lg;
-        const uint16_t r = f2bf(fmaxf(m + S.b1[co], 0.f));
-        S.r1[im][q] = r;
+        const uint16_t r = f2bf(fmaxf(m + bias1, 0.f));
+        S.r1[im][co * RP16 + c0 + lg] = r;
         S.r1n[im][c0 + lg][co] = r;
-        S.a1[im][q] = static_cast<unsigned char>(am);
+        S.a1[im][co * RP8 + c0 + lg] = static_cast<unsigned char>(am);
       } else {
         S.r1n[im][c0 + lg][co] = 0;  // ci padding 10..15
       }
     }
   }
-  {  // conv2 forward / dgrad fragments (loaded in P0): pre-laid-out bf16 MFMA order, straight 16-byte stores
+  if (stamps != nullptr) {  // diagnostic: conv1 done (this wave), before the fragment stores wait for P0's loads
+    if (t == 0) stamps[blockIdx.x * 16 + 13] = wall_clock64();
+  }
+  if (!(xmap & 2)) {  // conv2 forward fragments (loaded in P0): bf16 MFMA order, straight 16-byte stores
+    // (xmap & 2: timing diagnostic, the stores and their wait skipped -- results invalid)
     u16x8* dst = &S.w2f[0][0][0];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) dst[t + u * T] = fr[u];
+    dst[t] = fr[0];
+    if (t + T < NF2F) dst[t + T] = fr[1];
   }
   lds_sync();
   PDE_STAMP(2);
@@ -456,6 +487,12 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     const int jc = tc / NIN, i = tc - jc * NIN;
 #pragma unroll
     for (int u = 0; u < JPER; ++u) w6[u] = gFC1W[min(jc * JPER + u, F1 - 1) * NIN + i];
+  }
+  // conv2 data-gradient fragments for P7b: stored to LDS at the end of P6 (the w2d region is idle until then)
+  u16x8 fd[2];
+  if constexpr (!BREG) {
+    fd[0] = frag[NF2F + t];
+    fd[1] = frag[NF2F + min(t + T, NF2D - 1)];
   }
 
   // ---- P4: fc2 logits, then log_softmax + NLL + dlogits per image ---------------------------------
@@ -578,8 +615,22 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       for (int c = 0; c < NC2; ++c) s += S.dp2[im][co * NC2 + c];
     out_st<SM>(&slab[O_B2 + co], s);
   }
+  if constexpr (!BREG) {
+    u16x8* dst = &S.w2d[0][0];
+    dst[t] = fd[0];
+    if (t + T < NF2D) dst[t + T] = fd[1];
+  }
   lds_sync();
   PDE_STAMP(8);
+  // BREG: the first KSB k-steps' B fragments of P7b requested now, ahead of P7a's slab stores (vmcnt retires
+  // in issue order, so waiting for them never waits for those stores); P7b's k-step ks requests k-step
+  // ks + KSB (all 19 held at once: 76 VGPRs, spills)
+  constexpr int KSB = 8;
+  u16x8 bd[BREG ? KSD : 1];
+  if constexpr (BREG) {
+#pragma unroll
+    for (int ks = 0; ks < KSB; ++ks) bd[ks] = frag[NF2F + ks * 64 + lane];
+  }
 
   // ---- P7a: conv2 wgrad (MFMA): dW2[co][(ci,ky,kx)] = sum_(im,y,x) d2[co][y][x] * r1[ci][y+ky][x+kx].
   // M = co (2 tiles), N = 250 -> 16 tiles (NT2 per wave), K = (im, y, x) 256 = 8 k-steps.  An A fragment
@@ -593,7 +644,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     for (int u = 0; u < NT2; ++u) {
       const int kidx = (wid * NT2 + u) * 16 + lr, ci = kidx / 25, r = kidx - ci * 25, ky = r / 5, kx = r - ky * 5;
       nv[u] = kidx < K2;
-      nb[u] = nv[u] ? ci * NC1 + ky * P1 + kx : 0;
+      nb[u] = nv[u] ? ci * RP16 + ky * P1 + kx : 0;
     }
     f32x4 acc[2][NT2];
 #pragma unroll
@@ -643,6 +694,8 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     for (int u = 0; u < MAXT; ++u) {
       acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int tile = min(wid + u * NW, NI * MTD - 1);  // a 2-tile wave's third slot mirrors a real tile
+      // (4x4-block tiles model fewer bank conflicts, 6.8 -> 6.0 LDS cycles per A read, but measured slower:
+      // P7b 5.76 -> 5.96 us, r4t)
       const int im = tile / MTD, pos = (tile % MTD) * 16 + lr;
       ty[u] = pos / P1;
       tx[u] = pos - ty[u] * P1;
@@ -651,10 +704,12 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     const uint16_t* base = &S.d2n[0][0][0];
     const int zoff = static_cast<int>(&S.zero16[0] - base);
     const int ntile = wid < NI * MTD - 2 * NW ? 3 : 2;  // wave-uniform (36 tiles over 16 waves)
+
     auto load = [&](int ks, u16x8 (&a)[MAXT], u16x8& b) {
       const int g = ks * 4 + lg, tap = g / CG, cg = g - tap * CG, ky = tap / KS, kx = tap - ky * KS;
       const int tofs = -(ky * O2 + kx) * C2P + cg * 8;
-      b = S.w2d[ks][lane];
+      if constexpr (BREG) b = bd[ks];
+      else b = S.w2d[ks][lane];
 #pragma unroll
       for (int u = 0; u < MAXT; ++u) {
         const bool ok = g < NGD && static_cast<unsigned>(ty[u] - ky) < O2 && static_cast<unsigned>(tx[u] - kx) < O2;
@@ -668,6 +723,9 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       u16x8 ac[MAXT], bc = bn;
 #pragma unroll
       for (int u = 0; u < MAXT; ++u) ac[u] = an[u];
+      if constexpr (BREG) {
+        if (ks + KSB < KSD) bd[ks + KSB] = frag[NF2F + (ks + KSB) * 64 + lane];
+      }
       if (ks + 1 < KSD) load(ks + 1, an, bn);
       acc[0] = mfma(ac[0], bc, acc[0]);
       acc[1] = mfma(ac[1], bc, acc[1]);
@@ -681,7 +739,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
         const int im = tile / MTD;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int q = ci * NC1 + (tile % MTD) * 16 + lg * 4 + r;
+          const int q = ci * RP16 + (tile % MTD) * 16 + lg * 4 + r;
           S.dr1[im][q] = S.r1[im][q] != 0 ? f2bf(acc[u][r]) : 0;  // r1 is relu'd: r1 == 0 <=> dead
         }
       }
@@ -701,33 +759,41 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     for (int u = 0; u < 2; ++u) {
       const int kidx = u * 16 + lr;
       nv[u] = kidx < 25;
-      nb[u] = nv[u] ? (kidx / 5) * H0 + kidx % 5 : 0;
+      nb[u] = nv[u] ? (kidx / 5) * XP + kidx % 5 : 0;
       xw[u] = (nv[u] && ((kidx % 5) & 1)) ? &S.x1[0][0] - 1 : &S.x[0][0];
     }
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     const int co = lr;
-    for (int ks = wid; ks < NI * KSW1; ks += NW) {
+    // a fixed trip count (72 k-steps over 16 waves: 5 slots, the last one live on 8 waves): every slot's LDS
+    // reads are issued before the first MFMA (a data-dependent loop ran them one k-step at a time)
+    constexpr int NK9 = (NI * KSW1 + NW - 1) / NW;
+    u16x8 a9[NK9], b9[NK9][2];
+#pragma unroll
+    for (int u9 = 0; u9 < NK9; ++u9) {
+      const int ksr = wid + u9 * NW;
+      const bool kv = ksr < NI * KSW1;  // wave-uniform
+      const int ks = kv ? ksr : 0;
       const int im = ks / KSW1, p0 = (ks - im * KSW1) * 32 + lg * 8;
       const int y = p0 / O1, x0 = p0 - y * O1;  // 8 positions: row y, x0..x0+7 (x0 % 8 == 0)
       u16x8 a = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (co < C1) {
-        const int cbase = co * NC1 + (y >> 1) * P1 + (x0 >> 1);
+      if (co < C1 && kv) {
+        const int cell = (y >> 1) * P1 + (x0 >> 1);
         const int ty = (y & 1) * 2;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const int q = cbase + c;
-          const int am = S.a1[im][q];
-          const uint16_t g = S.dr1[im][q];
+          const int am = S.a1[im][co * RP8 + cell + c];
+          const uint16_t g = S.dr1[im][co * RP16 + cell + c];
           a[2 * c] = am == ty ? g : 0;
           a[2 * c + 1] = am == ty + 1 ? g : 0;
         }
       }
+      a9[u9] = a;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        // 8 consecutive pixels from offset nb + y H0 + x0 (x0 % 8 == 0): four aligned 4-byte reads of x (kx
+        // 8 consecutive pixels from offset nb + y XP + x0 (x0 % 8 == 0): four aligned 4-byte reads of x (kx
         // even) or of the shifted copy x1 (kx odd) -- never one 16-byte read at a 2-byte-aligned address,
         // which the LDS would replay as an unaligned access
-        const uint16_t* src = xw[u] + im * NX + nb[u] + y * H0 + x0;
+        const uint16_t* src = xw[u] + im * NXP + nb[u] + y * XP + x0;
         u16x8 b;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
@@ -735,9 +801,13 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
           b[2 * p] = static_cast<uint16_t>(v);
           b[2 * p + 1] = static_cast<uint16_t>(v >> 16);
         }
-        acc[u] = mfma(a, b, acc[u]);
+        b9[u9][u] = b;
       }
     }
+#pragma unroll
+    for (int u9 = 0; u9 < NK9; ++u9)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) acc[u] = mfma(a9[u9], b9[u9][u], acc[u]);  // a slot past 72: a == 0
     lds_sync();  // w2f / w2d are dead after P7b: reuse them for the per-wave partials
     f32x4* part = reinterpret_cast<f32x4*>(&S.w2f[0][0][0]);
     part[(wid * 2 + 0) * 64 + lane] = acc[0];
@@ -754,7 +824,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       const int c = t - 256;
       float s = 0.f;
       for (int im = 0; im < NI; ++im)
-        for (int q = 0; q < NC1; ++q) s += bf2f(S.dr1[im][c * NC1 + q]);
+        for (int q = 0; q < NC1; ++q) s += bf2f(S.dr1[im][c * RP16 + q]);
       out_st<SM>(&slab[O_B1 + c], s);
     }
   }
@@ -1167,10 +1237,13 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
   // 0.0381 ms/step; non-temporal 0.0390).  PDE_CNN_XMAP=1: XCD-grouped images (r4k: level, off)
   static const int smode = std::getenv("PDE_CNN_STORE") ? std::atoi(std::getenv("PDE_CNN_STORE")) : 2;
   static const int xmap_env = std::getenv("PDE_CNN_XMAP") ? std::atoi(std::getenv("PDE_CNN_XMAP")) : 0;
-  const int xmap = xmap_env != 0 && nwg % 8 == 0 ? 1 : 0;
-  auto train = smode == 1 ? &k_cnn_train<1> : smode == 2 ? &k_cnn_train<2> : &k_cnn_train<0>;
-  static bool attr[3] = {false, false, false};
-  const int si = smode == 1 || smode == 2 ? smode : 0;
+  static const int diag_frag = std::getenv("PDE_CNN_DIAG_FRAG") ? 2 : 0;  // timing only: see k_cnn_train
+  const int xmap = (xmap_env != 0 && nwg % 8 == 0 ? 1 : 0) | diag_frag;
+  static const bool breg = std::getenv("PDE_CNN_BREG") != nullptr && std::getenv("PDE_CNN_BREG")[0] == '1';
+  auto train = breg ? (smode == 1 ? &k_cnn_train<1, true> : smode == 2 ? &k_cnn_train<2, true> : &k_cnn_train<0, true>)
+                    : (smode == 1 ? &k_cnn_train<1, false> : smode == 2 ? &k_cnn_train<2, false> : &k_cnn_train<0, false>);
+  static bool attr[6] = {false, false, false, false, false, false};
+  const int si = (smode == 1 || smode == 2 ? smode : 0) + (breg ? 3 : 0);
   if (!attr[si]) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(train), hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(sm));

@@ -27,6 +27,8 @@ names = ["P0 load", "P1 conv1", "P2 conv2", "P3 fc1", "P4a fc2", "P4b loss", "P5
          "P7a c2wgrad", "P7b c2dgrad", "P9 conv1wgrad"]
 for i, n in enumerate(names):
     print(f"{n:14s} median {d[:, i].median().item():7.2f} us  max {d[:, i].max().item():7.2f} us")
+print("P1 conv1 MFMA part (stamp 1 -> 13) median", ((st[:, 13] - st[:, 1]) / 100.0).median().item(), "us;",
+      "fragment wait + stores (13 -> 2)", ((st[:, 2] - st[:, 13]) / 100.0).median().item(), "us")
 print("total median", (st[:, 11] - st[:, 0]).median().item() / 100.0, "us")
 print("span (first start -> last stamp)", (st[:, 11].max() - st[:, 0].min()).item() / 100.0, "us")
 print("workgroup start spread (last - first stamp 0)", (st[:, 0].max() - st[:, 0].min()).item() / 100.0, "us")
