@@ -1123,7 +1123,7 @@ Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, 
   auto fo = images.options();
   Tensor slabs = at::empty({static_cast<long>(n) * pde::cnn_slab_floats()}, fo);
   Tensor part = at::empty({n}, fo);
-  Tensor acts = at::empty({static_cast<long>(pde::cnn_act_rows()) * n * ni}, fo);
+  Tensor acts = at::empty({static_cast<long>(pde::cnn_act_rows()) * pde::cnn_act_pitch(n)}, fo.dtype(at::kBFloat16));
   Tensor loss = at::empty({}, fo);
   Tensor frag;
   if (frag_buf.has_value() && frag_buf->defined()) {
@@ -1143,7 +1143,7 @@ Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, 
                              frag.data_ptr(),
                              reinterpret_cast<unsigned long long*>(rng.data_ptr()), static_cast<float>(p_drop2),
                              static_cast<float>(p_drop1), training ? 1 : 0, slabs.data_ptr<float>(),
-                             part.data_ptr<float>(), acts.data_ptr<float>(), n, loss.data_ptr<float>(), grads.data_ptr<float>(), cf32(gscale),
+                             part.data_ptr<float>(), reinterpret_cast<uint16_t*>(acts.data_ptr()), n, loss.data_ptr<float>(), grads.data_ptr<float>(), cf32(gscale),
                              accumulate ? 1 : 0, cur_stream(),
                              stamps.has_value() && stamps->defined()
                                  ? reinterpret_cast<unsigned long long*>(stamps->data_ptr())

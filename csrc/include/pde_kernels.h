@@ -275,7 +275,7 @@ hipError_t embbag_fwd(const float* w, const int64_t* idx, const int64_t* off, in
 // ---------------------------------------------------------------------------------------------
 // Fused MNIST-CNN training step (cnn_fused.hip): forward + NLL + backward of horovod/mnist_horovod.py's
 // Net per image in LDS.  params: flat fp32 in torch parameter order (cnn_num_params() floats).
-// slabs: nwg * cnn_slab_floats() floats; loss_part: nwg floats; acts: cnn_act_rows() x (nwg * 4) floats.
+// slabs: nwg * cnn_slab_floats() floats; loss_part: nwg floats; acts: cnn_act_rows() x cnn_act_pitch(nwg) bf16.
 // ---------------------------------------------------------------------------------------------
 int cnn_num_params();
 size_t cnn_smem_bytes();
@@ -291,9 +291,10 @@ size_t cnn_frag_bytes();  // workspace for the per-step bf16 weight-fragment ima
 // rank order (x xscale), so the update stays fused at any world size -- 2 launches per step.
 int cnn_slab_floats();  // per-workgroup slab (every gradient except fc1's weight)
 int cnn_act_rows();     // rows of the per-batch activation image feeding the fc1 weight-gradient GEMM
+int cnn_act_pitch(int nwg);  // its row pitch (bf16 elements)
 hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float* params, void* frag,
                            unsigned long long* rng, float p_drop2, float p_drop1, int training, float* slabs,
-                           float* loss_part, float* acts, int nwg, float* loss, float* grads, const float* gscale,
+                           float* loss_part, uint16_t* acts, int nwg, float* loss, float* grads, const float* gscale,
                            int accumulate, hipStream_t s, unsigned long long* stamps = nullptr, int prep = 1,
                            const float* sgd_hp = nullptr, int stop_after = -1, int* sgd_step = nullptr,
                            const XgmiView* xv = nullptr, float xscale = 1.f);

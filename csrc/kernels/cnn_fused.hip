@@ -80,6 +80,8 @@ constexpr int O_W1 = 0, O_B1 = O_W1 + W1N, O_W2 = O_B1 + C1, O_B2 = O_W2 + W2N, 
 constexpr int NSLAB = NPARAM - FC1N;                     // 5,840 slab floats per workgroup
 constexpr int S_FC1B = O_FC1B - FC1N, S_FC2W = O_FC2W - FC1N, S_FC2B = O_FC2B - FC1N;
 constexpr int NACT = F1 + NIN;                           // activation rows: dH^T (50) then R2^T (320)
+// row pitch (bf16 elements) of the activation image: the batch columns rounded up to 8 (16-byte operand loads)
+__host__ __device__ constexpr int act_pitch(int nwg) { return (nwg * NI + 7) & ~7; }
 static_assert(O_FC1W % 4 == 0 && FC1N % 4 == 0 && NSLAB % 4 == 0, "float4 slab columns");
 
 __device__ __forceinline__ float hash_u01(unsigned long long seed, unsigned long long id) {
@@ -177,7 +179,7 @@ struct CnnTail {
   int accumulate, B, on, pad;
 };
 __device__ void cnn_fused_tail(const CnnTail& tl, int rb, f32x4* part, uint32_t* s_epoch, int* s_fail,
-                               const float* slabs, int nwg, const float* acts, const float* loss_part);
+                               const float* slabs, int nwg, const uint16_t* acts, const float* loss_part);
 
 // Grid barrier over co-resident workgroups: every wave's global stores complete, one agent-scope release +
 // arrival per workgroup; the last arrival resets the counter and bumps the generation; the others poll it
@@ -218,6 +220,11 @@ __device__ __forceinline__ void out_st(float* p, float v) {
   else *p = v;
 }
 template <int SM>
+__device__ __forceinline__ void out_st_u16x4(uint16_t* p, u16x4 v) {
+  if constexpr (SM == 1) __builtin_nontemporal_store(v, reinterpret_cast<u16x4*>(p));
+  else st_vec(reinterpret_cast<u16x4*>(p), v, SM == 2);
+}
+template <int SM>
 __device__ __forceinline__ void out_st4(float* p, f32x4 v) {
   if constexpr (SM == 1) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
   else if constexpr (SM == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
@@ -233,7 +240,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
                                                  const u16x8* __restrict__ frag,
                                                  const unsigned long long* __restrict__ rng, float p_drop2,
                                                  float p_drop1, int training, float* __restrict__ slabs,
-                                                 float* __restrict__ loss_part, float* __restrict__ acts,
+                                                 float* __restrict__ loss_part, uint16_t* __restrict__ acts,
                                                  unsigned long long* __restrict__ stamps, int stop_after,
                                                  CnnTail tail, int xmap) {
   // optional phase timestamps (diagnostic only: stamps == nullptr in production launches); stop_after = k
@@ -553,15 +560,18 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   PDE_STAMP(7);
 
   // ---- P6: fc1 backward: dH / R2 columns for the batch-wide dW GEMM (k_cnn_reduce), db to the slab, and
-  // dp2 = grad at the pooled conv2 output.  Columns n0..n0+3 of the K-contiguous [row][Bk] image: one
-  // 16-byte store per row (rows 0..49 dH^T, 50..369 R2^T).
+  // dp2 = grad at the pooled conv2 output.  Columns n0..n0+3 of the K-contiguous bf16 [row][Bkp] image (the
+  // reduction's bf16 MFMA operands): one 8-byte store per row (rows 0..49 dH^T, 50..369 R2^T); the workgroup
+  // owning the last columns also zeroes the row padding up to Bkp (a multiple of 8).
   {
-    const int Bk = gridDim.x * NI;
+    const int Bk = gridDim.x * NI, Bkp = act_pitch(gridDim.x);
+    const bool pad = Bkp != Bk && n0 + NI == Bk;
     for (int row = t; row < NACT; row += T) {
-      f32x4 v;
+      u16x4 v;
 #pragma unroll
-      for (int im = 0; im < NI; ++im) v[im] = row < F1 ? S.dh[im][row] : S.r2[im][row - F1];
-      out_st4<SM>(acts + static_cast<long>(row) * Bk + n0, v);
+      for (int im = 0; im < NI; ++im) v[im] = f2bf(row < F1 ? S.dh[im][row] : S.r2[im][row - F1]);
+      out_st_u16x4<SM>(acts + static_cast<long>(row) * Bkp + n0, v);
+      if (pad) out_st_u16x4<SM>(acts + static_cast<long>(row) * Bkp + n0 + NI, u16x4{0, 0, 0, 0});
     }
   }
   if (t < F1) {
@@ -922,10 +932,11 @@ __global__ __launch_bounds__(256) void k_cnn_sgd(float* __restrict__ params, con
 //  * slab blocks (blockIdx < RED_SLAB_BLOCKS): 8 waves over 16 float4 slab columns; lane = column + 16 x
 //    slab-lane, so one load instruction of a wave reads 4 slabs x 256 B and each thread keeps nwg/32
 //    independent float4 loads in flight;
-//  * fc1 blocks: one 16 x 16 tile of dW_fc1[j][i] = sum_n dH[n][j] R2[n][i] on the f32 matrix cores
-//    (v_mfma_f32_16x16x4_f32, exact f32 products), the batch K split over the 8 waves, partials summed in
-//    wave order.  Lane (lr, lg) loads 16 B of row j (A) / row i (B) at k = kb + 4 lg: MFMA s of the chunk
-//    uses component s, the same k on both operands;
+//  * fc1 blocks: one 16 x 16 tile of dW_fc1[j][i] = sum_n dH[n][j] R2[n][i] on the bf16 matrix cores
+//    (16x16x32, fp32 accumulation; the operands are the bf16 activation columns, like every other weight
+//    gradient here -- fp32 columns with f32 MFMAs moved twice the bytes, r4u), the batch K split over the 8
+//    waves, partials summed in wave order.  Lane (lr, lg) loads 16 B (8 columns) of row j (A) / row i (B) at
+//    k = kb + 8 lg;
 //  * block 0 also reduces the per-workgroup loss partials and advances the dropout RNG counter.
 // With hp (single process, no all-reduce in between) every block also applies the SGD update to the
 // parameters it reduced and refreshes their bf16 fragment slots.
@@ -935,7 +946,7 @@ constexpr int RED_SLAB_BLOCKS = (NSLAB4 + RED_COLS - 1) / RED_COLS;
 constexpr int FC1_JT = (F1 + 15) / 16, FC1_IT = NIN / 16;   // 4 x 20 output tiles
 constexpr int RED_BLOCKS = RED_SLAB_BLOCKS + FC1_JT * FC1_IT;
 static_assert(NIN % 16 == 0, "fc1 input tiles");
-static_assert(NI == 4, "activation columns are written as one float4 per row");
+static_assert(NI == 4, "activation columns are written as one 8-byte bf16 quad per row");
 
 // w0 = params[p] and the hyper-parameters loaded at the start of the role (off the reduction's dependent chain)
 __device__ __forceinline__ void sgd_update(float* params, float lr, float gsc, uint16_t* frag, int p, float w0,
@@ -951,7 +962,7 @@ __device__ __forceinline__ void sgd_update(float* params, float lr, float gsc, u
 // (one role per block) and, single process, by k_cnn_train's workgroups after a grid barrier.
 __device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s_epoch, int* s_fail,
                                                 const float* __restrict__ slabs, int nwg,
-                                                const float* __restrict__ acts, const float* __restrict__ gscale,
+                                                const uint16_t* __restrict__ acts, const float* __restrict__ gscale,
                                                 float* __restrict__ grads, int accumulate,
                                                 const float* __restrict__ loss_part, int B, float* __restrict__ loss,
                                                 unsigned long long* __restrict__ rng, float* __restrict__ params,
@@ -1029,9 +1040,9 @@ __device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s
     const int fb = rb - RED_SLAB_BLOCKS;
     const int j0 = (fb / FC1_IT) * 16, i0 = (fb % FC1_IT) * 16;
     const int lane = tid & 63, wid = tid >> 6, lr = lane & 15, lg = lane >> 4;
-    const int Bk = nwg * NI;
-    const int kper = ((Bk + 8 * 16 - 1) / (8 * 16)) * 16;  // this wave's K slice, a multiple of 16
-    const int k0 = wid * kper, k1 = act ? min(Bk, k0 + kper) : k0;
+    const int Bkp = act_pitch(nwg);  // columns Bk.. are zero
+    const int kper = ((Bkp + 8 * 32 - 1) / (8 * 32)) * 32;  // this wave's K slice, a multiple of 32
+    const int k0 = wid * kper, k1 = act ? min(Bkp, k0 + kper) : k0;
     const bool jv = j0 + lr < F1;
     float w0[4] = {0.f, 0.f, 0.f, 0.f}, g0[4] = {0.f, 0.f, 0.f, 0.f};  // wave 0's outputs (j0 + 4 lg + r, i0 + lr)
     if (wid == 0 && act) {
@@ -1045,25 +1056,24 @@ __device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s
         }
       }
     }
-    const float* arow = acts + static_cast<long>(jv ? j0 + lr : 0) * Bk;
-    const float* brow = acts + static_cast<long>(F1 + i0 + lr) * Bk;
+    const uint16_t* arow = acts + static_cast<long>(jv ? j0 + lr : 0) * Bkp;
+    const uint16_t* brow = acts + static_cast<long>(F1 + i0 + lr) * Bkp;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-    constexpr int CH = 8;  // 16-deep chunks per pass: all 2 x CH loads in flight before the first MFMA
-    for (int kb = k0; kb < k1; kb += 16 * CH) {
-      f32x4 a[CH], b[CH];
+    constexpr int CH = 4;  // 32-deep chunks per pass: all 2 x CH loads in flight before the first MFMA
+    const u16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int kb = k0; kb < k1; kb += 32 * CH) {
+      u16x8 a[CH], b[CH];
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
-        const int k = kb + 16 * c + 4 * lg;
+        const int k = kb + 32 * c + 8 * lg;  // 8 whole columns: k and Bkp are multiples of 8
         const bool ok = k < k1;
-        a[c] = (ok && jv) ? *reinterpret_cast<const f32x4*>(arow + k) : f32x4{0.f, 0.f, 0.f, 0.f};
-        b[c] = ok ? *reinterpret_cast<const f32x4*>(brow + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+        a[c] = (ok && jv) ? *reinterpret_cast<const u16x8*>(arow + k) : z8;
+        b[c] = ok ? *reinterpret_cast<const u16x8*>(brow + k) : z8;
       }
 #pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][0], b[c][0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][1], b[c][1], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][2], b[c][2], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][3], b[c][3], acc1, 0, 0, 0);
+      for (int c = 0; c < CH; c += 2) {
+        acc0 = mfma(a[c], b[c], acc0);
+        acc1 = mfma(a[c + 1], b[c + 1], acc1);
       }
     }
     f32x4* wpart = part;
@@ -1133,7 +1143,7 @@ __device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s
 }
 
 __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ slabs, int nwg,
-                                                      const float* __restrict__ acts,
+                                                      const uint16_t* __restrict__ acts,
                                                       const float* __restrict__ gscale, float* __restrict__ grads,
                                                       int accumulate, const float* __restrict__ loss_part, int B,
                                                       float* __restrict__ loss, unsigned long long* __restrict__ rng,
@@ -1148,7 +1158,7 @@ __global__ __launch_bounds__(RED_T) void k_cnn_reduce(const float* __restrict__ 
 }
 
 __device__ void cnn_fused_tail(const CnnTail& tl, int rb, f32x4* part, uint32_t* s_epoch, int* s_fail,
-                               const float* slabs, int nwg, const float* acts, const float* loss_part) {
+                               const float* slabs, int nwg, const uint16_t* acts, const float* loss_part) {
   if (rb >= RED_BLOCKS) return;  // block-uniform: workgroups past the roles are done
   XgmiView one{};
   one.size = 1;
@@ -1214,10 +1224,11 @@ int cnn_images_per_workgroup() { return NI; }
 
 int cnn_slab_floats() { return NSLAB; }
 int cnn_act_rows() { return NACT; }
+int cnn_act_pitch(int nwg) { return act_pitch(nwg); }
 
 hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float* params, void* frag,
                            unsigned long long* rng, float p_drop2, float p_drop1, int training, float* slabs,
-                           float* loss_part, float* acts, int nwg, float* loss, float* grads, const float* gscale,
+                           float* loss_part, uint16_t* acts, int nwg, float* loss, float* grads, const float* gscale,
                            int accumulate, hipStream_t s, unsigned long long* stamps, int prep,
                            const float* sgd_hp, int stop_after, int* sgd_step, const XgmiView* xv,
                            float xscale) {
