@@ -62,6 +62,11 @@ def init_distributed(backend: str | None = None, device: str | None = None, time
         ndev = torch.cuda.device_count()
         dev = torch.device("cuda", local_rank % max(1, ndev))
         torch.cuda.set_device(dev)
+        if env_int("LOCAL_WORLD_SIZE", 1) > ndev:
+            # ranks share a GPU (rehearsals): the one-launch BatchNorm needs its whole grid co-resident, which
+            # another process's kernels on the same CUs can prevent (its bounded wait then reports a timeout,
+            # ops.functional.check_device_errors) -- use the multi-launch BatchNorm instead
+            os.environ.setdefault("PDE_BN_FUSED", "0")
     else:
         dev = torch.device("cpu")
     if backend == "gloo" and os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
