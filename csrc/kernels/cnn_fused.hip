@@ -78,6 +78,8 @@ constexpr int O_W1 = 0, O_B1 = O_W1 + W1N, O_W2 = O_B1 + C1, O_B2 = O_W2 + W2N, 
 // fc1 output gradients dH and inputs R2 (370 floats per image, K-contiguous) and k_cnn_reduce computes
 // it as one f32-MFMA GEMM -- 1.5 MB of activations instead of 16 MB of slabs written and read back.
 constexpr int NSLAB = NPARAM - FC1N;                     // 5,840 slab floats per workgroup
+// (the slab's conv2-weight block [O_W2, O_W2 + W2N) holds dW2 TRANSPOSED, [kidx][co]: 16-byte stores in P7a)
+static_assert(O_W2 % 4 == 0 && C2 % 4 == 0 && W2N % 4 == 0, "W2T: float4 columns of 4 co");
 constexpr int S_FC1B = O_FC1B - FC1N, S_FC2W = O_FC2W - FC1N, S_FC2B = O_FC2B - FC1N;
 constexpr int NACT = F1 + NIN;                           // activation rows: dH^T (50) then R2^T (320)
 // row pitch (bf16 elements) of the activation image: the batch columns rounded up to 8 (16-byte operand loads)
@@ -677,16 +679,15 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
         acc[1][u] = mfma(a[1], b, acc[1][u]);
       }
     }
+    // the slab's conv2-weight block is kept TRANSPOSED, [kidx][co] (see W2T): a lane's 4 accumulator rows are 4
+    // consecutive co of one kidx, so they leave as one 16-byte store (5000 dword stores per workgroup before;
+    // narrow write-through stores cost several times the bytes' time, MI355X_MICROARCH.md store rows)
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int u = 0; u < NT2; ++u) {
-        const int kidx = (wid * NT2 + u) * 16 + lr;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int co = mt * 16 + lg * 4 + r;
-          if (co < C2 && kidx < K2) out_st<SM>(&slab[O_W2 + co * K2 + kidx], acc[mt][u][r]);
-        }
+        const int kidx = (wid * NT2 + u) * 16 + lr, co0 = mt * 16 + lg * 4;
+        if (co0 < C2 && kidx < K2) out_st4<SM>(&slab[O_W2 + kidx * C2 + co0], acc[mt][u]);
       }
   }
   PDE_STAMP(9);
@@ -984,10 +985,27 @@ __device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s
     const f32x4* s4 = reinterpret_cast<const f32x4*>(slabs);
     f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
     const bool owner = act && sl == 0 && c4 < NSLAB4;
-    const int p4 = c4 < O_FC1W / 4 ? c4 : c4 + FC1N / 4;  // slab column -> parameter float4
+    // slab column -> parameter float4 (the xGMI staging index too); the conv2-weight block is transposed in
+    // the slab ([kidx][co], W2T): its columns hold 4 co of one kidx, parameters K2 apart
+    const int p4 = c4 < O_FC1W / 4 ? c4 : c4 + FC1N / 4;
+    const bool w2t = c4 >= O_W2 / 4 && c4 < (O_W2 + W2N) / 4;
+    int pj[4];
+    {
+      const int q = c4 - O_W2 / 4, kidx = q / (C2 / 4), co0 = (q - kidx * (C2 / 4)) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pj[j] = w2t ? O_W2 + (co0 + j) * K2 + kidx : p4 * 4 + j;
+    }
     f32x4 w0 = a0, g0 = a0;
-    if (owner && hp) w0 = reinterpret_cast<const f32x4*>(params)[p4];
-    if (owner && accumulate) g0 = reinterpret_cast<const f32x4*>(grads)[p4];
+    if (owner && w2t) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (hp) w0[j] = params[pj[j]];
+        if (accumulate) g0[j] = grads[pj[j]];
+      }
+    } else {
+      if (owner && hp) w0 = reinterpret_cast<const f32x4*>(params)[p4];
+      if (owner && accumulate) g0 = reinterpret_cast<const f32x4*>(grads)[p4];
+    }
     if (act && c4 < NSLAB4) {
       int b = sl;
       for (; b + 7 * RED_LANES < nwg; b += 8 * RED_LANES) {  // 8 independent loads in flight
@@ -1028,12 +1046,16 @@ __device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s
       xgmi_finish(xv, rb, epoch);
     }
     if (owner && ok) {
-      f32x4* g4 = reinterpret_cast<f32x4*>(grads) + p4;
       if (accumulate) v += g0;
-      *g4 = v;
+      if (w2t) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) grads[pj[j]] = v[j];
+      } else {
+        reinterpret_cast<f32x4*>(grads)[p4] = v;
+      }
       if (hp) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) sgd_update(params, lrate, gsc, frag, p4 * 4 + j, w0[j], v[j]);
+        for (int j = 0; j < 4; ++j) sgd_update(params, lrate, gsc, frag, pj[j], w0[j], v[j]);
       }
     }
   } else {
