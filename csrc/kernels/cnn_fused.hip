@@ -78,8 +78,12 @@ constexpr int O_W1 = 0, O_B1 = O_W1 + W1N, O_W2 = O_B1 + C1, O_B2 = O_W2 + W2N, 
 // fc1 output gradients dH and inputs R2 (370 floats per image, K-contiguous) and k_cnn_reduce computes
 // it as one f32-MFMA GEMM -- 1.5 MB of activations instead of 16 MB of slabs written and read back.
 constexpr int NSLAB = NPARAM - FC1N;                     // 5,840 slab floats per workgroup
-// (the slab's conv2-weight block [O_W2, O_W2 + W2N) holds dW2 TRANSPOSED, [kidx][co]: 16-byte stores in P7a)
+// (the slab's conv2-weight block [O_W2, O_W2 + W2N) holds dW2 as [co group of 4][kidx][4]: P7a's 16-byte
+// stores of 16 consecutive kidx are 256 contiguous bytes; SLAB_OFS puts that block on a 128-byte line boundary
+// and NSLABP pads each workgroup's slab to whole lines, so those stores are full-line writes)
 static_assert(O_W2 % 4 == 0 && C2 % 4 == 0 && W2N % 4 == 0, "W2T: float4 columns of 4 co");
+constexpr int SLAB_OFS = (32 - O_W2 % 32) % 32;                       // floats
+constexpr int NSLABP = (SLAB_OFS + NSLAB + 31) / 32 * 32;             // slab pitch per workgroup (floats)
 constexpr int S_FC1B = O_FC1B - FC1N, S_FC2W = O_FC2W - FC1N, S_FC2B = O_FC2B - FC1N;
 constexpr int NACT = F1 + NIN;                           // activation rows: dH^T (50) then R2^T (320)
 // row pitch (bf16 elements) of the activation image: the batch columns rounded up to 8 (16-byte operand loads)
@@ -327,7 +331,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     S.valid[im] = ok ? 1.f : 0.f;
     S.label[im] = ok ? static_cast<int>(tgt[n0 + im]) : 0;
   }
-  float* slab = slabs + static_cast<long>(blockIdx.x) * NSLAB;
+  float* slab = slabs + static_cast<long>(blockIdx.x) * NSLABP + SLAB_OFS;
   fr[0] = frag[t];  // conv2 forward fragments: stored to LDS at the end of P1
   fr[1] = frag[min(t + T, NF2F - 1)];
   lds_sync();
@@ -679,15 +683,16 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
         acc[1][u] = mfma(a[1], b, acc[1][u]);
       }
     }
-    // the slab's conv2-weight block is kept TRANSPOSED, [kidx][co] (see W2T): a lane's 4 accumulator rows are 4
-    // consecutive co of one kidx, so they leave as one 16-byte store (5000 dword stores per workgroup before;
-    // narrow write-through stores cost several times the bytes' time, MI355X_MICROARCH.md store rows)
+    // the slab's conv2-weight block is kept as [co group][kidx][4] (see SLAB_OFS): a lane's 4 accumulator rows
+    // are 4 consecutive co of one kidx, so they leave as one 16-byte store, and the 16 lanes of a co group write
+    // 256 contiguous bytes (5000 dword stores per workgroup before; narrow write-through stores cost several
+    // times the bytes' time, MI355X_MICROARCH.md store rows)
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int u = 0; u < NT2; ++u) {
-        const int kidx = (wid * NT2 + u) * 16 + lr, co0 = mt * 16 + lg * 4;
-        if (co0 < C2 && kidx < K2) out_st4<SM>(&slab[O_W2 + kidx * C2 + co0], acc[mt][u]);
+        const int kidx = (wid * NT2 + u) * 16 + lr, cg = mt * 4 + lg;
+        if (cg * 4 < C2 && kidx < K2) out_st4<SM>(&slab[O_W2 + (cg * K2 + kidx) * 4], acc[mt][u]);
       }
   }
   PDE_STAMP(9);
@@ -985,15 +990,15 @@ __device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s
     const f32x4* s4 = reinterpret_cast<const f32x4*>(slabs);
     f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
     const bool owner = act && sl == 0 && c4 < NSLAB4;
-    // slab column -> parameter float4 (the xGMI staging index too); the conv2-weight block is transposed in
-    // the slab ([kidx][co], W2T): its columns hold 4 co of one kidx, parameters K2 apart
+    // slab column -> parameter float4 (the xGMI staging index too); the conv2-weight block is [co group][kidx]
+    // [4] in the slab (SLAB_OFS): its columns hold 4 co of one kidx, parameters K2 apart
     const int p4 = c4 < O_FC1W / 4 ? c4 : c4 + FC1N / 4;
     const bool w2t = c4 >= O_W2 / 4 && c4 < (O_W2 + W2N) / 4;
     int pj[4];
     {
-      const int q = c4 - O_W2 / 4, kidx = q / (C2 / 4), co0 = (q - kidx * (C2 / 4)) * 4;
+      const int q = c4 - O_W2 / 4, cg = q / K2, kidx = q - cg * K2;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) pj[j] = w2t ? O_W2 + (co0 + j) * K2 + kidx : p4 * 4 + j;
+      for (int j = 0; j < 4; ++j) pj[j] = w2t ? O_W2 + (cg * 4 + j) * K2 + kidx : p4 * 4 + j;
     }
     f32x4 w0 = a0, g0 = a0;
     if (owner && w2t) {
@@ -1011,13 +1016,13 @@ __device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s
       for (; b + 7 * RED_LANES < nwg; b += 8 * RED_LANES) {  // 8 independent loads in flight
         f32x4 v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = s4[static_cast<long>(b + u * RED_LANES) * NSLAB4 + c4];
+        for (int u = 0; u < 8; ++u) v[u] = s4[static_cast<long>(b + u * RED_LANES) * (NSLABP / 4) + SLAB_OFS / 4 + c4];
         a0 += v[0] + v[4];
         a1 += v[1] + v[5];
         a2 += v[2] + v[6];
         a3 += v[3] + v[7];
       }
-      for (; b < nwg; b += RED_LANES) a0 += s4[static_cast<long>(b) * NSLAB4 + c4];
+      for (; b < nwg; b += RED_LANES) a0 += s4[static_cast<long>(b) * (NSLABP / 4) + SLAB_OFS / 4 + c4];
     }
     if (act) part[sl * RED_COLS + col] = (a0 + a1) + (a2 + a3);
     __syncthreads();
@@ -1244,7 +1249,7 @@ size_t cnn_frag_bytes() { return sizeof(u16x8) * NFRAG; }
 size_t cnn_smem_bytes() { return sizeof(CnnSmem); }
 int cnn_images_per_workgroup() { return NI; }
 
-int cnn_slab_floats() { return NSLAB; }
+int cnn_slab_floats() { return NSLABP; }  // per workgroup, padded (SLAB_OFS)
 int cnn_act_rows() { return NACT; }
 int cnn_act_pitch(int nwg) { return act_pitch(nwg); }
 
