@@ -23,7 +23,6 @@ Commits are device-resident clones (one D2D copy per tensor, 288 GB of HBM leave
 """
 from __future__ import annotations
 
-import copy
 import datetime
 import os
 import time
@@ -33,6 +32,7 @@ import torch.distributed as dist
 
 from .. import _native
 from . import fault
+from ..utils.state import clone_state as _clone
 from .rendezvous import RendezvousClient
 
 
@@ -326,16 +326,6 @@ class RoundComm:
                 dist.destroy_process_group()
         except Exception:  # noqa: BLE001 - a group with a dead member may fail to tear down cleanly
             pass
-
-
-def _clone(obj):
-    if torch.is_tensor(obj):
-        return obj.detach().clone()
-    if isinstance(obj, dict):
-        return type(obj)((k, _clone(v)) for k, v in obj.items())
-    if isinstance(obj, (list, tuple)):
-        return type(obj)(_clone(v) for v in obj)
-    return copy.deepcopy(obj)
 
 
 def _to_cpu(obj):

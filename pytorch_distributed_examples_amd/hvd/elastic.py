@@ -21,18 +21,9 @@ import functools
 import torch
 
 from . import core
+from ..utils.state import clone_state as _clone
 from .exceptions import HorovodInternalError, HostsUpdatedInterrupt
 from .functions import broadcast_optimizer_state, broadcast_parameters
-
-
-def _clone(obj):
-    if torch.is_tensor(obj):
-        return obj.detach().clone()
-    if isinstance(obj, dict):
-        return type(obj)((k, _clone(v)) for k, v in obj.items())
-    if isinstance(obj, (list, tuple)):
-        return type(obj)(_clone(v) for v in obj)
-    return copy.deepcopy(obj)
 
 
 class State:

@@ -19,6 +19,8 @@ executor thread.
 """
 from __future__ import annotations
 
+import threading
+
 import torch
 import torch.distributed.rpc as rpc
 
@@ -36,6 +38,30 @@ def _ring_slot_bytes() -> int:
     return int(float(os.environ.get("PDE_P2P_SLOT_MB", "4")) * (1 << 20))
 
 
+def _ring_ordered_submit(srv, caller: str, idx: int, fn) -> torch.futures.Future:
+    """Run ``fn`` on the owner's executor in ring-message order for ``caller``: ``idx`` is the caller's index
+    of the ring message ``fn`` receives.  The caller sends its gradient messages in autograd order but their
+    RPCs may be delivered out of order by the agent's thread pool (several remote calls per context), and a
+    receive must take the message that belongs to its call -- so receives are queued by index, not arrival."""
+    out = torch.futures.Future()
+    lock = srv.__dict__.setdefault("_ring_lock", threading.Lock())
+    with lock:
+        st = srv.__dict__.setdefault("_ring_order", {}).setdefault(caller, {"next": 0, "pending": {}})
+        st["pending"][idx] = (fn, out)
+        while st["next"] in st["pending"]:
+            f, fut = st["pending"].pop(st["next"])
+            st["next"] += 1
+
+            def _relay(done, fut=fut):
+                try:
+                    fut.set_result(done.value())
+                except Exception as exc:  # noqa: BLE001 - the RPC caller sees the owner's error
+                    fut.set_exception(exc)
+
+            srv.submit(f).add_done_callback(_relay)  # FIFO executor: submission order is execution order
+    return out
+
+
 def _rm_open_ring(srv_rref, caller: str, caller_handle: bytes):
     """Owner side of the ring handshake: a ring for ``caller``, mapped to the caller's; returns its handle."""
     from .. import _native
@@ -47,6 +73,7 @@ def _rm_open_ring(srv_rref, caller: str, caller_handle: bytes):
         ring = _native.comm().P2PRing(srv.device.index, _ring_slot_bytes(), 60.0)
         ring.open(caller_handle)
         rings[caller] = ring
+        srv.__dict__.setdefault("_ring_order", {}).pop(caller, None)  # a new ring restarts the message index
         return ring.ipc_handle()
 
     return srv.submit(run).wait()
@@ -82,18 +109,18 @@ def _rm_forward_ring(srv_rref, ctx_id, call_id, caller, args):
 
 
 @rpc.functions.async_execution
-def _rm_backward_ring(srv_rref, ctx_id, call_id, caller, shape):
+def _rm_backward_ring(srv_rref, ctx_id, call_id, caller, shape, ring_idx):
     srv = srv_rref.local_value()
 
     def run():
         _, out = srv.saved.pop((ctx_id, call_id))
         g = torch.empty(shape, dtype=torch.float32, device=srv.device)
-        srv.rings[caller].recv(g)  # caller GPU -> owner GPU
+        srv.rings[caller].recv(g)  # caller GPU -> owner GPU: message ring_idx of this caller
         torch.autograd.backward(out, g.to(out.dtype))
         core.accumulate_grads(srv, ctx_id)
         return True
 
-    return srv.submit(run)
+    return _ring_ordered_submit(srv, caller, ring_idx, run)
 
 
 @rpc.functions.async_execution
@@ -144,11 +171,13 @@ class RemoteModule:
             me = rpc.get_worker_info().name
             ring.open(rpc.rpc_sync(self.worker, _rm_open_ring, args=(self.server, me, ring.ipc_handle())))
             self.__dict__["_p2p"] = ring
+            self.__dict__["_p2p_sent"] = 0  # index of the next message this process sends on the ring
         return ring
 
     def close(self):
         """Tear down this process's ring towards the owner (and the owner's side); both drain first."""
         ring = self.__dict__.pop("_p2p", None)
+        self.__dict__.pop("_p2p_sent", None)
         if ring is not None:
             torch.cuda.synchronize()
             rpc.rpc_sync(self.worker, _rm_close_ring, args=(self.server, rpc.get_worker_info().name))
@@ -157,6 +186,7 @@ class RemoteModule:
     def __getstate__(self):  # the handle travels to other processes; a ring is per process
         d = dict(self.__dict__)
         d.pop("_p2p", None)
+        d.pop("_p2p_sent", None)
         return d
 
     def uses_ring(self, out_device) -> bool:
@@ -182,9 +212,13 @@ class RemoteModule:
 
     def _backward_ring(self, owner, ctx_id, call_id, grad):
         g = grad.float().contiguous()
-        self._ring(g.device).send(g)
+        ring = self._ring(g.device)
+        idx = self.__dict__["_p2p_sent"]
+        self.__dict__["_p2p_sent"] = idx + 1
+        ring.send(g)
         me = rpc.get_worker_info().name
-        return rpc.rpc_async(self.worker, _rm_backward_ring, args=(self.server, ctx_id, call_id, me, tuple(g.shape)))
+        return rpc.rpc_async(self.worker, _rm_backward_ring,
+                             args=(self.server, ctx_id, call_id, me, tuple(g.shape), idx))
 
     __call__ = forward
 
