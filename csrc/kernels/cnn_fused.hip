@@ -218,7 +218,8 @@ __device__ __forceinline__ void cnn_grid_barrier(unsigned* bar, unsigned n, int*
 
 // Stores of the per-workgroup outputs the reduction launch reads (slabs, activation columns, loss partials):
 // SM 0 plain, 1 non-temporal, 2 write-through (sc1: the bytes leave the XCD's L2 under the remaining phases
-// instead of at the kernel boundary).  Vector stores only.
+// instead of at the kernel boundary), 3 write-through for the 8- / 16-byte stores only, the dword ones plain
+// (narrow write-through stores cost several times their bytes' time).  Vector stores only.
 template <int SM>
 __device__ __forceinline__ void out_st(float* p, float v) {
   if constexpr (SM == 1) __builtin_nontemporal_store(v, p);
@@ -228,12 +229,12 @@ __device__ __forceinline__ void out_st(float* p, float v) {
 template <int SM>
 __device__ __forceinline__ void out_st_u16x4(uint16_t* p, u16x4 v) {
   if constexpr (SM == 1) __builtin_nontemporal_store(v, reinterpret_cast<u16x4*>(p));
-  else st_vec(reinterpret_cast<u16x4*>(p), v, SM == 2);
+  else st_vec(reinterpret_cast<u16x4*>(p), v, SM >= 2);
 }
 template <int SM>
 __device__ __forceinline__ void out_st4(float* p, f32x4 v) {
   if constexpr (SM == 1) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
-  else if constexpr (SM == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (SM >= 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
   else *reinterpret_cast<f32x4*>(p) = v;
 }
 
@@ -1278,14 +1279,17 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
   static const int diag_frag = std::getenv("PDE_CNN_DIAG_FRAG") ? 2 : 0;  // timing only: see k_cnn_train
   const int xmap = (xmap_env != 0 && nwg % 8 == 0 ? 1 : 0) | diag_frag;
   static const bool breg = std::getenv("PDE_CNN_BREG") != nullptr && std::getenv("PDE_CNN_BREG")[0] == '1';
-  auto train = breg ? (smode == 1 ? &k_cnn_train<1, true> : smode == 2 ? &k_cnn_train<2, true> : &k_cnn_train<0, true>)
-                    : (smode == 1 ? &k_cnn_train<1, false> : smode == 2 ? &k_cnn_train<2, false> : &k_cnn_train<0, false>);
-  static bool attr[6] = {false, false, false, false, false, false};
-  const int si = (smode == 1 || smode == 2 ? smode : 0) + (breg ? 3 : 0);
-  if (!attr[si]) {
+  using TrainFn = decltype(&k_cnn_train<0, false>);
+  static const TrainFn kTrain[2][4] = {
+      {&k_cnn_train<0, false>, &k_cnn_train<1, false>, &k_cnn_train<2, false>, &k_cnn_train<3, false>},
+      {&k_cnn_train<0, true>, &k_cnn_train<1, true>, &k_cnn_train<2, true>, &k_cnn_train<3, true>}};
+  const int si = smode >= 0 && smode <= 3 ? smode : 0;
+  const TrainFn train = kTrain[breg ? 1 : 0][si];
+  static bool attr[2][4] = {};
+  if (!attr[breg ? 1 : 0][si]) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(train), hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(sm));
-    attr[si] = true;
+    attr[breg ? 1 : 0][si] = true;
   }
   if (reinterpret_cast<uintptr_t>(frag) & 15) return hipErrorInvalidValue;
   if (prep)
