@@ -830,20 +830,37 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     part[(wid * 2 + 0) * 64 + lane] = acc[0];
     part[(wid * 2 + 1) * 64 + lane] = acc[1];
     lds_sync();
+    // conv1's weight and bias gradients (slab [O_W1, O_B1 + C1), contiguous) gathered in LDS behind the
+    // partials, then written as 65 16-byte stores instead of 260 dword ones (r4ac: the dword stores cost the
+    // step ~0.8 us)
+    static_assert(O_W1 == 0 && O_B1 == W1N && (W1N + C1) % 4 == 0, "conv1 gradients: one float4 run");
+    static_assert(NW * 2 * 64 * sizeof(f32x4) + (W1N + C1) * sizeof(float) <=
+                      sizeof(u16x8) * (KS2 * 2 * 64 + KSD * 64), "conv1 gradient staging fits behind the partials");
+    float* w1g = reinterpret_cast<float*>(part + NW * 2 * 64);
     if (t < W1N) {
       const int c = t / 25, kidx = t - c * 25, u = kidx >> 4;
       const int l = (c >> 2) * 16 + (kidx & 15), r = c & 3;
       float s = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) s += part[(w * 2 + u) * 64 + l][r];
-      out_st<SM>(&slab[O_W1 + t], s);
-    } else if (t >= 256 && t < 256 + C1) {
-      const int c = t - 256;
+      w1g[t] = s;
+    } else if (wid >= NW - C1) {
+      // conv1's bias gradient: one wave per channel, 9 cells per lane, then a wave sum (a single thread per
+      // channel summing its 576 cells was a ~4 us serial tail at the end of the kernel, r4ad)
+      static_assert(W1N <= (NW - C1) * 64 && (NI * NC1) % 64 == 0, "conv1 bias waves");
+      const int c = wid - (NW - C1);
       float s = 0.f;
-      for (int im = 0; im < NI; ++im)
-        for (int q = 0; q < NC1; ++q) s += bf2f(S.dr1[im][c * RP16 + q]);
-      out_st<SM>(&slab[O_B1 + c], s);
+#pragma unroll
+      for (int k = 0; k < NI * NC1 / 64; ++k) {
+        const int i = lane + 64 * k, im = i / NC1, q = i - im * NC1;
+        s += bf2f(S.dr1[im][c * RP16 + q]);
+      }
+      s = wave_sum(s);
+      if (lane == 0) w1g[W1N + c] = s;
     }
+    lds_sync();
+    if (t < (W1N + C1) / 4 && !(xmap & 4))  // (xmap & 4: timing diagnostic, stores skipped)
+      out_st4<SM>(&slab[O_W1 + 4 * t], *reinterpret_cast<const f32x4*>(&w1g[4 * t]));
   }
   PDE_STAMP(11);
 
@@ -1276,7 +1293,8 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
   // 0.0381 ms/step; non-temporal 0.0390).  PDE_CNN_XMAP=1: XCD-grouped images (r4k: level, off)
   static const int smode = std::getenv("PDE_CNN_STORE") ? std::atoi(std::getenv("PDE_CNN_STORE")) : 2;
   static const int xmap_env = std::getenv("PDE_CNN_XMAP") ? std::atoi(std::getenv("PDE_CNN_XMAP")) : 0;
-  static const int diag_frag = std::getenv("PDE_CNN_DIAG_FRAG") ? 2 : 0;  // timing only: see k_cnn_train
+  static const int diag_frag = (std::getenv("PDE_CNN_DIAG_FRAG") ? 2 : 0) |  // timing only: see k_cnn_train
+                               (std::getenv("PDE_CNN_DIAG_P9ST") ? 4 : 0);
   const int xmap = (xmap_env != 0 && nwg % 8 == 0 ? 1 : 0) | diag_frag;
   static const bool breg = std::getenv("PDE_CNN_BREG") != nullptr && std::getenv("PDE_CNN_BREG")[0] == '1';
   using TrainFn = decltype(&k_cnn_train<0, false>);
@@ -1305,7 +1323,7 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
     tail.err = berr; tail.accumulate = accumulate; tail.B = B; tail.on = 1;
   }
   // PDE_CNN_DIAG (timing diagnostics only, results invalid): 1 no reduce launch, 2 no train launch, 4 reduce
-  // slab-column roles only, 8 reduce fc1-tile roles only
+  // slab-column roles only, 8 reduce fc1-tile roles only, 16 no SGD update / fragment refresh in the reduce
   static const int diag = std::getenv("PDE_CNN_DIAG") ? std::atoi(std::getenv("PDE_CNN_DIAG")) : 0;
   if (!(diag & 2))
     hipLaunchKernelGGL(train, dim3(nwg), dim3(T), sm, s, images, tgt, B, params,
@@ -1315,8 +1333,8 @@ hipError_t cnn_train_fused(const float* images, const int64_t* tgt, int B, float
     const int rb0 = (diag & 8) ? RED_SLAB_BLOCKS : 0;
     const int nrb = (diag & 4) ? RED_SLAB_BLOCKS : (diag & 8) ? RED_BLOCKS - RED_SLAB_BLOCKS : RED_BLOCKS;
     hipLaunchKernelGGL(k_cnn_reduce, dim3(nrb), dim3(RED_T), 0, s, slabs, nwg, acts, gscale, grads,
-                       accumulate, loss_part, B, loss, rng, params, sgd_hp, static_cast<uint16_t*>(frag), sgd_step,
-                       view, xscale, rb0);
+                       accumulate, loss_part, B, loss, rng, params, (diag & 16) ? nullptr : sgd_hp,
+                       static_cast<uint16_t*>(frag), sgd_step, view, xscale, rb0);
   }
   return hipGetLastError();
 }
