@@ -627,10 +627,12 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   }
   if (t >= 448 && t < 448 + C2) {
     const int co = t - 448;
-    float s = 0.f;
+    f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
     for (int im = 0; im < NI; ++im)
-      for (int c = 0; c < NC2; ++c) s += S.dp2[im][co * NC2 + c];
-    out_st<SM>(&slab[O_B2 + co], s);
+#pragma unroll
+      for (int c = 0; c < NC2; c += 4) s4 += *reinterpret_cast<const f32x4*>(&S.dp2[im][co * NC2 + c]);
+    out_st<SM>(&slab[O_B2 + co], (s4[0] + s4[1]) + (s4[2] + s4[3]));
   }
   if constexpr (!BREG) {
     u16x8* dst = &S.w2d[0][0];
