@@ -48,6 +48,7 @@ constexpr int RP16 = 146, RP8 = 148;
 // gathers take 2.75 LDS cycles per instruction instead of 4 (r4t model; columns 28.. are read by the zero-weight
 // kx = 5 taps only)
 constexpr int XP = 36, NXP = H0 * XP;
+constexpr int DHP = 52;  // LDS row pitch (floats) of dh: 16-byte rows, P6 reads them as float4
 constexpr int W1N = C1 * KS * KS, W2N = C2 * C1 * KS * KS, FC1N = F1 * NIN, FC2N = F2 * F1;
 constexpr int K2 = C1 * KS * KS;       // 250: conv2 reduction (ci,ky,kx) in the weight's own order
 // conv2 fwd: K ordered (tap, ci) with ci padded to 16 over a channel-last copy of r1, so a lane's 8
@@ -130,7 +131,8 @@ struct CnnSmem {
   alignas(16) float fc2b[F2];
   alignas(16) float r2[NI][NIN];       // fc1 input (NCHW flatten order); read as float4 in P3
   alignas(16) float dp2[NI][NIN];      // grad at the pooled conv2 output (dropout2d applied)
-  float h1[NI][F1], m1[NI][F1], h1d[NI][F1], dh[NI][F1];
+  float h1[NI][F1], m1[NI][F1], h1d[NI][F1];
+  alignas(16) float dh[NI][DHP];       // rows padded to 16-byte multiples: P6 reads them as float4
   float mc2[NI][C2];
   float logit[NI][F2], dlog[NI][F2];
   float valid[NI];
@@ -149,7 +151,9 @@ static_assert(offsetof(CnnSmem, w1f) == offsetof(CnnSmem, w2d) + sizeof(u16x8) *
 // chunk of fc1 outputs).  Their partial sums live in the w2f region (dead after P2), combined in a fixed
 // order (deterministic).
 constexpr int FC1_KC = NIN / 32;        // 10 input chunks
-constexpr int DP2_JC = 3;               // fc1-output chunks for dp2 (17, 17, 16 rows)
+constexpr int DP2_JC = 3;               // fc1-output chunks for dp2 (16, 16, 18 rows: float4-aligned starts)
+constexpr int DP2_J = 16;               // rows per chunk (the last one takes the rest)
+static_assert(F1 - DP2_J * (DP2_JC - 1) <= 20 && DP2_J % 4 == 0 && DHP >= DP2_J * (DP2_JC - 1) + 20, "dp2 chunks");
 static_assert(F1 * FC1_KC <= T && NIN * DP2_JC <= T, "fc1 work split");
 static_assert(sizeof(float) * NI * F1 * FC1_KC <= sizeof(u16x8) * KS2 * 2 * 64, "fc1 partials alias w2f");
 static_assert(sizeof(float) * NI * NIN * DP2_JC <= sizeof(u16x8) * KS2 * 2 * 64, "dp2 partials alias w2f");
@@ -397,8 +401,10 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       }
     }
   }
-  if (stamps != nullptr) {  // diagnostic: conv1 done (this wave), before the fragment stores wait for P0's loads
+  if (stamps != nullptr) {  // diagnostic: conv1 done (waves 0 / 7 / 15), before the fragment stores
     if (t == 0) stamps[blockIdx.x * 16 + 13] = wall_clock64();
+    if (t == 7 * 64) stamps[blockIdx.x * 16 + 14] = wall_clock64();
+    if (t == 15 * 64) stamps[blockIdx.x * 16 + 15] = wall_clock64();
   }
   if (!(xmap & 2)) {  // conv2 forward fragments (loaded in P0): bf16 MFMA order, straight 16-byte stores
     // (xmap & 2: timing diagnostic, the stores and their wait skipped -- results invalid)
@@ -494,13 +500,13 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   // latency hides under P4 / P5
   // (unconditional loads from clamped addresses -- no divergent branch around them, so the compiler tracks
   // them precisely; rows past the chunk / threads past NIN x DP2_JC load a valid element P6 never uses)
-  constexpr int JPER = (F1 + DP2_JC - 1) / DP2_JC;
+  constexpr int JPER = F1 - DP2_J * (DP2_JC - 1);  // 18: the longest chunk
   float w6[JPER];
   {
     const int tc = min(t, NIN * DP2_JC - 1);
     const int jc = tc / NIN, i = tc - jc * NIN;
 #pragma unroll
-    for (int u = 0; u < JPER; ++u) w6[u] = gFC1W[min(jc * JPER + u, F1 - 1) * NIN + i];
+    for (int u = 0; u < JPER; ++u) w6[u] = gFC1W[min(jc * DP2_J + u, F1 - 1) * NIN + i];
   }
   // conv2 data-gradient fragments for P7b: stored to LDS at the end of P6 (the w2d region is idle until then)
   u16x8 fd[2];
@@ -590,14 +596,22 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   float* dpart = reinterpret_cast<float*>(&S.w2f[0][0][0]);  // [jc][im][i]
   if (t < NIN * DP2_JC) {  // thread (i, jc): sum over fc1 outputs j in chunk jc (column loads coalesced)
     const int jc = t / NIN, i = t - jc * NIN;
-    const int j0 = jc * JPER, j1 = min(F1, j0 + JPER);
+    const int j0 = jc * DP2_J, nj = jc == DP2_JC - 1 ? F1 - j0 : DP2_J;
     const float* w = w6;  // loaded before P4
     float s4[NI] = {0.f, 0.f, 0.f, 0.f};
+    // dh read as float4 (5 per image instead of 18 scalars); products past the chunk are selected away
+    // (the padding columns are never written: select, not multiply by zero)
 #pragma unroll
-    for (int u = 0; u < JPER; ++u)
-      if (j0 + u < j1)
+    for (int im = 0; im < NI; ++im)
 #pragma unroll
-        for (int im = 0; im < NI; ++im) s4[im] += w[u] * S.dh[im][j0 + u];
+      for (int q = 0; q < (JPER + 3) / 4; ++q) {
+        const f32x4 d = *reinterpret_cast<const f32x4*>(&S.dh[im][j0 + 4 * q]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int u = 4 * q + e;
+          if (u < JPER) s4[im] += u < nj ? w[u] * d[e] : 0.f;
+        }
+      }
 #pragma unroll
     for (int im = 0; im < NI; ++im) dpart[(jc * NI + im) * NIN + i] = s4[im];
   }
