@@ -116,6 +116,7 @@ struct CnnSmem {
   alignas(16) uint16_t d2[NI][C2][D2R];    // rows padded to 144 B: the 16 co rows of a wgrad A fragment hit
                                            // 16 distinct 16-B bank groups (128-B rows: 4-8-way conflicts)
   alignas(16) uint16_t zero16[8];      // 16 zero bytes: the target of every out-of-range operand read
+  alignas(8) uint32_t p7tab[KSD * 4][2];  // P7b k-group g: {(ky << 16) | kx, d2n offset of the tap + co group}
   uint16_t x[NI][NXP];                 // images, rows of XP (columns 28.. zero)
   uint16_t xpad[18];                   // x1 starts 9 banks after x: P1 / P9 pixel-pair reads of x and x1 by
                                        // the same instruction no longer collide (8064-byte arrays)
@@ -315,6 +316,11 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     *reinterpret_cast<u16x8*>(&S.d2n[0][pos][16 + 8 * h]) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
   if (t < 8) S.zero16[t] = 0;
+  if (t < KSD * 4) {  // P7b's per-k-group tap table (groups past NGD never match: ky = kx = 0x8000)
+    const int g = t, tap = g / CG, cg = g - tap * CG, ky = tap / KS, kx = tap - ky * KS;
+    S.p7tab[g][0] = g < NGD ? (static_cast<uint32_t>(ky) << 16) | static_cast<uint32_t>(kx) : 0x80008000u;
+    S.p7tab[g][1] = static_cast<uint32_t>(g < NGD ? -(ky * O2 + kx) * C2P + cg * 8 : 0);
+  }
   for (int i = t; i < C1; i += T) S.b1[i] = params[O_B1 + i];
   for (int i = t; i < C2; i += T) S.b2[i] = params[O_B2 + i];
   for (int i = t; i < F1; i += T) S.fc1b[i] = gFC1B[i];
@@ -723,6 +729,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     constexpr int MAXT = (NI * MTD + NW - 1) / NW;  // 3
     f32x4 acc[MAXT];
     int ty[MAXT], tx[MAXT], tb[MAXT];
+    u16x2 tyx[MAXT];  // (ty, tx) packed: one packed subtract checks both tap offsets
 #pragma unroll
     for (int u = 0; u < MAXT; ++u) {
       acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -733,19 +740,24 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       ty[u] = pos / P1;
       tx[u] = pos - ty[u] * P1;
       tb[u] = ((im * O2 * O2) + ty[u] * O2 + tx[u]) * C2P;  // element offset at tap (0,0), channel 0
+      tyx[u] = u16x2{static_cast<uint16_t>(tx[u]), static_cast<uint16_t>(ty[u])};
     }
     const uint16_t* base = &S.d2n[0][0][0];
     const int zoff = static_cast<int>(&S.zero16[0] - base);
     const int ntile = wid < NI * MTD - 2 * NW ? 3 : 2;  // wave-uniform (36 tiles over 16 waves)
 
+    // k-step ks, lane group lg: tap / co group of k-group g = 4 ks + lg from the LDS table (one 8-byte read
+    // instead of the divisions), validity of (Y - ky, X - kx) for all tiles by one packed 16-bit subtract each
+    // (r4af: P7b was the phase with the most VALU instructions)
     auto load = [&](int ks, u16x8 (&a)[MAXT], u16x8& b) {
-      const int g = ks * 4 + lg, tap = g / CG, cg = g - tap * CG, ky = tap / KS, kx = tap - ky * KS;
-      const int tofs = -(ky * O2 + kx) * C2P + cg * 8;
+      const u32x2 e = *reinterpret_cast<const u32x2*>(&S.p7tab[ks * 4 + lg][0]);
+      const u16x2 kyx = __builtin_bit_cast(u16x2, e[0]);
+      const int tofs = static_cast<int>(e[1]);
       if constexpr (BREG) b = bd[ks];
       else b = S.w2d[ks][lane];
 #pragma unroll
       for (int u = 0; u < MAXT; ++u) {
-        const bool ok = g < NGD && static_cast<unsigned>(ty[u] - ky) < O2 && static_cast<unsigned>(tx[u] - kx) < O2;
+        const bool ok = (__builtin_bit_cast(uint32_t, static_cast<u16x2>(tyx[u] - kyx)) & 0xFFF8FFF8u) == 0u;
         a[u] = *reinterpret_cast<const u16x8*>(base + (ok ? tb[u] + tofs : zoff));
       }
     };

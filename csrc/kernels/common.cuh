@@ -13,6 +13,7 @@ typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 
 // 16- / 8-byte global store, write-through (sc1) when `wt`: the bytes leave the XCD's L2 while the kernel
 // runs, so the next launch (its blocks on any XCD) does not first wait for an end-of-kernel write-back of
