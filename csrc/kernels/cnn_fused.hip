@@ -44,6 +44,7 @@ constexpr int NX = H0 * H0, NC1 = P1 * P1, NR1 = C1 * NC1, NC2 = P2 * P2, NIN = 
 // channels a wave touches at once fall in different banks (ds_*_b32 banks are (a / 4) mod 32; at a 288-byte
 // pitch channels 0, 4, 8 share one: P1's stores and P9's reads ran 3-6 LDS cycles per instruction, r4s)
 constexpr int RP16 = 146, RP8 = 148;
+static_assert(RP16 >= NC1 + 2 && RP8 >= NC1 + 4 && 16 - 10 <= 10, "padding cells park conv1's dead lanes");
 // LDS row pitch of the images x / x1 (28 pixels + 8 zero columns): with x1 9 banks after x, P1's pixel-pair
 // gathers take 2.75 LDS cycles per instruction instead of 4 (r4t model; columns 28.. are read by the zero-weight
 // kx = 5 taps only)
@@ -364,16 +365,17 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     const u16x8 bw = S.w1f[lane];
     const int tap = lr & 3, dy = tap >> 1, dx = tap & 1;
     const uint16_t* xsrc = dx ? &S.x1[0][0] - 1 : &S.x[0][0];  // x1[i - 1] = x[i]: odd starts become even
+    // a tile is 4 consecutive pooling cells of one cell row (12 % 4 == 0): image, cell row and first column
+    // are wave-uniform (scalar), the lane adds its cell (lr >> 2) and tap -- no per-lane division
+    static_assert(P1 % 4 == 0 && MT1 * 4 == NC1, "conv1 tiles: 4 cells of one row");
+    const uint16_t* xlane = xsrc + dy * XP + 2 * (lr >> 2) + dx;
     auto gather = [&](int tile, u16x8& a) {
-      const int im = tile / MT1, c0 = (tile - im * MT1) * 4;
-      const int cell = c0 + (lr >> 2), py = cell / P1, px = cell - py * P1;
-      const uint16_t* xb = xsrc + im * NXP + (2 * py + dy) * XP + 2 * px + dx;
+      const int im = tile / MT1, t4 = tile - im * MT1, py = t4 / (P1 / 4), px0 = (t4 - py * (P1 / 4)) * 4;
+      const uint16_t* xb = xlane + im * NXP + 2 * py * XP + 2 * px0;
+      u32x4 v;
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const uint32_t v = *reinterpret_cast<const uint32_t*>(xb + koff[p]) & kmsk[p];
-        a[2 * p] = static_cast<uint16_t>(v);
-        a[2 * p + 1] = static_cast<uint16_t>(v >> 16);
-      }
+      for (int p = 0; p < 4; ++p) v[p] = *reinterpret_cast<const uint32_t*>(xb + koff[p]) & kmsk[p];
+      a = __builtin_bit_cast(u16x8, v);
     };
     static_assert((NI * MT1) % NW == 0, "every wave runs the same number of conv1 tiles");
     constexpr int NT1 = NI * MT1 / NW;  // 9 tiles per wave
@@ -392,19 +394,18 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       const int im = tile / MT1, c0 = (tile - im * MT1) * 4;
       const f32x4 acc = accs[u];
       const int co = lr;  // rows (lg*4 + r) = taps r of cell c0 + lg
-      if (co < C1) {
-        int am = 0;
-        float m = acc[0];
-        if (acc[1] > m) { m = acc[1]; am = 1; }
-        if (acc[2] > m) { m = acc[2]; am = 2; }
-        if (acc[3] > m) { m = acc[3]; am = 3; }
-        const uint16_t r = f2bf(fmaxf(m + bias1, 0.f));
-        S.r1[im][co * RP16 + c0 + lg] = r;
-        S.r1n[im][c0 + lg][co] = r;
-        S.a1[im][co * RP8 + c0 + lg] = static_cast<unsigned char>(am);
-      } else {
-        S.r1n[im][c0 + lg][co] = 0;  // ci padding 10..15
-      }
+      // branch-free: lanes co >= C1 write 0 to r1n's ci padding and park their r1 / a1 stores in the planes'
+      // padding cells (144..) of channel co - C1, never read
+      const bool live = co < C1;
+      int am = 0;
+      float m = acc[0];
+      if (acc[1] > m) { m = acc[1]; am = 1; }
+      if (acc[2] > m) { m = acc[2]; am = 2; }
+      if (acc[3] > m) { m = acc[3]; am = 3; }
+      const uint16_t r = live ? f2bf(fmaxf(m + bias1, 0.f)) : static_cast<uint16_t>(0);
+      S.r1n[im][c0 + lg][co] = r;
+      S.r1[im][live ? co * RP16 + c0 + lg : (co - C1) * RP16 + NC1 + (lg & 1)] = r;
+      S.a1[im][live ? co * RP8 + c0 + lg : (co - C1) * RP8 + NC1 + lg] = static_cast<unsigned char>(am);
     }
   }
   if (stamps != nullptr) {  // diagnostic: conv1 done (waves 0 / 7 / 15), before the fragment stores
