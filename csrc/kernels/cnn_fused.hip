@@ -45,6 +45,7 @@ constexpr int NX = H0 * H0, NC1 = P1 * P1, NR1 = C1 * NC1, NC2 = P2 * P2, NIN = 
 // pitch channels 0, 4, 8 share one: P1's stores and P9's reads ran 3-6 LDS cycles per instruction, r4s)
 constexpr int RP16 = 146, RP8 = 148;
 static_assert(RP16 >= NC1 + 2 && RP8 >= NC1 + 4 && 16 - 10 <= 10, "padding cells park conv1's dead lanes");
+static_assert(RP16 % 2 == 0 && RP8 % 4 == 0, "P9 reads 4 cells as aligned 4-byte words");
 // LDS row pitch of the images x / x1 (28 pixels + 8 zero columns): with x1 9 banks after x, P1's pixel-pair
 // gathers take 2.75 LDS cycles per instruction instead of 4 (r4t model; columns 28.. are read by the zero-weight
 // kx = 5 taps only)
@@ -123,8 +124,8 @@ struct CnnSmem {
                                        // the same instruction no longer collide (8064-byte arrays)
   uint16_t x1[NI][NXP];                 // images shifted by one element (x1[i] = x[i + 1]): every pair of
                                        // consecutive pixels is ONE aligned 4-byte LDS read from x or x1
-  uint16_t r1[NI][C1 * RP16];          // relu(maxpool(conv1)), [ci][cell] (pitch RP16)
-  uint16_t dr1[NI][C1 * RP16];               // grad at r1 (relu'-masked) == conv1-output grad at argmax taps
+  alignas(16) uint16_t r1[NI][C1 * RP16];   // relu(maxpool(conv1)), [ci][cell] (pitch RP16)
+  alignas(16) uint16_t dr1[NI][C1 * RP16];               // grad at r1 (relu'-masked) == conv1-output grad at argmax taps
   // fp32 head
   alignas(16) float b1[C1];
   alignas(16) float b2[C2];
@@ -139,7 +140,7 @@ struct CnnSmem {
   float logit[NI][F2], dlog[NI][F2];
   float valid[NI];
   int label[NI];
-  unsigned char a1[NI][C1 * RP8];
+  alignas(16) unsigned char a1[NI][C1 * RP8];
   unsigned char a2[NI][NIN];
 };
 static_assert(sizeof(CnnSmem) <= 160 * 1024, "LDS budget");
@@ -821,33 +822,35 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       const int ks = kv ? ksr : 0;
       const int im = ks / KSW1, p0 = (ks - im * KSW1) * 32 + lg * 8;
       const int y = p0 / O1, x0 = p0 - y * O1;  // 8 positions: row y, x0..x0+7 (x0 % 8 == 0)
-      u16x8 a = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (co < C1 && kv) {
-        const int cell = (y >> 1) * P1 + (x0 >> 1);
-        const int ty = (y & 1) * 2;
+      // branch-free: the 4 cells' argmax bytes as one 4-byte read, their gradients as two (cells 4-aligned, the
+      // plane pitches multiples of 4); lanes co >= C1 read channel 0 and select zeros
+      const int cell = (y >> 1) * P1 + (x0 >> 1);
+      const int ty = (y & 1) * 2;
+      const int cr = co < C1 ? co : 0;
+      const uint32_t am4 = *reinterpret_cast<const uint32_t*>(&S.a1[im][cr * RP8 + cell]);
+      const uint32_t* gp = reinterpret_cast<const uint32_t*>(&S.dr1[im][cr * RP16 + cell]);  // 4-byte aligned only
+      const uint32_t g2[2] = {gp[0], gp[1]};
+      const bool av = co < C1 && kv;
+      u16x8 a;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int am = S.a1[im][co * RP8 + cell + c];
-          const uint16_t g = S.dr1[im][co * RP16 + cell + c];
-          a[2 * c] = am == ty ? g : 0;
-          a[2 * c + 1] = am == ty + 1 ? g : 0;
-        }
+      for (int c = 0; c < 4; ++c) {
+        const int am = (am4 >> (8 * c)) & 0xff;
+        const uint16_t g = av ? static_cast<uint16_t>(g2[c >> 1] >> (16 * (c & 1))) : static_cast<uint16_t>(0);
+        a[2 * c] = am == ty ? g : 0;
+        a[2 * c + 1] = am == ty + 1 ? g : 0;
       }
       a9[u9] = a;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         // 8 consecutive pixels from offset nb + y XP + x0 (x0 % 8 == 0): four aligned 4-byte reads of x (kx
         // even) or of the shifted copy x1 (kx odd) -- never one 16-byte read at a 2-byte-aligned address,
-        // which the LDS would replay as an unaligned access
+        // which the LDS would replay as an unaligned access; kidx >= 25 reads offset 0 and is masked
         const uint16_t* src = xw[u] + im * NXP + nb[u] + y * XP + x0;
-        u16x8 b;
+        const uint32_t msk = nv[u] ? 0xFFFFFFFFu : 0u;
+        u32x4 v;
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          const uint32_t v = nv[u] ? *reinterpret_cast<const uint32_t*>(src + 2 * p) : 0u;
-          b[2 * p] = static_cast<uint16_t>(v);
-          b[2 * p + 1] = static_cast<uint16_t>(v >> 16);
-        }
-        b9[u9][u] = b;
+        for (int p = 0; p < 4; ++p) v[p] = *reinterpret_cast<const uint32_t*>(src + 2 * p) & msk;
+        b9[u9][u] = __builtin_bit_cast(u16x8, v);
       }
     }
 #pragma unroll
