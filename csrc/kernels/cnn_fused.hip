@@ -677,8 +677,9 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   // M = co (2 tiles), N = 250 -> 16 tiles (NT2 per wave), K = (im, y, x) 256 = 8 k-steps.  An A fragment
   // is one 16-byte row of the d2 plane.
   {
-    // the B gathers stay CONDITIONAL u16 reads: unconditional ones are merged by the compiler into one
-    // 16-byte read at a 2-byte-aligned address, which LDS replays as an unaligned access (64 cycles)
+    // B gathers: the 8 consecutive u16 of a fragment start at a 2-byte-aligned address, so they are read as the
+    // 5 aligned words covering them and funnel-shifted (v_alignbyte) when the start is odd -- one 16-byte read
+    // there would be an unaligned LDS access (64 cycles), 8 masked u16 reads cost an exec round trip each
     int nb[NT2];
     bool nv[NT2];
 #pragma unroll
@@ -700,10 +701,18 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       }
 #pragma unroll
       for (int u = 0; u < NT2; ++u) {
-        const uint16_t* src = S.r1[im] + nb[u] + y * P1;  // unmerged u16 reads (see P9)
-        u16x8 b;
+        const int e0 = nb[u] + y * P1;  // first element (kidx >= K2: offset 0, masked below)
+        // (index arithmetic, not pointer casts: the loads must stay LDS loads, not generic flat ones)
+        const uint32_t* wp = reinterpret_cast<const uint32_t*>(&S.r1[im][0]) + (e0 >> 1);
+        const uint32_t sh = static_cast<uint32_t>(e0 & 1) * 2;  // 0 or 2 bytes
+        uint32_t w[5];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) b[j] = nv[u] ? src[j] : 0;
+        for (int q = 0; q < 5; ++q) w[q] = wp[q];
+        const uint32_t msk = nv[u] ? 0xFFFFFFFFu : 0u;
+        u32x4 v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh) & msk;
+        const u16x8 b = __builtin_bit_cast(u16x8, v);
         acc[0][u] = mfma(a[0], b, acc[0][u]);
         acc[1][u] = mfma(a[1], b, acc[1][u]);
       }
