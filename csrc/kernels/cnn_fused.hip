@@ -1005,7 +1005,10 @@ __global__ __launch_bounds__(256) void k_cnn_sgd(float* __restrict__ params, con
 //  * block 0 also reduces the per-workgroup loss partials and advances the dropout RNG counter.
 // With hp (single process, no all-reduce in between) every block also applies the SGD update to the
 // parameters it reduced and refreshes their bf16 fragment slots.
-constexpr int RED_T = 512, RED_COLS = 16, RED_LANES = RED_T / RED_COLS;  // 32 slab lanes
+#ifndef PDE_CNN_RED_COLS
+#define PDE_CNN_RED_COLS 16  // slab columns per reduce block (8: 183 blocks, measured slower, r4ag)
+#endif
+constexpr int RED_T = 512, RED_COLS = PDE_CNN_RED_COLS, RED_LANES = RED_T / RED_COLS;  // slab lanes per column
 constexpr int NSLAB4 = NSLAB / 4;
 constexpr int RED_SLAB_BLOCKS = (NSLAB4 + RED_COLS - 1) / RED_COLS;
 constexpr int FC1_JT = (F1 + 15) / 16, FC1_IT = NIN / 16;   // 4 x 20 output tiles
@@ -1080,6 +1083,15 @@ __device__ __forceinline__ void cnn_reduce_role(int rb, f32x4* part, uint32_t* s
         a1 += v[1] + v[5];
         a2 += v[2] + v[6];
         a3 += v[3] + v[7];
+      }
+      for (; b + 3 * RED_LANES < nwg; b += 4 * RED_LANES) {  // 4 in flight (nwg / RED_LANES < 8)
+        f32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = s4[static_cast<long>(b + u * RED_LANES) * (NSLABP / 4) + SLAB_OFS / 4 + c4];
+        a0 += v[0];
+        a1 += v[1];
+        a2 += v[2];
+        a3 += v[3];
       }
       for (; b < nwg; b += RED_LANES) a0 += s4[static_cast<long>(b) * (NSLABP / 4) + SLAB_OFS / 4 + c4];
     }
