@@ -760,8 +760,10 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     // k-step ks, lane group lg: tap / co group of k-group g = 4 ks + lg from the LDS table (one 8-byte read
     // instead of the divisions), validity of (Y - ky, X - kx) for all tiles by one packed 16-bit subtract each
     // (r4af: P7b was the phase with the most VALU instructions)
-    auto load = [&](int ks, u16x8 (&a)[MAXT], u16x8& b) {
-      const u32x2 e = *reinterpret_cast<const u32x2*>(&S.p7tab[ks * 4 + lg][0]);
+    // (table entries are read one k-step before the loads that use them: the read's latency hides under the
+    // previous k-step's MFMAs)
+    auto tab = [&](int ks) { return *reinterpret_cast<const u32x2*>(&S.p7tab[min(ks, KSD - 1) * 4 + lg][0]); };
+    auto load = [&](int ks, const u32x2& e, u16x8 (&a)[MAXT], u16x8& b) {
       const u16x2 kyx = __builtin_bit_cast(u16x2, e[0]);
       const int tofs = static_cast<int>(e[1]);
       if constexpr (BREG) b = bd[ks];
@@ -773,7 +775,8 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       }
     };
     u16x8 an[MAXT], bn;
-    load(0, an, bn);
+    load(0, tab(0), an, bn);
+    u32x2 en = tab(1);
 #pragma unroll
     for (int ks = 0; ks < KSD; ++ks) {  // reads of k-step ks+1 are issued before the MFMAs of ks
       u16x8 ac[MAXT], bc = bn;
@@ -782,7 +785,11 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       if constexpr (BREG) {
         if (ks + KSB < KSD) bd[ks + KSB] = frag[NF2F + (ks + KSB) * 64 + lane];
       }
-      if (ks + 1 < KSD) load(ks + 1, an, bn);
+      if (ks + 1 < KSD) {
+        const u32x2 e = en;
+        en = tab(ks + 2);
+        load(ks + 1, e, an, bn);
+      }
       acc[0] = mfma(ac[0], bc, acc[0]);
       acc[1] = mfma(ac[1], bc, acc[1]);
       if (ntile == 3) acc[2] = mfma(ac[2], bc, acc[2]);
