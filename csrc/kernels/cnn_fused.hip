@@ -624,20 +624,18 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     for (int im = 0; im < NI; ++im) dpart[(jc * NI + im) * NIN + i] = s4[im];
   }
   lds_sync();
-  for (int it = t; it < NI * NIN; it += T) {
-    const int im = it / NIN, i = it - im * NIN, co = i / NC2;
-    float s1 = 0.f;
-#pragma unroll
-    for (int jc = 0; jc < DP2_JC; ++jc) s1 += dpart[(jc * NI + im) * NIN + i];
-    S.dp2[im][i] = (S.r2[im][i] > 0.f) ? s1 * S.mc2[im][co] : 0.f;
-  }
-  lds_sync();
-  // scatter dp2 to the argmax taps (both layouts; every tap of every window is written); conv2 bias
-  // grad alongside
+  // dp2 = grad at the pooled conv2 output, scattered to the argmax taps by the thread that combines it (both
+  // layouts; every tap of every window is written) -- no barrier between the two; the conv2 bias gradient,
+  // which needs every dp2 of a channel, runs after the phase's closing barrier
   for (int it = t; it < NI * NIN; it += T) {
     const int im = it / NIN, q = it - im * NIN, co = q / NC2, cell = q - co * NC2;
+    float s1 = 0.f;
+#pragma unroll
+    for (int jc = 0; jc < DP2_JC; ++jc) s1 += dpart[(jc * NI + im) * NIN + q];
+    const float v = (S.r2[im][q] > 0.f) ? s1 * S.mc2[im][co] : 0.f;
+    S.dp2[im][q] = v;
     const int py = cell >> 2, px = cell & 3, a = S.a2[im][q];
-    const uint16_t g = f2bf(S.dp2[im][q]);
+    const uint16_t g = f2bf(v);
     const int p00 = (2 * py) * O2 + 2 * px;
     const uint32_t gv = g;
     *reinterpret_cast<uint32_t*>(&S.d2[im][co][p00]) = a == 0 ? gv : (a == 1 ? gv << 16 : 0u);
@@ -647,7 +645,14 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     S.d2n[im][p00 + O2][co] = a == 2 ? g : 0;
     S.d2n[im][p00 + O2 + 1][co] = a == 3 ? g : 0;
   }
-  if (t >= 448 && t < 448 + C2) {
+  if constexpr (!BREG) {
+    u16x8* dst = &S.w2d[0][0];
+    dst[t] = fd[0];
+    if (t + T < NF2D) dst[t + T] = fd[1];
+  }
+  lds_sync();
+  PDE_STAMP(8);
+  if (t >= 448 && t < 448 + C2) {  // conv2 bias gradient (dp2 is not overwritten before P9)
     const int co = t - 448;
     f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -656,13 +661,6 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       for (int c = 0; c < NC2; c += 4) s4 += *reinterpret_cast<const f32x4*>(&S.dp2[im][co * NC2 + c]);
     out_st<SM>(&slab[O_B2 + co], (s4[0] + s4[1]) + (s4[2] + s4[3]));
   }
-  if constexpr (!BREG) {
-    u16x8* dst = &S.w2d[0][0];
-    dst[t] = fd[0];
-    if (t + T < NF2D) dst[t + T] = fd[1];
-  }
-  lds_sync();
-  PDE_STAMP(8);
   // BREG: the first KSB k-steps' B fragments of P7b requested now, ahead of P7a's slab stores (vmcnt retires
   // in issue order, so waiting for them never waits for those stores); P7b's k-step ks requests k-step
   // ks + KSB (all 19 held at once: 76 VGPRs, spills)
