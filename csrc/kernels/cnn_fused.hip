@@ -138,6 +138,7 @@ struct CnnSmem {
   alignas(16) float dh[NI][DHP];       // rows padded to 16-byte multiples: P6 reads them as float4
   float mc2[NI][C2];
   float logit[NI][F2], dlog[NI][F2];
+  float lossim[NI];                    // per-image loss terms (P4), summed at the end
   float valid[NI];
   int label[NI];
   alignas(16) unsigned char a1[NI][C1 * RP8];
@@ -523,67 +524,71 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     fd[1] = frag[NF2F + min(t + T, NF2D - 1)];
   }
 
-  // ---- P4: fc2 logits, then log_softmax + NLL + dlogits per image ---------------------------------
-  if (t < NI * F2) {
-    const int im = t / F2, v = t - im * F2;
-    float s = S.fc2b[v];
+  // ---- P4: fc2 logits, then log_softmax + NLL + dlogits: ONE WAVE PER IMAGE, no block barrier in between.
+  // Lane l < 4 F2 computes a quarter of logit v = l / 4 (rows j = l % 4 + 4 k), the quad sums it; the softmax
+  // reductions run across the wave's lanes (one thread per image summing serially took ~1.5 us).
+  static_assert(NI <= NW && 4 * F2 <= 64, "P4: a wave per image, a lane quad per logit");
+  if (wid < NI) {
+    const int im = wid, v = lane >> 2, p = lane & 3;
+    const bool lv = v < F2;
+    const int vr = lv ? v : 0;
+    float s = 0.f;
     // (fully unrolled, like every loop between the w6 prefetch and P6: a loop header makes the compiler wait
     // for ALL outstanding global loads, w6 included)
 #pragma unroll
-    for (int j = 0; j < F1; ++j) s += S.fc2w[v * F1 + j] * S.h1d[im][j];
-    S.logit[im][v] = s;
-  }
-  lds_sync();
-  PDE_STAMP(5);
-  float loss_acc = 0.f;
-  if (t < NI) {
-    const int im = t;
-    float m = S.logit[im][0];
-#pragma unroll
-    for (int v = 1; v < F2; ++v) m = fmaxf(m, S.logit[im][v]);
-    float se = 0.f;
-#pragma unroll
-    for (int v = 0; v < F2; ++v) se += __expf(S.logit[im][v] - m);
+    for (int k = 0; k < (F1 + 3) / 4; ++k) {
+      const int j = p + 4 * k;
+      if (j < F1) s += S.fc2w[vr * F1 + j] * S.h1d[im][j];
+    }
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    const float logit = s + S.fc2b[vr];
+    const float m = wave_max(lv ? logit : -INFINITY);
+    const float ex = __expf(logit - m);
+    const float se = wave_sum(lv && p == 0 ? ex : 0.f);
     const float lse = m + __logf(se);
     const float val = S.valid[im];
     const int y = S.label[im];  // (loaded in P0: a global load here would wait behind the w6 prefetch)
-    loss_acc = val * (lse - S.logit[im][y]);
+    const float ly = __shfl(logit, 4 * y, 64);
     const float inv_b = val / static_cast<float>(B);
+    const float dl = (__expf(logit - lse) - (v == y ? 1.f : 0.f)) * inv_b;  // d logit v (lanes of quad v)
+    if (lv && p == 0) S.dlog[im][v] = dl;
+    if (lane == 0) S.lossim[im] = val * (lse - ly);
+    // P5's dh = relu'(h1) * mask * (W2^T dlog) of THIS image, in the same wave: lane j < F1 gathers the 10
+    // d logits from the quads by shuffles (the fc2 weight / bias gradients, which sum over the images, are
+    // taken in P6 after the barrier)
+    static_assert(F1 <= 64, "P4: a lane per fc1 output");
+    const int j = lane < F1 ? lane : 0;
+    float sh = 0.f;
 #pragma unroll
-    for (int v = 0; v < F2; ++v) S.dlog[im][v] = (__expf(S.logit[im][v] - lse) - (v == y ? 1.f : 0.f)) * inv_b;
+    for (int vv = 0; vv < F2; ++vv) sh += S.fc2w[vv * F1 + j] * __shfl(dl, 4 * vv, 64);
+    if (lane < F1) S.dh[im][lane] = (S.h1[im][lane] > 0.f) ? sh * S.m1[im][lane] : 0.f;
   }
   lds_sync();
+  PDE_STAMP(5);
   PDE_STAMP(6);
-
-  // ---- P5: fc2 backward; dh = relu'(h1) * mask * (W2^T dlog) ------------------------------------
-  static_assert(FC2N <= T, "fc2 weight gradient: one element per thread");
-  if (t < FC2N) {
-    const int v = t / F1, j = t - v * F1;
-    float s = 0.f;
-#pragma unroll
-    for (int im = 0; im < NI; ++im) s += S.dlog[im][v] * S.h1d[im][j];
-    out_st<SM>(&slab[S_FC2W + t], s);
-  }
-  if (t < F2) {
-    float s = 0.f;
-#pragma unroll
-    for (int im = 0; im < NI; ++im) s += S.dlog[im][t];
-    out_st<SM>(&slab[S_FC2B + t], s);
-  }
-  if (t >= 256 && t < 256 + NI * F1) {
-    const int u = t - 256, im = u / F1, j = u - im * F1;
-    float s = 0.f;
-#pragma unroll
-    for (int v = 0; v < F2; ++v) s += S.fc2w[v * F1 + j] * S.dlog[im][v];
-    S.dh[im][j] = (S.h1[im][j] > 0.f) ? s * S.m1[im][j] : 0.f;
-  }
-  lds_sync();
   PDE_STAMP(7);
+
+  // ---- P5 (fc2 backward) now lives in P4 (dh, per image) and P6 (the fc2 weight / bias gradients) -------
 
   // ---- P6: fc1 backward: dH / R2 columns for the batch-wide dW GEMM (k_cnn_reduce), db to the slab, and
   // dp2 = grad at the pooled conv2 output.  Columns n0..n0+3 of the K-contiguous bf16 [row][Bkp] image (the
   // reduction's bf16 MFMA operands): one 8-byte store per row (rows 0..49 dH^T, 50..369 R2^T); the workgroup
   // owning the last columns also zeroes the row padding up to Bkp (a multiple of 8).
+  static_assert(FC2N + F2 <= T, "fc2 weight / bias gradients: one element per thread");
+  if (t < FC2N) {  // fc2 weight gradient (all images' dlog / h1d, complete since P4's barrier)
+    const int v = t / F1, j = t - v * F1;
+    float s = 0.f;
+#pragma unroll
+    for (int im = 0; im < NI; ++im) s += S.dlog[im][v] * S.h1d[im][j];
+    out_st<SM>(&slab[S_FC2W + t], s);
+  } else if (t < FC2N + F2) {
+    const int v = t - FC2N;
+    float s = 0.f;
+#pragma unroll
+    for (int im = 0; im < NI; ++im) s += S.dlog[im][v];
+    out_st<SM>(&slab[S_FC2B + v], s);
+  }
   {
     const int Bk = gridDim.x * NI, Bkp = act_pitch(gridDim.x);
     const bool pad = Bkp != Bk && n0 + NI == Bk;
@@ -910,9 +915,9 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   }
   PDE_STAMP(11);
 
-  // loss partial: threads 0..NI-1 of wave 0 hold it
+  // loss partial: the images' terms from P4
   if (wid == 0) {
-    const float l = wave_sum(loss_acc);
+    const float l = wave_sum(lane < NI ? S.lossim[lane] : 0.f);
     if (lane == 0) out_st<SM>(&loss_part[blockIdx.x], l);
   }
   if (stamps != nullptr) {  // diagnostic: every wave's stores drained, then the workgroup's last stamp
