@@ -322,7 +322,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   if (t < KSD * 4) {  // P7b's per-k-group tap table (groups past NGD never match: ky = kx = 0x8000)
     const int g = t, tap = g / CG, cg = g - tap * CG, ky = tap / KS, kx = tap - ky * KS;
     S.p7tab[g][0] = g < NGD ? (static_cast<uint32_t>(ky) << 16) | static_cast<uint32_t>(kx) : 0x80008000u;
-    S.p7tab[g][1] = static_cast<uint32_t>(g < NGD ? -(ky * O2 + kx) * C2P + cg * 8 : 0);
+    S.p7tab[g][1] = static_cast<uint32_t>(g < NGD ? (-(ky * O2 + kx) * C2P + cg * 8) * 2 : 0);  // bytes
   }
   for (int i = t; i < C1; i += T) S.b1[i] = params[O_B1 + i];
   for (int i = t; i < C2; i += T) S.b2[i] = params[O_B2 + i];
@@ -753,11 +753,14 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       const int im = tile / MTD, pos = (tile % MTD) * 16 + lr;
       ty[u] = pos / P1;
       tx[u] = pos - ty[u] * P1;
-      tb[u] = ((im * O2 * O2) + ty[u] * O2 + tx[u]) * C2P;  // element offset at tap (0,0), channel 0
+      tb[u] = ((im * O2 * O2) + ty[u] * O2 + tx[u]) * C2P * 2;  // byte offset at tap (0,0), channel 0
       tyx[u] = u16x2{static_cast<uint16_t>(tx[u]), static_cast<uint16_t>(ty[u])};
     }
-    const uint16_t* base = &S.d2n[0][0][0];
-    const int zoff = static_cast<int>(&S.zero16[0] - base);
+    const char* base = reinterpret_cast<const char*>(&S.d2n[0][0][0]);
+    const char* zp = reinterpret_cast<const char*>(&S.zero16[0]);
+    const char* tp[MAXT];  // each tile's tap-(0,0) address: a k-step adds the tap offset and selects
+#pragma unroll
+    for (int u = 0; u < MAXT; ++u) tp[u] = base + tb[u];
     const int ntile = wid < NI * MTD - 2 * NW ? 3 : 2;  // wave-uniform (36 tiles over 16 waves)
 
     // k-step ks, lane group lg: tap / co group of k-group g = 4 ks + lg from the LDS table (one 8-byte read
@@ -774,7 +777,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
 #pragma unroll
       for (int u = 0; u < MAXT; ++u) {
         const bool ok = (__builtin_bit_cast(uint32_t, static_cast<u16x2>(tyx[u] - kyx)) & 0xFFF8FFF8u) == 0u;
-        a[u] = *reinterpret_cast<const u16x8*>(base + (ok ? tb[u] + tofs : zoff));
+        a[u] = *reinterpret_cast<const u16x8*>(ok ? tp[u] + tofs : zp);
       }
     };
     u16x8 an[MAXT], bn;
