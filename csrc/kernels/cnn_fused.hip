@@ -40,12 +40,18 @@ constexpr int NW = T / 64;
 constexpr int NI = 4;             // images per workgroup
 constexpr int C1 = 10, C2 = 20, KS = 5, H0 = 28, O1 = 24, P1 = 12, O2 = 8, P2 = 4, F1 = 50, F2 = 10;
 constexpr int NX = H0 * H0, NC1 = P1 * P1, NR1 = C1 * NC1, NC2 = P2 * P2, NIN = C2 * NC2;  // 784 144 1440 16 320
-// LDS channel pitches of the [ci][cell] planes (r1 / dr1 in u16, a1 in bytes): 144 cells padded so that the
+// LDS channel pitches of the [ci][cell] planes (r1 in u16, a1 in bytes, e1 in u32): 144 cells padded so that the
 // channels a wave touches at once fall in different banks (ds_*_b32 banks are (a / 4) mod 32; at a 288-byte
 // pitch channels 0, 4, 8 share one: P1's stores and P9's reads ran 3-6 LDS cycles per instruction, r4s)
 constexpr int RP16 = 146, RP8 = 148;
 static_assert(RP16 >= NC1 + 2 && RP8 >= NC1 + 4 && 16 - 10 <= 10, "padding cells park conv1's dead lanes");
-static_assert(RP16 % 2 == 0 && RP8 % 4 == 0, "P9 reads 4 cells as aligned 4-byte words");
+static_assert(RP16 % 2 == 0 && RP8 % 4 == 0, "P9 reads 4 cells' argmax bytes as one aligned 4-byte word");
+// e1: the conv1-output gradient of every pooled cell, written by P7b's epilogue as a bf16 pair positioned at its
+// argmax tap's column (tap dx = 0 -> low half, 1 -> high half; 0 for a relu-dead cell) and read by P9 as 4 cells
+// per 16-byte load.  592-byte channel rows: 16-byte aligned, and the 10 channels of a 16-lane b128 phase start
+// 20 banks apart (disjoint 4-bank spans)
+constexpr int EP = 148;
+constexpr unsigned char AM_DEAD = 0xFF;  // a1 of a relu-dead cell (r1 == 0): no tap carries a gradient
 // LDS row pitch of the images x / x1 (28 pixels + 8 zero columns): with x1 9 banks after x, P1's pixel-pair
 // gathers take 2.75 LDS cycles per instruction instead of 4 (r4t model; columns 28.. are read by the zero-weight
 // kx = 5 taps only)
@@ -108,16 +114,18 @@ __device__ __forceinline__ f32x4 mfma(const u16x8& a, const u16x8& b, const f32x
 
 struct CnnSmem {
   // bf16 MFMA operands
-  alignas(16) u16x8 w2f[KS2][2][64];   // conv2 fwd B fragments [kstep][ntile][lane]; P9 partials later
+  alignas(16) uint16_t r1n[NI][NC1][C1P];  // relu(maxpool(conv1)) channel-last, ci padded with zeros; e1 (P7b-P9)
+                                           // later, spanning r1n and the front of w2f (both dead after P2)
+  alignas(16) u16x8 w2f[KS2][2][64];   // conv2 fwd B fragments [kstep][ntile][lane]
   alignas(16) u16x8 w2d[KSD][64];      // conv2 dgrad B fragments [kstep][lane]: B[k=(tap,co)][n=ci]
   alignas(16) u16x8 w1f[64];           // conv1 B fragment
-  alignas(16) uint16_t r1n[NI][NC1][C1P];  // relu(maxpool(conv1)) channel-last, ci padded with zeros
   // conv2-output gradient (non-zero only at the argmax taps), twice: channel-last for the dgrad A
   // fragments (co padded to 32 with zeros) and as 8x8 planes for the wgrad A fragments
   alignas(16) uint16_t d2n[NI][O2 * O2][C2P];
   alignas(16) uint16_t d2[NI][C2][D2R];    // rows padded to 144 B: the 16 co rows of a wgrad A fragment hit
                                            // 16 distinct 16-B bank groups (128-B rows: 4-8-way conflicts)
   alignas(16) uint16_t zero16[8];      // 16 zero bytes: the target of every out-of-range operand read
+  alignas(16) uint16_t one16[8];       // 8 x bf16 1.0: P9's B column 25 (conv1's bias gradient)
   alignas(8) uint32_t p7tab[KSD * 4][2];  // P7b k-group g: {(ky << 16) | kx, d2n offset of the tap + co group}
   uint16_t x[NI][NXP];                 // images, rows of XP (columns 28.. zero)
   uint16_t xpad[18];                   // x1 starts 9 banks after x: P1 / P9 pixel-pair reads of x and x1 by
@@ -125,7 +133,6 @@ struct CnnSmem {
   uint16_t x1[NI][NXP];                 // images shifted by one element (x1[i] = x[i + 1]): every pair of
                                        // consecutive pixels is ONE aligned 4-byte LDS read from x or x1
   alignas(16) uint16_t r1[NI][C1 * RP16];   // relu(maxpool(conv1)), [ci][cell] (pitch RP16)
-  alignas(16) uint16_t dr1[NI][C1 * RP16];               // grad at r1 (relu'-masked) == conv1-output grad at argmax taps
   // fp32 head
   alignas(16) float b1[C1];
   alignas(16) float b2[C2];
@@ -145,8 +152,12 @@ struct CnnSmem {
   unsigned char a2[NI][NIN];
 };
 static_assert(sizeof(CnnSmem) <= 160 * 1024, "LDS budget");
-static_assert(sizeof(u16x8) * (KS2 * 2 * 64 + KSD * 64) >= NW * 2 * 64 * sizeof(f32x4),
-              "P9 partials alias w2f + w2d");
+static_assert(offsetof(CnnSmem, w2f) == offsetof(CnnSmem, r1n) + sizeof(uint16_t) * NI * NC1 * C1P &&
+                  sizeof(uint32_t) * NI * C1 * EP <= sizeof(uint16_t) * NI * NC1 * C1P + sizeof(u16x8) * KS2 * 2 * 64,
+              "e1 aliases r1n + w2f");
+static_assert(offsetof(CnnSmem, d2n) == offsetof(CnnSmem, w1f) + sizeof(u16x8) * 64 &&
+                  NW * 2 * 64 * sizeof(f32x4) <= sizeof(u16x8) * (KSD * 64 + 64) + sizeof(uint16_t) * NI * O2 * O2 * C2P,
+              "P9 partials alias w2d + w1f + d2n (not e1)");
 static_assert(offsetof(CnnSmem, w2d) == offsetof(CnnSmem, w2f) + sizeof(u16x8) * KS2 * 2 * 64, "w2f, w2d adjacent");
 constexpr int NT2 = 16 / NW;  // conv2-wgrad N-tiles (250 -> 16 x 16) per wave
 constexpr int NFRAG = KS2 * 2 * 64 + KSD * 64 + 64;  // bf16 MFMA weight fragments (w2f, w2d, w1f)
@@ -319,6 +330,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     *reinterpret_cast<u16x8*>(&S.d2n[0][pos][16 + 8 * h]) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
   if (t < 8) S.zero16[t] = 0;
+  if (t >= 8 && t < 16) S.one16[t - 8] = 0x3F80;
   if (t < KSD * 4) {  // P7b's per-k-group tap table (groups past NGD never match: ky = kx = 0x8000)
     const int g = t, tap = g / CG, cg = g - tap * CG, ky = tap / KS, kx = tap - ky * KS;
     S.p7tab[g][0] = g < NGD ? (static_cast<uint32_t>(ky) << 16) | static_cast<uint32_t>(kx) : 0x80008000u;
@@ -405,6 +417,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       if (acc[2] > m) { m = acc[2]; am = 2; }
       if (acc[3] > m) { m = acc[3]; am = 3; }
       const uint16_t r = live ? f2bf(fmaxf(m + bias1, 0.f)) : static_cast<uint16_t>(0);
+      if (r == 0) am = AM_DEAD;  // relu-dead: P7b's epilogue and P9 read the mask from a1
       S.r1n[im][c0 + lg][co] = r;
       S.r1[im][live ? co * RP16 + c0 + lg : (co - C1) * RP16 + NC1 + (lg & 1)] = r;
       S.a1[im][live ? co * RP8 + c0 + lg : (co - C1) * RP8 + NC1 + lg] = static_cast<unsigned char>(am);
@@ -412,7 +425,6 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   }
   if (stamps != nullptr) {  // diagnostic: conv1 done (waves 0 / 7 / 15), before the fragment stores
     if (t == 0) stamps[blockIdx.x * 16 + 13] = wall_clock64();
-    if (t == 7 * 64) stamps[blockIdx.x * 16 + 14] = wall_clock64();
     if (t == 15 * 64) stamps[blockIdx.x * 16 + 15] = wall_clock64();
   }
   if (!(xmap & 2)) {  // conv2 forward fragments (loaded in P0): bf16 MFMA order, straight 16-byte stores
@@ -800,17 +812,23 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       acc[1] = mfma(ac[1], bc, acc[1]);
       if (ntile == 3) acc[2] = mfma(ac[2], bc, acc[2]);
     }
+    // epilogue: the lane's 4 consecutive cells as e1 words (relu'(r1) from a1's dead mark), one 16-byte store.
+    // e1 aliases r1n / w2f, which no P7a / P7b wave reads (r1 itself is still P7a's B operand: no barrier here)
+    uint32_t* e1 = reinterpret_cast<uint32_t*>(&S.r1n[0][0][0]);
 #pragma unroll
     for (int u = 0; u < MAXT; ++u) {
       const int tile = wid + u * NW;
       const int ci = lr;
       if (tile < NI * MTD && ci < C1) {
-        const int im = tile / MTD;
+        const int im = tile / MTD, cell = (tile % MTD) * 16 + lg * 4;
+        const uint32_t am4 = *reinterpret_cast<const uint32_t*>(&S.a1[im][ci * RP8 + cell]);
+        u32x4 e;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int q = ci * RP16 + (tile % MTD) * 16 + lg * 4 + r;
-          S.dr1[im][q] = S.r1[im][q] != 0 ? f2bf(acc[u][r]) : 0;  // r1 is relu'd: r1 == 0 <=> dead
+          const uint32_t am = (am4 >> (8 * r)) & 0xFFu;
+          e[r] = am == AM_DEAD ? 0u : static_cast<uint32_t>(f2bf(acc[u][r])) << (16 * (am & 1u));
         }
+        *reinterpret_cast<u32x4*>(&e1[(im * C1 + ci) * EP + cell]) = e;
       }
     }
   }
@@ -818,103 +836,89 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   PDE_STAMP(10);
 
   // ---- P9: conv1 wgrad (MFMA): dW1[co][(ky,kx)] = sum_(im,y,x) dconv1[co][y][x] * x[y+ky][x+kx], with
-  // dconv1 = dr1 at the argmax tap of each pooling window.  M = co, N = 25 -> 2 tiles, K = (im,y,x)
-  // 2304 = 72 k-steps split over the waves; partials combined in LDS in a fixed order.
+  // dconv1 = the cell's gradient (e1) at its argmax tap.  M = co, N = 25 taps + the bias column (B = 1) -> 2
+  // tiles, K = (im,y,x) 2304 = 72 k-steps split over the waves; partials combined in LDS in a fixed order.
   {
-    int nb[2];
-    bool nv[2];
-    const uint16_t* xw[2];  // x for even kx, x1 - 1 for odd kx (aligned pairs either way)
+    const uint16_t* xw[2];  // per N-tile: x (kx even) or x1 - 1 (kx odd) at the tap offset; one16 / zero16
+    uint32_t om[2];         // for the bias column and the dead columns, whose offsets are masked to 0
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int kidx = u * 16 + lr;
-      nv[u] = kidx < 25;
-      nb[u] = nv[u] ? (kidx / 5) * XP + kidx % 5 : 0;
-      xw[u] = (nv[u] && ((kidx % 5) & 1)) ? &S.x1[0][0] - 1 : &S.x[0][0];
+      const bool nv = kidx < 25;
+      const int nb = nv ? (kidx / 5) * XP + kidx % 5 : 0;
+      xw[u] = nv ? ((kidx % 5) & 1 ? &S.x1[0][0] - 1 : &S.x[0][0]) + nb : (kidx == 25 ? &S.one16[0] : &S.zero16[0]);
+      om[u] = nv ? 0xFFFFFFFFu : 0u;
     }
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     const int co = lr;
-    // a fixed trip count (72 k-steps over 16 waves: 5 slots, the last one live on 8 waves): every slot's LDS
-    // reads are issued before the first MFMA (a data-dependent loop ran them one k-step at a time)
+    const int cr = co < C1 ? co : 0;  // rows co >= C1 are discarded: they read channel 0's (finite) data
+    const uint32_t* e1 = reinterpret_cast<const uint32_t*>(&S.r1n[0][0][0]);
+    // a fixed trip count (72 k-steps over 16 waves: 5 slots, the last one live on 8 waves -- a wave-uniform
+    // skip): every slot's LDS reads are issued before the first MFMA
     constexpr int NK9 = (NI * KSW1 + NW - 1) / NW;
     u16x8 a9[NK9], b9[NK9][2];
 #pragma unroll
     for (int u9 = 0; u9 < NK9; ++u9) {
-      const int ksr = wid + u9 * NW;
-      const bool kv = ksr < NI * KSW1;  // wave-uniform
-      const int ks = kv ? ksr : 0;
+      const int ks = wid + u9 * NW;
+      if (ks >= NI * KSW1) break;  // wave-uniform
       const int im = ks / KSW1, p0 = (ks - im * KSW1) * 32 + lg * 8;
       const int y = p0 / O1, x0 = p0 - y * O1;  // 8 positions: row y, x0..x0+7 (x0 % 8 == 0)
-      // branch-free: the 4 cells' argmax bytes as one 4-byte read, their gradients as two (cells 4-aligned, the
-      // plane pitches multiples of 4); lanes co >= C1 read channel 0 and select zeros
+      // A: 4 cells' e1 words (one 16-byte read), each kept when its argmax row is y's row within the window
       const int cell = (y >> 1) * P1 + (x0 >> 1);
-      const int ty = (y & 1) * 2;
-      const int cr = co < C1 ? co : 0;
+      const uint32_t tyb = static_cast<uint32_t>(y & 1);
       const uint32_t am4 = *reinterpret_cast<const uint32_t*>(&S.a1[im][cr * RP8 + cell]);
-      const uint32_t* gp = reinterpret_cast<const uint32_t*>(&S.dr1[im][cr * RP16 + cell]);  // 4-byte aligned only
-      const uint32_t g2[2] = {gp[0], gp[1]};
-      const bool av = co < C1 && kv;
-      u16x8 a;
+      const u32x4 e4 = *reinterpret_cast<const u32x4*>(&e1[(im * C1 + cr) * EP + cell]);
+      u32x4 a;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int am = (am4 >> (8 * c)) & 0xff;
-        const uint16_t g = av ? static_cast<uint16_t>(g2[c >> 1] >> (16 * (c & 1))) : static_cast<uint16_t>(0);
-        a[2 * c] = am == ty ? g : 0;
-        a[2 * c + 1] = am == ty + 1 ? g : 0;
-      }
-      a9[u9] = a;
+      for (int c = 0; c < 4; ++c) a[c] = ((am4 >> (8 * c + 1)) & 1u) == tyb ? e4[c] : 0u;  // dead: e1 == 0
+      a9[u9] = __builtin_bit_cast(u16x8, a);
+      const int off = im * NXP + y * XP + x0;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        // 8 consecutive pixels from offset nb + y XP + x0 (x0 % 8 == 0): four aligned 4-byte reads of x (kx
-        // even) or of the shifted copy x1 (kx odd) -- never one 16-byte read at a 2-byte-aligned address,
-        // which the LDS would replay as an unaligned access; kidx >= 25 reads offset 0 and is masked
-        const uint16_t* src = xw[u] + im * NXP + nb[u] + y * XP + x0;
-        const uint32_t msk = nv[u] ? 0xFFFFFFFFu : 0u;
+        // 8 consecutive pixels (x0 % 8 == 0): four aligned 4-byte reads of x (kx even) or of the shifted copy
+        // x1 (kx odd) -- never one 16-byte read at a 2-byte-aligned address, which the LDS would replay as an
+        // unaligned access
+        const uint16_t* src = xw[u] + (off & om[u]);
         u32x4 v;
 #pragma unroll
-        for (int p = 0; p < 4; ++p) v[p] = *reinterpret_cast<const uint32_t*>(src + 2 * p) & msk;
+        for (int p = 0; p < 4; ++p) v[p] = *reinterpret_cast<const uint32_t*>(src + 2 * p);
         b9[u9][u] = __builtin_bit_cast(u16x8, v);
       }
     }
 #pragma unroll
-    for (int u9 = 0; u9 < NK9; ++u9)
+    for (int u9 = 0; u9 < NK9; ++u9) {
+      if (wid + u9 * NW >= NI * KSW1) break;
 #pragma unroll
-      for (int u = 0; u < 2; ++u) acc[u] = mfma(a9[u9], b9[u9][u], acc[u]);  // a slot past 72: a == 0
-    lds_sync();  // w2f / w2d are dead after P7b: reuse them for the per-wave partials
-    f32x4* part = reinterpret_cast<f32x4*>(&S.w2f[0][0][0]);
+      for (int u = 0; u < 2; ++u) acc[u] = mfma(a9[u9], b9[u9][u], acc[u]);
+    }
+    // w2d / w1f / d2n are dead after P7b (its last reads precede the barrier before P9): the per-wave partials go
+    // there without another barrier (e1, still read by slower waves, lies before them)
+    f32x4* part = reinterpret_cast<f32x4*>(&S.w2d[0][0]);
     part[(wid * 2 + 0) * 64 + lane] = acc[0];
     part[(wid * 2 + 1) * 64 + lane] = acc[1];
     lds_sync();
-    // conv1's weight and bias gradients (slab [O_W1, O_B1 + C1), contiguous) gathered in LDS behind the
-    // partials, then written as 65 16-byte stores instead of 260 dword ones (r4ac: the dword stores cost the
-    // step ~0.8 us)
+    if (stamps != nullptr && t == 0) stamps[blockIdx.x * 16 + 14] = wall_clock64();  // diagnostic: partials in LDS
+    // conv1's weight and bias gradients (slab [O_W1, O_B1 + C1), contiguous): thread t sums gradient t over the
+    // waves in a fixed order (bias c = B column 25 of channel c), each quad gathers its 4 sums with DPP and its
+    // first lane writes them as one 16-byte store (r4ac: dword stores cost the step ~0.8 us; a staging pass
+    // through LDS cost a barrier, and separate bias waves summing dr1 another ~0.3 us)
     static_assert(O_W1 == 0 && O_B1 == W1N && (W1N + C1) % 4 == 0, "conv1 gradients: one float4 run");
-    static_assert(NW * 2 * 64 * sizeof(f32x4) + (W1N + C1) * sizeof(float) <=
-                      sizeof(u16x8) * (KS2 * 2 * 64 + KSD * 64), "conv1 gradient staging fits behind the partials");
-    float* w1g = reinterpret_cast<float*>(part + NW * 2 * 64);
-    if (t < W1N) {
-      const int c = t / 25, kidx = t - c * 25, u = kidx >> 4;
+    if (wid * 64 < W1N + C1) {  // wave-uniform: waves 0-4
+      const bool live = t < W1N + C1;
+      const int c = t < W1N ? t / 25 : (live ? t - W1N : 0);
+      const int kidx = t < W1N ? t - c * 25 : 25;
+      const int u = kidx >> 4;
       const int l = (c >> 2) * 16 + (kidx & 15), r = c & 3;
       float s = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) s += part[(w * 2 + u) * 64 + l][r];
-      w1g[t] = s;
-    } else if (wid >= NW - C1) {
-      // conv1's bias gradient: one wave per channel, 9 cells per lane, then a wave sum (a single thread per
-      // channel summing its 576 cells was a ~4 us serial tail at the end of the kernel, r4ad)
-      static_assert(W1N <= (NW - C1) * 64 && (NI * NC1) % 64 == 0, "conv1 bias waves");
-      const int c = wid - (NW - C1);
-      float s = 0.f;
-#pragma unroll
-      for (int k = 0; k < NI * NC1 / 64; ++k) {
-        const int i = lane + 64 * k, im = i / NC1, q = i - im * NC1;
-        s += bf2f(S.dr1[im][c * RP16 + q]);
-      }
-      s = wave_sum(s);
-      if (lane == 0) w1g[W1N + c] = s;
+      const int si = __builtin_bit_cast(int, s);
+      const f32x4 q{s, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, si, 0x55, 0xF, 0xF, false)),
+                    __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, si, 0xAA, 0xF, 0xF, false)),
+                    __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, si, 0xFF, 0xF, 0xF, false))};
+      if (live && (t & 3) == 0 && !(xmap & 4))  // (xmap & 4: timing diagnostic, stores skipped)
+        out_st4<SM>(&slab[O_W1 + t], q);
     }
-    lds_sync();
-    if (t < (W1N + C1) / 4 && !(xmap & 4))  // (xmap & 4: timing diagnostic, stores skipped)
-      out_st4<SM>(&slab[O_W1 + 4 * t], *reinterpret_cast<const f32x4*>(&w1g[4 * t]));
   }
   PDE_STAMP(11);
 

@@ -29,8 +29,10 @@ for i, n in enumerate(names):
     print(f"{n:14s} median {d[:, i].median().item():7.2f} us  max {d[:, i].max().item():7.2f} us")
 print("P1 conv1 MFMA part (stamp 1 -> 13) median", ((st[:, 13] - st[:, 1]) / 100.0).median().item(), "us;",
       "fragment wait + stores (13 -> 2)", ((st[:, 2] - st[:, 13]) / 100.0).median().item(), "us")
-print("P1 conv1 MFMA part by wave: 0 / 7 / 15 median",
-      [round(((st[:, k] - st[:, 1]) / 100.0).median().item(), 2) for k in (13, 14, 15)], "us")
+print("P1 conv1 MFMA part by wave: 0 / 15 median",
+      [round(((st[:, k] - st[:, 1]) / 100.0).median().item(), 2) for k in (13, 15)], "us")
+print("P9 split: loads + MFMAs + partials (10 -> 14)", ((st[:, 14] - st[:, 10]) / 100.0).median().item(),
+      "us; combine + stores (14 -> 11)", ((st[:, 11] - st[:, 14]) / 100.0).median().item(), "us")
 print("total median", (st[:, 11] - st[:, 0]).median().item() / 100.0, "us")
 print("span (first start -> last stamp)", (st[:, 11].max() - st[:, 0].min()).item() / 100.0, "us")
 print("workgroup start spread (last - first stamp 0)", (st[:, 0].max() - st[:, 0].min()).item() / 100.0, "us")
