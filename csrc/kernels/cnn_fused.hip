@@ -26,6 +26,7 @@
 // advances, so hipGraph replays draw fresh masks.  Precision: bf16 MFMA operands (images, conv weights,
 // conv activations and their gradients), fp32 accumulation, fp32 fc layers / loss / gradients.
 #include <cstddef>
+#include <type_traits>
 
 #include "common.cuh"
 #include "pde_kernels.h"
@@ -44,7 +45,7 @@ constexpr int NX = H0 * H0, NC1 = P1 * P1, NR1 = C1 * NC1, NC2 = P2 * P2, NIN = 
 // channels a wave touches at once fall in different banks (ds_*_b32 banks are (a / 4) mod 32; at a 288-byte
 // pitch channels 0, 4, 8 share one: P1's stores and P9's reads ran 3-6 LDS cycles per instruction, r4s)
 constexpr int RP16 = 146, RP8 = 148;
-static_assert(RP16 >= NC1 + 2 && RP8 >= NC1 + 4 && 16 - 10 <= 10, "padding cells park conv1's dead lanes");
+static_assert(RP16 >= NC1 && RP8 >= NC1, "channel planes hold the 144 cells");
 static_assert(RP16 % 2 == 0 && RP8 % 4 == 0, "P9 reads 4 cells' argmax bytes as one aligned 4-byte word");
 // e1: the conv1-output gradient of every pooled cell, written by P7b's epilogue as a bf16 pair positioned at its
 // argmax tap's column (tap dx = 0 -> low half, 1 -> high half; 0 for a relu-dead cell) and read by P9 as 4 cells
@@ -65,16 +66,21 @@ constexpr int C1P = 16;
 constexpr int KS2 = (KS * KS * C1P + 31) / 32;  // 13 k-steps (the last one half padding)
 constexpr int KSW2 = NI * 8 * 8 / 32;           // 8 conv2-wgrad k-steps: K = (image, y, x)
 // conv2 dgrad: K = (tap, co) with co padded to 24 = 3 groups of 8, packed: k-step ks, lane group lg holds
-// group g = 4 ks + lg = (tap g / 3, channels 8 (g % 3) .. +7).  The gradient is kept channel-last
-// (d2n[pos][co], co 20..23 zero), so a lane's 8 k-values are ONE 16-byte LDS read of its own position.
+// group g = 4 ks + lg = (tap g / 3, channels 8 (g % 3) .. +7).  The gradient is kept with each co group of 8
+// contiguous (co 20..23 zero), so a lane's 8 k-values are ONE 16-byte LDS read of its own position.
 constexpr int CG = 3;                                // co groups of 8 per tap
 constexpr int NGD = KS * KS * CG;                    // 75 (tap, co-group) pairs
 constexpr int KSD = (NGD + 3) / 4;                   // 19 k-steps (25 with one k-step per tap)
-#ifndef PDE_CNN_C2P
-#define PDE_CNN_C2P 40
-#endif
-constexpr int C2P = PDE_CNN_C2P;  // 80-byte rows: a ds_read_b128 lane octet spans all 64 banks (conflict-free)
-static_assert(C2P >= 24 && C2P % 8 == 0, "d2n rows: co padded to >= 24, 16-byte aligned");
+// d2n layout (u16 units): element (im, Y, X, co) at im D2N_IM + Y D2N_RP + X D2N_P + (co / 8) D2N_Q + co % 8 --
+// 48-byte positions, 528-byte rows, co groups 256 bytes apart (interleaved with other positions' slots).  A P7b
+// A read (a 16-lane b128 group mixes two k-groups and two rows of the tile) models 5.6 LDS cycles per
+// wave-instruction against 6.75 for plain [pos][40] rows (scripts/p7b_lds_model.py; 4 is conflict-free)
+constexpr int D2N_P = 24, D2N_RP = 264, D2N_Q = 128;
+constexpr int D2N_IM = 7 * D2N_RP + 7 * D2N_P + 2 * D2N_Q + 8;  // 2280: one past the last slot of an image
+static_assert(D2N_IM % 8 == 0 && D2N_P % 8 == 0 && D2N_RP % 8 == 0 && D2N_Q % 8 == 0, "d2n: 16-byte slots");
+__host__ __device__ constexpr int d2n_ofs(int im, int y, int x, int co) {
+  return im * D2N_IM + y * D2N_RP + x * D2N_P + (co >> 3) * D2N_Q + (co & 7);
+}
 constexpr int D2R = O2 * O2 + 8;       // d2 plane row stride (u16): 144 B
 constexpr int MT1 = O1 * O1 / 16;      // 36 conv1 M-tiles per image (4 cells x 4 taps each)
 constexpr int MTD = NC1 * 1 / 16;      // 9 conv2-dgrad M-tiles per image (144 r1 positions)
@@ -121,17 +127,17 @@ struct CnnSmem {
   alignas(16) u16x8 w1f[64];           // conv1 B fragment
   // conv2-output gradient (non-zero only at the argmax taps), twice: channel-last for the dgrad A
   // fragments (co padded to 32 with zeros) and as 8x8 planes for the wgrad A fragments
-  alignas(16) uint16_t d2n[NI][O2 * O2][C2P];
+  alignas(16) uint16_t d2n[NI * D2N_IM];     // (d2n_ofs layout)
   alignas(16) uint16_t d2[NI][C2][D2R];    // rows padded to 144 B: the 16 co rows of a wgrad A fragment hit
                                            // 16 distinct 16-B bank groups (128-B rows: 4-8-way conflicts)
   alignas(16) uint16_t zero16[8];      // 16 zero bytes: the target of every out-of-range operand read
-  alignas(16) uint16_t one16[8];       // 8 x bf16 1.0: P9's B column 25 (conv1's bias gradient)
   alignas(8) uint32_t p7tab[KSD * 4][2];  // P7b k-group g: {(ky << 16) | kx, d2n offset of the tap + co group}
   uint16_t x[NI][NXP];                 // images, rows of XP (columns 28.. zero)
   uint16_t xpad[18];                   // x1 starts 9 banks after x: P1 / P9 pixel-pair reads of x and x1 by
                                        // the same instruction no longer collide (8064-byte arrays)
   uint16_t x1[NI][NXP];                 // images shifted by one element (x1[i] = x[i + 1]): every pair of
                                        // consecutive pixels is ONE aligned 4-byte LDS read from x or x1
+  alignas(16) uint16_t xone[NI][NXP];  // bf16 1.0 everywhere: P9's B column 25 reads it (conv1's bias gradient)
   alignas(16) uint16_t r1[NI][C1 * RP16];   // relu(maxpool(conv1)), [ci][cell] (pitch RP16)
   // fp32 head
   alignas(16) float b1[C1];
@@ -156,7 +162,7 @@ static_assert(offsetof(CnnSmem, w2f) == offsetof(CnnSmem, r1n) + sizeof(uint16_t
                   sizeof(uint32_t) * NI * C1 * EP <= sizeof(uint16_t) * NI * NC1 * C1P + sizeof(u16x8) * KS2 * 2 * 64,
               "e1 aliases r1n + w2f");
 static_assert(offsetof(CnnSmem, d2n) == offsetof(CnnSmem, w1f) + sizeof(u16x8) * 64 &&
-                  NW * 2 * 64 * sizeof(f32x4) <= sizeof(u16x8) * (KSD * 64 + 64) + sizeof(uint16_t) * NI * O2 * O2 * C2P,
+                  NW * 2 * 64 * sizeof(f32x4) <= sizeof(u16x8) * (KSD * 64 + 64) + sizeof(uint16_t) * NI * D2N_IM,
               "P9 partials alias w2d + w1f + d2n (not e1)");
 static_assert(offsetof(CnnSmem, w2d) == offsetof(CnnSmem, w2f) + sizeof(u16x8) * KS2 * 2 * 64, "w2f, w2d adjacent");
 constexpr int NT2 = 16 / NW;  // conv2-wgrad N-tiles (250 -> 16 x 16) per wave
@@ -324,17 +330,18 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     (&S.x1[0][0])[r * XP + H0 - 1 + c] = 0;
   }
   if (t < 64) S.w1f[t] = fw1;
-  constexpr int PADG = (C2P - 16) / 8;  // co padding groups of 8 (co 16..C2P-1; 16..19 rewritten per step)
-  for (int i = t; i < NI * O2 * O2 * PADG; i += T) {
-    const int pos = i / PADG, h = i - pos * PADG;
-    *reinterpret_cast<u16x8*>(&S.d2n[0][pos][16 + 8 * h]) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = t; i < NI * O2 * O2; i += T) {  // co group 2 zeroed (co 20..23 stay zero; 16..19 rewritten per step)
+    const int im = i / (O2 * O2), pos = i - im * (O2 * O2);
+    *reinterpret_cast<u16x8*>(&S.d2n[d2n_ofs(im, pos / O2, pos % O2, 16)]) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
   if (t < 8) S.zero16[t] = 0;
-  if (t >= 8 && t < 16) S.one16[t - 8] = 0x3F80;
+  static_assert((NI * NXP) % 8 == 0 && NI * NXP / 8 <= T, "xone: one 16-byte store per thread");
+  if (t < NI * NXP / 8)
+    reinterpret_cast<u16x8*>(&S.xone[0][0])[t] = u16x8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
   if (t < KSD * 4) {  // P7b's per-k-group tap table (groups past NGD never match: ky = kx = 0x8000)
     const int g = t, tap = g / CG, cg = g - tap * CG, ky = tap / KS, kx = tap - ky * KS;
     S.p7tab[g][0] = g < NGD ? (static_cast<uint32_t>(ky) << 16) | static_cast<uint32_t>(kx) : 0x80008000u;
-    S.p7tab[g][1] = static_cast<uint32_t>(g < NGD ? (-(ky * O2 + kx) * C2P + cg * 8) * 2 : 0);  // bytes
+    S.p7tab[g][1] = static_cast<uint32_t>(g < NGD ? (-(ky * D2N_RP + kx * D2N_P) + cg * D2N_Q) * 2 : 0);  // bytes
   }
   for (int i = t; i < C1; i += T) S.b1[i] = params[O_B1 + i];
   for (int i = t; i < C2; i += T) S.b2[i] = params[O_B2 + i];
@@ -368,13 +375,12 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   // pixels, read as ONE aligned 4-byte LDS load -- from x when the window starts on an even column (dx = 0),
   // from the shifted copy x1 otherwise: 4 gathers per fragment instead of 8.
   {
-    int koff[4];       // pair p: k = 8 lg + 2p = (ky, kx) offset into the image; pairs past k = 30 are zero
-    uint32_t kmsk[4];
+    int koff[4];  // pair p: k = 8 lg + 2p = (ky, kx) offset into the image; pairs past k = 30 read offset 0
+                  // (finite pixels times w1f's zero rows: no mask)
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int k = lg * 8 + 2 * p;
       koff[p] = k < KS * 6 ? (k / 6) * XP + (k % 6) : 0;
-      kmsk[p] = k < KS * 6 ? 0xFFFFFFFFu : 0u;
     }
     const u16x8 bw = S.w1f[lane];
     const int tap = lr & 3, dy = tap >> 1, dx = tap & 1;
@@ -388,7 +394,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       const uint16_t* xb = xlane + im * NXP + 2 * py * XP + 2 * px0;
       u32x4 v;
 #pragma unroll
-      for (int p = 0; p < 4; ++p) v[p] = *reinterpret_cast<const uint32_t*>(xb + koff[p]) & kmsk[p];
+      for (int p = 0; p < 4; ++p) v[p] = *reinterpret_cast<const uint32_t*>(xb + koff[p]);
       a = __builtin_bit_cast(u16x8, v);
     };
     static_assert((NI * MT1) % NW == 0, "every wave runs the same number of conv1 tiles");
@@ -408,19 +414,21 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       const int im = tile / MT1, c0 = (tile - im * MT1) * 4;
       const f32x4 acc = accs[u];
       const int co = lr;  // rows (lg*4 + r) = taps r of cell c0 + lg
-      // branch-free: lanes co >= C1 write 0 to r1n's ci padding and park their r1 / a1 stores in the planes'
-      // padding cells (144..) of channel co - C1, never read
+      // lanes co >= C1: w1f's columns and bias1 are zero there, so r == 0 -- r1n's ci padding gets its zeros;
+      // their r1 / a1 stores are masked off (exec, no per-lane address selects)
       const bool live = co < C1;
       int am = 0;
       float m = acc[0];
       if (acc[1] > m) { m = acc[1]; am = 1; }
       if (acc[2] > m) { m = acc[2]; am = 2; }
       if (acc[3] > m) { m = acc[3]; am = 3; }
-      const uint16_t r = live ? f2bf(fmaxf(m + bias1, 0.f)) : static_cast<uint16_t>(0);
+      const uint16_t r = f2bf(fmaxf(m + bias1, 0.f));
       if (r == 0) am = AM_DEAD;  // relu-dead: P7b's epilogue and P9 read the mask from a1
       S.r1n[im][c0 + lg][co] = r;
-      S.r1[im][live ? co * RP16 + c0 + lg : (co - C1) * RP16 + NC1 + (lg & 1)] = r;
-      S.a1[im][live ? co * RP8 + c0 + lg : (co - C1) * RP8 + NC1 + lg] = static_cast<unsigned char>(am);
+      if (live) {
+        S.r1[im][co * RP16 + c0 + lg] = r;
+        S.a1[im][co * RP8 + c0 + lg] = static_cast<unsigned char>(am);
+      }
     }
   }
   if (stamps != nullptr) {  // diagnostic: conv1 done (waves 0 / 7 / 15), before the fragment stores
@@ -657,10 +665,11 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     const uint32_t gv = g;
     *reinterpret_cast<uint32_t*>(&S.d2[im][co][p00]) = a == 0 ? gv : (a == 1 ? gv << 16 : 0u);
     *reinterpret_cast<uint32_t*>(&S.d2[im][co][p00 + O2]) = a == 2 ? gv : (a == 3 ? gv << 16 : 0u);
-    S.d2n[im][p00][co] = a == 0 ? g : 0;
-    S.d2n[im][p00 + 1][co] = a == 1 ? g : 0;
-    S.d2n[im][p00 + O2][co] = a == 2 ? g : 0;
-    S.d2n[im][p00 + O2 + 1][co] = a == 3 ? g : 0;
+    uint16_t* dn = &S.d2n[d2n_ofs(im, 2 * py, 2 * px, co)];
+    dn[0] = a == 0 ? g : 0;
+    dn[D2N_P] = a == 1 ? g : 0;
+    dn[D2N_RP] = a == 2 ? g : 0;
+    dn[D2N_RP + D2N_P] = a == 3 ? g : 0;
   }
   if constexpr (!BREG) {
     u16x8* dst = &S.w2d[0][0];
@@ -765,10 +774,10 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       const int im = tile / MTD, pos = (tile % MTD) * 16 + lr;
       ty[u] = pos / P1;
       tx[u] = pos - ty[u] * P1;
-      tb[u] = ((im * O2 * O2) + ty[u] * O2 + tx[u]) * C2P * 2;  // byte offset at tap (0,0), channel 0
+      tb[u] = d2n_ofs(im, ty[u], tx[u], 0) * 2;  // byte offset at tap (0,0), channel 0
       tyx[u] = u16x2{static_cast<uint16_t>(tx[u]), static_cast<uint16_t>(ty[u])};
     }
-    const char* base = reinterpret_cast<const char*>(&S.d2n[0][0][0]);
+    const char* base = reinterpret_cast<const char*>(&S.d2n[0]);
     const char* zp = reinterpret_cast<const char*>(&S.zero16[0]);
     const char* tp[MAXT];  // each tile's tap-(0,0) address: a k-step adds the tap offset and selects
 #pragma unroll
@@ -781,37 +790,43 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     // (table entries are read one k-step before the loads that use them: the read's latency hides under the
     // previous k-step's MFMAs)
     auto tab = [&](int ks) { return *reinterpret_cast<const u32x2*>(&S.p7tab[min(ks, KSD - 1) * 4 + lg][0]); };
-    auto load = [&](int ks, const u32x2& e, u16x8 (&a)[MAXT], u16x8& b) {
+    auto load = [&](auto ntc, int ks, const u32x2& e, u16x8 (&a)[MAXT], u16x8& b) {
       const u16x2 kyx = __builtin_bit_cast(u16x2, e[0]);
       const int tofs = static_cast<int>(e[1]);
       if constexpr (BREG) b = bd[ks];
       else b = S.w2d[ks][lane];
 #pragma unroll
-      for (int u = 0; u < MAXT; ++u) {
+      for (int u = 0; u < decltype(ntc)::value; ++u) {
         const bool ok = (__builtin_bit_cast(uint32_t, static_cast<u16x2>(tyx[u] - kyx)) & 0xFFF8FFF8u) == 0u;
         a[u] = *reinterpret_cast<const u16x8*>(ok ? tp[u] + tofs : zp);
       }
     };
-    u16x8 an[MAXT], bn;
-    load(0, tab(0), an, bn);
-    u32x2 en = tab(1);
+    // the k-loop per tile count: a 2-tile wave neither reads nor multiplies a third tile (the phase is bound by
+    // LDS bandwidth, and the mirrored third tile's A reads were ~20% of its bytes)
+    auto kloop = [&](auto ntc) {
+      constexpr int NT = decltype(ntc)::value;
+      u16x8 an[MAXT], bn;
+      load(ntc, 0, tab(0), an, bn);
+      u32x2 en = tab(1);
 #pragma unroll
-    for (int ks = 0; ks < KSD; ++ks) {  // reads of k-step ks+1 are issued before the MFMAs of ks
-      u16x8 ac[MAXT], bc = bn;
+      for (int ks = 0; ks < KSD; ++ks) {  // reads of k-step ks+1 are issued before the MFMAs of ks
+        u16x8 ac[MAXT], bc = bn;
 #pragma unroll
-      for (int u = 0; u < MAXT; ++u) ac[u] = an[u];
-      if constexpr (BREG) {
-        if (ks + KSB < KSD) bd[ks + KSB] = frag[NF2F + (ks + KSB) * 64 + lane];
+        for (int u = 0; u < NT; ++u) ac[u] = an[u];
+        if constexpr (BREG) {
+          if (ks + KSB < KSD) bd[ks + KSB] = frag[NF2F + (ks + KSB) * 64 + lane];
+        }
+        if (ks + 1 < KSD) {
+          const u32x2 e = en;
+          en = tab(ks + 2);
+          load(ntc, ks + 1, e, an, bn);
+        }
+#pragma unroll
+        for (int u = 0; u < NT; ++u) acc[u] = mfma(ac[u], bc, acc[u]);
       }
-      if (ks + 1 < KSD) {
-        const u32x2 e = en;
-        en = tab(ks + 2);
-        load(ks + 1, e, an, bn);
-      }
-      acc[0] = mfma(ac[0], bc, acc[0]);
-      acc[1] = mfma(ac[1], bc, acc[1]);
-      if (ntile == 3) acc[2] = mfma(ac[2], bc, acc[2]);
-    }
+    };
+    if (ntile == 3) kloop(std::integral_constant<int, 3>{});
+    else kloop(std::integral_constant<int, 2>{});
     // epilogue: the lane's 4 consecutive cells as e1 words (relu'(r1) from a1's dead mark), one 16-byte store.
     // e1 aliases r1n / w2f, which no P7a / P7b wave reads (r1 itself is still P7a's B operand: no barrier here)
     uint32_t* e1 = reinterpret_cast<uint32_t*>(&S.r1n[0][0][0]);
@@ -836,60 +851,69 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   PDE_STAMP(10);
 
   // ---- P9: conv1 wgrad (MFMA): dW1[co][(ky,kx)] = sum_(im,y,x) dconv1[co][y][x] * x[y+ky][x+kx], with
-  // dconv1 = the cell's gradient (e1) at its argmax tap.  M = co, N = 25 taps + the bias column (B = 1) -> 2
-  // tiles, K = (im,y,x) 2304 = 72 k-steps split over the waves; partials combined in LDS in a fixed order.
+  // dconv1 = the pooled cell's gradient (e1) at its argmax tap.  M = co, N = 25 taps + the bias column (B = 1)
+  // -> 2 tiles, K = (im, y, x) 2304 = 72 k-steps split over the waves; partials combined in LDS in a fixed order.
+  // K order: a lane's 8 k-elements are 2 horizontally adjacent pooled cells x their 2x2 pooling windows, so its A
+  // fragment is the 2 cells' e1 words placed by the argmax row (no per-position selects) and its B fragment 4
+  // aligned pixel pairs (2 rows x 2 column pairs) of x or x1.
   {
-    const uint16_t* xw[2];  // per N-tile: x (kx even) or x1 - 1 (kx odd) at the tap offset; one16 / zero16
-    uint32_t om[2];         // for the bias column and the dead columns, whose offsets are masked to 0
+    const uint16_t* xw[2];  // per N-tile column kidx: x (kx even) or x1 - 1 (kx odd) at the tap offset; the ones
+                            // plane for the bias column 25; x for the discarded columns 26..31
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int kidx = u * 16 + lr;
       const bool nv = kidx < 25;
       const int nb = nv ? (kidx / 5) * XP + kidx % 5 : 0;
-      xw[u] = nv ? ((kidx % 5) & 1 ? &S.x1[0][0] - 1 : &S.x[0][0]) + nb : (kidx == 25 ? &S.one16[0] : &S.zero16[0]);
-      om[u] = nv ? 0xFFFFFFFFu : 0u;
+      xw[u] = nv ? ((kidx % 5) & 1 ? &S.x1[0][0] - 1 : &S.x[0][0]) + nb : (kidx == 25 ? &S.xone[0][0] : &S.x[0][0]);
     }
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     const int co = lr;
     const int cr = co < C1 ? co : 0;  // rows co >= C1 are discarded: they read channel 0's (finite) data
     const uint32_t* e1 = reinterpret_cast<const uint32_t*>(&S.r1n[0][0][0]);
     // a fixed trip count (72 k-steps over 16 waves: 5 slots, the last one live on 8 waves -- a wave-uniform
-    // skip): every slot's LDS reads are issued before the first MFMA
+    // skip): every slot's LDS reads are issued before the first select / MFMA
     constexpr int NK9 = (NI * KSW1 + NW - 1) / NW;
-    u16x8 a9[NK9], b9[NK9][2];
+    static_assert(KSW1 * 4 * 2 == NC1 && P1 % 2 == 0, "P9: 4 lane groups x 2 cells per k-step");
+    uint32_t m9[NK9];
+    u32x2 e9[NK9];
+    u16x8 b9[NK9][2];
 #pragma unroll
     for (int u9 = 0; u9 < NK9; ++u9) {
       const int ks = wid + u9 * NW;
       if (ks >= NI * KSW1) break;  // wave-uniform
-      const int im = ks / KSW1, p0 = (ks - im * KSW1) * 32 + lg * 8;
-      const int y = p0 / O1, x0 = p0 - y * O1;  // 8 positions: row y, x0..x0+7 (x0 % 8 == 0)
-      // A: 4 cells' e1 words (one 16-byte read), each kept when its argmax row is y's row within the window
-      const int cell = (y >> 1) * P1 + (x0 >> 1);
-      const uint32_t tyb = static_cast<uint32_t>(y & 1);
-      const uint32_t am4 = *reinterpret_cast<const uint32_t*>(&S.a1[im][cr * RP8 + cell]);
-      const u32x4 e4 = *reinterpret_cast<const u32x4*>(&e1[(im * C1 + cr) * EP + cell]);
-      u32x4 a;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) a[c] = ((am4 >> (8 * c + 1)) & 1u) == tyb ? e4[c] : 0u;  // dead: e1 == 0
-      a9[u9] = __builtin_bit_cast(u16x8, a);
-      const int off = im * NXP + y * XP + x0;
+      const int im = ks / KSW1;
+      const uint32_t gi = static_cast<uint32_t>((ks - im * KSW1) * 4 + lg);  // cell pair 0..71 of the image
+      const uint32_t py = (gi * 43u) >> 8, pc = gi - py * 6u;               // gi / 6, gi % 6 (gi < 72)
+      const int cell = static_cast<int>(py * P1 + pc * 2);
+      m9[u9] = *reinterpret_cast<const uint16_t*>(&S.a1[im][cr * RP8 + cell]);
+      e9[u9] = *reinterpret_cast<const u32x2*>(&e1[(im * C1 + cr) * EP + cell]);
+      const int off = im * NXP + static_cast<int>(py * 2 * XP + pc * 4);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        // 8 consecutive pixels (x0 % 8 == 0): four aligned 4-byte reads of x (kx even) or of the shifted copy
-        // x1 (kx odd) -- never one 16-byte read at a 2-byte-aligned address, which the LDS would replay as an
-        // unaligned access
-        const uint16_t* src = xw[u] + (off & om[u]);
+        // k order (dy, cell c, dx): pixel pairs (row 2py + dy, columns 4pc + 2c + {0, 1}), one ds_read2 per row
+        // filling adjacent operand registers; never a 16-byte read at a 2-byte-aligned address, which the LDS
+        // would replay as an unaligned access
+        const uint16_t* src = xw[u] + off;
         u32x4 v;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) v[p] = *reinterpret_cast<const uint32_t*>(src + 2 * p);
+        v[0] = *reinterpret_cast<const uint32_t*>(src);
+        v[1] = *reinterpret_cast<const uint32_t*>(src + 2);
+        v[2] = *reinterpret_cast<const uint32_t*>(src + XP);
+        v[3] = *reinterpret_cast<const uint32_t*>(src + XP + 2);
         b9[u9][u] = __builtin_bit_cast(u16x8, v);
       }
     }
 #pragma unroll
     for (int u9 = 0; u9 < NK9; ++u9) {
       if (wid + u9 * NW >= NI * KSW1) break;
+      u32x4 a;
 #pragma unroll
-      for (int u = 0; u < 2; ++u) acc[u] = mfma(a9[u9], b9[u9][u], acc[u]);
+      for (int c = 0; c < 2; ++c) {
+        const bool lower = (m9[u9] >> (8 * c + 1)) & 1u;  // argmax in the window's second row (dead: e1 == 0)
+        a[c] = lower ? 0u : e9[u9][c];
+        a[2 + c] = lower ? e9[u9][c] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) acc[u] = mfma(__builtin_bit_cast(u16x8, a), b9[u9][u], acc[u]);
     }
     // w2d / w1f / d2n are dead after P7b (its last reads precede the barrier before P9): the per-wave partials go
     // there without another barrier (e1, still read by slower waves, lies before them)

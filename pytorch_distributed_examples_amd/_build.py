@@ -48,8 +48,6 @@ HIP_FLAGS = {
 for _knob in ("PDE_FAST_STAGES", "PDE_GEMM_SUB", "PDE_GEMM_WPE"):  # GEMM ring depth / K-tiles per barrier sweeps (gemm.hip)
     if os.environ.get(_knob):
         HIP_FLAGS.setdefault("kernels/gemm.hip", []).append(f"-D{_knob}={int(os.environ[_knob])}")
-if os.environ.get("PDE_CNN_C2P"):  # fused-CNN d2n row pitch sweep (cnn_fused.hip)
-    HIP_FLAGS["kernels/cnn_fused.hip"].append(f"-DPDE_CNN_C2P={int(os.environ['PDE_CNN_C2P'])}")
 
 
 def _torch_paths():
