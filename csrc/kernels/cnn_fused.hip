@@ -118,6 +118,28 @@ __device__ __forceinline__ f32x4 mfma(const u16x8& a, const u16x8& b, const f32x
                                                  0, 0);
 }
 
+// Cross-lane helpers on DPP row operations and lane reads: no LDS round trip (a __shfl_xor butterfly is a chain
+// of dependent ds_bpermutes, ~0.1 us each: P4's softmax ran 15 of them back to back).  Whole wave active.
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lanef(float v, int l) {  // l wave-uniform
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
+// every lane: op over the wave (quads, 8-lane halves, 16-lane rows by DPP, then the 4 rows' values by lane reads)
+template <class Op>
+__device__ __forceinline__ float wave_all(float v, Op op) {
+  v = op(v, dppf<DPP_XOR1>(v));
+  v = op(v, dppf<DPP_XOR2>(v));
+  v = op(v, dppf<DPP_HALF_MIRROR>(v));
+  v = op(v, dppf<DPP_MIRROR>(v));
+  return op(op(lanef(v, 0), lanef(v, 16)), op(lanef(v, 32), lanef(v, 48)));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) { return wave_all(v, [](float a, float b) { return a + b; }); }
+__device__ __forceinline__ float wave_max_dpp(float v) { return wave_all(v, [](float a, float b) { return fmaxf(a, b); }); }
+
 struct CnnSmem {
   // bf16 MFMA operands
   alignas(16) uint16_t r1n[NI][NC1][C1P];  // relu(maxpool(conv1)) channel-last, ci padded with zeros; e1 (P7b-P9)
@@ -560,16 +582,16 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       const int j = p + 4 * k;
       if (j < F1) s += S.fc2w[vr * F1 + j] * S.h1d[im][j];
     }
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
+    s += dppf<DPP_XOR1>(s);
+    s += dppf<DPP_XOR2>(s);
     const float logit = s + S.fc2b[vr];
-    const float m = wave_max(lv ? logit : -INFINITY);
+    const float m = wave_max_dpp(lv ? logit : -INFINITY);
     const float ex = __expf(logit - m);
-    const float se = wave_sum(lv && p == 0 ? ex : 0.f);
+    const float se = wave_sum_dpp(lv && p == 0 ? ex : 0.f);
     const float lse = m + __logf(se);
     const float val = S.valid[im];
     const int y = S.label[im];  // (loaded in P0: a global load here would wait behind the w6 prefetch)
-    const float ly = __shfl(logit, 4 * y, 64);
+    const float ly = lanef(logit, __builtin_amdgcn_readfirstlane(4 * y));  // y: the wave's image label
     const float inv_b = val / static_cast<float>(B);
     const float dl = (__expf(logit - lse) - (v == y ? 1.f : 0.f)) * inv_b;  // d logit v (lanes of quad v)
     if (lv && p == 0) S.dlog[im][v] = dl;
@@ -581,7 +603,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     const int j = lane < F1 ? lane : 0;
     float sh = 0.f;
 #pragma unroll
-    for (int vv = 0; vv < F2; ++vv) sh += S.fc2w[vv * F1 + j] * __shfl(dl, 4 * vv, 64);
+    for (int vv = 0; vv < F2; ++vv) sh += S.fc2w[vv * F1 + j] * lanef(dl, 4 * vv);
     if (lane < F1) S.dh[im][lane] = (S.h1[im][lane] > 0.f) ? sh * S.m1[im][lane] : 0.f;
   }
   lds_sync();
@@ -948,7 +970,7 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
 
   // loss partial: the images' terms from P4
   if (wid == 0) {
-    const float l = wave_sum(lane < NI ? S.lossim[lane] : 0.f);
+    const float l = wave_sum_dpp(lane < NI ? S.lossim[lane] : 0.f);
     if (lane == 0) out_st<SM>(&loss_part[blockIdx.x], l);
   }
   if (stamps != nullptr) {  // diagnostic: every wave's stores drained, then the workgroup's last stamp
