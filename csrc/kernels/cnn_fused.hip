@@ -159,6 +159,8 @@ struct CnnSmem {
                                        // the same instruction no longer collide (8064-byte arrays)
   uint16_t x1[NI][NXP];                 // images shifted by one element (x1[i] = x[i + 1]): every pair of
                                        // consecutive pixels is ONE aligned 4-byte LDS read from x or x1
+  uint16_t xonepad[48];                // xone starts 4 banks after x (36 words): P9's bias-column reads no longer
+                                       // share a bank with the tap-(4,4) column (scripts/p9_lds_model.py)
   alignas(16) uint16_t xone[NI][NXP];  // bf16 1.0 everywhere: P9's B column 25 reads it (conv1's bias gradient)
   alignas(16) uint16_t r1[NI][C1 * RP16];   // relu(maxpool(conv1)), [ci][cell] (pitch RP16)
   // fp32 head
@@ -180,6 +182,9 @@ struct CnnSmem {
   unsigned char a2[NI][NIN];
 };
 static_assert(sizeof(CnnSmem) <= 160 * 1024, "LDS budget");
+static_assert((offsetof(CnnSmem, x1) - offsetof(CnnSmem, x)) / 4 % 32 == 9 &&
+                  (offsetof(CnnSmem, xone) - offsetof(CnnSmem, x)) / 4 % 32 == 4,
+              "x1 / xone bank offsets from x (P1 gathers, P9 B reads: scripts/p9_lds_model.py)");
 static_assert(offsetof(CnnSmem, w2f) == offsetof(CnnSmem, r1n) + sizeof(uint16_t) * NI * NC1 * C1P &&
                   sizeof(uint32_t) * NI * C1 * EP <= sizeof(uint16_t) * NI * NC1 * C1P + sizeof(u16x8) * KS2 * 2 * 64,
               "e1 aliases r1n + w2f");
@@ -880,13 +885,13 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
   // aligned pixel pairs (2 rows x 2 column pairs) of x or x1.
   {
     const uint16_t* xw[2];  // per N-tile column kidx: x (kx even) or x1 - 1 (kx odd) at the tap offset; the ones
-                            // plane for the bias column 25; x for the discarded columns 26..31
+                            // plane for the bias column 25; the discarded columns 26..31 read column 17's pixels
+                            // (same addresses: a broadcast, no extra bank traffic)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int kidx = u * 16 + lr;
-      const bool nv = kidx < 25;
-      const int nb = nv ? (kidx / 5) * XP + kidx % 5 : 0;
-      xw[u] = nv ? ((kidx % 5) & 1 ? &S.x1[0][0] - 1 : &S.x[0][0]) + nb : (kidx == 25 ? &S.xone[0][0] : &S.x[0][0]);
+      const int k0 = u * 16 + lr, kidx = k0 > 25 ? 17 : k0;
+      const int nb = (kidx / 5) * XP + kidx % 5;
+      xw[u] = kidx == 25 ? &S.xone[0][0] : ((kidx % 5) & 1 ? &S.x1[0][0] - 1 : &S.x[0][0]) + nb;
     }
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     const int co = lr;
