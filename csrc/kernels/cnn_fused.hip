@@ -731,14 +731,17 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
     // B gathers: the 8 consecutive u16 of a fragment start at a 2-byte-aligned address, so they are read as the
     // 5 aligned words covering them and funnel-shifted (v_alignbyte) when the start is odd -- one 16-byte read
     // there would be an unaligned LDS access (64 cycles), 8 masked u16 reads cost an exec round trip each
+    // (columns kidx >= K2 and rows co >= C2 of the outputs are never stored: their lanes read real, finite
+    // operands -- offset 0 / channel C2 - 1 -- instead of selecting zeros every k-step)
     int nb[NT2];
-    bool nv[NT2];
 #pragma unroll
     for (int u = 0; u < NT2; ++u) {
       const int kidx = (wid * NT2 + u) * 16 + lr, ci = kidx / 25, r = kidx - ci * 25, ky = r / 5, kx = r - ky * 5;
-      nv[u] = kidx < K2;
-      nb[u] = nv[u] ? ci * RP16 + ky * P1 + kx : 0;
+      nb[u] = kidx < K2 ? ci * RP16 + ky * P1 + kx : 0;
     }
+    const uint16_t* arow[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) arow[mt] = &S.d2[0][min(mt * 16 + lr, C2 - 1)][0];
     f32x4 acc[2][NT2];
 #pragma unroll
     for (int u = 0; u < NT2; ++u) acc[0][u] = acc[1][u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -746,23 +749,19 @@ __global__ __launch_bounds__(T) void k_cnn_train(const float* __restrict__ image
       const int im = ks >> 1, y = (ks & 1) * 4 + lg;  // this lane's 8 positions: row y, x = 0..7
       u16x8 a[2];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const int co = mt * 16 + lr;  // rows 20..31 read the zero block
-        a[mt] = *reinterpret_cast<const u16x8*>(co < C2 ? &S.d2[im][co][y * O2] : &S.zero16[0]);
-      }
+      for (int mt = 0; mt < 2; ++mt) a[mt] = *reinterpret_cast<const u16x8*>(arow[mt] + im * C2 * D2R + y * O2);
 #pragma unroll
       for (int u = 0; u < NT2; ++u) {
-        const int e0 = nb[u] + y * P1;  // first element (kidx >= K2: offset 0, masked below)
+        const int e0 = nb[u] + y * P1;  // first element
         // (index arithmetic, not pointer casts: the loads must stay LDS loads, not generic flat ones)
         const uint32_t* wp = reinterpret_cast<const uint32_t*>(&S.r1[im][0]) + (e0 >> 1);
         const uint32_t sh = static_cast<uint32_t>(e0 & 1) * 2;  // 0 or 2 bytes
         uint32_t w[5];
 #pragma unroll
         for (int q = 0; q < 5; ++q) w[q] = wp[q];
-        const uint32_t msk = nv[u] ? 0xFFFFFFFFu : 0u;
         u32x4 v;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh) & msk;
+        for (int q = 0; q < 4; ++q) v[q] = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);
         const u16x8 b = __builtin_bit_cast(u16x8, v);
         acc[0][u] = mfma(a[0], b, acc[0][u]);
         acc[1][u] = mfma(a[1], b, acc[1][u]);
