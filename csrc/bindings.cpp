@@ -1094,9 +1094,9 @@ Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, 
   pde::XgmiView xv{};
   const bool have_xv = xgmi_view.has_value();
   if (have_xv) {  // XgmiAllreduce.view(): base[8], state, timeout_ticks, flag_bytes, slot_bytes, rank, size, blocks,
-                  // read_delay_ticks
+                  // read_delay_ticks, host
     const auto& w = *xgmi_view;
-    TORCH_CHECK(w.size() == pde::kXgmiMaxRanks + 8, "cnn_train: malformed xgmi view");
+    TORCH_CHECK(w.size() == pde::kXgmiMaxRanks + 9, "cnn_train: malformed xgmi view");
     for (int r = 0; r < pde::kXgmiMaxRanks; ++r) xv.base[r] = reinterpret_cast<char*>(w[r]);
     xv.state = reinterpret_cast<uint32_t*>(w[8]);
     xv.timeout_ticks = static_cast<uint64_t>(w[9]);
@@ -1106,6 +1106,7 @@ Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, 
     xv.size = static_cast<int>(w[13]);
     xv.blocks = static_cast<int>(w[14]);
     xv.read_delay_ticks = static_cast<uint64_t>(w[15]);
+    xv.host = reinterpret_cast<uint32_t*>(w[16]);
     TORCH_CHECK(!accumulate, "cnn_train: the xGMI gradient exchange replaces accumulation");
   }
   CHECK_F32(images); CHECK_F32(params); CHECK_F32(grads);

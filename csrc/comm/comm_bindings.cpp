@@ -60,11 +60,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("parent"), py::arg("exclude"), py::arg("abort_parent") = false)
       .def_static("shrink_supported", &RcclComm::shrink_supported)
       .def("split_from",
-           [](RcclComm& c, RcclComm& parent, int color, int key) {
+           [](RcclComm& c, RcclComm& parent, int color, int key, double timeout_s) {
              py::gil_scoped_release nogil;
-             return c.split_from(parent, color, key);
+             return c.split_from(parent, color, key, timeout_s);
            },
-           py::arg("parent"), py::arg("color"), py::arg("key"))
+           py::arg("parent"), py::arg("color"), py::arg("key"), py::arg("timeout_s") = 300.0)
       .def("destroy", [](RcclComm& c) { py::gil_scoped_release nogil; c.destroy(); })
       .def_property_readonly("valid", &RcclComm::valid)
       .def_property_readonly("rank", &RcclComm::rank)
@@ -160,10 +160,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              w.push_back(v.size);
              w.push_back(v.blocks);
              w.push_back(static_cast<int64_t>(v.read_delay_ticks));
+             w.push_back(reinterpret_cast<int64_t>(v.host));
              return w;
            })
       .def("set_read_delay_us", &XgmiAllreduce::set_read_delay_us)
-      .def("error", [](XgmiAllreduce& x) { py::gil_scoped_release nogil; return x.error(); })
+      .def("error", [](XgmiAllreduce& x, bool sync) { py::gil_scoped_release nogil; return x.error(sync); },
+           py::arg("sync") = true)
+      .def("clear_error", [](XgmiAllreduce& x) { py::gil_scoped_release nogil; x.clear_error(); })
+      .def("abort", &XgmiAllreduce::abort)
+      .def("reset_abort", &XgmiAllreduce::reset_abort)
+      .def_property_readonly("aborted", &XgmiAllreduce::aborted)
       .def("close", [](XgmiAllreduce& x) { py::gil_scoped_release nogil; x.close(); })
       .def_property_readonly("rank", &XgmiAllreduce::rank)
       .def_property_readonly("size", &XgmiAllreduce::size)
@@ -200,6 +206,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("allreduce_inline", &FusionEngine::allreduce_inline, py::arg("tensors"), py::arg("op"),
            py::arg("prescale") = 1.0, py::arg("postscale") = 1.0, py::arg("compress") = false)
       .def("cached", &FusionEngine::cached)
+      .def("set_graph_mode", &FusionEngine::set_graph_mode, py::arg("on"), py::arg("tensors"))
+      .def("check_xgmi", &FusionEngine::check_xgmi)
       .def("set_py_backend", &FusionEngine::set_py_backend)
       .def("set_control", &FusionEngine::set_control, py::arg("process_group"))
       .def("set_timeout", &FusionEngine::set_timeout)

@@ -167,7 +167,7 @@ int RcclComm::shrink_from(RcclComm& parent, const std::vector<int>& exclude, boo
   return 2;
 }
 
-bool RcclComm::split_from(RcclComm& parent, int color, int key) {
+bool RcclComm::split_from(RcclComm& parent, int color, int key, double timeout_s) {
   if (parent.comm_ == nullptr) throw std::runtime_error("pde rccl: split from an invalid communicator");
   if (comm_ != nullptr) abort();
   hip_check(hipSetDevice(parent.device_), "hipSetDevice");
@@ -176,9 +176,32 @@ bool RcclComm::split_from(RcclComm& parent, int color, int key) {
     hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priority range");
     hip_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "comm stream");
   }
+  // non-blocking: a member that dies between the control-plane agreement and the split would otherwise
+  // hang every survivor inside ncclCommSplit; here the split is polled against the round's timeout and
+  // aborted on expiry (the caller turns the exception into a peer failure and re-wires)
   ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
   ncclComm_t out = nullptr;
-  check(ncclCommSplit(parent.comm_, color < 0 ? NCCL_SPLIT_NOCOLOR : color, key, &out, &cfg), "ncclCommSplit");
+  ncclResult_t r = ncclCommSplit(parent.comm_, color < 0 ? NCCL_SPLIT_NOCOLOR : color, key, &out, &cfg);
+  check(r, "ncclCommSplit");
+  if (out != nullptr) {
+    const auto t0 = std::chrono::steady_clock::now();
+    ncclResult_t st = ncclInProgress;
+    for (;;) {
+      ncclCommGetAsyncError(out, &st);
+      if (st != ncclInProgress) break;
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+        ncclCommAbort(out);
+        throw std::runtime_error("pde rccl: ncclCommSplit did not complete within " + std::to_string(timeout_s) +
+                                 " s (a member is gone)");
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    if (st != ncclSuccess) {
+      ncclCommAbort(out);
+      check(st, "ncclCommSplit(async)");
+    }
+  }
   comm_ = out;
   device_ = parent.device_;
   if (comm_ == nullptr) return false;

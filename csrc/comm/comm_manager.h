@@ -42,7 +42,8 @@ class RcclComm {
   // Planned membership change with every parent rank alive (elastic scale-down): ncclCommSplit over the
   // parent, collective over ALL parent ranks.  color < 0 = leaving (NCCL_SPLIT_NOCOLOR: no communicator,
   // returns false); `key` orders the ranks of the child.  No unique-id exchange, topology reused.
-  bool split_from(RcclComm& parent, int color, int key);
+  // bounded: a split that does not complete within timeout_s (a member died) is aborted and throws
+  bool split_from(RcclComm& parent, int color, int key, double timeout_s = 300.0);
   void destroy();  // ncclCommDestroy after a clean finish
   bool valid() const { return comm_ != nullptr; }
   int rank() const { return rank_; }

@@ -250,6 +250,7 @@ at::Tensor FusionEngine::wait(int64_t h) {
           std::lock_guard<std::mutex> g(mu_);
           if (!error_.empty()) err = error_;
         }
+        if (err.empty()) err = xgmi_failure();
         if (err.empty() && comm_) {
           const int ae = comm_->async_error();
           if (ae != ncclSuccess && ae != ncclInProgress) err = std::string("RCCL async error: ") +
@@ -381,12 +382,68 @@ void FusionEngine::set_error(const std::string& err) {
     if (error_.empty()) error_ = err;
     fail_all_locked(error_);
   }
-  // release any collective hung on a dead peer (kernels spinning on a connection exit on abort)
+  // release any collective hung on a dead peer (kernels spinning on a connection exit on abort; xGMI
+  // exchanges give up on the host abort word)
   if (comm_) comm_->abort();
+  if (xgmi_) xgmi_->abort();
+}
+
+std::string FusionEngine::xgmi_failure() {
+  if (xgmi_ && xgmi_->error(false) != 0)
+    return "xGMI peer exchange: a wait for a peer timed out (peer dead or stalled); its result was dropped";
+  return std::string();
+}
+
+void FusionEngine::check_xgmi() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!error_.empty()) throw std::runtime_error("HorovodInternalError: " + error_);
+  }
+  const std::string err = xgmi_failure();
+  if (!err.empty()) {
+    set_error(err);
+    throw std::runtime_error("HorovodInternalError: " + err);
+  }
+}
+
+void FusionEngine::set_graph_mode(bool on, const std::vector<at::Tensor>& tensors) {
+  int64_t need = 0;
+  for (const auto& t : tensors) need += t.numel() * 4;  // fp32 staging covers every wire format
+  if (on && !tensors.empty() && tensors.front().is_cuda() && need > 0) {
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(tensors.front().device());
+    if (!inline_fused_.defined() || inline_fused_.numel() < need)
+      inline_fused_ = at::empty({need + 4096}, tensors.front().options().dtype(at::kByte));
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    graph_mode_ = on;
+  }
+  cv_.notify_all();
+}
+
+void FusionEngine::ensure_stage(at::Tensor& stage, const at::Tensor& like, int64_t bytes, hipStream_t s,
+                                bool inline_mode) {
+  if (stage.defined() && stage.device() == like.device() && stage.numel() >= bytes) return;
+  if (inline_mode) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    hip_ok(hipStreamIsCapturing(s, &st), "capture status");
+    // growing here would synchronise a capturing stream (breaking the capture) or free storage an earlier
+    // capture still points at: graph mode sizes its buffer up front (set_graph_mode)
+    TORCH_CHECK(st == hipStreamCaptureStatusNone && !stage.defined(),
+                "fusion engine: graph-mode staging buffer too small (", bytes,
+                " B); call set_graph_mode with the gradient set before capturing");
+  } else if (stage.defined()) {
+    hip_ok(hipStreamSynchronize(s), "sync before regrow");
+  }
+  stage = at::empty({bytes + (1 << 20)}, like.options().dtype(at::kByte));
 }
 
 void FusionEngine::check_inflight() {
-  if (inflight_.empty()) return;
+  if (inflight_.empty()) {
+    const std::string e = xgmi_failure();
+    if (!e.empty()) set_error(e);
+    return;
+  }
   std::string err;
   size_t k = 0;
   for (auto& f : inflight_) {
@@ -401,6 +458,7 @@ void FusionEngine::check_inflight() {
     inflight_[k++] = f;
   }
   inflight_.resize(k);
+  if (err.empty()) err = xgmi_failure();
   if (err.empty() && comm_ && !inflight_.empty()) {
     const int ae = comm_->async_error();
     if (ae != ncclSuccess && ae != ncclInProgress)
@@ -425,7 +483,7 @@ void FusionEngine::loop() {
       // tensor blocks in the control-plane all-gather until every peer joins the cycle, so an idle peer
       // (running eval, writing a checkpoint) must keep taking part -- Horovod's background loop does the
       // same.  Idle cycles back off to idle_ms_ so an idle job costs one small all-gather per few ms.
-      const bool lockstep = size_ > 1 && control_ && error_.empty();
+      const bool lockstep = size_ > 1 && control_ && error_.empty() && !graph_mode_;
       if (!has_work()) {
         if (lockstep)
           cv_.wait_for(lk, std::chrono::microseconds(static_cast<int64_t>(idle_ms_ * 1e3)), has_work);
@@ -741,7 +799,7 @@ void FusionEngine::execute(Batch& b) {
     if (gpu) {
       hip_ok(hipSetDevice(r0.tensor.device().index()), "set device");
       if (r0.type == ReqType::ALLREDUCE) {
-        run_allreduce_gpu(b, engine_stream());
+        run_allreduce_gpu(b, engine_stream(), fused_, false);
       } else if (comm_) {
         TORCH_CHECK(comm_->valid(), "RCCL communicator is not valid (aborted?)");
         run_single_gpu(b.reqs.front());
@@ -795,7 +853,7 @@ static bool adjacent_inplace(const Batch& b) {
   return true;
 }
 
-void FusionEngine::run_allreduce_gpu(Batch& b, hipStream_t s) {
+void FusionEngine::run_allreduce_gpu(Batch& b, hipStream_t s, at::Tensor& stage, bool inline_mode) {
   const int dev = b.reqs.front().tensor.device().index();
   for (auto& r : b.reqs)
     if (r.ready) hip_ok(hipStreamWaitEvent(s, r.ready, 0), "wait producer");
@@ -813,10 +871,7 @@ void FusionEngine::run_allreduce_gpu(Batch& b, hipStream_t s) {
       float* p = static_cast<float*>(r0.tensor.data_ptr());
       xgmi_->allreduce(p, p, total, scale, s, r0.compress);
     } else {
-      if (!fused_.defined() || fused_.device() != r0.tensor.device() || fused_.numel() < total * 4) {
-        if (fused_.defined()) hip_ok(hipStreamSynchronize(s), "sync before regrow");
-        fused_ = at::empty({total * 4 + (1 << 20)}, r0.tensor.options().dtype(at::kByte));
-      }
+      ensure_stage(stage, r0.tensor, total * 4, s, inline_mode);
       PackTable tab;
       int64_t off = 0;
       size_t i = 0;
@@ -834,9 +889,9 @@ void FusionEngine::run_allreduce_gpu(Batch& b, hipStream_t s) {
         }
         (void)off0;
         (void)first;
-        hip_ok(fusion_pack(tab, fused_.data_ptr(), 0, 1.0f, s), "pack");
+        hip_ok(fusion_pack(tab, stage.data_ptr(), 0, 1.0f, s), "pack");
       }
-      float* f = static_cast<float*>(fused_.data_ptr());
+      float* f = static_cast<float*>(stage.data_ptr());
       xgmi_->allreduce(f, f, total, scale, s, r0.compress);
       off = 0;
       i = 0;
@@ -850,7 +905,7 @@ void FusionEngine::run_allreduce_gpu(Batch& b, hipStream_t s) {
           sg.ptr = b.reqs[i].output.data_ptr();
           off += sg.n;
         }
-        hip_ok(fusion_unpack(tab, fused_.data_ptr(), 0, 1.0f, s), "unpack");
+        hip_ok(fusion_unpack(tab, stage.data_ptr(), 0, 1.0f, s), "unpack");
       }
     }
     for (auto& r : b.reqs) {
@@ -874,10 +929,7 @@ void FusionEngine::run_allreduce_gpu(Batch& b, hipStream_t s) {
   TORCH_CHECK(dt == 0 || dt == 1, "fusion engine: fused batches support fp32/bf16 tensors");
   const int wire = (r0.compress || dt == 1) ? 1 : 0;
   const int64_t need = total * (wire == 1 ? 2 : 4);
-  if (!fused_.defined() || fused_.device() != r0.tensor.device() || fused_.numel() < need) {
-    if (fused_.defined()) hip_ok(hipStreamSynchronize(s), "sync before regrow");
-    fused_ = at::empty({need + (1 << 20)}, r0.tensor.options().dtype(at::kByte));
-  }
+  ensure_stage(stage, r0.tensor, need, s, inline_mode);
   // pack (pre-scale) in chunks of kMaxPackSegs tensors
   PackTable tab;
   auto each_chunk = [&](auto&& fn) {
@@ -899,12 +951,12 @@ void FusionEngine::run_allreduce_gpu(Batch& b, hipStream_t s) {
   const float pre = static_cast<float>(r0.prescale), post = static_cast<float>(r0.postscale);
   each_chunk([&](size_t first) {
     for (int k = 0; k < tab.count; ++k) tab.seg[k].ptr = b.reqs[first + k].tensor.data_ptr();
-    hip_ok(fusion_pack(tab, fused_.data_ptr(), wire, pre, s), "pack");
+    hip_ok(fusion_pack(tab, stage.data_ptr(), wire, pre, s), "pack");
   });
-  comm_->allreduce(fused_.data_ptr(), fused_.data_ptr(), total, wire, r0.op, s);
+  comm_->allreduce(stage.data_ptr(), stage.data_ptr(), total, wire, r0.op, s);
   each_chunk([&](size_t first) {
     for (int k = 0; k < tab.count; ++k) tab.seg[k].ptr = b.reqs[first + k].output.data_ptr();
-    hip_ok(fusion_unpack(tab, fused_.data_ptr(), wire, post, s), "unpack");
+    hip_ok(fusion_unpack(tab, stage.data_ptr(), wire, post, s), "unpack");
   });
   for (auto& r : b.reqs) {
     record_on(r.tensor, s, dev);
@@ -953,7 +1005,7 @@ void FusionEngine::allreduce_inline(const std::vector<at::Tensor>& tensors, int 
   }
   hipStream_t s = at::hip::getCurrentHIPStream(tensors.front().device().index()).stream();
   std::vector<Batch> batches = make_batches(reqs);
-  for (auto& b : batches) run_allreduce_gpu(b, s);
+  for (auto& b : batches) run_allreduce_gpu(b, s, inline_fused_, true);
 }
 
 void FusionEngine::run_single_gpu(Request& r) {

@@ -121,6 +121,14 @@ class FusionEngine {
   // stream, without negotiation -- the caller guarantees every rank makes the same call (cached tensor set)
   void allreduce_inline(const std::vector<at::Tensor>& tensors, int op, double prescale, double postscale,
                         bool compress);
+  // graph mode on: (1) the idle loop parks on its condition variable instead of cycling the lockstep bit
+  // all-reduce (the captured step bypasses the engine; every rank wakes when it enqueues again -- SPMD, as
+  // allreduce_inline already requires); (2) `tensors` size the inline staging buffer ONCE, so a replayed
+  // graph never points at storage a later regrow frees
+  void set_graph_mode(bool on, const std::vector<at::Tensor>& tensors);
+  // graph mode's health check (replays bypass the engine thread): a timed-out xGMI exchange puts the engine
+  // into the error state and raises HorovodInternalError; a plain host read, no device sync
+  void check_xgmi();
   bool cached(const std::string& name) {
     std::lock_guard<std::mutex> g(mu_);
     return cache_.count(name) > 0;
@@ -153,7 +161,10 @@ class FusionEngine {
   void loop();
   void negotiate(std::vector<Request>& announce, std::vector<Request>& ready, bool& stop);
   void execute(Batch& b);
-  void run_allreduce_gpu(Batch& b, hipStream_t s);
+  // stage: the fusion buffer to use (the engine thread's fused_, or graph mode's inline_fused_, which may
+  // not grow while the stream is capturing)
+  void run_allreduce_gpu(Batch& b, hipStream_t s, at::Tensor& stage, bool inline_mode);
+  void ensure_stage(at::Tensor& stage, const at::Tensor& like, int64_t bytes, hipStream_t s, bool inline_mode);
   void single_gpu_via_host(Request& r);
   hipStream_t engine_stream();  // the RCCL communicator's stream, else one of the engine's own
   void run_allreduce_cpu(Batch& b);
@@ -163,6 +174,7 @@ class FusionEngine {
   void fail_all_locked(const std::string& err);
   void set_error(const std::string& err);
   void check_inflight();
+  std::string xgmi_failure();  // non-empty once the attached xGMI exchange reported a timed-out wait
   std::vector<Batch> make_batches(std::vector<Request>& ready);
   double now() const;
   void trace(const std::string& name, const std::string& phase, double t0, double t1, int64_t bytes);
@@ -203,7 +215,9 @@ class FusionEngine {
   bool stopped_ = false;
   std::string error_;
   std::thread worker_;
-  at::Tensor fused_;  // reusable fusion buffer (device or host)
+  at::Tensor fused_;  // reusable fusion buffer (device or host), engine thread only
+  at::Tensor inline_fused_;  // graph mode's staging buffer (caller's stream), sized by set_graph_mode
+  bool graph_mode_ = false;
   std::vector<Inflight> inflight_;
 
   // stats

@@ -46,7 +46,18 @@ class XgmiAllreduce {
   XgmiView view() const;  // device view for kernels that fold the exchange in (xgmi_device.h)
   // test hook: every workgroup of this rank stalls `us` microseconds between its flag wait and its peer reads
   void set_read_delay_us(double us) { read_delay_ticks_ = static_cast<uint64_t>(us * 100.0); }
-  int error();   // 0, or 1 when some workgroup timed out waiting for a peer (synchronises the device)
+  // 0, or 1 when some workgroup timed out waiting for a peer (or gave up on the host's abort word).
+  // sync: wait for the device first (every queued call has run); otherwise a plain read of the host-mapped
+  // status word -- cheap enough for a per-step check or a watchdog thread.
+  int error(bool sync = true);
+  // reset the error words after the host has handled a failure (synchronises the device: no call is in
+  // flight while the device-side fail-fast word is cleared)
+  void clear_error();
+  // host-side abort: every current and later peer wait gives up within ~0.1 ms (its result is dropped and
+  // the error word set) until reset_abort(); safe from any thread while kernels spin
+  void abort();
+  void reset_abort();
+  bool aborted() const;
   void close();
   int rank() const { return rank_; }
   int size() const { return size_; }
@@ -60,6 +71,8 @@ class XgmiAllreduce {
   uint64_t read_delay_ticks_ = 0;
   char* local_ = nullptr;       // my exported allocation
   uint32_t* state_ = nullptr;   // kXgmiStateWords: call epoch, done count, error word (device-local)
+  uint32_t* host_ = nullptr;    // kXgmiHostWords, pinned host memory mapped into the device (status / abort)
+  uint32_t* host_dev_ = nullptr;  // its device-side address
   std::vector<char*> peers_;    // mapped bases, peers_[rank_] == local_
   bool opened_ = false;
   int64_t calls_ = 0;

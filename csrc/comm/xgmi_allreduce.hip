@@ -173,6 +173,13 @@ XgmiAllreduce::XgmiAllreduce(int rank, int size, int device, int64_t max_bytes, 
   hip_check(hipMalloc(&st, kXgmiStateWords * 4), "hipMalloc state");
   state_ = static_cast<uint32_t*>(st);
   hip_check(hipMemset(state_, 0, kXgmiStateWords * 4), "zero state");
+  void* hp = nullptr;
+  hip_check(hipHostMalloc(&hp, kXgmiHostWords * 4, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+  host_ = static_cast<uint32_t*>(hp);
+  std::memset(host_, 0, kXgmiHostWords * 4);
+  void* hd = nullptr;
+  hip_check(hipHostGetDevicePointer(&hd, hp, 0), "hipHostGetDevicePointer");
+  host_dev_ = static_cast<uint32_t*>(hd);
   hip_check(hipDeviceSynchronize(), "sync after init");  // flags are zero before any peer can map them
   peers_.assign(size, nullptr);
   peers_[rank] = local_;
@@ -243,6 +250,7 @@ XgmiView XgmiAllreduce::view() const {
   XgmiView v{};
   for (int r = 0; r < size_; ++r) v.base[r] = peers_[r];
   v.state = state_;
+  v.host = host_dev_;
   v.timeout_ticks = timeout_ticks_;
   v.read_delay_ticks = read_delay_ticks_;
   v.flag_bytes = flag_bytes_;
@@ -253,12 +261,34 @@ XgmiView XgmiAllreduce::view() const {
   return v;
 }
 
-int XgmiAllreduce::error() {
-  uint32_t e = 0;
+int XgmiAllreduce::error(bool sync) {
+  if (host_ == nullptr) return 0;
+  if (sync) {
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    hip_check(hipDeviceSynchronize(), "sync");
+  }
+  return __atomic_load_n(host_ + kXgmiHostError, __ATOMIC_ACQUIRE) != 0u ? 1 : 0;
+}
+
+void XgmiAllreduce::clear_error() {
+  if (host_ == nullptr) return;
   hip_check(hipSetDevice(device_), "hipSetDevice");
   hip_check(hipDeviceSynchronize(), "sync");
-  hip_check(hipMemcpy(&e, state_ + kXgmiStateError, 4, hipMemcpyDeviceToHost), "read error word");
-  return static_cast<int>(e);
+  hip_check(hipMemset(state_ + kXgmiStateError, 0, 4), "clear error word");
+  hip_check(hipDeviceSynchronize(), "sync");
+  __atomic_store_n(host_ + kXgmiHostError, 0u, __ATOMIC_RELEASE);
+}
+
+void XgmiAllreduce::abort() {
+  if (host_ != nullptr) __atomic_store_n(host_ + kXgmiHostAbort, 1u, __ATOMIC_RELEASE);
+}
+
+void XgmiAllreduce::reset_abort() {
+  if (host_ != nullptr) __atomic_store_n(host_ + kXgmiHostAbort, 0u, __ATOMIC_RELEASE);
+}
+
+bool XgmiAllreduce::aborted() const {
+  return host_ != nullptr && __atomic_load_n(host_ + kXgmiHostAbort, __ATOMIC_ACQUIRE) != 0u;
 }
 
 void XgmiAllreduce::close() {
@@ -270,8 +300,10 @@ void XgmiAllreduce::close() {
   peers_.clear();
   (void)hipFree(local_);
   (void)hipFree(state_);
+  if (host_ != nullptr) (void)hipHostFree(host_);
   local_ = nullptr;
   state_ = nullptr;
+  host_ = host_dev_ = nullptr;
   opened_ = false;
 }
 

@@ -36,7 +36,8 @@ __device__ __forceinline__ float* xgmi_slot(const XgmiView& v, int r, uint32_t e
 // Block-collective, after every thread issued its stores into xgmi_slot(v, v.rank, epoch):
 //   every storing wave drains, the workgroup meets, one lane releases at system scope, one lane per rank
 //   raises flag (b, my rank) in that rank's flag array; one lane per rank polls my flag (b, r) until it
-//   reaches the epoch (bounded by wall clock: a timeout sets the error word and the result is dropped),
+//   reaches the epoch (bounded by wall clock or the host's abort word: a timeout sets the error words -- the
+//   device one for fail-fast, the host-mapped one the host polls without a sync -- and the result is dropped),
 //   then one lane acquires at system scope and the workgroup meets again.
 // Returns true when every rank's chunk of workgroup b may be read.
 __device__ __forceinline__ bool xgmi_publish_and_wait(const XgmiView& v, int b, uint32_t epoch, int* s_fail) {
@@ -54,13 +55,22 @@ __device__ __forceinline__ bool xgmi_publish_and_wait(const XgmiView& v, int b, 
     __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t* mine = reinterpret_cast<uint32_t*>(v.base[v.rank]) + b * kXgmiMaxRanks + tid;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t polls = 0;
     while (static_cast<int32_t>(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-      // fail fast once any wait of this instance timed out (the error word stays set until the host reads and
-      // resets it at a commit point): a dead peer costs ONE timeout, not one per queued call of a graph replay
-      if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks ||
-          __hip_atomic_load(v.state + kXgmiStateError, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+      // Give up on: the wall-clock bound; an earlier timed-out wait of this instance (fail fast: a dead peer
+      // costs ONE timeout, not one per queued call of a graph replay -- the word is cleared by the host's
+      // check at its next sync point, XgmiAllreduce::clear_error); or the host's abort word (an elastic
+      // driver published a new round / the engine failed), polled over PCIe every 64th spin.
+      bool give_up = __builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks ||
+                     __hip_atomic_load(v.state + kXgmiStateError, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+      if (!give_up && v.host != nullptr && (++polls & 63u) == 0u)
+        give_up = __hip_atomic_load(v.host + kXgmiHostAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+      if (give_up) {
         *s_fail = 1;
         __hip_atomic_store(v.state + kXgmiStateError, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // (a plain system-scope store, not an atomic: PCIe atomics to host memory are not assumed)
+        if (v.host != nullptr) __hip_atomic_store(v.host + kXgmiHostError, epoch + 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(2);

@@ -194,7 +194,10 @@ class RoundComm:
             return ("leave", None) if leaving else ("none", None)
         child = self._comm_cls()()
         try:
-            made = child.split_from(self.rccl, -1 if leaving else 0, 0 if leaving else members.index(rdzv.wid))
+            # bounded by the round's timeout (non-blocking ncclCommSplit polled on the host): a member that dies
+            # between the agreement above and the split turns into a PeerFailure, not a hang
+            made = child.split_from(self.rccl, -1 if leaving else 0, 0 if leaving else members.index(rdzv.wid),
+                                    timeout_s=self.timeout_s)
         except RuntimeError as exc:
             raise PeerFailure(str(exc)) from exc
         if leaving or not made:

@@ -27,6 +27,7 @@ where one exists):
 """
 from __future__ import annotations
 
+import contextlib
 import datetime
 import os
 import threading
@@ -169,7 +170,10 @@ def init(comm=None, device: str | None = None):
             comm.init(uid, _ctx.rank, _ctx.size, _ctx.device.index, True)
             eng.set_rccl(comm)
             _ctx.comm = comm
-        if _ctx.size > 1 and plane in ("auto", "xgmi"):
+        # the one-shot exchange maps every peer's buffer over IPC: one node only (a multi-host job stays on
+        # RCCL, whose transport spans hosts)
+        single_node = _ctx.local_size == _ctx.size
+        if _ctx.size > 1 and (plane == "xgmi" or (plane == "auto" and single_node)):
             # latency-bound fused batches (the CNN's 87 KB of gradients) take the one-shot peer exchange
             from ..parallel.xgmi_allreduce import DEFAULT_THRESHOLD, XgmiAllreduce
 
@@ -444,14 +448,16 @@ def join(device=-1) -> int:
     """Barrier; returns the last rank to join (Horovod semantics for uneven inputs, simplified)."""
     _need()
     t = torch.tensor([_ctx.rank], dtype=torch.float32)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=_ctx.group)
+    with _control_plane("join"):
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=_ctx.group)
     return int(t.item())
 
 
 def barrier():
     _need()
     if _ctx.size > 1:
-        dist.barrier(group=_ctx.group)
+        with _control_plane("barrier"):
+            dist.barrier(group=_ctx.group)
 
 
 def broadcast_object(obj, root_rank=0, name=None):
@@ -459,15 +465,46 @@ def broadcast_object(obj, root_rank=0, name=None):
     if _ctx.size == 1:
         return obj
     lst = [obj if _ctx.rank == root_rank else None]
-    dist.broadcast_object_list(lst, src=root_rank, group=_ctx.group)
+    with _control_plane("broadcast_object"):
+        dist.broadcast_object_list(lst, src=root_rank, group=_ctx.group)
     return lst[0]
 
 
 def allgather_object(obj, name=None):
     _need()
     out = [None] * _ctx.size
-    dist.all_gather_object(out, obj, group=_ctx.group)
+    with _control_plane("allgather_object"):
+        dist.all_gather_object(out, obj, group=_ctx.group)
     return out
+
+
+@contextlib.contextmanager
+def _control_plane(what: str):
+    """Failures of the gloo control plane are peer failures by construction (a dead or unreachable rank:
+    connection reset, closed pair, store timeout): typed as HorovodInternalError HERE, at the source, so
+    ``hvd.elastic.run`` never has to guess from message text."""
+    try:
+        yield
+    except HorovodInternalError:
+        raise
+    except (RuntimeError, ConnectionError, TimeoutError) as exc:  # c10d DistError subclasses RuntimeError
+        raise HorovodInternalError(f"control plane ({what}): {str(exc).splitlines()[0] if str(exc) else exc!r}") \
+            from exc
+
+
+def check_health():
+    """Raise HorovodInternalError if the GPU data plane reported a failure that no engine cycle saw: a
+    timed-out xGMI exchange inside a replayed graph (graph mode bypasses the engine thread).  A plain read
+    of host-mapped status words: call it at every commit / step boundary."""
+    _need()
+    _enqueue(_ctx.engine.check_xgmi)
+
+
+def set_graph_mode(on: bool, tensors=()):
+    """Engine side of :meth:`DistributedOptimizer.enable_graph_mode`: size the inline staging buffer once
+    for ``tensors`` and park the idle negotiation loop (no lockstep bit all-reduces while replays run)."""
+    _need()
+    _ctx.engine.set_graph_mode(bool(on), list(tensors))
 
 
 def allreduce_inline_(tensors, op=ReduceOp.Average, prescale_factor=1.0, postscale_factor=1.0,
@@ -477,8 +514,8 @@ def allreduce_inline_(tensors, op=ReduceOp.Average, prescale_factor=1.0, postsca
     same call with the same tensors in the same order -- what a cached (already negotiated) tensor set
     guarantees; :meth:`DistributedOptimizer.enable_graph_mode` checks that first."""
     _need()
-    _ctx.engine.allreduce_inline(list(tensors), int(op), float(prescale_factor), float(postscale_factor),
-                                 bool(compression_bf16))
+    _enqueue(_ctx.engine.allreduce_inline, list(tensors), int(op), float(prescale_factor), float(postscale_factor),
+             bool(compression_bf16))
 
 
 def is_cached(name: str) -> bool:

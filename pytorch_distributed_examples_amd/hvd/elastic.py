@@ -5,9 +5,13 @@ Used by the reference at horovod/horovod_mnist_elastic.py:55,72,80-82,104-106.
 * ``TorchState(model, optimizer, **kw)`` keeps an in-memory commit of the model/optimizer state dicts and
   the extra attributes (``batch``, ``epoch``).  Commits are DEVICE-resident clones (an MI355X has 288 GB
   of HBM; a clone is one D2D copy instead of a PCIe round trip) -- ``restore()`` copies them back.
-* ``commit()`` = ``save()`` + ``check_host_updates()`` (raises :class:`HostsUpdatedInterrupt` when the
-  elastic driver published a membership change).
+* ``commit()`` = ``core.check_health()`` (a timed-out xGMI exchange inside a replayed graph raises
+  :class:`HorovodInternalError` BEFORE the suspect state is saved) + ``save()`` + ``check_host_updates()``
+  (raises :class:`HostsUpdatedInterrupt` when the elastic driver published a membership change).
 * ``sync()`` broadcasts the state from the new rank 0 (always a survivor holding the latest commit).
+* Failures are TYPED at their source (no message matching): the engine, ``core.check_health()`` and every
+  gloo control-plane call (``core._control_plane``) raise :class:`HorovodInternalError`; any other exception
+  is a bug and propagates.
 * ``@run`` retries ``func(state)``: on :class:`HorovodInternalError` (a peer died mid-collective) it
   restores the last commit; on ``HostsUpdatedInterrupt`` it keeps the state; both then ``reset()``:
   in-process ``shutdown()`` + ``init()`` into the driver's next rendezvous round (new process group, new
@@ -39,6 +43,7 @@ class State:
             cb()
 
     def commit(self):
+        core.check_health()
         self.save()
         self.check_host_updates()
 
@@ -50,10 +55,8 @@ class State:
         # every rank must agree (a rank that saw the flag late would otherwise keep training alone)
         # gloo control plane (host tensor): a dead peer is a connection error here, not a hung GPU collective
         flag = torch.tensor([1.0 if updated else 0.0])
-        try:
+        with core._control_plane("check_host_updates"):  # a dead peer surfaces here, typed
             torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX, group=core._ctx.group)
-        except Exception as exc:  # noqa: BLE001 - a dead peer surfaces here
-            raise HorovodInternalError(str(exc)) from exc
         if flag.item() > 0:
             raise HostsUpdatedInterrupt(skip_sync=False)
 
@@ -146,12 +149,6 @@ def run(func):
                 skip_sync = False
             except HostsUpdatedInterrupt as e:
                 skip_sync = e.skip_sync
-            except RuntimeError as e:  # c10d errors from a dead peer during sync / control collectives
-                if "HorovodInternalError" not in str(e) and "Connection" not in str(e) and "closed" not in str(e) \
-                        and "timed out" not in str(e).lower():
-                    raise
-                state.restore()
-                skip_sync = False
             reset()
             state.on_reset()
 

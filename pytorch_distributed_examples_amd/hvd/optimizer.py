@@ -131,7 +131,16 @@ class _DistributedOptimizerMixin:
             missing = [n for n in self._param_names.values() if not core.is_cached(n)]
             if missing:
                 raise RuntimeError(f"graph mode needs a negotiated step first; not cached: {missing[:4]}")
+            # size the engine's inline staging buffer for this gradient set now (never while capturing) and
+            # park its idle negotiation loop: replays bypass it (health: core.check_health at commits)
+            core.set_graph_mode(True, [p.grad if p.grad is not None else p for p in self._param_names])
         self._graph = True
+        return self
+
+    def disable_graph_mode(self):
+        if self._graph and core.size() > 1:
+            core.set_graph_mode(False)
+        self._graph = False
         return self
 
     def _graph_synchronize(self):

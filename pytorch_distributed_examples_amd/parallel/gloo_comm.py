@@ -44,7 +44,7 @@ class GlooComm:
                                         datetime.timedelta(seconds=timeout_s))
         self.rank, self.size = rank, size
 
-    def split_from(self, parent: "GlooComm", color: int, key: int) -> bool:
+    def split_from(self, parent: "GlooComm", color: int, key: int, timeout_s: float = 300.0) -> bool:
         """ncclCommSplit semantics: every parent rank calls; ranks with ``color >= 0`` form the child ordered by
         ``key``; ``color < 0`` gets no communicator (returns False)."""
         if parent.pg is None:

@@ -33,7 +33,9 @@ DEFAULT_THRESHOLD = int(os.environ.get("PDE_XGMI_THRESHOLD", str(1 << 20)))
 
 class XgmiAllreduce:
     def __init__(self, device: torch.device, group=None, max_bytes: int = 4 << 20, blocks: int = 256,
-                 timeout_s: float = 5.0, read_delay_us: float = 0.0, key: str | None = None):
+                 timeout_s: float | None = None, read_delay_us: float = 0.0, key: str | None = None):
+        if timeout_s is None:  # PDE_XGMI_TIMEOUT_S: the bounded peer wait (seconds)
+            timeout_s = float(os.environ.get("PDE_XGMI_TIMEOUT_S", "5.0"))
         assert device.type == "cuda", "the xGMI all-reduce is a GPU data plane"
         self.device = device
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -67,10 +69,28 @@ class XgmiAllreduce:
         epilogue: the fused CNN's gradient reduction (``FusedCNN.forward_backward(..., xgmi=self)``)."""
         return self.impl.view()
 
-    def check(self) -> None:
-        """Raise if any call timed out waiting for a peer (synchronises the device)."""
-        if self.impl.error():
+    def check(self, clear: bool = True) -> None:
+        """Raise if any call timed out waiting for a peer (or gave up on ``abort()``); synchronises the
+        device.  ``clear``: reset the error words first, so the instance is usable again once the caller has
+        handled the failure (re-synced the replicas) -- the device-side fail-fast word would otherwise make
+        every later call drop its result."""
+        if self.impl.error(True):
+            if clear:
+                self.impl.clear_error()
             raise RuntimeError("xGMI all-reduce: a workgroup timed out waiting for a peer's flag")
+
+    def failed(self) -> bool:
+        """Non-blocking: True once a queued call has timed out (a plain read of the host-mapped status word;
+        calls still in flight are not waited for).  Cheap enough for every step."""
+        return bool(self.impl.error(False))
+
+    def abort(self) -> None:
+        """Make every spinning and later peer wait give up at once (from any thread; e.g. the elastic
+        membership watcher when the driver publishes a new round)."""
+        self.impl.abort()
+
+    def reset_abort(self) -> None:
+        self.impl.reset_abort()
 
     def close(self):
         if self.impl is not None:
