@@ -1183,6 +1183,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("step") = py::none());
   m.def("clear_last_error", []() { return static_cast<int>(hipGetLastError()); },
         "Read and reset the HIP last-error state (after an aborted stream capture).");
+  m.def("graph_upload",
+        [](int64_t exec) {  // torch.cuda.CUDAGraph.raw_cuda_graph_exec(): upload the executable graph's launch
+                            // resources NOW (current stream), not inside the first timed replay
+          const hipError_t e = hipGraphUpload(reinterpret_cast<hipGraphExec_t>(exec),
+                                              cur_stream());
+          return static_cast<int>(e);
+        },
+        py::arg("exec"));
   m.def("cnn_frag_bytes", &pde::cnn_frag_bytes);
   m.def("cnn_num_params", &pde::cnn_num_params);
   m.def("cnn_smem_bytes", &pde::cnn_smem_bytes);

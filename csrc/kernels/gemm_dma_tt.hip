@@ -1,0 +1,11 @@
+// LDS-DMA GEMM kernels with K-contiguous A and K-contiguous B operands (gemm_device.h); a translation unit of its own so the
+// instantiations compile in parallel with gemm.hip.
+#include "gemm_device.h"
+
+namespace pde {
+
+bool dma_launch_tt(int cfg, int s64, dim3 grid, hipStream_t s, const GemmArgs& ka, int tm, int tn, int kps) {
+  return launch_dma_cfg<true, true>(cfg, s64, grid, s, ka, tm, tn, kps);
+}
+
+}  // namespace pde

@@ -27,7 +27,8 @@ ARCH = os.environ.get("PDE_OFFLOAD_ARCH", "gfx950")
 EXTENSIONS = {
     # module name -> (hip sources, host C++ sources)
     "_C": (
-        ["kernels/gemm.hip", "kernels/elementwise.hip", "kernels/loss.hip", "kernels/optim.hip",
+        ["kernels/gemm.hip", "kernels/gemm_dma_tt.hip", "kernels/gemm_dma_tf.hip", "kernels/gemm_dma_ft.hip",
+         "kernels/gemm_dma_ff.hip", "kernels/gemm_dma_pair.hip", "kernels/elementwise.hip", "kernels/loss.hip", "kernels/optim.hip",
          "kernels/norm_pool.hip", "kernels/cnn_fused.hip"],
         ["bindings.cpp"],
     ),
@@ -45,9 +46,13 @@ EXTENSIONS = {
 HIP_FLAGS = {
     "kernels/cnn_fused.hip": ["-Xclang", "-target-feature", "-Xclang", "-unaligned-access-mode"],
 }
-for _knob in ("PDE_FAST_STAGES", "PDE_GEMM_SUB", "PDE_GEMM_WPE"):  # GEMM ring depth / K-tiles per barrier sweeps (gemm.hip)
+# GEMM ring depth / K-tiles per barrier / DMA ring slots / default core sweeps (gemm_device.h)
+_GEMM_SRCS = ("kernels/gemm.hip", "kernels/gemm_dma_tt.hip", "kernels/gemm_dma_tf.hip", "kernels/gemm_dma_ft.hip",
+              "kernels/gemm_dma_ff.hip", "kernels/gemm_dma_pair.hip")
+for _knob in ("PDE_FAST_STAGES", "PDE_GEMM_SUB", "PDE_GEMM_WPE", "PDE_DMA_STAGES", "PDE_GEMM_CORE_DEFAULT"):
     if os.environ.get(_knob):
-        HIP_FLAGS.setdefault("kernels/gemm.hip", []).append(f"-D{_knob}={int(os.environ[_knob])}")
+        for _src in _GEMM_SRCS:
+            HIP_FLAGS.setdefault(_src, []).append(f"-D{_knob}={int(os.environ[_knob])}")
 
 
 def _torch_paths():

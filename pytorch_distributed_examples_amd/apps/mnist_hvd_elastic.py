@@ -14,6 +14,10 @@ Launch (the reference's horovodrun line, :108):
 
 Deliberate differences: skipped batches are not loaded (sampler offset, quirk Q10); the batch index
 bookkeeping keeps the reference's "state.batch updated after the commit check" order.
+
+On a GPU the step is :class:`..hvd.cnn_step.FusedHvdStep`: the fused whole-network CNN kernel, the fusion
+engine's in-place all-reduce and the multi-tensor AdamW, captured into one hipGraph after the first (negotiated)
+step and recaptured after every reset (``--no-graph``: eager; ``--layers``: the autograd layer path).
 """
 from __future__ import annotations
 
@@ -42,6 +46,8 @@ def main(argv=None):
     ap.add_argument("--train-size", type=int, default=60000)
     ap.add_argument("--test-size", type=int, default=10000)
     ap.add_argument("--device", default="auto", choices=["auto", "cpu", "gpu"])
+    ap.add_argument("--layers", action="store_true", help="GPU: the autograd layer path instead of the fused step")
+    ap.add_argument("--no-graph", action="store_true", help="GPU fused step without hipGraph capture")
     add_runtime_args(ap)
     args = ap.parse_args(argv)
     _cfg = rtconfig.apply(rtconfig.from_args(args))
@@ -57,6 +63,11 @@ def main(argv=None):
     optimizer = FusedAdamW(model.parameters(), lr=lr / math.sqrt(hvd.size()))
     optimizer = hvd.DistributedOptimizer(optimizer, named_parameters=model.named_parameters())
     step_counter = {"n": 0}
+    fused_step = None
+    if dev.type == "cuda" and not args.layers:
+        from ..hvd.cnn_step import FusedHvdStep
+
+        fused_step = FusedHvdStep(model, optimizer, args.batch_size, graph=not args.no_graph)
 
     def get_dataset():
         return ShardedLoader(train_set, args.batch_size, hvd.size(), hvd.rank(), shuffle=True)
@@ -70,11 +81,14 @@ def main(argv=None):
         for state.epoch in range(state.epoch, epochs):
             train_loader.start_batch = batch_offset
             for batch_idx, (data, target) in enumerate(train_loader, start=batch_offset):
-                optimizer.zero_grad()
-                output = model(data)
-                loss = OF.nll_loss(output, target)
-                loss.backward()
-                optimizer.step()
+                if fused_step is not None:
+                    loss = fused_step(data, target)  # forward + backward + all-reduce + AdamW (one graph replay)
+                else:
+                    optimizer.zero_grad()
+                    output = model(data)
+                    loss = OF.nll_loss(output, target)
+                    loss.backward()
+                    optimizer.step()
                 fault.maybe_fault(step_counter["n"], hvd.rank())
                 step_counter["n"] += 1
                 if state.batch % batches_per_commit == 0:
@@ -88,6 +102,9 @@ def main(argv=None):
     def on_state_reset():
         for param_group in optimizer.param_groups:
             param_group["lr"] = lr / math.sqrt(hvd.size())
+        if fused_step is not None:  # new engine / world / learning rate: renegotiate and recapture
+            fused_step.reset()
+        print(f"[elastic] reset: world {hvd.size()}, lr {lr / math.sqrt(hvd.size()):.6f}", flush=True)
 
     @torch.no_grad()
     def test():

@@ -119,8 +119,13 @@ def worker(args) -> None:
     a.commit_every = 2
     a.round_warmup = max(1, args.warmup // max(1, args.graph_steps))
     a.round_replays = max(1, args.steps // max(1, args.graph_steps))
-    a.total_steps = 10 ** 9
-    a.total_epochs = 1
-    a.train_size = 60000
+    a.total_steps = 10 ** 9  # the bench ends through report()
+    a.total_epochs = 10 ** 6
+    a.train_size = 60000  # the reference's MNIST train set (HBM-resident synthetic samples) ...
+    a.test_size = 10000
+    # ... over a longer virtual epoch, so every round's timed window fits in whole replays of one epoch
+    a.virtual_train_size = max(60000, (a.round_warmup + a.round_replays + 2) * a.graph_steps * a.batch_size *
+                               max(n_target, int(args.gpus or 2)))
+    a.save_every = 0
     a.device = args.device
     run_elastic_fused(a, report=report)

@@ -19,6 +19,11 @@ Workloads (``--model``), one process per GPU, synthetic data resident in HBM, ra
   mode (the cached batches enqueued stream-ordered: one in-place one-shot xGMI all-reduce of the fused
   model's flat gradient buffer) and the whole step records into a hipGraph.  World 1: Horovod's all-reduce is
   the identity, so the step is the fused kernel with the SGD update in its reduction (2 launches).
+* ``hvd_cnn_elastic`` -- the Horovod-ELASTIC script's step (horovod/horovod_mnist_elastic.py:41-52): batch 128,
+  ``hvd.DistributedOptimizer(AdamW(lr=0.01/sqrt(size)))``; the fused kernel's gradients (weight fragments rebuilt
+  in-kernel every step: the optimiser is not the fused SGD), the engine's in-place all-reduce in graph mode and
+  the multi-tensor AdamW, recorded into hipGraphs (:class:`..hvd.cnn_step.FusedHvdStep` is the same step in the
+  elastic script itself).
 * ``resnet50_pp`` -- BASELINE configs 3 and 4: the 2-stage ResNet-50 of rpc/model_parallel_ResNet50.py
   (stem+layer1+layer2 | layer3+layer4+fc, :85-139), batch 32 split into micro-batches of ``--split-size``
   (the reference's ``split_size`` semantics, :171, quirk Q2), one stage per GPU, activations and their
@@ -50,6 +55,7 @@ from ..utils.log import NO_PHASES, PhaseTimer
 METRIC = "images/sec (whole node) MNIST DDP + ResNet50 RPC-MP at 1/2/4/8 MI355X"
 BASELINE_CONFIG = {"cnn": "1: MNIST CNN DDP bf16, RCCL allreduce over xGMI",
                    "hvd_cnn": "1 via the Horovod API (horovod/mnist_horovod.py DistributedOptimizer)",
+                   "hvd_cnn_elastic": "the Horovod-elastic script's step (horovod_mnist_elastic.py: AdamW, batch 128)",
                    "mlp": "0/1 workload of mnist_ddp_elastic.py (5x1024 MLP DDP)",
                    "resnet50": "ResNet-50 128px data parallel (no BASELINE config; kernel reference point)",
                    "resnet50_stage": "one stage of configs 3/4 at micro-batch size (per-stage kernel time)",
@@ -59,8 +65,8 @@ BASELINE_CONFIG = {"cnn": "1: MNIST CNN DDP bf16, RCCL allreduce over xGMI",
 # Only same-workload, same-world comparisons are reported.
 REFERENCE_IMG_S = {("mlp", 1): 7452.0, ("mlp", 2): 2630.0, ("mlp", 4): 4620.0,
                    ("resnet50_pp", 2): 18.0}
-DEFAULT_BATCH = {"cnn": 1024, "hvd_cnn": 1024, "mlp": 128, "resnet50": 32, "resnet50_stage": 8, "resnet50_pp": 32}
-MODEL_NAMES = {"cnn": "mnist_cnn_Net", "hvd_cnn": "mnist_cnn_Net", "mlp": "mnist_mlp_5x1024", "resnet50": "resnet50_128px",
+DEFAULT_BATCH = {"cnn": 1024, "hvd_cnn": 1024, "hvd_cnn_elastic": 128, "mlp": 128, "resnet50": 32, "resnet50_stage": 8, "resnet50_pp": 32}
+MODEL_NAMES = {"cnn": "mnist_cnn_Net", "hvd_cnn": "mnist_cnn_Net", "hvd_cnn_elastic": "mnist_cnn_Net", "mlp": "mnist_mlp_5x1024", "resnet50": "resnet50_128px",
                "resnet50_stage": "resnet50_128px_stage", "resnet50_pp": "resnet50_128px_2stage"}
 
 
@@ -71,7 +77,7 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", default="cnn",
-                    choices=["cnn", "hvd_cnn", "mlp", "resnet50", "resnet50_stage", "resnet50_pp",
+                    choices=["cnn", "hvd_cnn", "hvd_cnn_elastic", "mlp", "resnet50", "resnet50_stage", "resnet50_pp",
                              "resnet50_hybrid", "elastic_cnn"])
     ap.add_argument("--stage", type=int, default=1, choices=[1, 2], help="resnet50_stage: which pipeline stage")
     ap.add_argument("--scale-to", type=int, default=None, help="elastic_cnn: world size after the first round")
@@ -340,7 +346,40 @@ def build_data_parallel(args, ctx, batch) -> Workload:
     w.phase_step = phase_step
     w.phase_inputs = lambda: list(batch_fn(0))
     w.phase_call = lambda timer, x, y: train_step(x, y, timer)
+    if fused is not None and ctx.world_size == 1:
+        w.kernel_stamps = _cnn_kernel_stamps(fused, batch, dev)
     return w
+
+
+def _cnn_kernel_stamps(fused, batch, dev):
+    """(enable, summarize) of the fused CNN kernel's in-kernel phase stamps (100 MHz wall clock per workgroup;
+    scripts/cnn_phase_stamps.py names them): the config-1 JSON explains its one graph phase by them."""
+    names = ["P0_load", "P1_conv1", "P2_conv2", "P3_fc1", "P4a_fc2", "P4b_loss", "P5_fc2_bwd", "P6_fc1_bwd",
+             "P7a_conv2_wgrad", "P7b_conv2_dgrad", "P9_conv1_wgrad"]
+
+    def enable():
+        fused.stamps = torch.zeros(fused._nwg(batch), 16, dtype=torch.long, device=dev)
+
+    def summarize(t_start, t_end, hz):
+        """Per-phase us of the last stamped replay: the phase's stamp kernels bracket [t_start, t_end]."""
+        st = fused.stamps.cpu().double() * (1e6 / hz)  # us
+        d = st[:, 1:12] - st[:, 0:11]
+        med = {n: round(float(d[:, i].median()), 3) for i, n in enumerate(names)}
+        wg_med = float((st[:, 11] - st[:, 0]).median())
+        t0, t1 = t_start * 1e6 / hz, t_end * 1e6 / hz
+        first, drained = float(st[:, 0].min()), float(st[:, 12].max())
+        out = {"launch_to_first_workgroup": round(first - t0, 3)}
+        out.update(med)
+        out["workgroup_skew_and_drain"] = round(drained - first - wg_med, 3)
+        out["reduce_sgd_kernel_and_boundaries"] = round(t1 - drained, 3)
+        out["sum"] = round(sum(v for v in out.values()), 3)
+        out["span"] = round(t1 - t0, 3)
+        return out
+
+    def disable():
+        fused.stamps = None
+
+    return enable, summarize, disable
 
 
 def build_hvd_cnn(args, ctx, batch) -> Workload:
@@ -350,8 +389,11 @@ def build_hvd_cnn(args, ctx, batch) -> Workload:
     from ..data.synthetic import SyntheticMNIST
     from ..models.cnn import Net
     from ..ops import functional as OF
-    from ..ops.optim import FusedSGD
+    import math
 
+    from ..ops.optim import FusedAdamW, FusedSGD
+
+    elastic = args.model == "hvd_cnn_elastic"
     dev = ctx.device
     on_gpu = dev.type == "cuda"
     hvd.init(device="cpu" if not on_gpu else None)
@@ -364,7 +406,10 @@ def build_hvd_cnn(args, ctx, batch) -> Workload:
 
         fused = FusedCNN(model)
         grads = fused.grad_buffer()  # p.grad = views of one flat buffer: the engine reduces it in place
-    opt = hvd.DistributedOptimizer(FusedSGD(model.parameters(), lr=0.01), named_parameters=model.named_parameters())
+        fused.always_prep = elastic  # AdamW updates the weights: fragments rebuilt in-kernel every step
+    inner = (FusedAdamW(model.parameters(), lr=0.01 / math.sqrt(hvd.size())) if elastic
+             else FusedSGD(model.parameters(), lr=0.01))
+    opt = hvd.DistributedOptimizer(inner, named_parameters=model.named_parameters())
     hvd.broadcast_parameters(model.state_dict(), root_rank=0)
     if fused is not None:
         fused.invalidate()
@@ -375,6 +420,10 @@ def build_hvd_cnn(args, ctx, batch) -> Workload:
             opt.zero_grad()
             loss = OF.nll_loss(model(x), y)
             loss.backward()
+            opt.step()
+            return loss
+        if elastic:  # AdamW: the engine's all-reduce (graph mode: stream-ordered) + the multi-tensor update
+            loss = fused.forward_backward(x, y, grad_out=grads)
             opt.step()
             return loss
         if world == 1:  # all-reduce = identity: the SGD update rides in the reduction kernel
@@ -406,6 +455,7 @@ def build_hvd_cnn(args, ctx, batch) -> Workload:
     w = Workload(step, batch * world, f"dp{world}", hipgraph=one is not None, fused_step=fused is not None,
                  steps_per_graph=group.steps if group is not None else (1 if one is not None else 0),
                  api="horovod DistributedOptimizer + broadcast_parameters",
+                 optimizer="adamw (FusedAdamW, lr 0.01/sqrt(size))" if elastic else "sgd (fused into the reduction)",
                  allreduce=("none (world 1)" if world == 1 else
                             f"fusion engine: {'xgmi-oneshot' if st.get('xgmi_batches') else st.get('backend')}"
                             f"{' graph mode' if on_gpu else ''}"))
@@ -537,16 +587,54 @@ def _graph_phases(work, ctx, args):
 
     timer = GraphPhaseTimer(ctx.device)
     inputs = work.phase_inputs()
+    ks = getattr(work, "kernel_stamps", None)
+    if ks is not None:
+        ks[0]()  # the captured kernels write their in-kernel phase stamps on every replay
 
     def fn(*xs):  # events only in the captured step, not in the capture's eager warm-up
         return work.phase_call(timer if torch.cuda.is_current_stream_capturing() else NO_PHASES, *xs)
 
-    one = CapturedStep(fn, inputs, warmup=1).capture()
-    for _ in range(PHASE_STEPS):
-        one(*inputs)
+    try:
+        one = CapturedStep(fn, inputs, warmup=1).capture()
+        for _ in range(PHASE_STEPS):
+            one(*inputs)
+            torch.cuda.synchronize()
+            timer.replayed()
+        out = timer.summary()
+        if ks is not None:  # the one phase broken down by the kernel's own stamps (last replay)
+            t = timer.buf[:2].tolist()
+            out["kernel_us"] = ks[1](t[0], t[1], timer._hz)
+    finally:
+        if ks is not None:
+            ks[2]()
+    return out
+
+
+def _region_overheads(work, ctx, reps: int = 5):
+    """Where the fixed cost of a timed region goes: wall time of a region with 0 / 1 / 2
+    multi-step graph replays between barrier + synchronize brackets (medians of ``reps``), after the timed region.
+    One replay's device time = t(2) - t(1); the fixed cost = t(1) - that (graph launch, first-node latency,
+    the synchronize); the host-side launch = time until replay() returns."""
+    import statistics
+
+    def region(n):
+        pdist.barrier(ctx)
         torch.cuda.synchronize()
-        timer.replayed()
-    return timer.summary()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            work.group.replay()
+        th = time.perf_counter()
+        pdist.barrier(ctx)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, th - t0
+
+    res = {n: [region(n) for _ in range(reps)] for n in (0, 1, 2)}
+    med = {n: statistics.median(r[0] for r in res[n]) * 1e3 for n in res}
+    per = med[2] - med[1]
+    return {"method": f"median of {reps} regions with 0/1/2 replays of the {work.group.steps}-step graph",
+            "empty_region_ms": round(med[0], 4), "one_replay_region_ms": round(med[1], 4),
+            "replay_device_ms": round(per, 4), "fixed_region_ms": round(med[1] - per, 4),
+            "replay_host_launch_ms": round(statistics.median(r[1] for r in res[1]) * 1e3, 4)}
 
 
 def _measure_phases(work, ctx, args):
@@ -612,7 +700,7 @@ def main(argv=None):
 
     if args.model == "resnet50_pp":
         work = build_pipeline(args, ctx, batch)
-    elif args.model == "hvd_cnn":
+    elif args.model in ("hvd_cnn", "hvd_cnn_elastic"):
         work = build_hvd_cnn(args, ctx, batch)
     else:
         work = build_data_parallel(args, ctx, batch)
@@ -633,6 +721,12 @@ def main(argv=None):
     dt = pdist.max_over_ranks(dt, ctx.device)
     final_loss = _report_loss(work, ctx, loss)
     phases = _measure_phases(work, ctx, args) if os.environ.get("PDE_BENCH_PHASES", "1") != "0" else None
+    overheads = None
+    if on_gpu and work.group is not None and os.environ.get("PDE_BENCH_OVERHEADS", "1") != "0":
+        try:
+            overheads = _region_overheads(work, ctx)
+        except Exception as exc:  # noqa: BLE001 - diagnostics never cost the headline line
+            overheads = {"error": repr(exc)[:200]}
     value = work.images_per_step * args.steps / dt
     secondary = None
     mode = os.environ.get("PDE_BENCH_SECONDARY", "1")  # 0: off; force: also on CPU/gloo (plumbing tests)
@@ -645,11 +739,13 @@ def main(argv=None):
         name = MODEL_NAMES[args.model] + (str(args.stage) if args.model == "resnet50_stage" else "")
         cfg = {"model": name, "baseline_config": BASELINE_CONFIG[args.model],
                "global_batch": work.images_per_step, "seq_len": None,
-               "image": "1x28x28" if args.model in ("cnn", "hvd_cnn", "mlp") else f"3x{args.image or 128}x{args.image or 128}",
+               "image": "1x28x28" if args.model in ("cnn", "hvd_cnn", "hvd_cnn_elastic", "mlp") else f"3x{args.image or 128}x{args.image or 128}",
                "parallelism": work.parallelism, "final_loss": round(final_loss, 4)}
         cfg.update(work.info)
         if phases is not None:
             cfg["phases"] = phases
+        if overheads is not None:
+            cfg["region_overheads"] = overheads
         if secondary is not None:
             cfg["secondary"] = secondary
         print(json.dumps({

@@ -47,8 +47,8 @@ def maybe_fault_in(lo: int, hi: int, rank: int) -> None:
     if marker:
         if os.path.exists(marker):
             return
-        with open(marker, "w") as f:
-            f.write(f"rank {rank} step {step} mode {mode}\n")
+        with open(marker, "w") as f:  # t=: wall clock of the fault (survivors report their detection latency)
+            f.write(f"rank {rank} step {step} mode {mode} t={time.time():.6f}\n")
     print(f"[fault-injector] rank {rank} step {step}: {mode}", flush=True)
     if mode == "exit":
         sys.stdout.flush()

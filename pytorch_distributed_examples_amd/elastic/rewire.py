@@ -502,21 +502,89 @@ def _test(model, loader, dev, comm, log):
     model.train(was)
 
 
+class _FailureWatch:
+    """Background watcher of one round: when the elastic driver reports a failed member of THIS round
+    (``failed/<round>`` in its store, set the moment it reaps the dead process) it raises the xGMI exchange's
+    host abort word, so the survivors' spinning in-kernel exchanges give up within ~0.1 ms instead of waiting
+    out their timeout (detection used to cost the 5 s timeout plus a commit interval).
+    A planned membership change (hosts added / removed by discovery) publishes no failure: it is handled at the
+    next commit point without dropping any step."""
+
+    def __init__(self, rdzv: RendezvousClient, rnd: int, xa, period_s: float = 0.02):
+        import threading
+
+        self.rnd, self.xa, self.period_s = rnd, xa, period_s
+        self.fired_at = None
+        self._stop = threading.Event()
+        host, port = os.environ["PDE_ELASTIC_STORE"].rsplit(":", 1)
+        # a client of its own: never interleaves with the main thread's store traffic
+        self._store = dist.TCPStore(host, int(port), is_master=False, timeout=datetime.timedelta(seconds=30),
+                                    wait_for_workers=False)
+        self._th = threading.Thread(target=self._run, daemon=True)
+        self._th.start()
+
+    def _run(self):
+        key = f"failed/{self.rnd}"
+        while not self._stop.wait(self.period_s):
+            try:
+                if self._store.check([key]):
+                    self.fired_at = time.time()
+                    if self.xa is not None and self.xa.impl is not None:
+                        self.xa.abort()
+                    return
+            except Exception:  # noqa: BLE001 - the driver went away: the main thread sees it too
+                return
+
+    def stop(self):
+        self._stop.set()
+        self._th.join(timeout=1.0)
+
+
+def _fault_time():
+    """Wall-clock time the injected fault fired (PDE_FAULT_ONCE marker, elastic/fault.py), if any."""
+    marker = os.environ.get("PDE_FAULT_ONCE")
+    if not marker or not os.path.exists(marker):
+        return None
+    try:
+        for tok in open(marker).read().split():
+            if tok.startswith("t="):
+                return float(tok[2:])
+    except (OSError, ValueError):
+        return None
+    return None
+
+
 def run_elastic_fused(args, report=None):
     """``mnist_ddp_elastic.py --rewire --model cnn --fused`` and the elastic bench (BASELINE config 2).
 
-    The fused whole-network CNN step with the gradient exchange over xGMI INSIDE its reduction kernel
-    (``FusedCNN.forward_backward(..., xgmi=...)``: 2 launches per step at any world size) and the SGD update
-    fused in; ``graph_steps`` steps recorded into ONE hipGraph per round (recaptured after every membership
-    change: the xGMI view and the world size are baked in).  No host liveness wait per step: a dead peer
-    makes the exchange time out (bounded spin, error word) and surfaces at the next commit point
-    (``xgmi.check()`` + the gloo ``agree``), every ``commit_every`` graph replays.
+    The reference trainer's semantics (pytorch_elastic/mnist_ddp_elastic.py:82-114) on the fused path:
+    epochs over this rank's ``DistributedSampler`` shard of the training set (:class:`..data.loader.ShardedLoader`,
+    re-sharded for the new world after every membership change and resumed at the first batch the whole group
+    has not consumed, ``pos["seen"]``), a test pass over the sharded test set after every epoch (accuracy
+    all-reduced), and rank 0's snapshot every ``save_every`` epochs with the reference's keys.
 
-    ``report(round, rank, size, info)`` (bench): called by every rank after each round's timed window with
-    img/s and the re-wire latency (membership change seen -> first step of the new round complete)."""
+    The step is the fused whole-network CNN with the gradient exchange over xGMI INSIDE its reduction kernel
+    (``FusedCNN.forward_backward(..., xgmi=...)``: 2 launches per step at any world size) and the SGD update fused
+    in.  ``graph_steps`` steps are recorded into ONE hipGraph per round whose inputs are ``graph_steps`` static
+    batch slots: before each replay the next ``graph_steps`` batches of the shard are gathered into the slots
+    (one index-gather per replay), so every replay trains on NEW data; an epoch's tail (fewer batches than a
+    replay, or a short last batch) runs as eager fused steps.  The graph is recaptured after every membership
+    change (xGMI view and world size are baked in).
+
+    Failure handling: a dead peer makes the exchange give up -- at once when the driver reports the failure
+    (:class:`_FailureWatch` raises the exchange's host abort word), else at its timeout -- and the next commit
+    point (every ``commit_every`` replays: ``xgmi.check()`` + the gloo ``agree``) turns it into PeerFailure:
+    the survivors restore their last commit and re-join in-process.  ``detect_s`` (the fault -> PeerFailure
+    latency, from the injector's timestamp) is reported with the re-wire breakdown.
+
+    ``report(round, rank, size, info)`` (bench): called by every rank after each round's timed window (whole
+    replays inside one epoch, so no test pass or epoch tail falls inside it) with img/s and the re-wire latency
+    (membership change seen -> first step of the new round complete); returning True ends training."""
     import time as _time
 
-    from ..data.synthetic import SyntheticMNIST
+    from ..data.loader import ShardedLoader
+    from ..data.synthetic import mnist_splits
+    from ..elastic.snapshot import save_snapshot
     from ..models.cnn import Net
     from ..models.cnn_fused import FusedCNN
     from ..ops.optim import FusedSGD
@@ -545,17 +613,40 @@ def run_elastic_fused(args, report=None):
     def sync():
         if on_gpu:
             torch.cuda.synchronize()
+
     batch = int(args.batch_size)
     G = max(1, int(getattr(args, "graph_steps", 10)))
-    data = SyntheticMNIST(max(8 * batch, 1024 if not on_gpu else 16384), device=dev, seed=local + 1)
-    batches = [data.batch(j, batch) for j in range(G)]
+    # the reference's MNIST sizes (synthetic, HBM-resident); a bench may ask for a longer VIRTUAL epoch
+    # (indices wrap around the real samples) so its timed window never straddles an epoch boundary
+    real_train = int(getattr(args, "train_size", 60000))
+    virt_train = int(getattr(args, "virtual_train_size", 0) or real_train)
+    train_set, test_set = mnist_splits(device=dev, train=real_train, test=int(getattr(args, "test_size", 10000)))
+    train_view = train_set
+    if virt_train != real_train:
+        class _Virtual:  # a longer epoch over the same samples (ShardedLoader only needs len())
+            def __len__(self):
+                return virt_train
+        train_view = _Virtual()
+    total_epochs = int(getattr(args, "total_epochs", 1))
+    total_steps = int(getattr(args, "total_steps", 0) or 0)  # > 0: stop after this many steps (bench)
+    save_every = int(getattr(args, "save_every", 0) or 0)
+    snapshot_path = getattr(args, "snapshot_path", None)
+    # static batch slots of the captured group (GPU): replay j trains on slot j
+    xbuf = torch.empty(G * batch, 1, 28, 28, device=dev)
+    ybuf = torch.zeros(G * batch, dtype=torch.long, device=dev)
+    slots = [(xbuf[j * batch:(j + 1) * batch], ybuf[j * batch:(j + 1) * batch]) for j in range(G)]
     pos = {"epoch": 0, "seen": 0, "step": 0}
     commit = Commit(model, opt, pos)
     commit_every = max(1, int(getattr(args, "commit_every", 10)))  # graph replays between commit points
-    total_steps = int(getattr(args, "total_steps", 0) or 0)  # 0: train args.total_epochs epochs
-    steps_per_epoch = max(1, args.train_size // max(1, batch))
     changed_at = None
+    detect = None
     pid = os.getpid()
+
+    def gather(idx, lo, hi, xo, yo):
+        sl = idx[lo:hi] % real_train
+        torch.index_select(train_set.images, 0, sl, out=xo)
+        torch.index_select(train_set.labels, 0, sl, out=yo)
+
     while True:
         t_join = _time.perf_counter()
         rnd, rank, size = rdzv.join()
@@ -563,15 +654,12 @@ def run_elastic_fused(args, report=None):
         comm = RoundComm(rdzv, rank, size, dev, use_rccl=False)
         log = RankLogger(rank)
         xa = None
-        # re-wire breakdown (seconds): rendezvous = membership change seen -> this round joined (includes the
-        # driver noticing and publishing it); control = the round's gloo group; broadcast = rank 0's weights
-        # and position; map = xGMI IPC handle exchange + peer mapping; capture = hipGraph recapture
+        watch = None
         parts = {"rendezvous_s": t_joined - (changed_at if changed_at is not None else t_join),
                  "control_s": comm.timing.get("control_group_s", 0.0)}
         try:
-            # everybody adopts rank 0's weights and position (one 87 KB broadcast over the control plane)
             tb = _time.perf_counter()
-            if size > 1:
+            if size > 1:  # everybody adopts rank 0's weights and position (87 KB over the control plane)
                 if on_gpu:
                     comm.broadcast_(fused.flat, 0)
                 else:
@@ -592,7 +680,8 @@ def run_elastic_fused(args, report=None):
                 def train_step(x, y):
                     return fused.forward_backward(x, y, grad_out=grads, sgd=opt, xgmi=xa)
 
-                graph = CapturedSteps(train_step, batches, warmup=1).capture()
+                graph = CapturedSteps(train_step, slots, warmup=1).capture()
+                eager_step = train_step
             else:
                 from ..ops import functional as OF
                 from ..parallel.ddp import DistributedDataParallel
@@ -601,79 +690,147 @@ def run_elastic_fused(args, report=None):
                 parts["map_s"] = _time.perf_counter() - tm
                 tc = _time.perf_counter()
 
-                class _Eager:  # CapturedSteps' replay() surface over eager steps
+                def eager_step(x, y):
+                    ddp.zero_grad()
+                    out = OF.nll_loss(model(x), y)
+                    out.backward()
+                    ddp.sync_gradients()
+                    opt.step()
+                    return out
+
+                class _Eager:  # CapturedSteps' replay() surface over eager steps on the slots
                     def replay(self):
                         out = None
-                        for x, y in batches:
-                            ddp.zero_grad()
-                            out = OF.nll_loss(model(x), y)
-                            out.backward()
-                            ddp.sync_gradients()
-                            opt.step()
+                        for x, y in slots:
+                            out = eager_step(x, y)
                         return out
 
                 graph = _Eager()
             sync()
             parts["capture_s"] = _time.perf_counter() - tc
+            if detect is not None:
+                parts["detect_s"] = detect
             rewire_s = _time.perf_counter() - changed_at if changed_at is not None else None
-            changed_at = None
+            changed_at = detect = None
+            watch = _FailureWatch(rdzv, rnd, xa) if size > 1 else None
             plane = f"fused CNN + xGMI exchange, {G} steps per graph" if on_gpu else "CPU autograd + gloo DDP"
             log.print(f"[rewire] round {rnd}: rank {rank} of {size} (pid {pid}), {plane}" +
                       (f", re-wired in {rewire_s:.3f}s (" + ", ".join(f"{k[:-2]} {v:.3f}" for k, v in parts.items())
                        + ")" if rewire_s is not None else ""), all_ranks=True)
             commit.save()
-            # timed window of this round (the bench reads it through `report`)
-            warm, timed = int(getattr(args, "round_warmup", 2)), int(getattr(args, "round_replays", 10))
-            for _ in range(warm):
-                graph.replay()
-            sync()
-            comm.agree(False)  # barrier over the control plane
-            t0 = _time.perf_counter()
-            for _ in range(timed):
-                loss = graph.replay()
-            sync()
-            dt = _time.perf_counter() - t0
-            if xa is not None:
-                _as_peer_failure(xa.check)
-            t = torch.tensor([dt] + [rewire_s if rewire_s is not None else -1.0] + list(parts.values()))
-            if size > 1:  # the slowest member's window and re-wire (one MAX over the control plane)
-                _as_peer_failure(lambda: dist.all_reduce(t, op=dist.ReduceOp.MAX))
-            img_s = batch * size * G * timed / float(t[0].item())
-            pos["step"] += G * (warm + timed)
-            stop = False
-            if report is not None:
-                info = {"images_per_s": img_s, "ms_per_step": float(t[0].item()) / (G * timed) * 1e3,
-                        "rewire_s": float(t[1].item()) if t[1].item() >= 0 else None, "loss": float(loss.item())}
-                if t[1].item() >= 0:
-                    info["rewire_parts"] = {k: round(float(v), 4) for k, v in zip(parts, t[2:].tolist())}
-                stop = bool(report(rnd, rank, size, info))
-            # keep training; commit points every `commit_every` replays check liveness and membership
+            train_data = ShardedLoader(train_view, batch, size, rank, shuffle=True)
+            test_data = ShardedLoader(test_set, batch, size, rank, shuffle=False)
+            per_step = batch * size
+            n_batches = len(train_data)
+            window = None
+            if report is not None:  # the bench's timed window: warm-up + timed replays at an epoch start
+                window = {"warm": int(getattr(args, "round_warmup", 2)), "timed": int(getattr(args, "round_replays", 10)),
+                          "done": False}
+                if (window["warm"] + window["timed"]) * G > n_batches:
+                    raise SystemExit(f"elastic bench: the timed window needs {(window['warm'] + window['timed']) * G} "
+                                     f"batches per epoch, the shard has {n_batches}: raise virtual_train_size")
             since = 0
+            stop = False
             while not stop:
-                if total_steps and pos["step"] >= total_steps:
+                epoch = pos["epoch"]
+                if total_steps:
+                    if pos["step"] >= total_steps:
+                        break
+                elif epoch >= total_epochs:
                     break
-                if not total_steps and pos["step"] >= args.total_epochs * steps_per_epoch:
+                train_data.set_epoch(epoch)
+                idx = torch.tensor(list(iter(train_data.sampler)), dtype=torch.long).to(dev)
+                b = min(pos["seen"] // per_step, n_batches)  # resume after the group's consumed batches
+                log.print(f"Local Rank: {rdzv.wid} | Global Rank: {rank} | Epoch {epoch} | Batchsize: {batch} | "
+                          f"Steps: {n_batches} | start batch {b}", all_ranks=True)
+                # the bench window: whole replays inside this epoch (no test pass or eager tail inside it); a round
+                # resuming too close to the epoch's end times the next epoch
+                timing = window is not None and not window["done"] and \
+                    n_batches - b >= (window["warm"] + window["timed"]) * G
+                replays = 0
+                t0 = None
+                loss = None
+                while b < n_batches:
+                    if total_steps and pos["step"] >= total_steps:
+                        stop = True
+                        break
+                    step0 = pos["step"]
+                    if b + G <= n_batches and (b + G) * batch <= idx.numel():
+                        gather(idx, b * batch, (b + G) * batch, xbuf, ybuf)  # the next G batches -> the slots
+                        loss = graph.replay()
+                        n = G
+                        replays += 1
+                    else:  # epoch tail: fewer batches than a replay, or the short last batch
+                        lo, hi = b * batch, min((b + 1) * batch, idx.numel())
+                        x, y = xbuf[:hi - lo], ybuf[:hi - lo]
+                        gather(idx, lo, hi, x, y)
+                        loss = eager_step(x.contiguous(), y.contiguous())
+                        n = 1
+                    b += n
+                    pos["seen"] = b * per_step
+                    pos["step"] += n
+                    fault.maybe_fault_in(step0, step0 + n, rank)  # PDE_FAULT_*: a step of this replay
+                    if timing:
+                        if replays == window["warm"] and t0 is None:
+                            sync()
+                            comm.agree(False)  # barrier over the control plane
+                            t0 = _time.perf_counter()
+                        elif t0 is not None and replays == window["warm"] + window["timed"]:
+                            sync()
+                            dt = _time.perf_counter() - t0
+                            if xa is not None:
+                                _as_peer_failure(xa.check)
+                            t = torch.tensor([dt] + [rewire_s if rewire_s is not None else -1.0] + list(parts.values()))
+                            if size > 1:  # the slowest member's window and re-wire (one MAX over the control plane)
+                                _as_peer_failure(lambda: dist.all_reduce(t, op=dist.ReduceOp.MAX))
+                            info = {"images_per_s": per_step * G * window["timed"] / float(t[0].item()),
+                                    "ms_per_step": float(t[0].item()) / (G * window["timed"]) * 1e3,
+                                    "rewire_s": float(t[1].item()) if t[1].item() >= 0 else None,
+                                    "loss": float(loss.item())}
+                            if t[1].item() >= 0:
+                                info["rewire_parts"] = {k: round(float(v), 4) for k, v in zip(parts, t[2:].tolist())}
+                            window["done"] = True
+                            timing = False
+                            stop = bool(report(rnd, rank, size, info))
+                            if stop:
+                                break
+                    since += 1
+                    if since % commit_every == 0:  # commit point: liveness + membership
+                        sync()
+                        if xa is not None:
+                            _as_peer_failure(xa.check)
+                        commit.save()
+                        if comm.agree(rdzv.hosts_updated()):
+                            raise MembershipChanged()
+                if stop:
                     break
-                graph.replay()
-                fault.maybe_fault_in(pos["step"], pos["step"] + G, rank)  # PDE_FAULT_*: a step of this replay
-                pos["step"] += G
-                since += 1
-                if since % commit_every == 0:
-                    sync()
-                    if xa is not None:
-                        _as_peer_failure(xa.check)
-                    commit.save()
-                    if comm.agree(rdzv.hosts_updated()):
-                        raise MembershipChanged()
-            log.print(f"[rewire] finished {pos['step']} steps in round {rnd} (world {size}, pid {pid})", all_ranks=True)
+                # end of epoch (mnist_ddp_elastic.py:111-114): commit, test pass, snapshot
+                sync()
+                if xa is not None:
+                    _as_peer_failure(xa.check)
+                pos["epoch"], pos["seen"] = epoch + 1, 0
+                commit.save()
+                _test(model, test_data, dev, comm, log)
+                if rank == 0 and save_every and snapshot_path and epoch % save_every == 0:
+                    save_snapshot(snapshot_path, model.state_dict(), epoch, opt.state_dict())
+                    log.print(f"Epoch {epoch} | Training snapshot saved at {snapshot_path}")
+                if comm.agree(rdzv.hosts_updated()):
+                    raise MembershipChanged()
+            log.print(f"[rewire] finished {pos['step']} steps / {pos['epoch']} epochs in round {rnd} (world {size}, "
+                      f"pid {pid})", all_ranks=True)
+            if watch is not None:
+                watch.stop()
             if xa is not None:
                 xa.close()
             comm.close()
             break
         except PeerFailure as exc:
             changed_at = _time.perf_counter()
+            tf = _fault_time()
+            detect = (time.time() - tf) if tf is not None else None
             log.print(f"[rewire] round {rnd}: peer failure ({str(exc).splitlines()[0][:120]}); restoring commit "
-                      f"step {commit._pos['step']}", all_ranks=True)
+                      f"epoch {commit._pos['epoch']} step {commit._pos['step']}" +
+                      (f"; detected {detect:.3f}s after the fault" if detect is not None else ""), all_ranks=True)
             comm.close(abort=True)
             commit.restore()
             if fused is not None:
@@ -683,6 +840,8 @@ def run_elastic_fused(args, report=None):
             log.print(f"[rewire] round {rnd}: membership changed, re-joining", all_ranks=True)
             comm.close()
         finally:
+            if watch is not None:
+                watch.stop()
             if xa is not None and xa.impl is not None:
                 torch.cuda.synchronize()
                 xa.close()

@@ -181,6 +181,14 @@ def init(comm=None, device: str | None = None):
             eng.set_xgmi(_ctx.xgmi.impl, DEFAULT_THRESHOLD if plane == "auto" else _ctx.xgmi.max_bytes)
     _ctx.engine = eng
     _ctx.names = {}
+    _ctx.watch = None
+    if rendezvous.elastic_env() and _ctx.xgmi is not None:
+        # the driver reports a dead member of this round at once: spinning xGMI exchanges give up on the host
+        # abort word (elastic/rewire.py _FailureWatch) and the engine raises HorovodInternalError at the next
+        # synchronize / commit -- detection in ~0.1 s instead of the exchange timeout
+        from ..elastic.rewire import _FailureWatch
+
+        _ctx.watch = _FailureWatch(_ctx.rdzv, _ctx.generation, _ctx.xgmi)
     _ctx.initialized = True
 
 
@@ -188,6 +196,9 @@ def shutdown(abort: bool = False):
     """Tear down the engine, communicator and process group (in-process; used by elastic reset)."""
     if not _ctx.initialized:
         return
+    if getattr(_ctx, "watch", None) is not None:
+        _ctx.watch.stop()
+        _ctx.watch = None
     try:
         _ctx.engine.shutdown(abort)
     except Exception:  # noqa: BLE001 - a failed peer may leave the engine in an error state

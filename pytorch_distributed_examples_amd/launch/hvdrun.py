@@ -167,6 +167,10 @@ class Driver:
                       flush=True)
                 if w.wid in self.order:
                     changed = True
+                    # report the failure of this round's member AT ONCE (survivors abort their spinning xGMI
+                    # exchanges on it: elastic/rewire.py _FailureWatch); the new round follows below
+                    failed = [x for x in self.order if self.workers[x].finished and self.workers[x].proc.returncode]
+                    self.store.set(f"failed/{self.round}", ",".join(failed))
             for wid, dl in list(self.leaving.items()):
                 if self.workers[wid].proc.poll() is not None:
                     del self.leaving[wid]
@@ -181,7 +185,7 @@ class Driver:
                 self.store.set("shutdown", "1")
                 return 0 if ok else 1
             # discovery: add / remove workers
-            if time.time() - last_discovery >= self.args.discovery_interval and \
+            if (time.time() - last_discovery >= self.args.discovery_interval or changed) and \
                     (self.args.host_discovery_script or changed):
                 last_discovery = time.time()
                 slots = self.discovered_slots()

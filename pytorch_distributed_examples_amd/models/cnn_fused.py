@@ -66,6 +66,9 @@ class FusedCNN:
         self.stop_after = -1  # diagnostic: end the training kernel after phase stamp k (counter attribution)
         self.frag = torch.empty(C.cnn_frag_bytes(), dtype=torch.uint8, device=dev)
         self._frag_gen = None  # weight generation at which the fragment image was last made current
+        # an optimiser other than the fused SGD updates the weights every step (AdamW, hipGraph-replayed): the
+        # kernel rebuilds its bf16 fragment image from the fp32 weights at every step (k_cnn_prep fused in)
+        self.always_prep = False
 
     def invalidate(self):
         """The fp32 weights were written behind our back: rebuild the fragment image next step."""
@@ -129,7 +132,7 @@ class FusedCNN:
         x = x.float().contiguous()
         y = y.long().contiguous()
         training = self.net.training
-        prep = self._frag_gen is None or self._frag_gen != OF.weight_generation()
+        prep = self.always_prep or self._frag_gen is None or self._frag_gen != OF.weight_generation()
         (hp, step), params = self._sgd_hp(sgd) if sgd is not None else ((None, None), None)
         view, xscale = None, 1.0
         if xgmi is not None and xgmi.size > 1:

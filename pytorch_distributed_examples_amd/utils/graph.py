@@ -27,6 +27,18 @@ import torch
 from ..ops import functional as OF
 
 
+def upload(g: torch.cuda.CUDAGraph) -> None:
+    """hipGraphUpload the instantiated graph (its launch resources are set up now, so the first replay -- the
+    first step of a timed region -- does not pay for them).  Best effort: a runtime without it is left as is."""
+    try:
+        from .. import _native
+
+        _native.C().graph_upload(int(g.raw_cuda_graph_exec()))
+        torch.cuda.synchronize()
+    except Exception:  # noqa: BLE001 - an optimisation only
+        pass
+
+
 class CapturedStep:
     def __init__(self, step_fn, example_inputs, warmup: int = 3):
         self.step_fn = step_fn
@@ -50,6 +62,7 @@ class CapturedStep:
             with torch.cuda.graph(g):
                 self.static_out = self.step_fn(*self.static_inputs)
         torch.cuda.synchronize()
+        upload(g)
         self.graph = g
         return self
 
@@ -92,6 +105,7 @@ class CapturedSteps:
             with torch.cuda.graph(g):
                 self.outputs = [self.step_fn(*b) for b in self.batches]
         torch.cuda.synchronize()
+        upload(g)
         self.graph = g
         return self
 

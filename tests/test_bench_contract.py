@@ -118,7 +118,9 @@ def test_bench_elastic_survives_killed_worker_cpu():
     assert "[fault-injector] rank 1 step 20" in out and "peer failure" in out, out[-4000:]
     assert [r["world"] for r in rounds] == [2, 1] and len(final) == 1, out[-4000:]
     assert rounds[1]["rewire_s"] > 0 and set(rounds[1]["rewire_parts"]) == {
-        "rendezvous_s", "control_s", "broadcast_s", "map_s", "capture_s"}, rounds[1]
+        "rendezvous_s", "control_s", "broadcast_s", "map_s", "capture_s", "detect_s"}, rounds[1]
+    # detection: the fault -> PeerFailure latency (driver's failure report -> abort word / commit point)
+    assert 0 < rounds[1]["rewire_parts"]["detect_s"] < 10.0, rounds[1]
     assert "worker killed" in final[0]["config"]["parallelism"]
     pids = {}
     for ln in out.splitlines():

@@ -214,3 +214,29 @@ def test_rewire_shrink_needs_every_survivor():
         got = [open(os.path.join(d, f"r{r}")).read().split() for r in range(2)]
         assert [g[0] for g in got] == [want, want], (valid, supported, got)
         assert all(float(g[1]) == 3.0 for g in got), got  # the data plane works either way
+
+
+def test_rewire_fused_keeps_reference_trainer_semantics(tmp_path):
+    """--rewire --fused --model cnn (the fused elastic path of BASELINE config 2; here its CPU protocol): epochs
+    over the sharded training set, the per-epoch test pass and save_every snapshots of the reference Trainer
+    (mnist_ddp_elastic.py:82-114), a worker killed mid-epoch, and the survivor's detection latency reported."""
+    from dist_utils import run_cmd
+
+    snap = str(tmp_path / "snap.pt")
+    env = {"PDE_FAULT_AT_STEP": "25", "PDE_FAULT_RANK": "1", "PDE_FAULT_MODE": "exit",
+           "PDE_FAULT_ONCE": str(tmp_path / "once")}
+    rc, out = run_cmd(HVDRUN + ["-np", "2", "--min-np", "1", "--verbose", SCRIPT, "2", "1", "--rewire", "--fused",
+                                "--model", "cnn", "--device", "cpu", "--train_size", "8192", "--test_size", "512",
+                                "--batch_size", "128", "--commit_every", "1", "--snapshot_path", snap], env=env)
+    assert rc == 0, out[-4000:]
+    # the reference's per-rank epoch line over the SHARDED set: 8192 / 2 ranks / 128 = 32 steps
+    assert "| Global Rank: 1 | Epoch 0 | Batchsize: 128 | Steps: 32" in out, out[-4000:]
+    assert "[fault-injector] rank 1 step 25" in out and "peer failure" in out, out[-4000:]
+    m = re.search(r"detected ([\d.]+)s after the fault", out)
+    assert m and float(m.group(1)) < 30.0, out[-4000:]
+    # the next round (a replacement worker joins) resumes the epoch, re-sharded, at the group's committed position
+    assert re.search(r"round 1: rank 0 of \d \(pid \d+\), .*detect [\d.]+", out), out[-4000:]
+    assert re.search(r"Global Rank: 0 \| Epoch 0 \| Batchsize: 128 \| Steps: \d+ \| start batch [1-9]", out), out[-4000:]
+    assert "Global test accuracy" in out and "Epoch 0 | Training snapshot saved at" in out, out[-4000:]
+    assert re.search(r"\[rewire\] finished \d+ steps / 2 epochs in round \d+", out), out[-4000:]
+    assert load_snapshot(snap)["EPOCHS_RUN"] == 1
