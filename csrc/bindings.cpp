@@ -1183,6 +1183,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("step") = py::none());
   m.def("clear_last_error", []() { return static_cast<int>(hipGetLastError()); },
         "Read and reset the HIP last-error state (after an aborted stream capture).");
+  m.def("bn_reserve_headroom", &pde::bn_reserve_headroom, py::arg("blocks"),
+        "Reserve (> 0) / release (< 0) CUs for spinning side-stream kernels; returns the one-launch BatchNorm's "
+        "resident cap");
+  m.def("bn_launch_stats", []() {
+    long one = 0, multi = 0;
+    int last = 0, cap = 0;
+    pde::bn_launch_stats(&one, &multi, &last, &cap);
+    py::dict d;
+    d["one_launch"] = one;
+    d["multi_launch"] = multi;
+    d["last_grid"] = last;
+    d["cap"] = cap;
+    return d;
+  });
   m.def("graph_upload",
         [](int64_t exec) {  // torch.cuda.CUDAGraph.raw_cuda_graph_exec(): upload the executable graph's launch
                             // resources NOW (current stream), not inside the first timed replay

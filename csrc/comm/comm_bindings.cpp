@@ -180,6 +180,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def(py::init<int, int64_t, double>(), py::arg("device"), py::arg("slot_bytes"), py::arg("timeout_s") = 60.0)
       .def("ipc_handle", [](P2PRing& r) { return py::bytes(r.ipc_handle()); })
       .def("open", [](P2PRing& r, py::bytes h) { r.open(std::string(h)); })
+      .def("open_local", &P2PRing::open_local, py::arg("peer"))
+      .def_static("max_wg", &P2PRing::max_wg)
       // both stream-ordered on the caller's CURRENT stream, hipGraph-capturable; raw bytes of the tensor
       .def("send",
            [](P2PRing& r, const at::Tensor& t) {

@@ -43,6 +43,9 @@ class P2PRing {
 
   std::string ipc_handle() const;
   void open(const std::string& peer_handle);
+  // loopback: the peer ring lives in THIS process on the same device (no IPC; single-process rehearsals)
+  void open_local(P2PRing& peer);
+  static int max_wg();  // workgroups a send / recv kernel may keep spinning (PDE_P2P_MAX_WG)
   // stream-ordered; 16-B aligned buffers; a message larger than a slot goes as slot-sized pieces
   void send(const void* src, int64_t bytes, hipStream_t s);
   void recv(void* dst, int64_t bytes, hipStream_t s);
@@ -60,6 +63,7 @@ class P2PRing {
   char* peer_ = nullptr;       // the peer's, mapped
   uint32_t* state_ = nullptr;  // device-local: send seq, recv seq, send done, recv done, error
   bool opened_ = false;
+  bool peer_ipc_ = false;      // peer_ was mapped with hipIpcOpenMemHandle (else: a local ring's memory)
   int64_t sent_ = 0, received_ = 0;
 };
 

@@ -1,6 +1,8 @@
 // Stage-to-stage P2P channel over xGMI: see p2p_ring.h for the protocol.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
@@ -30,8 +32,19 @@ void hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("p2p ring: ") + what + ": " + hipGetErrorString(e));
 }
 
+// Workgroups per message, capped at PDE_P2P_MAX_WG (default 32, <= kMaxWg; the same on both sides): a send
+// that waits for credit keeps its whole grid spinning on a side stream, so the cap is also what the one-launch
+// BatchNorm must leave free (P2PRing::max_wg, bn_reserve_headroom).  32 workgroups already saturate one link.
+int ring_max_wg() {
+  static const int w = [] {
+    const char* e = std::getenv("PDE_P2P_MAX_WG");
+    const int v = e ? std::atoi(e) : 32;
+    return std::max(1, std::min(P2PRing::kMaxWg, v));
+  }();
+  return w;
+}
 int grid_of(int64_t bytes) {
-  return static_cast<int>(std::min<int64_t>(P2PRing::kMaxWg, std::max<int64_t>(1, (bytes + kWgBytes - 1) / kWgBytes)));
+  return static_cast<int>(std::min<int64_t>(ring_max_wg(), std::max<int64_t>(1, (bytes + kWgBytes - 1) / kWgBytes)));
 }
 int64_t chunk_of(int64_t bytes, int g) { return ((bytes + g - 1) / g + 15) / 16 * 16; }
 
@@ -178,8 +191,18 @@ void P2PRing::open(const std::string& peer_handle) {
   void* p = nullptr;
   hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
   peer_ = static_cast<char*>(p);
+  peer_ipc_ = true;
   opened_ = true;
 }
+
+void P2PRing::open_local(P2PRing& peer) {
+  if (peer.device_ != device_ || peer.local_ == nullptr) throw std::invalid_argument("p2p ring: local peer");
+  peer_ = peer.local_;
+  peer_ipc_ = false;
+  opened_ = true;
+}
+
+int P2PRing::max_wg() { return ring_max_wg(); }
 
 static RingArgs args_of(char* local, char* peer, uint32_t* state, int64_t flag_bytes, int64_t slot_bytes,
                         uint64_t timeout) {
@@ -235,7 +258,7 @@ void P2PRing::close() {
   if (local_ == nullptr) return;
   (void)hipSetDevice(device_);
   (void)hipDeviceSynchronize();
-  if (peer_ != nullptr) (void)hipIpcCloseMemHandle(peer_);
+  if (peer_ != nullptr && peer_ipc_) (void)hipIpcCloseMemHandle(peer_);
   (void)hipFree(local_);
   (void)hipFree(state_);
   local_ = peer_ = nullptr;

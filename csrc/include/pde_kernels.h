@@ -245,6 +245,12 @@ int bn_workspace_blocks(int P, int C, int groups = 1);
 // slabs != nullptr (splits > 1): x is the UNREDUCED output of a split-K conv GEMM (GemmArgs::splits_out):
 // the BatchNorm sums the fp32 slabs [splits][P][C] in z order, rounds to bf16, WRITES x and normalizes it --
 // the GEMM's separate slab-reduction launch is gone.
+// Co-residency budget of the one-launch BatchNorm: reserve (blocks > 0) / release (< 0) CUs that kernels on
+// other streams of this process may hold while it runs (spinning side-stream ring sends / receives, an
+// overlapped RCCL all-reduce); returns the resulting resident cap.  Grids shrink to the cap; a BatchNorm whose
+// minimal grid exceeds it is refused up front and runs multi-launch.
+int bn_reserve_headroom(int blocks);
+void bn_launch_stats(long* one_launch, long* multi_launch, int* last_grid, int* cap);
 hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, const float* beta, float eps,
                         float momentum, float* running_mean, float* running_var, float* save_mean,
                         float* save_invstd, float* scale_shift, float* ws, const uint16_t* res, int relu,

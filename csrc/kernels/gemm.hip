@@ -30,7 +30,7 @@
 //     cdna_hip_programming.md §5 "in-launch split-K reduction") -- measured slower here, see split_tickets.
 //   * Epilogue options: bias, ReLU, ReLU-mask (backward), fp32 / bf16 output, accumulate, and an OIHW
 //     remap that writes a conv weight gradient straight into the parameter's [Co][Ci][R][S] fp32 grad.
-#include "gemm_device.h"
+#include "gemm_ring.h"
 
 namespace pde {
 

@@ -1,6 +1,6 @@
-// LDS-DMA GEMM kernels with row-contiguous A and row-contiguous B operands (gemm_device.h); a translation unit of its own so the
+// LDS-DMA GEMM kernels with row-contiguous A and row-contiguous B operands (gemm_dma.h); a translation unit of its own so the
 // instantiations compile in parallel with gemm.hip.
-#include "gemm_device.h"
+#include "gemm_dma.h"
 
 namespace pde {
 

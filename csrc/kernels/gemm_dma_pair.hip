@@ -1,7 +1,7 @@
-// dgrad + wgrad pairs on the LDS-DMA core (gemm_dma_pair_kernel, gemm_device.h): the combinations that occur --
+// dgrad + wgrad pairs on the LDS-DMA core (gemm_dma_pair_kernel, gemm_dma.h): the combinations that occur --
 // data gradients: dgrad gather / dense dy x {dgrad-layout weights, forward copy read transposed}; weight gradients:
 // dy^T x {im2col^T gather, dense activation}.
-#include "gemm_device.h"
+#include "gemm_dma.h"
 
 namespace pde {
 

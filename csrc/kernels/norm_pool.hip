@@ -6,6 +6,7 @@
 // Backward = partials of (sum dy, sum dy*xhat) with the ReLU mask applied on the fly -> finalize ->
 // fused dx (+ residual grad).  Every pass streams 16 B (8 channels) per lane.
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 
 #include "common.cuh"
@@ -1569,9 +1570,9 @@ int bn_fin_grid(int P, int C, int& rpb, int groups = 1) {
   // r3af (tagged hand-off): 64 -> 128 chunks, ResNet-50 3.328 -> 3.284 ms (the C <= 128 layers get 128-256 blocks)
   static const int kChunks = std::getenv("PDE_BN_CHUNKS") ? std::atoi(std::getenv("PDE_BN_CHUNKS")) : 128;
   // r2m sweep at 512 threads per block: 256 blocks (one per CU, 8 waves) 3.83 -> 3.79 ms/step
-  static const int kTarget = std::min(bn_resident_cap(),
-                                      std::getenv("PDE_BN_BLOCKS") ? std::atoi(std::getenv("PDE_BN_BLOCKS")) : 256);
-  int nrb = std::max(1, std::min(kChunks, kTarget / (ncg * groups)));
+  static const int kBlocks = std::getenv("PDE_BN_BLOCKS") ? std::atoi(std::getenv("PDE_BN_BLOCKS")) : 256;
+  const int target = std::min(bn_resident_cap(), kBlocks);  // (side-stream headroom may change at run time)
+  int nrb = std::max(1, std::min(kChunks, target / (ncg * groups)));
   nrb = std::min(nrb, std::max(1, P / kBnRows));
   rpb = ceil_div(P, nrb);
   return ceil_div(P, rpb);
@@ -1661,9 +1662,17 @@ uint32_t* bn_flags(int n, hipStream_t s) { return reinterpret_cast<uint32_t*>(bn
 // count, minus PDE_BN_HEADROOM blocks (default 0) left for kernels that other streams keep spinning (ring
 // sends waiting for credit, an overlapped RCCL all-reduce).  A hand-off that still times out sets the error
 // word, which every sync point reads (ops.functional.check_device_errors) and raises on.
-int bn_resident_cap() {
-  static int cap = -1;
-  if (cap < 0) {
+// Blocks that kernels on OTHER streams of this process may keep resident while a one-launch BatchNorm runs --
+// spinning side-stream kernels (a pipeline's ring sends waiting for credit, an overlapped RCCL all-reduce,
+// bn_reserve_headroom) -- subtracted from the resident cap, so the BatchNorm grid shrinks (more rows per block)
+// instead of waiting on blocks that cannot be placed.
+std::atomic<int> g_bn_headroom{0};
+std::atomic<long> g_bn_one_launches{0}, g_bn_multi_launches{0};
+std::atomic<int> g_bn_last_grid{0};
+
+int bn_resident_base() {
+  static int base = -1;
+  if (base < 0) {
     int dev = 0, cus = 1;
     hipDeviceProp_t prop{};
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
@@ -1683,14 +1692,24 @@ int bn_resident_cap() {
     q(reinterpret_cast<const void*>(&k_bn_bwd_fused<8>));
     q(reinterpret_cast<const void*>(&k_bn_bwd_fused<16>));
     const int headroom = std::getenv("PDE_BN_HEADROOM") ? std::max(0, std::atoi(std::getenv("PDE_BN_HEADROOM"))) : 0;
-    cap = std::max(1, std::max(1, occ) * cus - headroom);
+    base = std::max(1, std::max(1, occ) * cus - headroom);
   }
-  return cap;
+  return base;
 }
+int bn_resident_cap() { return std::max(0, bn_resident_base() - g_bn_headroom.load()); }
 
 bool bn_one_launch(int blocks) {
   static const bool off = std::getenv("PDE_BN_FUSED") != nullptr && std::getenv("PDE_BN_FUSED")[0] == '0';
-  return !off && blocks <= bn_resident_cap();
+  // refused up front when the grid cannot be resident beside the reserved side-stream blocks: the caller runs
+  // the multi-launch BatchNorm instead of a flag wait that would time out
+  const bool ok = !off && blocks <= bn_resident_cap();
+  if (ok) {
+    ++g_bn_one_launches;
+    g_bn_last_grid = blocks;
+  } else {
+    ++g_bn_multi_launches;
+  }
+  return ok;
 }
 
 // flag hand-off without the agent-scope L2 write-back / invalidate (see bn_publish); r3w: ResNet-50
@@ -1966,6 +1985,19 @@ hipError_t embbag_bwd(const float* dy, const int64_t* idx, const int64_t* off, i
     hipLaunchKernelGGL(k_embbag_bwd_atomic, dim3(ceil_div(B, 4)), dim3(256), 0, s, dy, idx, off, B, L, D, dw);
   }
   return hipGetLastError();
+}
+
+int bn_reserve_headroom(int blocks) {
+  const int v = g_bn_headroom.fetch_add(blocks) + blocks;
+  if (v < 0) g_bn_headroom = 0;
+  return bn_resident_cap();
+}
+
+void bn_launch_stats(long* one, long* multi, int* last_grid, int* cap) {
+  *one = g_bn_one_launches.load();
+  *multi = g_bn_multi_launches.load();
+  *last_grid = g_bn_last_grid.load();
+  *cap = bn_resident_cap();
 }
 
 }  // namespace pde

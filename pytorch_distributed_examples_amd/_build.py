@@ -46,7 +46,7 @@ EXTENSIONS = {
 HIP_FLAGS = {
     "kernels/cnn_fused.hip": ["-Xclang", "-target-feature", "-Xclang", "-unaligned-access-mode"],
 }
-# GEMM ring depth / K-tiles per barrier / DMA ring slots / default core sweeps (gemm_device.h)
+# GEMM ring depth / K-tiles per barrier / DMA ring slots / default core sweeps (gemm_common.h / gemm_ring.h / gemm_dma.h)
 _GEMM_SRCS = ("kernels/gemm.hip", "kernels/gemm_dma_tt.hip", "kernels/gemm_dma_tf.hip", "kernels/gemm_dma_ft.hip",
               "kernels/gemm_dma_ff.hip", "kernels/gemm_dma_pair.hip")
 for _knob in ("PDE_FAST_STAGES", "PDE_GEMM_SUB", "PDE_GEMM_WPE", "PDE_DMA_STAGES", "PDE_GEMM_CORE_DEFAULT"):

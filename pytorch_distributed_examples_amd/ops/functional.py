@@ -120,6 +120,38 @@ def check_device_errors(where: str = "") -> None:
 # ---------------------------------------------------------------------------------------------
 # GEMM pairing
 # ---------------------------------------------------------------------------------------------
+class BnHeadroom:
+    """CUs reserved, for this object's lifetime, for kernels that keep spinning on OTHER streams of this process
+    while a one-launch BatchNorm may run -- a pipeline channel's ring sends waiting for credit, an overlapped RCCL
+    all-reduce (csrc/kernels/norm_pool.hip bn_reserve_headroom): the BatchNorm's grid shrinks to the remaining
+    resident cap, and a BatchNorm whose smallest grid does not fit is refused up front (multi-launch) instead of
+    timing out in its flag waits.  GPU only (a no-op without the native extension)."""
+
+    def __init__(self, blocks: int):
+        self.blocks = max(0, int(blocks))
+        self.cap = None
+        if self.blocks and torch.cuda.is_available():
+            self.cap = _C().bn_reserve_headroom(self.blocks)
+        else:
+            self.blocks = 0
+
+    def release(self):
+        if self.blocks:
+            _C().bn_reserve_headroom(-self.blocks)
+            self.blocks = 0
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
+def bn_launch_stats() -> dict:
+    """One-launch / multi-launch BatchNorm counts, the last one-launch grid and the current resident cap."""
+    return dict(_C().bn_launch_stats())
+
+
 class gemm_pair:
     """Context manager: the (at most two) GEMM ops issued inside are launched together as ONE paired launch
     when the block exits (``pde::gemm_bf16_pair``: the first op's tiles are scheduled first; both grids fill

@@ -97,6 +97,11 @@ class P2PChannel:
             self.ring = C.P2PRing(device.index, slot, float(os.environ.get("PDE_P2P_TIMEOUT_S", "60")))
             self._store.set(f"{self._key}/ring/{self.local_rank}", self.ring.ipc_handle())
             self.ring.open(self._store.get(f"{self._key}/ring/{self.peer_local}"))
+            # sends wait for credit on a side stream with their whole grid resident: keep that many CUs out of
+            # the one-launch BatchNorm's co-residency budget
+            from ..ops.functional import BnHeadroom
+
+            self._bn_headroom = BnHeadroom(C.P2PRing.max_wg())
             return
         if not self.rccl:
             return
@@ -209,6 +214,8 @@ class P2PChannel:
             self._store.get(f"{self._key}/closed/{self.peer_local}")
             self.ring.close()
             self.ring = None
+            if getattr(self, "_bn_headroom", None) is not None:
+                self._bn_headroom.release()
 
 
 class PipelineEngine:

@@ -15,6 +15,7 @@ Implements the communicator plug-in of :class:`.ddp.DistributedDataParallel` (``
 from __future__ import annotations
 
 import itertools
+import os
 
 import torch
 import torch.distributed as dist
@@ -74,6 +75,13 @@ class StreamComm:
         self.rccl = C.RcclComm()
         self.rccl.init(uid, self.rank, self.size, device.index, True)
         self.side = torch.cuda.Stream(device=device) if side_stream else None
+        self._bn_headroom = None
+        if self.side is not None:
+            # an overlapped all-reduce spins on its side stream while compute (a one-launch BatchNorm) runs:
+            # reserve RCCL's workgroups (PDE_RCCL_SIDE_BLOCKS, default 32 channels) out of that kernel's budget
+            from ..ops.functional import BnHeadroom
+
+            self._bn_headroom = BnHeadroom(int(os.environ.get("PDE_RCCL_SIDE_BLOCKS", "32")))
 
     def allreduce_async(self, t: torch.Tensor, avg: bool = False):
         if self.side is None:
@@ -98,3 +106,6 @@ class StreamComm:
         if self.rccl is not None:
             self.rccl.destroy()
             self.rccl = None
+        if self._bn_headroom is not None:
+            self._bn_headroom.release()
+            self._bn_headroom = None

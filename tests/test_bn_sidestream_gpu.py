@@ -1,0 +1,126 @@
+"""The production config-3/4 kernel mix rehearsed in ONE process on one GPU (VERDICT r4 ask 3).
+
+On a real node a pipeline stage runs the one-launch BatchNorm (a grid whose blocks wait on each other, so every
+block must be resident) while, on other streams of the same process, a ring send waits for credit and an RCCL /
+xGMI all-reduce overlaps -- kernels that keep CUs occupied while they spin.  The rehearsals that share a card
+between processes cannot show this (they force the multi-launch BatchNorm).  Here one process runs the stage-1
+step (ResNetShard1: stem + layer1 + layer2, training BatchNorm at the default one-launch setting) as a captured
+hipGraph on the main stream while a P2P ring RECEIVE spins on side stream 1 (its loopback peer sends only at the
+end of the step) and a world-1 RCCL all-reduce plus an xGMI one-shot run on side stream 2; the channel's
+workgroups are reserved out of the BatchNorm's co-residency budget (``BnHeadroom``), so its grid shrinks instead
+of waiting on blocks that cannot be placed.  A second test checks that a BatchNorm whose smallest grid does not
+fit beside the reserved blocks is refused up front (multi-launch) rather than timing out."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_stage_step_beside_spinning_side_stream_kernels(gpu):
+    from pytorch_distributed_examples_amd import _native
+    from pytorch_distributed_examples_amd.models.resnet import ResNetShard1
+    from pytorch_distributed_examples_amd.ops import functional as OF
+    from pytorch_distributed_examples_amd.ops.optim import FusedSGD
+    from pytorch_distributed_examples_amd.utils.graph import CapturedStep
+
+    assert os.environ.get("PDE_BN_FUSED", "1") != "0", "the rehearsal is about the one-launch BatchNorm"
+    C = _native.comm()
+    dev = gpu
+    nbytes = 4 << 20
+    ra = C.P2PRing(dev.index, nbytes, 20.0)
+    rb = C.P2PRing(dev.index, nbytes, 20.0)
+    ra.open_local(rb)
+    rb.open_local(ra)
+    # the spinning receive's grid stays resident beside the BatchNorm (the pipeline reserves its sends' grid the
+    # same way, parallel/pipeline.py)
+    headroom = OF.BnHeadroom(C.P2PRing.max_wg())
+    rccl = C.RcclComm()
+    rccl.init(C.rccl_unique_id(), 0, 1, dev.index, True)
+    xg = C.XgmiAllreduce(0, 1, dev.index, 1 << 20)
+
+    torch.manual_seed(0)
+    model = ResNetShard1().to(dev).train()
+    opt = FusedSGD(model.parameters(), lr=0.05)
+    x = torch.randn(8, 3, 128, 128, device=dev)
+    with torch.no_grad():
+        yshape = model(x).shape
+    dy = (torch.randn(yshape, device=dev) * 1e-3).to(torch.bfloat16)
+
+    def step(xs, g):
+        # gradients stay allocated (zeroed, not dropped): the optimiser's device table holds their pointers, and a
+        # fresh allocation inside the capture would rebuild it (a host->device copy the capture refuses)
+        model.zero_grad(set_to_none=False)
+        out = model(xs)
+        out.backward(g)
+        opt.step()
+        return out
+
+    graph = CapturedStep(step, [x, dy], warmup=2).capture()
+    before = OF.bn_launch_stats()
+    msg_out = torch.arange(nbytes // 4, dtype=torch.int32, device=dev)
+    msg_in = torch.zeros_like(msg_out)
+    gbuf = torch.ones(1 << 16, device=dev)
+    gbuf2 = torch.ones(1 << 14, device=dev)
+    s1, s2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    main = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize()
+    for it in range(50):
+        s1.wait_stream(main)
+        with torch.cuda.stream(s1):
+            rb.recv(msg_in)          # spins until ra's send at the end of this step
+        s2.wait_stream(main)
+        with torch.cuda.stream(s2):
+            rccl.allreduce_(gbuf, 0)
+            xg.allreduce_(gbuf2, 1.0, False)
+        graph(x, dy)                 # the stage step: one-launch BatchNorm among its kernels
+        msg_out.add_(1)
+        ra.send(msg_out)
+        main.wait_stream(s1)
+        main.wait_stream(s2)
+    torch.cuda.synchronize()
+    OF.check_device_errors("side-stream mix")  # no one-launch BatchNorm hand-off timed out
+    assert ra.error() == 0 and rb.error() == 0 and xg.error() == 0
+    assert torch.equal(msg_in, msg_out), "ring payload"
+    after = OF.bn_launch_stats()
+    # the captured step's BatchNorm ran one-launch (decided at capture, after the reservation), within the cap
+    assert after["one_launch"] > 0 and after["last_grid"] <= after["cap"], (before, after)
+    assert after["cap"] <= before["cap"]
+    headroom.release()
+    rccl.destroy()
+    xg.close()
+    ra.close()
+    rb.close()
+
+
+def test_bn_grid_beyond_headroom_is_refused_up_front(gpu):
+    from pytorch_distributed_examples_amd.ops import functional as OF
+
+    base = OF.bn_launch_stats()["cap"]
+    torch.manual_seed(1)
+    P, Cc = 4096, 512  # 8 channel groups of 64: the smallest one-launch grid has 8 blocks
+    x = (torch.randn(P, Cc, device=gpu) * 2 + 0.5).to(torch.bfloat16)
+    w = torch.rand(Cc, device=gpu) + 0.5
+    b = torch.randn(Cc, device=gpu) * 0.1
+
+    def run():
+        rm, rv = torch.zeros(Cc, device=gpu), torch.ones(Cc, device=gpu)
+        y = OF.batch_norm(x.view(1, 64, 64, Cc), w, b, rm, rv, True, relu=True)
+        torch.cuda.synchronize()
+        return y.view(P, Cc).float()
+
+    ref = torch.relu(torch.nn.functional.batch_norm(x.float(), None, None, w, b, True, 0.1, 1e-5))
+    h = OF.BnHeadroom(base - 4)  # leaves 4 resident blocks: fewer than the smallest grid
+    s0 = OF.bn_launch_stats()
+    y = run()
+    s1 = OF.bn_launch_stats()
+    assert s1["cap"] == 4
+    assert s1["multi_launch"] > s0["multi_launch"] and s1["one_launch"] == s0["one_launch"], (s0, s1)
+    assert torch.allclose(y, ref, atol=3e-2, rtol=2e-2)
+    h.release()
+    y2 = run()
+    s2 = OF.bn_launch_stats()
+    assert s2["cap"] == base and s2["one_launch"] > s1["one_launch"] and s2["last_grid"] <= base, (s1, s2)
+    assert torch.allclose(y2, ref, atol=3e-2, rtol=2e-2)
+    OF.check_device_errors("bn headroom")
