@@ -13,6 +13,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "mlp_train.h"
 #include "pde_kernels.h"
 
 namespace {
@@ -1157,6 +1158,112 @@ Tensor cnn_train(const Tensor& images, const Tensor& tgt, const Tensor& params, 
   return loss;
 }
 
+
+// Whole MLP training step in one persistent launch (mlp_fused.hip).  Per-layer lists (index l = layer); empty
+// tensors stand for absent state (mw / vw / mb / vb by mode, wtbf of layer 0, act / d of index 0).
+int mlp_train_grid_py() {
+  int dev = 0;
+  check(hipGetDevice(&dev), "hipGetDevice");
+  return pde::mlp_train_grid(dev);
+}
+
+void mlp_train(const Tensor& x, const Tensor& y, const std::vector<Tensor>& w, const std::vector<Tensor>& b,
+               const std::vector<Tensor>& gw, const std::vector<Tensor>& gb, const std::vector<Tensor>& mw,
+               const std::vector<Tensor>& vw, const std::vector<Tensor>& mb, const std::vector<Tensor>& vb,
+               const std::vector<Tensor>& wbf, const std::vector<Tensor>& wtbf, const std::vector<Tensor>& act,
+               const std::vector<Tensor>& actT, const std::vector<Tensor>& d, const std::vector<Tensor>& dT,
+               Tensor& dlog, Tensor& dlogT, Tensor& loss_part, Tensor& loss, const Tensor& hp, Tensor& step, int mode,
+               Tensor& bar, Tensor& err, int grid, const optional<Tensor>& stamps) {
+  const int nl = static_cast<int>(w.size());
+  TORCH_CHECK(nl >= 1 && nl <= pde::kMlpMaxLayers, "mlp_train: 1..8 layers");
+  for (const auto* v : {&b, &gw, &gb, &mw, &vw, &mb, &vb, &wbf, &wtbf, &act, &actT, &d, &dT})
+    TORCH_CHECK(static_cast<int>(v->size()) == nl, "mlp_train: every per-layer list has one entry per layer");
+  CHECK_IN(x); CHECK_F32(x); CHECK_IN(y);
+  TORCH_CHECK(y.scalar_type() == at::kLong && x.dim() == 2, "mlp_train: x [B, in] fp32, y int64");
+  const int B = static_cast<int>(x.size(0));
+  TORCH_CHECK(B % 32 == 0 && B > 0 && y.numel() == B, "mlp_train: batch must be a multiple of 32");
+  TORCH_CHECK(grid > 0, "mlp_train: no resident grid (mlp_train_grid() == 0)");
+  auto ptr = [](const Tensor& t) -> void* { return t.defined() && t.numel() > 0 ? t.data_ptr() : nullptr; };
+  auto aligned = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  pde::MlpTrainArgs a{};
+  a.nl = nl; a.B = B; a.mode = mode;
+  TORCH_CHECK(mode >= 0 && mode <= 2, "mlp_train: mode 0 SGD, 1 Adam, 2 AdamW");
+  a.x = x.data_ptr<float>(); a.y = y.data_ptr<int64_t>();
+  for (int l = 0; l < nl; ++l) {
+    const bool last = l == nl - 1;
+    CHECK_IN(w[l]); CHECK_F32(w[l]);
+    TORCH_CHECK(w[l].dim() == 2, "mlp_train: weights [out, in]");
+    const int out = static_cast<int>(w[l].size(0)), in = static_cast<int>(w[l].size(1));
+    TORCH_CHECK(in % 8 == 0 && in <= 1024 && (last ? out <= 16 : (out % 8 == 0 && out <= 1024)),
+                "mlp_train: in % 8 == 0, in <= 1024, hidden out % 8 == 0 (<= 1024), last out <= 16");
+    TORCH_CHECK(l == 0 ? in == x.size(1) : in == w[l - 1].size(0), "mlp_train: layer sizes do not chain");
+    auto f32n = [&](const Tensor& t, long n, const char* what) {
+      TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kFloat && t.numel() == n, "mlp_train: ",
+                  what, " of layer ", l);
+      return t.data_ptr<float>();
+    };
+    pde::MlpLayerArgs& L = a.L[l];
+    L.in = in; L.out = out;
+    L.w = w[l].data_ptr<float>();
+    L.b = f32n(b[l], out, "bias");
+    L.gw = f32n(gw[l], static_cast<long>(out) * in, "weight grad");
+    L.gb = f32n(gb[l], out, "bias grad");
+    const bool need_m = mode != 0 || (mw[l].defined() && mw[l].numel() > 0);
+    L.mw = need_m ? f32n(mw[l], static_cast<long>(out) * in, "exp_avg / momentum") : nullptr;
+    L.mb = need_m ? f32n(mb[l], out, "bias exp_avg / momentum") : nullptr;
+    L.vw = mode != 0 ? f32n(vw[l], static_cast<long>(out) * in, "exp_avg_sq") : nullptr;
+    L.vb = mode != 0 ? f32n(vb[l], out, "bias exp_avg_sq") : nullptr;
+    TORCH_CHECK(wbf[l].is_cuda() && wbf[l].scalar_type() == at::kBFloat16 && wbf[l].is_contiguous() &&
+                    wbf[l].numel() == static_cast<long>(out) * in && aligned(wbf[l].data_ptr()),
+                "mlp_train: bf16 weight copy of layer ", l);
+    L.wbf = u16(wbf[l]);
+    L.ldt = last ? 32 : out;
+    if (l == 0) {
+      L.wtbf = nullptr;
+    } else {
+      TORCH_CHECK(wtbf[l].is_cuda() && wtbf[l].scalar_type() == at::kBFloat16 && wtbf[l].is_contiguous() &&
+                      wtbf[l].dim() == 2 && wtbf[l].size(0) == in && wtbf[l].size(1) == L.ldt,
+                  "mlp_train: transposed bf16 copy of layer ", l, " must be [in, ", L.ldt, "]");
+      L.wtbf = u16(wtbf[l]);
+    }
+    auto bfbuf = [&](const Tensor& t, long r, long c, const char* what) {
+      TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kBFloat16 && t.dim() == 2 &&
+                      t.size(0) == r && t.size(1) == c && aligned(t.data_ptr()),
+                  "mlp_train: ", what, " ", l, " must be bf16 [", r, ", ", c, "]");
+      return u16(t);
+    };
+    a.actT[l] = bfbuf(actT[l], in, B, "actT");
+    if (l >= 1) {
+      a.act[l] = bfbuf(act[l], B, in, "act");
+      a.d[l] = bfbuf(d[l], B, in, "d");
+      a.dT[l] = bfbuf(dT[l], in, B, "dT");
+    }
+    for (void* p : {ptr(w[l]), ptr(gw[l]), ptr(mw[l]), ptr(vw[l])}) TORCH_CHECK(aligned(p), "mlp_train: alignment");
+  }
+  const int nout = static_cast<int>(w[nl - 1].size(0));
+  (void)nout;
+  a.dlog = [&] { TORCH_CHECK(dlog.numel() == static_cast<long>(B) * 32 && dlog.scalar_type() == at::kBFloat16,
+                             "mlp_train: dlog [B, 32] bf16"); return u16(dlog); }();
+  a.dlogT = [&] { TORCH_CHECK(dlogT.numel() == static_cast<long>(B) * 32 && dlogT.scalar_type() == at::kBFloat16,
+                              "mlp_train: dlogT [32, B] bf16"); return u16(dlogT); }();
+  TORCH_CHECK(loss_part.numel() >= B / 32 && loss_part.scalar_type() == at::kFloat, "mlp_train: loss_part");
+  TORCH_CHECK(loss.numel() == 1 && loss.scalar_type() == at::kFloat, "mlp_train: loss");
+  CHECK_IN(hp); CHECK_F32(hp);
+  TORCH_CHECK(hp.numel() >= pde::HP_COUNT, "mlp_train: hp");
+  TORCH_CHECK(step.is_cuda() && step.scalar_type() == at::kInt && step.numel() >= 1, "mlp_train: step int32");
+  TORCH_CHECK(bar.is_cuda() && bar.scalar_type() == at::kInt && bar.numel() >= 288 && reinterpret_cast<uintptr_t>(bar.data_ptr()) % 16 == 0, "mlp_train: bar int32[288], 16-B aligned");
+  TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt && err.numel() >= 1, "mlp_train: err int32");
+  a.loss_part = loss_part.data_ptr<float>(); a.loss = loss.data_ptr<float>();
+  a.hp = hp.data_ptr<float>(); a.step = step.data_ptr<int>();
+  a.bar = reinterpret_cast<unsigned*>(bar.data_ptr()); a.err = err.data_ptr<int>();
+  a.stamps = nullptr;
+  if (stamps.has_value() && stamps->defined()) {
+    TORCH_CHECK(stamps->is_cuda() && stamps->scalar_type() == at::kLong && stamps->numel() >= 128, "mlp_train: stamps int64[128]");
+    a.stamps = reinterpret_cast<long long*>(stamps->data_ptr());
+  }
+  check(pde::mlp_train_step(a, grid, cur_stream()), "mlp_train");
+}
+
 // Plain SGD on the flat CNN parameters + fragment-image refresh (after the gradient all-reduce).
 void cnn_sgd(Tensor& params, const Tensor& grads, const Tensor& hp, Tensor& frag, const optional<Tensor>& step) {
   CHECK_IN(params); CHECK_IN(grads); CHECK_IN(hp); CHECK_IN(frag);
@@ -1179,6 +1286,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gscale") = py::none(), py::arg("stamps") = py::none(), py::arg("frag") = py::none(),
         py::arg("prep") = true, py::arg("sgd_hp") = py::none(), py::arg("stop_after") = -1,
         py::arg("sgd_step") = py::none(), py::arg("xgmi_view") = py::none(), py::arg("xscale") = 1.0);
+  m.def("mlp_train_grid", &mlp_train_grid_py);
+  m.def("mlp_train", &mlp_train, py::arg("x"), py::arg("y"), py::arg("w"), py::arg("b"), py::arg("gw"), py::arg("gb"),
+        py::arg("mw"), py::arg("vw"), py::arg("mb"), py::arg("vb"), py::arg("wbf"), py::arg("wtbf"), py::arg("act"),
+        py::arg("actT"), py::arg("d"), py::arg("dT"), py::arg("dlog"), py::arg("dlogT"), py::arg("loss_part"),
+        py::arg("loss"), py::arg("hp"), py::arg("step"), py::arg("mode"), py::arg("bar"), py::arg("err"),
+        py::arg("grid"), py::arg("stamps") = py::none());
   m.def("cnn_sgd", &cnn_sgd, py::arg("params"), py::arg("grads"), py::arg("hp"), py::arg("frag"),
         py::arg("step") = py::none());
   m.def("clear_last_error", []() { return static_cast<int>(hipGetLastError()); },

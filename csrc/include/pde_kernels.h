@@ -316,4 +316,6 @@ hipError_t cnn_sgd_fused(float* params, const float* grads, const float* hp, voi
 hipError_t embbag_bwd(const float* dy, const int64_t* idx, const int64_t* off, int B, long L, int D, float* dw,
                       long rows, hipStream_t s);
 
+
+
 }  // namespace pde

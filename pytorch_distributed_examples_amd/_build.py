@@ -29,7 +29,7 @@ EXTENSIONS = {
     "_C": (
         ["kernels/gemm.hip", "kernels/gemm_dma_tt.hip", "kernels/gemm_dma_tf.hip", "kernels/gemm_dma_ft.hip",
          "kernels/gemm_dma_ff.hip", "kernels/gemm_dma_pair.hip", "kernels/elementwise.hip", "kernels/loss.hip", "kernels/optim.hip",
-         "kernels/norm_pool.hip", "kernels/cnn_fused.hip"],
+         "kernels/norm_pool.hip", "kernels/cnn_fused.hip", "kernels/mlp_fused.hip"],
         ["bindings.cpp"],
     ),
     "_comm": (

@@ -261,6 +261,16 @@ def build_data_parallel(args, ctx, batch) -> Workload:
     # world 1, fused MLP, PDE_MLP_FOLD_OPT=1: each layer's Adam update appended to the next backward GEMM launch
     # (default: the separate multi-tensor launch after backward -- measured faster, profiles/README.md r3k)
     fold_opt = fmlp is not None and ctx.world_size == 1 and os.environ.get("PDE_MLP_FOLD_OPT", "0") == "1"
+    # world 1, fused MLP: the whole step (forward, loss, backward, Adam) as ONE persistent launch
+    # (models/mlp_mega.py; PDE_MLP_MEGA=0: the layer-by-layer launches)
+    mega = None
+    if (fmlp is not None and ctx.world_size == 1 and not fold_opt and os.environ.get("PDE_MLP_MEGA", "1") != "0"
+            and batch % 32 == 0):
+        from ..models.mlp_mega import MegaMLP
+
+        mega = MegaMLP(model, opt)
+        if mega.grid() <= 0:
+            mega = None
     # world > 1 on the xGMI data plane: the fused CNN exchanges its gradients inside the slab reduction
     # (PDE_CNN_XCHG=0: all-reduce through the DDP communicator + a separate SGD launch instead)
     xgmi = getattr(comm, "xgmi", None) if fused is not None and os.environ.get("PDE_CNN_XCHG", "1") != "0" else None
@@ -281,6 +291,9 @@ def build_data_parallel(args, ctx, batch) -> Workload:
             with t.phase("opt"):
                 fused.sgd_step(opt, ddp.flat_grad)
             return loss
+        if mega is not None:
+            with t.phase("mega_fwd_loss_bwd_adam"):
+                return mega.step(x, y)
         if fmlp is not None:
             if fold_opt:  # one process: the optimiser step rides on the backward launches (FusedMLP)
                 with t.phase("fwd_bwd_opt"):
@@ -331,6 +344,8 @@ def build_data_parallel(args, ctx, batch) -> Workload:
     w = Workload(step, batch * ctx.world_size, f"dp{ctx.world_size}", **extra, hipgraph=one is not None,
                  fused_step=fused is not None or fmlp is not None, rccl_nranks=nranks,
                  **({"optimizer": "adam folded into the backward launches"} if fold_opt else {}),
+                 **({"mega_kernel": True, "launches_per_step": mega.kernel_launches_per_step(),
+                     "optimizer": "adam inside the step's single launch"} if mega is not None else {}),
                  steps_per_graph=group.steps if group is not None else (1 if one is not None else 0),
                  allreduce=("xgmi-in-reduce-kernel" if xgmi is not None else
                             "xgmi-oneshot<=%dB+rccl" % comm.threshold) if routed is not None else
@@ -338,6 +353,12 @@ def build_data_parallel(args, ctx, batch) -> Workload:
     w.group = group
     if routed is not None:
         w.check = comm.xgmi.check  # raises if any one-shot call timed out waiting for a peer
+    if mega is not None:
+        def mega_check():
+            if mega.errors():
+                raise RuntimeError("MegaMLP: a grid barrier timed out (workgroups not co-resident)")
+
+        w.check = mega_check
 
     def phase_step(i, timer):
         x, y = batch_fn(i)
@@ -474,10 +495,18 @@ def build_hvd_cnn(args, ctx, batch) -> Workload:
     return w
 
 
-# Why the default GPU pipeline unit is the whole step (scripts/pipeline_units.py, profiles/r4g_pipeline_units.md):
-# stage kernels are latency-bound at the reference's micro-batch, so fewer, larger units win despite no overlap.
-UNIT_CHOICE = ("measured best of --mb-group 1/2/4 (predicted 2-GPU img/s 3942 / 5344 / 5976, "
-               "profiles/r4g_pipeline_units.md); with one unit per step the two stages do not overlap")
+# The measured pipeline-unit table (scripts/pipeline_units.py --json over the stage benches of this round): the
+# default GPU unit size of resnet50_pp and the predicted-vs-1-GPU numbers its record carries.
+UNIT_TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "profiles",
+                          "r5_pipeline_units.json")
+
+
+def _unit_table():
+    try:
+        with open(os.environ.get("PDE_PIPE_UNIT_TABLE", UNIT_TABLE)) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
 
 
 def build_pipeline(args, ctx, batch) -> Workload:
@@ -487,8 +516,25 @@ def build_pipeline(args, ctx, batch) -> Workload:
 
     on_gpu = ctx.device.type == "cuda"
     nranks = _data_plane_check(ctx, None)
+    tab = _unit_table() if on_gpu else None
+    mb_group, choice = args.mb_group, {"source": "--mb-group" if args.mb_group else None}
+    if mb_group is None and os.environ.get("PDE_PIPE_MB_GROUP"):
+        choice["source"] = "PDE_PIPE_MB_GROUP"
+    elif mb_group is None and tab and tab.get("best"):
+        mb_group = tab["best"]["mb_per_unit"]  # the measured best unit size
+        choice["source"] = "measured table (best predicted 2-GPU rate)"
     pipe = ResNetPipelineDP(ctx, batch, args.split_size, args.image or 128, args.schedule, tag="bench",
-                            mb_group=args.mb_group)
+                            mb_group=mb_group)
+    if tab:
+        row = next((r for r in tab["rows"] if r["mb_per_unit"] == pipe.mb_group), None)
+        choice.update(table=os.path.relpath(os.environ.get("PDE_PIPE_UNIT_TABLE", UNIT_TABLE),
+                                            os.path.dirname(os.path.dirname(UNIT_TABLE))),
+                      formula=tab.get("formula"),
+                      rows={r["mb_per_unit"]: r["predicted_2gpu_img_s"] for r in tab["rows"]},
+                      predicted_2gpu_img_s=row["predicted_2gpu_img_s"] if row else None,
+                      one_gpu_img_s=tab.get("one_gpu_img_s"))
+    elif choice["source"] is None:
+        choice["source"] = "no measured table: one unit per step on the GPU"
     one = None
     if not args.no_graph and pipe.capturable:
         one, _ = _capture(pipe.step, [()], 1, ctx.rank)
@@ -500,7 +546,8 @@ def build_pipeline(args, ctx, batch) -> Workload:
                  fused_step=False, rccl_nranks=nranks, steps_per_graph=1 if one is not None else 0,
                  split_size=args.split_size, microbatches=batch // args.split_size, mb_per_unit=pipe.mb_group,
                  pipeline_units=pipe.n_mb, schedule=args.schedule, cross_stage_overlap=pipe.n_mb > 1,
-                 unit_choice=UNIT_CHOICE)
+                 unit_choice=choice, predicted_2gpu_img_s=choice.get("predicted_2gpu_img_s"),
+                 one_gpu_img_s=choice.get("one_gpu_img_s"))
     w.loss_rank = pipe.stages - 1
     w.close = pipe.close
     w.check = pipe.check
@@ -545,7 +592,9 @@ def _secondary_pipeline(ctx, timeout_s: float = 420.0):
                           global_batch=rec["config"]["global_batch"], final_loss=rec["config"]["final_loss"],
                           split_size=rec["config"].get("split_size"), mb_per_unit=rec["config"].get("mb_per_unit"),
                           cross_stage_overlap=rec["config"].get("cross_stage_overlap"),
-                          unit_choice=rec["config"].get("unit_choice"))
+                          unit_choice=rec["config"].get("unit_choice"),
+                          predicted_2gpu_img_s=rec["config"].get("predicted_2gpu_img_s"),
+                          one_gpu_img_s=rec["config"].get("one_gpu_img_s"))
     except subprocess.TimeoutExpired:
         result["error"] = f"timeout after {timeout_s:.0f} s"
     except Exception as exc:  # noqa: BLE001 - never let the secondary measurement cost the headline

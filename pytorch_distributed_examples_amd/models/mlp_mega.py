@@ -1,0 +1,139 @@
+"""The elastic-DDP MLP's whole training step as ONE persistent kernel launch (csrc/kernels/mlp_fused.hip).
+
+Reference: pytorch_elastic/mnist_ddp_elastic.py:133-173 (``Model``: Linear + ReLU stack, ``CrossEntropyLoss``,
+``optimizer.step()``); model of :mod:`.mlp`.  Single process (world 1: no gradient all-reduce sits between the
+backward and the update):
+
+    mega = MegaMLP(model, opt)        # opt: FusedAdam / FusedAdamW / FusedSGD over model.parameters() (one group)
+    loss = mega.step(x, y)            # forward + cross-entropy + backward + optimiser update: 1 launch
+
+Forward, loss, backward and the update of every layer run phase after phase inside one grid of one workgroup per
+CU (grid barriers between phases), each phase one global round trip.  The results are those of the layer-by-layer
+path (:class:`.mlp_fused.FusedMLP` + ``opt.step()``): same bf16 operands, fp32 accumulation, the optimiser's own
+per-element update (optim_device.h); gradients land in ``p.grad``, the optimiser state in ``opt.state``, the device
+step counter advances, and the bf16 weight copies the layers read are refreshed -- an eager ``model(x)`` after the
+step sees the updated weights.  ``kernel_launches_per_step() == 1``.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+from ..ops import functional as OF
+from ..ops.optim import _MODES
+
+
+class MegaMLP:
+    def __init__(self, net, opt):
+        self.net, self.opt = net, opt
+        self.layers = [net.input_layer, *net.hidden_layers, net.final_layer]
+        for i, L in enumerate(self.layers):
+            assert L.bias is not None and L.relu == (i < len(self.layers) - 1), "Linear+ReLU stack, plain last layer"
+        assert len(opt.param_groups) == 1, "one optimiser parameter group"
+        self.params = [p for L in self.layers for p in (L.weight, L.bias)]
+        assert [id(p) for p in opt.param_groups[0]["params"]] == [id(p) for p in self.params], \
+            "the optimiser must hold exactly the model's parameters, in model order"
+        self.mode = _MODES[opt.KIND]
+        self._bufs: dict = {}
+        self._grid = None
+        self.calls = 0
+        self.stamps = None  # set to a zeroed int64[128] GPU tensor: phase-boundary clocks (100 MHz), see phase_us
+
+    def _buffers(self, B: int, dev: torch.device):
+        key = (B, str(dev))
+        if key not in self._bufs:
+            bf = dict(dtype=torch.bfloat16, device=dev)
+            act, actT, d, dT = [], [], [], []
+            for i, L in enumerate(self.layers):
+                fin = L.in_features
+                actT.append(torch.empty(fin, B, **bf))
+                if i == 0:
+                    act.append(torch.empty(0, **bf)); d.append(torch.empty(0, **bf)); dT.append(torch.empty(0, **bf))
+                else:
+                    act.append(torch.empty(B, fin, **bf))
+                    d.append(torch.empty(B, fin, **bf))
+                    dT.append(torch.empty(fin, B, **bf))
+            self._bufs[key] = dict(
+                act=act, actT=actT, d=d, dT=dT,
+                dlog=torch.zeros(B, 32, **bf), dlogT=torch.zeros(32, B, **bf),  # zero padding is never written
+                loss_part=torch.zeros(B // 32, dtype=torch.float32, device=dev),
+                bar=torch.zeros(512, dtype=torch.int32, device=dev), err=torch.zeros(1, dtype=torch.int32, device=dev))
+        return self._bufs[key]
+
+    def grid(self) -> int:
+        if self._grid is None:
+            self._grid = int(_native.C().mlp_train_grid())
+        return self._grid
+
+    @torch.no_grad()
+    def step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        """One training step on (x [B, 784] fp32 images or [B, 1, 28, 28], y [B] labels); returns the mean loss."""
+        C = _native.C()
+        B = x.shape[0]
+        if B % 32:
+            raise ValueError(f"MegaMLP: batch {B} must be a multiple of 32")
+        for p in self.params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        group = self.opt.param_groups[0]
+        st = self.opt._group_dev(0, group, self.params)  # state tensors, device hyper-parameters and step counter
+        nl = len(self.layers)
+        wbf, wtbf = [], []
+        for i, L in enumerate(self.layers):
+            wbf.append(OF._maintained(L.weight, "bf16"))
+            wtbf.append(OF.maintain_transposed_copy(L.weight, 32 if i == nl - 1 else L.out_features) if i > 0
+                        else torch.empty(0, dtype=torch.bfloat16, device=x.device))
+        bufs = self._buffers(B, x.device)
+        state = self.opt.state
+        none = torch.empty(0, device=x.device)
+
+        def st_of(p, key):
+            return state[p].get(key, none)
+
+        mkey = "exp_avg" if self.mode != 0 else "momentum_buffer"
+        loss = torch.empty(1, dtype=torch.float32, device=x.device)
+        C.mlp_train(x.reshape(B, -1).float().contiguous(), y.long().contiguous(),
+                    [L.weight for L in self.layers], [L.bias for L in self.layers],
+                    [L.weight.grad for L in self.layers], [L.bias.grad for L in self.layers],
+                    [st_of(L.weight, mkey) for L in self.layers], [st_of(L.weight, "exp_avg_sq") for L in self.layers],
+                    [st_of(L.bias, mkey) for L in self.layers], [st_of(L.bias, "exp_avg_sq") for L in self.layers],
+                    wbf, wtbf, bufs["act"], bufs["actT"], bufs["d"], bufs["dT"], bufs["dlog"], bufs["dlogT"],
+                    bufs["loss_part"], loss, st["hp"], st["step"], self.mode, bufs["bar"], bufs["err"], self.grid(),
+                    self.stamps)
+        # the weights changed on the device: the in-place writes bypass the version counters, so stamp the
+        # copies current (they were refreshed by the same kernel) and invalidate generation-keyed caches
+        for L in self.layers:
+            d = L.weight.__dict__.get("_pde_maint")
+            if d is not None:
+                d["version"] = L.weight._version
+        OF.bump_weight_generation()
+        self.calls += 1
+        return loss[0]
+
+    def phase_us(self):
+        """Phase durations of the last step from :attr:`stamps` (synchronises; re-zeroes the latest-workgroup half):
+        [(name, workgroup 0 us, latest workgroup us), ...] -- the latest workgroup's column is the time from the
+        previous boundary's latest arrival to this one's."""
+        t = self.stamps.tolist()
+        self.stamps[64:].zero_()
+        nl = len(self.layers)
+        names = []
+        for l in range(nl - 1):
+            names += [f"F{l}", f"bar F{l}"]
+        names += ["CE", "bar CE"]
+        for j in range(nl - 1, 0, -1):
+            names += [f"B{j} dgrad+wgrad", f"B{j} arrive+update L{j + 1}" if j + 1 < nl else f"B{j} arrive",
+                      f"bar B{j} wait"]
+        names += ["B0 wgrad", "update L1 + L0"]
+        out = []
+        for i, n in enumerate(names):
+            out.append((n, (t[i + 1] - t[i]) / 100.0, (t[64 + i + 1] - t[64 + i]) / 100.0 if i > 0 else 0.0))
+        return out
+
+    def errors(self) -> int:
+        """Non-zero if a grid barrier of a step timed out (a workgroup could not be resident): synchronises."""
+        return int(sum(int(b["err"].item()) for b in self._bufs.values()))
+
+    @staticmethod
+    def kernel_launches_per_step() -> int:
+        return 1

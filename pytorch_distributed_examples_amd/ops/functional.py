@@ -262,6 +262,23 @@ def _derive_copies(p: torch.Tensor, d: dict):
         _C().conv_w_dgrad(w, cp, cop, d["conv_dgrad"])
     else:
         _C().cast_bf16_into(w, d["bf16"])
+    if "bf16_t" in d:  # the transposed copy (models/mlp_mega.py: the dgrad operand), padded columns stay zero
+        d["bf16_t"][:, :w.shape[0]].copy_(w.t())
+
+
+def maintain_transposed_copy(p: torch.Tensor, ldt: int) -> torch.Tensor:
+    """Also keep a transposed bf16 copy [in, ldt] (columns past ``out`` zero) of a linear weight in sync: the fused
+    MLP step (mlp_fused.hip) refreshes it with the update and reads it as the data-gradient operand; a write
+    outside it is detected by the version counter like the other copies (:func:`_maintained`)."""
+    d = p.__dict__.get("_pde_maint") or maintain_compute_copies(p)
+    if d is None:
+        raise ValueError("maintain_transposed_copy: a GPU fp32 linear weight is required")
+    t = d.get("bf16_t")
+    if t is None or t.shape[1] != ldt:
+        d["bf16_t"] = torch.zeros(p.shape[1], ldt, dtype=torch.bfloat16, device=p.device)
+        _derive_copies(p, d)
+        d["version"] = p._version
+    return _maintained(p, "bf16_t")
 
 
 def release_compute_copies(p: torch.Tensor) -> None:

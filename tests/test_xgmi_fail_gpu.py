@@ -109,8 +109,14 @@ hvd.barrier()
 if r == 1:
     time.sleep(1.5)
 g.fill_(float(r + 1))
-hvd.core.allreduce_inline_([g], op=hvd.Sum)      # graph-mode path: no engine cycle sees this call
-torch.cuda.synchronize()
+try:
+    hvd.core.allreduce_inline_([g], op=hvd.Sum)  # graph-mode path: no engine cycle sees this call
+    torch.cuda.synchronize()
+except HorovodInternalError as e:
+    # the late rank: by now rank 0's engine has failed and stopped its lockstep loop, so this rank's engine
+    # already saw the peer failure on the control plane (typed, never a hang)
+    assert r == 1, e
+    print("PEER_FAILURE_SEEN", r, str(e)[:80])
 if r == 0:
     try:
         hvd.core.check_health()
