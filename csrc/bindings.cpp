@@ -1257,6 +1257,7 @@ void mlp_train(const Tensor& x, const Tensor& y, const std::vector<Tensor>& w, c
   a.hp = hp.data_ptr<float>(); a.step = step.data_ptr<int>();
   a.bar = reinterpret_cast<unsigned*>(bar.data_ptr()); a.err = err.data_ptr<int>();
   a.stamps = nullptr;
+  a.flags = (std::getenv("PDE_MLP_PRELOAD") != nullptr && std::getenv("PDE_MLP_PRELOAD")[0] == '0') ? 1 : 0;
   if (stamps.has_value() && stamps->defined()) {
     TORCH_CHECK(stamps->is_cuda() && stamps->scalar_type() == at::kLong && stamps->numel() >= 128, "mlp_train: stamps int64[128]");
     a.stamps = reinterpret_cast<long long*>(stamps->data_ptr());

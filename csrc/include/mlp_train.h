@@ -38,6 +38,7 @@ struct MlpTrainArgs {
   unsigned* bar;  // [288], 16-B aligned: the grid barrier's counters (zeroed by a memset before every launch)
   int* err;
   long long* stamps;  // optional [128]: workgroup 0's / the latest workgroup's wall clock at each phase boundary
+  int flags;          // bit 0: do not load the update state during the backward GEMMs (PDE_MLP_PRELOAD=0)
 };
 int mlp_train_grid(int device);  // workgroups of the persistent launch (one per CU), 0 if it cannot be resident
 hipError_t mlp_train_step(const MlpTrainArgs& a, int grid, hipStream_t s);

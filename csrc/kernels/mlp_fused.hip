@@ -483,7 +483,10 @@ __device__ __forceinline__ void dgrad_prefetch(const MlpTrainArgs& a, int j, Row
 }
 
 // Backward phase of layer j: this workgroup's dgrad tile(s) (weights prefetched) and weight-gradient tile(s).
-__device__ void bwd_phase(const MlpTrainArgs& a, int j, RowLoads& R, Smem& sm) {
+// `U`: the optimiser state of this workgroup's first update tile of layer j + 1 (`UL`), loaded right behind the
+// GEMM operands so that its HBM traffic overlaps the GEMMs' latency; the update itself runs after the arrive.
+__device__ __forceinline__ void bwd_phase(const MlpTrainArgs& a, int j, RowLoads& R, Smem& sm, UpLoads& U, bool pre,
+                                          const MlpLayerArgs& UL, bool use_m, bool use_v) {
   const MlpLayerArgs& L = a.L[j];
   const bool last = j == a.nl - 1;
   const int B = a.B, mt = B / 32, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -568,6 +571,10 @@ __device__ void bwd_phase(const MlpTrainArgs& a, int j, RowLoads& R, Smem& sm) {
   const int wo0 = (t % ot) * 64, wi0 = (t / ot) * 64;
   if (do_dg) dgrad_load(t);
   if (do_wg) wg_load(Wg, rg, ra, B, L.out, L.in, wo0, wi0, 0, wi0 == 0);
+  if (pre) {
+    const int uot = (UL.out + 63) / 64, nup = uot * ((UL.in + 63) / 64);
+    if (t < nup) up_load(U, UL, (t % uot) * 64, (t / uot) * 64, use_m, use_v);
+  }
   if (do_dg) dgrad_finish(t);
   if (do_wg) wgrad_finish(Wg, wo0, wi0);
   for (int tt = t + gridDim.x; tt < g.n; tt += gridDim.x) {  // more tiles than workgroups: one after another
@@ -583,12 +590,17 @@ __device__ void bwd_phase(const MlpTrainArgs& a, int j, RowLoads& R, Smem& sm) {
 
 // The update of layer l (tiles of this workgroup: the ones whose weight gradient it computed)
 template <int MODE>
-__device__ void update_layer(const MlpTrainArgs& a, int l, const optdev::Hyper& h, bool use_m, Smem& sm) {
+__device__ __forceinline__ void update_layer(const MlpTrainArgs& a, int l, const optdev::Hyper& h, bool use_m, Smem& sm,
+                                             UpLoads& P, bool pre) {
   const MlpLayerArgs& L = a.L[l];
   const int uot = (L.out + 63) / 64, nup = uot * ((L.in + 63) / 64);
   for (int t = blockIdx.x; t < nup; t += gridDim.x) {
     UpLoads U;
     const int o0 = (t % uot) * 64, i0 = (t / uot) * 64;
+    if (pre && t == static_cast<int>(blockIdx.x)) {
+      up_finish<MODE>(P, L, h, o0, i0, use_m, sm);  // the first tile's state was loaded during the GEMMs
+      continue;
+    }
     up_load(U, L, o0, i0, use_m, MODE != 0);
     up_finish<MODE>(U, L, h, o0, i0, use_m, sm);
   }
@@ -668,21 +680,29 @@ __global__ __launch_bounds__(MT) void k_mlp_train(MlpTrainArgs a) {
   // B(nl-1) .. B1: dgrad + wgrad, then -- between arrive and wait -- the update of layer j + 1 (its weight
   // gradient tiles are this workgroup's from B(j+1); every dgrad that read its W^T finished before that barrier)
   // and the next dgrad's weight fragments
+  UpLoads U;
   for (int j = nl - 1; j >= 1; --j) {
-    bwd_phase(a, j, R, sm);
+    const bool up = j + 1 < nl;
+    const bool pre = up && (a.flags & 1) == 0;
+    bwd_phase(a, j, R, sm, U, pre, a.L[up ? j + 1 : j], use_m, MODE != 0);
     stamp(a, ks);
     grid_arrive(a.bar, kb);
-    if (j + 1 < nl) update_layer<MODE>(a, j + 1, h, use_m, sm);
+    if (up) update_layer<MODE>(a, j + 1, h, use_m, sm, U, pre);
     dgrad_prefetch(a, j - 1, R);
     stamp(a, ks);
     grid_wait(a.bar, a.err, kb++);
     stamp(a, ks);
   }
   // B0: layer 0's weight gradient; then the updates of layers 1 and 0 (no hand-off left: no barrier)
-  bwd_phase(a, 0, R, sm);
+  const bool pre0 = nl > 1 && (a.flags & 1) == 0;
+  bwd_phase(a, 0, R, sm, U, pre0, a.L[nl > 1 ? 1 : 0], use_m, MODE != 0);
   stamp(a, ks);
-  if (nl > 1) update_layer<MODE>(a, 1, h, use_m, sm);
-  update_layer<MODE>(a, 0, h, use_m, sm);
+  if (nl > 1) update_layer<MODE>(a, 1, h, use_m, sm, U, pre0);
+  // layer 0's weight / bias gradient tiles were stored by OTHER threads of this workgroup just above (B0): drain
+  // them and meet before the update reads them (the other layers have a grid barrier in between)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  update_layer<MODE>(a, 0, h, use_m, sm, U, false);
   stamp(a, ks);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     float s = 0.f;

@@ -664,6 +664,17 @@ __device__ __forceinline__ bool bn_partials_tagged(const float (&s1)[8], const f
   }
   __syncthreads();  // also publishes the epoch (bn_gen_start) to the block
   const uint32_t tag = *s_epoch + 1u;
+  if (nrb == 1) {  // one row chunk (small tensors, bn_fin_grid): the block's own sums ARE the totals -- no hand-off
+    if (tid < 2 * kBnCG) {
+      const int which = tid / kBnCG, ch = tid % kBnCG;
+      float v = 0.f;
+      for (int r = 0; r < kBnRows; ++r) v += red[which][r][ch];
+      (which ? tot2 : tot1)[ch] = v;
+    }
+    if (tid == 0) __hip_atomic_store(hdr, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    return true;
+  }
   if (tid < 2 * kBnCG) {
     const int which = tid / kBnCG, ch = tid % kBnCG;
     float v = 0.f;
@@ -1574,6 +1585,12 @@ int bn_fin_grid(int P, int C, int& rpb, int groups = 1) {
   const int target = std::min(bn_resident_cap(), kBlocks);  // (side-stream headroom may change at run time)
   int nrb = std::max(1, std::min(kChunks, target / (ncg * groups)));
   nrb = std::min(nrb, std::max(1, P / kBnRows));
+  // r5 (opt-in): tensors of <= PDE_BN_SINGLE_ROWS rows per group take ONE row chunk per channel group -- the block
+  // reads all rows of its 64 channels and needs no cross-block exchange.  Measured slower at every threshold
+  // (profiles/r5m_bench.jsonl: 512 / 1024 / 2048 rows, ResNet-50 3.227 -> 3.31 / 3.31 / 4.30 ms, stage 2 at m = 8
+  // 1.497 -> 1.77 ms): the exchange of 16-128 blocks is cheaper than one block streaming every row.  Default off.
+  static const int kSingleRows = std::getenv("PDE_BN_SINGLE_ROWS") ? std::atoi(std::getenv("PDE_BN_SINGLE_ROWS")) : 0;
+  if (P <= kSingleRows) nrb = 1;
   rpb = ceil_div(P, nrb);
   return ceil_div(P, rpb);
 }

@@ -482,15 +482,23 @@ def build_hvd_cnn(args, ctx, batch) -> Workload:
                             f"{' graph mode' if on_gpu else ''}"))
     w.group = group
 
+    keys = ("requests", "batches", "string_gathers", "bit_allreduces", "cache_hits", "cache_entries", "xgmi_batches",
+            "rccl_batches", "inplace_batches", "inline_calls")
+    marks = {}
+
+    def mark():  # engine counters at the start of the timed region
+        marks.update(hvd.engine_stats())
+
     def check():
         s2 = hvd.engine_stats()
-        w.info["engine"] = {k: s2[k] for k in ("requests", "batches", "string_gathers", "bit_allreduces",
-                                               "cache_hits", "cache_entries", "xgmi_batches", "rccl_batches",
-                                               "inplace_batches", "inline_calls") if k in s2}
+        w.info["engine"] = {k: s2[k] for k in keys if k in s2}
+        if marks:  # the timed region alone: in graph mode no negotiation cycle runs (bit_allreduces ~0)
+            w.info["engine_timed_region"] = {k: s2[k] - marks.get(k, 0) for k in keys if k in s2}
         if s2.get("error"):
             raise RuntimeError(f"hvd engine error: {s2['error']}")
 
     w.check = check
+    w.mark = mark
     w.close = hvd.shutdown
     return w
 
@@ -756,6 +764,8 @@ def main(argv=None):
     run_steps(work, 0, args.warmup)
     pdist.barrier(ctx)
     sync()
+    if hasattr(work, "mark"):
+        work.mark()
     t0 = time.perf_counter()
     loss = run_steps(work, args.warmup, args.steps)
     pdist.barrier(ctx)

@@ -50,7 +50,9 @@ def test_mega_step_matches_layerwise_path(gpu, cfg):
             # updates: identical math on (nearly) identical gradients; Adam's normalised step can differ by up to
             # 2 lr where a gradient component is ~0 and its sign flips between the two accumulation orders
             dp = (pa.detach() - pb.detach()).abs()
-            tol = 2.5e-3 if cfg == "reference_adam" else 5e-3
+            # SGD: the same update of the same gradient up to summation order (a stale-gradient race showed up here
+            # as 1e-4 differences in the first layer)
+            tol = 2.5e-3 if cfg == "reference_adam" else 2e-5
             assert dp.max().item() <= tol, (step, n, dp.max().item())
             assert (dp > 1e-4).float().mean().item() < 0.02, (step, n)
     assert mega.errors() == 0
