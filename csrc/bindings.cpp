@@ -1251,12 +1251,14 @@ void mlp_train(const Tensor& x, const Tensor& y, const std::vector<Tensor>& w, c
   CHECK_IN(hp); CHECK_F32(hp);
   TORCH_CHECK(hp.numel() >= pde::HP_COUNT, "mlp_train: hp");
   TORCH_CHECK(step.is_cuda() && step.scalar_type() == at::kInt && step.numel() >= 1, "mlp_train: step int32");
-  TORCH_CHECK(bar.is_cuda() && bar.scalar_type() == at::kInt && bar.numel() >= 288 && reinterpret_cast<uintptr_t>(bar.data_ptr()) % 16 == 0, "mlp_train: bar int32[288], 16-B aligned");
+  TORCH_CHECK(bar.is_cuda() && bar.scalar_type() == at::kInt && bar.numel() >= 320 && reinterpret_cast<uintptr_t>(bar.data_ptr()) % 16 == 0, "mlp_train: bar int32[320] (zeroed once), 16-B aligned");
   TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt && err.numel() >= 1, "mlp_train: err int32");
   a.loss_part = loss_part.data_ptr<float>(); a.loss = loss.data_ptr<float>();
   a.hp = hp.data_ptr<float>(); a.step = step.data_ptr<int>();
   a.bar = reinterpret_cast<unsigned*>(bar.data_ptr()); a.err = err.data_ptr<int>();
   a.stamps = nullptr;
+  // bit 0: the update state is loaded after the weight-gradient tiles instead of behind their operands
+  // (PDE_MLP_PRELOAD=0, A/B)
   a.flags = (std::getenv("PDE_MLP_PRELOAD") != nullptr && std::getenv("PDE_MLP_PRELOAD")[0] == '0') ? 1 : 0;
   if (stamps.has_value() && stamps->defined()) {
     TORCH_CHECK(stamps->is_cuda() && stamps->scalar_type() == at::kLong && stamps->numel() >= 128, "mlp_train: stamps int64[128]");

@@ -35,10 +35,10 @@ struct MlpTrainArgs {
   float *loss_part, *loss;
   const float* hp;
   int* step;
-  unsigned* bar;  // [288], 16-B aligned: the grid barrier's counters (zeroed by a memset before every launch)
+  unsigned* bar;  // [320], zeroed ONCE: the grid barrier's counters and launch word (monotonic across launches)
   int* err;
   long long* stamps;  // optional [128]: workgroup 0's / the latest workgroup's wall clock at each phase boundary
-  int flags;          // bit 0: do not load the update state during the backward GEMMs (PDE_MLP_PRELOAD=0)
+  int flags;          // bit 0: load the update state after the weight-gradient tiles, not with them (PDE_MLP_PRELOAD=0)
 };
 int mlp_train_grid(int device);  // workgroups of the persistent launch (one per CU), 0 if it cannot be resident
 hipError_t mlp_train_step(const MlpTrainArgs& a, int grid, hipStream_t s);

@@ -94,30 +94,36 @@ __device__ __forceinline__ float row16(float v, Op op) {
 // Grid barrier k, split and XCD-hierarchical: grid_arrive -- every wave drains its stores (the hand-off bytes, all
 // sc1), then lane 0 adds one arrival to its group's counter (group = workgroup index mod 8, the XCD round-robin of
 // the dispatcher; only the contention depends on that, not correctness), and the group's last arrival adds one to
-// the top counter; grid_wait -- lane 0 polls the top counter (sc1) until (k + 1) x groups have arrived.  Counters
-// are monotonic within a launch, each on its own 128-byte line, zeroed by a memset node before every launch.  Work
-// that neither produces nor consumes a hand-off (the optimiser update, prefetching the next phase's weight
-// fragments) runs between the two and hides the barrier's latency.
-constexpr int kBarGroups = 8, kBarStride = 32;  // counters 128 bytes apart: top at [0], group g at [32 (g + 1)]
-constexpr int kBarWords = kBarStride * (kBarGroups + 1);
-__device__ __forceinline__ void grid_arrive(unsigned* bar, int k) {
+// the top counter; grid_wait -- lane 0 polls the top counter (sc1) until this barrier's count has arrived.  Counters
+// are monotonic ACROSS launches (each on its own 128-byte line): barrier k of launch n waits for (n x nbar + k + 1)
+// arrivals per member, n = the launch word every workgroup reads at its start and workgroup 0 advances at its end
+// (after its last barrier, so every workgroup of the launch has read it) -- no memset node per launch.  Work that
+// neither produces nor consumes a hand-off (the optimiser update, prefetching the next phase's weight fragments)
+// runs between arrive and wait and hides the barrier's latency.
+constexpr int kBarGroups = 8, kBarStride = 32;  // top at [0], group g at [32 (g + 1)], the launch word at [32 x 9]
+constexpr int kBarWords = kBarStride * (kBarGroups + 2);
+struct Bar {
+  unsigned* w;
+  unsigned base;  // n x nbar
+};
+__device__ __forceinline__ void grid_arrive(const Bar& b, int k) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (threadIdx.x == 0) {
     const unsigned g = blockIdx.x % kBarGroups, grid = gridDim.x;
     const unsigned members = (grid - g + kBarGroups - 1) / kBarGroups;
-    const unsigned old = __hip_atomic_fetch_add(bar + kBarStride * (g + 1), 1u, __ATOMIC_RELAXED,
+    const unsigned old = __hip_atomic_fetch_add(b.w + kBarStride * (g + 1), 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1 == static_cast<unsigned>(k + 1) * members)
-      __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == (b.base + static_cast<unsigned>(k) + 1) * members)
+      __hip_atomic_fetch_add(b.w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
-__device__ __forceinline__ void grid_wait(unsigned* bar, int* err, int k) {
+__device__ __forceinline__ void grid_wait(const Bar& b, int* err, int k) {
   if (threadIdx.x == 0) {
     const unsigned groups = gridDim.x < kBarGroups ? gridDim.x : kBarGroups;
-    const unsigned target = static_cast<unsigned>(k + 1) * groups;
+    const unsigned target = (b.base + static_cast<unsigned>(k) + 1) * groups;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    while (__hip_atomic_load(b.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -485,8 +491,10 @@ __device__ __forceinline__ void dgrad_prefetch(const MlpTrainArgs& a, int j, Row
 // Backward phase of layer j: this workgroup's dgrad tile(s) (weights prefetched) and weight-gradient tile(s).
 // `U`: the optimiser state of this workgroup's first update tile of layer j + 1 (`UL`), loaded right behind the
 // GEMM operands so that its HBM traffic overlaps the GEMMs' latency; the update itself runs after the arrive.
-__device__ __forceinline__ void bwd_phase(const MlpTrainArgs& a, int j, RowLoads& R, Smem& sm, UpLoads& U, bool pre,
-                                          const MlpLayerArgs& UL, bool use_m, bool use_v) {
+// part 0: the dgrad tiles (the phase's hand-off, before the barrier's arrive); part 1: the weight-gradient tiles,
+// with the update state of layer j + 1 loaded behind their operands (between arrive and wait).
+__device__ __forceinline__ void bwd_phase(const MlpTrainArgs& a, int j, int part, RowLoads& R, Smem& sm, UpLoads& U,
+                                          bool pre, const MlpLayerArgs& UL, bool use_m, bool use_v) {
   const MlpLayerArgs& L = a.L[j];
   const bool last = j == a.nl - 1;
   const int B = a.B, mt = B / 32, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -566,21 +574,22 @@ __device__ __forceinline__ void bwd_phase(const MlpTrainArgs& a, int j, RowLoads
   };
 
   const int t = blockIdx.x;
+  if (part == 0) {
+    for (int tt = t; tt < g.n; tt += gridDim.x) {  // (more tiles than workgroups: one after another)
+      dgrad_load(tt);
+      dgrad_finish(tt);
+    }
+    return;
+  }
   WgLoads Wg;
-  const bool do_dg = t < g.n, do_wg = t < nwg;
+  const bool do_wg = t < nwg;
   const int wo0 = (t % ot) * 64, wi0 = (t / ot) * 64;
-  if (do_dg) dgrad_load(t);
   if (do_wg) wg_load(Wg, rg, ra, B, L.out, L.in, wo0, wi0, 0, wi0 == 0);
   if (pre) {
     const int uot = (UL.out + 63) / 64, nup = uot * ((UL.in + 63) / 64);
     if (t < nup) up_load(U, UL, (t % uot) * 64, (t / uot) * 64, use_m, use_v);
   }
-  if (do_dg) dgrad_finish(t);
   if (do_wg) wgrad_finish(Wg, wo0, wi0);
-  for (int tt = t + gridDim.x; tt < g.n; tt += gridDim.x) {  // more tiles than workgroups: one after another
-    dgrad_load(tt);
-    dgrad_finish(tt);
-  }
   for (int tt = t + gridDim.x; tt < nwg; tt += gridDim.x) {
     const int o0 = (tt % ot) * 64, i0 = (tt / ot) * 64;
     wg_load(Wg, rg, ra, B, L.out, L.in, o0, i0, 0, i0 == 0);
@@ -617,14 +626,33 @@ __device__ __forceinline__ void stamp(const MlpTrainArgs& a, int& k) {
   ++k;
 }
 
+// x^T (bf16, the first layer's weight-gradient operand, read in B0): 8 batch rows of one input column per thread
+__device__ __forceinline__ void write_xT(const MlpTrainArgs& a) {
+  const int in0 = a.L[0].in, nb = a.B / 8;
+  const rsrc_t rx = mkbuf(a.actT[0], static_cast<long>(in0) * a.B * 2);
+  for (int e = blockIdx.x * MT + threadIdx.x; e < in0 * nb; e += gridDim.x * MT) {
+    const int i = e / nb, m = (e % nb) * 8;
+    u16x8 o;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) o[jj] = f2bf(a.x[static_cast<long>(m + jj) * in0 + i]);
+    bst16_sc1(rx, (i * a.B + m) * 2, o);
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(MT) void k_mlp_train(MlpTrainArgs a) {
   __shared__ Smem sm;
   __shared__ int s_step;
+  __shared__ unsigned s_launch;
   int ks = 0, kb = 0;
   stamp(a, ks);
-  if (threadIdx.x == 0) s_step = __hip_atomic_load(a.step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  if (threadIdx.x == 0) {
+    s_step = __hip_atomic_load(a.step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    s_launch = __hip_atomic_load(a.bar + kBarStride * (kBarGroups + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   __syncthreads();
+  const int nbar = 2 * a.nl - 1;  // F0..F(L-2), CE, B(L-1)..B1
+  const Bar bar{a.bar, s_launch * static_cast<unsigned>(nbar)};
   optdev::Hyper h;
   h.lr = a.hp[HP_LR]; h.b1 = a.hp[HP_BETA1]; h.b2 = a.hp[HP_BETA2]; h.eps = a.hp[HP_EPS];
   h.wd = a.hp[HP_WD]; h.mom = a.hp[HP_MOMENTUM]; h.gscale = a.hp[HP_GRAD_SCALE];
@@ -641,65 +669,58 @@ __global__ __launch_bounds__(MT) void k_mlp_train(MlpTrainArgs a) {
   const int nl = a.nl, B = a.B;
   RowLoads R;
   if (nl > 1) fwd_prefetch(a, 0, R); else ce_prefetch(a, R);
-  // x^T (bf16, the first layer's weight-gradient operand): 8 batch rows of one input column per thread
-  {
-    const int in0 = a.L[0].in, nb = B / 8;
-    const rsrc_t rx = mkbuf(a.actT[0], static_cast<long>(in0) * B * 2);
-    for (int e = blockIdx.x * MT + threadIdx.x; e < in0 * nb; e += gridDim.x * MT) {
-      const int i = e / nb, m = (e % nb) * 8;
-      u16x8 o;
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) o[jj] = f2bf(a.x[static_cast<long>(m + jj) * in0 + i]);
-      bst16_sc1(rx, (i * B + m) * 2, o);
-    }
-  }
   if (nl > 1) {
     fwd_phase<true>(a, 0, R, sm);
     stamp(a, ks);
-    grid_arrive(a.bar, kb);
+    grid_arrive(bar, kb);
+    write_xT(a);  // drained by the next arrive, read only in B0
     if (nl > 2) fwd_prefetch(a, 1, R); else ce_prefetch(a, R);
-    grid_wait(a.bar, a.err, kb++);
+    grid_wait(bar, a.err, kb++);
     stamp(a, ks);
     for (int l = 1; l < nl - 1; ++l) {
       fwd_phase<false>(a, l, R, sm);
       stamp(a, ks);
-      grid_arrive(a.bar, kb);
+      grid_arrive(bar, kb);
       if (l + 1 < nl - 1) fwd_prefetch(a, l + 1, R); else ce_prefetch(a, R);
-      grid_wait(a.bar, a.err, kb++);
+      grid_wait(bar, a.err, kb++);
       stamp(a, ks);
     }
     ce_phase<false>(a, R, sm);
   } else {
+    write_xT(a);
     ce_phase<true>(a, R, sm);
   }
   stamp(a, ks);
-  grid_arrive(a.bar, kb);
+  grid_arrive(bar, kb);
   dgrad_prefetch(a, nl - 1, R);
-  grid_wait(a.bar, a.err, kb++);
+  grid_wait(bar, a.err, kb++);
   stamp(a, ks);
-  // B(nl-1) .. B1: dgrad + wgrad, then -- between arrive and wait -- the update of layer j + 1 (its weight
-  // gradient tiles are this workgroup's from B(j+1); every dgrad that read its W^T finished before that barrier)
-  // and the next dgrad's weight fragments
+  // B(nl-1) .. B1: the dgrad tiles (the hand-off), then -- between arrive and wait -- the weight-gradient tiles of
+  // layer j, the update of layer j + 1 (its weight-gradient tiles are this workgroup's from B(j+1)'s window; every
+  // dgrad that read its W^T finished before that barrier) and the next dgrad's weight fragments
   UpLoads U;
   for (int j = nl - 1; j >= 1; --j) {
     const bool up = j + 1 < nl;
     const bool pre = up && (a.flags & 1) == 0;
-    bwd_phase(a, j, R, sm, U, pre, a.L[up ? j + 1 : j], use_m, MODE != 0);
+    bwd_phase(a, j, 0, R, sm, U, false, a.L[j], use_m, MODE != 0);
     stamp(a, ks);
-    grid_arrive(a.bar, kb);
+    grid_arrive(bar, kb);
+    bwd_phase(a, j, 1, R, sm, U, pre, a.L[up ? j + 1 : j], use_m, MODE != 0);
     if (up) update_layer<MODE>(a, j + 1, h, use_m, sm, U, pre);
     dgrad_prefetch(a, j - 1, R);
     stamp(a, ks);
-    grid_wait(a.bar, a.err, kb++);
+    grid_wait(bar, a.err, kb++);
     stamp(a, ks);
   }
-  // B0: layer 0's weight gradient; then the updates of layers 1 and 0 (no hand-off left: no barrier)
+  // B0: layer 0's weight gradient and the updates of layers 1 and 0 (no hand-off left: no barrier).  Gradient tiles
+  // stored by OTHER threads of this workgroup earlier (layer 1 in B1's window, layer 0 just below) are drained and
+  // met before the updates read them (the other layers have a grid barrier's arrive in between)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   const bool pre0 = nl > 1 && (a.flags & 1) == 0;
-  bwd_phase(a, 0, R, sm, U, pre0, a.L[nl > 1 ? 1 : 0], use_m, MODE != 0);
+  bwd_phase(a, 0, 1, R, sm, U, pre0, a.L[nl > 1 ? 1 : 0], use_m, MODE != 0);
   stamp(a, ks);
   if (nl > 1) update_layer<MODE>(a, 1, h, use_m, sm, U, pre0);
-  // layer 0's weight / bias gradient tiles were stored by OTHER threads of this workgroup just above (B0): drain
-  // them and meet before the update reads them (the other layers have a grid barrier in between)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   update_layer<MODE>(a, 0, h, use_m, sm, U, false);
@@ -708,8 +729,9 @@ __global__ __launch_bounds__(MT) void k_mlp_train(MlpTrainArgs a) {
     float s = 0.f;
     for (int t = 0; t < B / 32; ++t) s += __hip_atomic_load(a.loss_part + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     a.loss[0] = s / static_cast<float>(B);
-    // every workgroup read the old count at its start, before the first barrier
+    // every workgroup read the old count (and the launch word) at its start, before the first barrier
     __hip_atomic_store(a.step, s_step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.bar + kBarStride * (kBarGroups + 1), s_launch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -728,9 +750,6 @@ int mlp_train_grid(int device) {
 
 hipError_t mlp_train_step(const MlpTrainArgs& a, int grid, hipStream_t s) {
   if (grid <= 0 || a.nl < 1 || a.nl > kMlpMaxLayers || a.B % 32 != 0) return hipErrorInvalidValue;
-  // the barrier's arrival counter starts at zero in every launch (a memset node ahead of the kernel in a graph)
-  hipError_t e = hipMemsetAsync(a.bar, 0, kBarWords * sizeof(unsigned), s);
-  if (e != hipSuccess) return e;
   switch (a.mode) {
     case 0: hipLaunchKernelGGL(k_mlp_train<0>, dim3(grid), dim3(MT), 0, s, a); break;
     case 1: hipLaunchKernelGGL(k_mlp_train<1>, dim3(grid), dim3(MT), 0, s, a); break;

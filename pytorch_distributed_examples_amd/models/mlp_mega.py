@@ -122,7 +122,7 @@ class MegaMLP:
             names += [f"F{l}", f"bar F{l}"]
         names += ["CE", "bar CE"]
         for j in range(nl - 1, 0, -1):
-            names += [f"B{j} dgrad+wgrad", f"B{j} arrive+update L{j + 1}" if j + 1 < nl else f"B{j} arrive",
+            names += [f"B{j} dgrad", f"B{j} arrive+wgrad+update L{j + 1}" if j + 1 < nl else f"B{j} arrive+wgrad",
                       f"bar B{j} wait"]
         names += ["B0 wgrad", "update L1 + L0"]
         out = []
@@ -131,8 +131,16 @@ class MegaMLP:
         return out
 
     def errors(self) -> int:
-        """Non-zero if a grid barrier of a step timed out (a workgroup could not be resident): synchronises."""
-        return int(sum(int(b["err"].item()) for b in self._bufs.values()))
+        """Non-zero if a grid barrier of a step timed out (a workgroup could not be resident): synchronises.  The
+        barrier counters run across launches; after a timeout they are re-zeroed here (with the error word)."""
+        n = 0
+        for b in self._bufs.values():
+            e = int(b["err"].item())
+            if e:
+                b["bar"].zero_()
+                b["err"].zero_()
+            n += e
+        return n
 
     @staticmethod
     def kernel_launches_per_step() -> int:
