@@ -503,10 +503,10 @@ def build_hvd_cnn(args, ctx, batch) -> Workload:
     return w
 
 
-# The measured pipeline-unit table (scripts/pipeline_units.py --json over the stage benches of this round): the
-# default GPU unit size of resnet50_pp and the predicted-vs-1-GPU numbers its record carries.
-UNIT_TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "profiles",
-                          "r5_pipeline_units.json")
+# The measured pipeline-unit table (scripts/pipeline_units.py --json over the stage benches of this round; a copy
+# of profiles/r5_pipeline_units.json shipped with the package, so every GPU box has it): the default GPU unit size
+# of resnet50_pp and the predicted-vs-1-GPU numbers its record carries.
+UNIT_TABLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "pipeline_units.json")
 
 
 def _unit_table():
@@ -535,8 +535,7 @@ def build_pipeline(args, ctx, batch) -> Workload:
                             mb_group=mb_group)
     if tab:
         row = next((r for r in tab["rows"] if r["mb_per_unit"] == pipe.mb_group), None)
-        choice.update(table=os.path.relpath(os.environ.get("PDE_PIPE_UNIT_TABLE", UNIT_TABLE),
-                                            os.path.dirname(os.path.dirname(UNIT_TABLE))),
+        choice.update(table=tab.get("source_table", "profiles/r5_pipeline_units.json"),
                       formula=tab.get("formula"),
                       rows={r["mb_per_unit"]: r["predicted_2gpu_img_s"] for r in tab["rows"]},
                       predicted_2gpu_img_s=row["predicted_2gpu_img_s"] if row else None,

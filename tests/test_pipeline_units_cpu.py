@@ -70,6 +70,6 @@ def test_committed_table_is_readable():
     from pytorch_distributed_examples_amd.bench import harness
 
     tab = harness._unit_table()
-    assert tab is not None, "profiles/r5_pipeline_units.json is the measured table the GPU default comes from"
+    assert tab is not None, "bench/pipeline_units.json (= profiles/r5_pipeline_units.json) is the measured table"
     assert tab["best"]["mb_per_unit"] in {r["mb_per_unit"] for r in tab["rows"]}
     assert tab["one_gpu_img_s"] and all("predicted_2gpu_img_s" in r for r in tab["rows"])
