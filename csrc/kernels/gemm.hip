@@ -288,13 +288,22 @@ TileCfg choose_tiles(const GemmArgs& a, int& split, bool wide = false) {
 #ifndef PDE_GEMM_CORE_DEFAULT
 #define PDE_GEMM_CORE_DEFAULT 0
 #endif
-bool dma_core_on() {
-  static const bool on = [] {
+// 0 ring, 1 dma, 2 hybrid: the DMA core for the shapes where it measured faster (profiles/r5d: 3x3 forward
+// convolutions up to M = 8192, and long-K problems with M <= 2048), the ring core elsewhere
+int gemm_core_mode() {
+  static const int mode = [] {
     const char* e = std::getenv("PDE_GEMM_CORE");
-    if (e == nullptr) return PDE_GEMM_CORE_DEFAULT != 0;
-    return std::strcmp(e, "dma") == 0;
+    if (e == nullptr) return static_cast<int>(PDE_GEMM_CORE_DEFAULT);
+    if (std::strcmp(e, "dma") == 0) return 1;
+    if (std::strcmp(e, "hybrid") == 0) return 2;
+    return 0;
   }();
-  return on;
+  return mode;
+}
+bool dma_core_on() { return gemm_core_mode() != 0; }
+bool dma_shape_ok(const GemmArgs& a) {
+  if (gemm_core_mode() != 2) return true;
+  return (a.a.kind == 1 && a.M <= 8192) || (a.K >= 512 && a.M <= 2048);
 }
 enum DmaCfg { kD64 = 0, kD128x64 = 1, kD64x128 = 2, kD128 = 3 };
 int dma_forced_tile() {
@@ -403,6 +412,7 @@ bool launch_dma(int cfg, bool akc, bool bkc, const GemmArgs& a, hipStream_t s, i
 template <bool AKC, bool BKC>
 bool dispatch_dma(const GemmArgs& a, hipStream_t s, hipError_t& err) {
   if (!dma_core_on() || generic_only() || a.bn_in.ss != nullptr) return false;  // (BN fold: ring core only)
+  if (!dma_shape_ok(a)) return false;
   if (!fast_ok(a, a.a, AKC, a.M) || !fast_ok(a, a.b, BKC, a.N)) return false;
   int split = 1;
   const int cfg = choose_dma(a, split);
@@ -440,7 +450,7 @@ bool bn_stats_ok_impl(const GemmArgs& a, hipStream_t s) {
   if (skinny_ok(a) || !is_kc(a.a) || !is_kc(a.b)) return false;
   int split = 1;
   if (!fast_ok(a, a.a, true, a.M) || !fast_ok(a, a.b, true, a.N)) return false;
-  if (dma_core_on()) {  // the DMA core emits statistics on every tile; a tile must not straddle two groups
+  if (dma_core_on() && dma_shape_ok(a)) {  // the DMA core emits statistics on every tile: no tile across groups
     static const int bm[4] = {64, 128, 64, 128};
     if (a.bn_out.rows_per_group % bm[choose_dma(a, split)] != 0) return false;
   } else if (choose_tiles(a, split, true) != kTile64) {
@@ -661,7 +671,7 @@ hipError_t gemm_bf16_pair(const GemmArgs& a0_in, const GemmArgs& a1_in, hipStrea
   }
   d = PairDims{};
   sp1 = 1;
-  const bool dma = dma_core_on();
+  const bool dma = gemm_core_mode() == 1;  // (hybrid: paired launches stay on the ring core)
   const bool ok = gemm_pair_enabled() &&
                   pair_member_plan(a0, d.tm[0], d.tn[0], d.kps[0], sp0, d.av[0], d.bv[0], dma) &&
                   pair_member_plan(a1, d.tm[1], d.tn[1], d.kps[1], sp1, d.av[1], d.bv[1], dma) &&
