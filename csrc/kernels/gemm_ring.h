@@ -400,16 +400,24 @@ __device__ __forceinline__ void splitk_reduce4_block(const GemmArgs& args, int s
   const int col = threadIdx.x % COLS, sl = threadIdx.x / COLS;
   const int c4 = block * COLS + col;
   const f32x4* w4 = reinterpret_cast<const f32x4*>(args.workspace);
-  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
   if (c4 < total4) {
+    // four slabs per trip, all loads issued before the adds (a lane sums <= 4 slabs at every split count the
+    // lane choice allows: one memory round trip instead of two or four dependent ones)
     int z = sl;
-    for (; z + LANES < splits; z += 2 * LANES) {
-      a0 += w4[static_cast<long>(z) * total4 + c4];
-      a1 += w4[static_cast<long>(z + LANES) * total4 + c4];
+    for (; z + 3 * LANES < splits; z += 4 * LANES) {
+      const f32x4 x0 = w4[static_cast<long>(z) * total4 + c4];
+      const f32x4 x1 = w4[static_cast<long>(z + LANES) * total4 + c4];
+      const f32x4 x2 = w4[static_cast<long>(z + 2 * LANES) * total4 + c4];
+      const f32x4 x3 = w4[static_cast<long>(z + 3 * LANES) * total4 + c4];
+      a0 += x0;
+      a1 += x1;
+      a2 += x2;
+      a3 += x3;
     }
     for (; z < splits; z += LANES) a0 += w4[static_cast<long>(z) * total4 + c4];
   }
-  f32x4 v = a0 + a1;
+  f32x4 v = (a0 + a1) + (a2 + a3);
   if constexpr (LANES > 1) {
     part[sl][col] = v;
     __syncthreads();
