@@ -198,6 +198,13 @@ class direct_grad_accumulation:
         _DIRECT_GRAD[0] = self._old
 
 
+def _sink_accum(g) -> bool:
+    """Whether a kernel writing into the gradient sink ``g`` must ADD: False for the first writer after a
+    zero-filling ``zero_grad`` (parallel/ddp.py marks the views) -- it stores, bitwise the same as adding to zero,
+    without reading the gradient back (the scattered OIHW epilogues read-modify-wrote every element)."""
+    return not g.__dict__.pop("_pde_fresh", False)
+
+
 def _grad_sink(p):
     """``p.grad`` when a kernel may accumulate straight into it, else None (return the grad to autograd)."""
     if p is None or not _DIRECT_GRAD[0]:
@@ -337,7 +344,7 @@ class _LinearFn(torch.autograd.Function):
             # dgrad + wgrad as ONE paired GEMM launch (the dgrad's tiles first: it feeds the next layer)
             with gemm_pair(defer_second=True):
                 dx = _C().linear_dgrad(dy, wb, x if ctx.mask_input_grad else None)
-                _C().linear_wgrad(dy, x, wsink, True)
+                _C().linear_wgrad(dy, x, wsink, _sink_accum(wsink))
             if bsink is not None:
                 _C().colsum(dy, -1, bsink, True)
             elif ctx.has_bias and ctx.needs_input_grad[2]:
@@ -347,7 +354,7 @@ class _LinearFn(torch.autograd.Function):
                 and ctx.needs_input_grad[0] and streams.active_for(dy):
             # weight / bias gradients go straight into .grad on the side stream, concurrent with the dgrad
             with streams.fork(dy, x):
-                _C().linear_wgrad(dy, x, wsink, True)
+                _C().linear_wgrad(dy, x, wsink, _sink_accum(wsink))
                 if bsink is not None:
                     _C().colsum(dy, -1, bsink, True)
             dx = _C().linear_dgrad(dy, wb, x if ctx.mask_input_grad else None)
@@ -355,7 +362,7 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = _C().linear_dgrad(dy, wb, x if ctx.mask_input_grad else None)
         if ctx.needs_input_grad[1]:
-            dw = _C().linear_wgrad(dy, x, wsink, wsink is not None)
+            dw = _C().linear_wgrad(dy, x, wsink, wsink is not None and _sink_accum(wsink))
             if wsink is not None:
                 dw = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
@@ -449,9 +456,9 @@ def _conv_backward(ctx, dy, x, weight, y=None):
             # the weight (and bias) gradient is off the critical path: side stream, issued BEFORE the dgrad so
             # the fork point does not wait for it (ops/streams.py)
             with streams.fork(dy, x):
-                _C().conv_wgrad(dy, x, r, s, stride, pad, co, ci, wsink, True)
+                _C().conv_wgrad(dy, x, r, s, stride, pad, co, ci, wsink, _sink_accum(wsink))
                 if bsink is not None:
-                    _C().colsum(dy, co, bsink, True)
+                    _C().colsum(dy, co, bsink, _sink_accum(bsink))
         paired = wsink is not None and ctx.needs_input_grad[0] and not side
         if paired:
             # dgrad + wgrad as ONE paired GEMM launch (dgrad tiles first); the dgrad op is issued first
@@ -476,7 +483,7 @@ def _conv_backward(ctx, dy, x, weight, y=None):
                 dx = None
         if paired:
             try:
-                _C().conv_wgrad(dy, x, r, s, stride, pad, co, ci, wsink, True)
+                _C().conv_wgrad(dy, x, r, s, stride, pad, co, ci, wsink, _sink_accum(wsink))
             except BaseException as exc:
                 pair.__exit__(type(exc), exc, None)
                 raise
@@ -490,7 +497,7 @@ def _conv_backward(ctx, dy, x, weight, y=None):
             return dx, None, None
         if ctx.needs_input_grad[1]:
             # OIHW epilogue: the GEMM writes the parameter's layout (and adds into .grad when it exists)
-            dw = _C().conv_wgrad(dy, x, r, s, stride, pad, co, ci, wsink, wsink is not None)
+            dw = _C().conv_wgrad(dy, x, r, s, stride, pad, co, ci, wsink, wsink is not None and _sink_accum(wsink))
             if wsink is not None:
                 dw = None
         if ctx.has_bias and ctx.needs_input_grad[2]:

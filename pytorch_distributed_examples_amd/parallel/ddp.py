@@ -224,6 +224,9 @@ class DistributedDataParallel(nn.Module):
         for p in self._params:
             if p.grad is None or p.grad.data_ptr() != self._views[p].data_ptr():
                 p.grad = self._views[p]
+            # zero-filled: the first weight-gradient kernel of the step may store instead of add
+            # (ops.functional._sink_accum; bitwise the same as adding to zero, no read-modify-write)
+            p.grad.__dict__["_pde_fresh"] = True
 
     def remove_hooks(self):
         """Detach from the parameters (before wrapping the same module in a new DDP, e.g. per round)."""
