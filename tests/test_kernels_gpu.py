@@ -526,3 +526,45 @@ def test_inkernel_splitk_path(gpu):
                           f"{here}::test_linear_fwd_bwd", f"{here}::test_conv_fwd_bwd"],
                          env=env, capture_output=True, text=True, timeout=300, cwd=os.path.dirname(os.path.dirname(here)))
     assert res.returncode == 0, res.stdout[-3000:] + res.stderr[-3000:]
+
+
+def test_first_write_after_zero_grad_stores(gpu):
+    """DDP.zero_grad marks the flat gradient's views freshly zeroed; the first weight-gradient kernel of the step
+    then stores instead of adding (no read-modify-write), later kernels of the same step add.  Garbage planted in
+    the buffer AFTER zero_grad is overwritten by the first backward; a second backward accumulates."""
+    from pytorch_distributed_examples_amd.ops import layers as L
+    from pytorch_distributed_examples_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(5)
+    conv = L.Conv2d(16, 24, 3, stride=1, padding=1).to(gpu)
+    conv1 = L.Conv2d(24, 32, 1).to(gpu)
+    bn = L.BatchNorm2d(32).to(gpu)
+    fc = L.Linear(32, 10).to(gpu)
+    model = torch.nn.ModuleList([conv, conv1, bn, fc])
+    x = OF.to_native_image(torch.randn(4, 16, 12, 12, device=gpu))
+
+    def loss():
+        h = bn(conv1(conv(x)), relu=True)
+        return OF.mse_loss(fc(OF.global_avg_pool_flat(h), out_f32=True), torch.ones(4, 10, device=gpu))
+
+    params = list(model.parameters())
+    with OF.direct_grad_accumulation(False):
+        for p in params:
+            p.grad = None
+        loss().backward()
+    ref1 = [p.grad.clone() for p in params]
+    ddp = DistributedDataParallel(model, overlap=False)
+    ddp.zero_grad()
+    weights = [conv.weight, conv1.weight, fc.weight]
+    for w in weights:
+        w.grad.fill_(123.0)  # would survive a read-modify-write; a first write must replace it
+    loss().backward()
+    for p, r in zip(params, ref1):
+        if any(p is w for w in weights):
+            assert rel_err(p.grad, r) < 1e-5
+    for w in weights:
+        assert "_pde_fresh" not in w.grad.__dict__
+    loss().backward()  # same step, no zero_grad: adds
+    for p, r in zip(params, ref1):
+        if any(p is w for w in weights):
+            assert rel_err(p.grad, 2 * r) < 1e-5
