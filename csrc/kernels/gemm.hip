@@ -224,8 +224,10 @@ struct TilePolicy {
   // r2j sweep (FAST loaders): ResNet-50 4.66 -> 4.48 ms; r2m sweep after dgrad/wgrad pairing (a paired
   // launch already fills the chip with two grids, so each member needs less split-K): split targets
   // 512 -> 256 blocks, small outputs >= 8 K-tiles per split -- ResNet-50 3.97 -> 3.84 ms, MLP 0.235 -> 0.228 ms
+  // r5x re-sweep after the first-write gradient change: K-tiles per split 16 -> 8 -- ResNet-50 level (3.134 ms),
+  // pipeline stage 2 at m = 8 1.398 -> 1.353 ms (profiles/r5x_split_policy_sweep.txt)
   long t128_min = 2048, split_target = 256, small_mn = 262144, small_split_target = 256;
-  int split_min_kt = 16, small_split_min_kt = 8;
+  int split_min_kt = 8, small_split_min_kt = 8;
   // 128x64 tile (64x32 per wave: 25 % less LDS traffic per MFMA than the 64x64 tile's 32x32 wave tiles) for
   // unpaired GEMMs with at least wide_min 64x64 tiles (0: off)
   long wide_min = 0;
