@@ -281,10 +281,15 @@ def _cache_worker(rank, world):
 
     step()
     step()
+    # the engine cycles in the background: without a barrier a rank that finished early would already
+    # announce the next (uncached) allgather below, and the other rank would count that cycle's string gather
+    # inside its own steady-state window.  The barrier runs on the c10d control group, not through the engine.
+    hvd.barrier()
     s0 = hvd.engine_stats()
     for _ in range(10):
         step()
     s1 = hvd.engine_stats()
+    hvd.barrier()
     assert s1["string_gathers"] == s0["string_gathers"], (s0, s1)  # steady state: no string negotiation
     assert s1["cache_hits"] - s0["cache_hits"] >= 10 * len(list(m.parameters())), (s0, s1)
     assert s1["bit_allreduces"] > s0["bit_allreduces"] and s1["cache_entries"] >= 8
