@@ -1260,6 +1260,8 @@ void mlp_train(const Tensor& x, const Tensor& y, const std::vector<Tensor>& w, c
   // bit 0: the update state is loaded after the weight-gradient tiles instead of behind their operands
   // (PDE_MLP_PRELOAD=0, A/B)
   a.flags = (std::getenv("PDE_MLP_PRELOAD") != nullptr && std::getenv("PDE_MLP_PRELOAD")[0] == '0') ? 1 : 0;
+  // (PDE_MLP_FUSE=0: the update of layer j one window after its weight gradient, read back from gw -- A/B)
+  if (std::getenv("PDE_MLP_FUSE") != nullptr && std::getenv("PDE_MLP_FUSE")[0] == '0') a.flags |= 2;
   if (stamps.has_value() && stamps->defined()) {
     TORCH_CHECK(stamps->is_cuda() && stamps->scalar_type() == at::kLong && stamps->numel() >= 128, "mlp_train: stamps int64[128]");
     a.stamps = reinterpret_cast<long long*>(stamps->data_ptr());

@@ -39,6 +39,7 @@ struct MlpTrainArgs {
   int* err;
   long long* stamps;  // optional [128]: workgroup 0's / the latest workgroup's wall clock at each phase boundary
   int flags;          // bit 0: load the update state after the weight-gradient tiles, not with them (PDE_MLP_PRELOAD=0)
+                      // bit 1: no fused wgrad + update (PDE_MLP_FUSE=0)
 };
 int mlp_train_grid(int device);  // workgroups of the persistent launch (one per CU), 0 if it cannot be resident
 hipError_t mlp_train_step(const MlpTrainArgs& a, int grid, hipStream_t s);

@@ -22,9 +22,11 @@
 // Phases for L layers (L = 7 for the reference model: 15 phases, 14 grid barriers):
 //   F0..F(L-2)  hidden forwards (F0 also writes x^T, the first layer's wgrad operand; x fp32 -> bf16 on load)
 //   CE          last layer's logits + softmax cross-entropy (mean) + d logits, per 32-row tile (DPP row reductions)
-//   Bj (j = L-1..0): dgrad of layer j (j >= 1), weight + bias gradient of layer j, and the UPDATE of layer j + 1
-//               (its gradients were completed in B(j+1) by this same workgroup, and no later phase reads it)
-//   U0          update of layer 0, the step's mean loss, the device step counter
+//   Bj (j = L-1..0): dgrad of layer j (j >= 1), then the weight + bias gradient of layer j and its UPDATE straight
+//               from the accumulators (the W^T tile parked in LDS until the next window: W^T is still being read
+//               by other workgroups' dgrads until this phase's barrier) -- every layer's 64x64 gradient tiles fit
+//               the grid; otherwise (PDE_MLP_FUSE=0 too) the update of layer j + 1, read back from gw, one window
+//               later.  After B0: the step's mean loss, the device step counter
 //
 // Inter-workgroup visibility (MI355X_MICROARCH.md, "Valid forms"; cdna_hip_programming.md Guideline 16): every byte
 // handed from one workgroup to another inside the launch (activations, gradients, d logits, x^T, loss partials) is
@@ -138,7 +140,9 @@ __device__ __forceinline__ void grid_wait(const Bar& b, int* err, int k) {
 struct Smem {
   f32x4 red[3][2][64];      // row-GEMM: waves 1..3's K-quarter partials
   uint16_t ep[32][24];      // row-GEMM epilogue: the 32x16 bf16 tile (wave 0)
-  uint16_t tr[64][72];      // update: the W^T tile
+  uint16_t tr[64][72];      // update: the W^T tile (fused form: parked here until the next window)
+  float gt[64][68];         // fused form: the weight-gradient tile, accumulator layout -> update layout
+  float gb[64];             //             and its bias gradients
 };
 
 // ---- row-GEMM tile: C[m0, m0+32) x [n0, n0+16) of A[M][K] . W[N][K]^T, K split over the 4 waves ----------------
@@ -287,14 +291,15 @@ struct UpLoads {
   float bp, bg, bm, bv;
 };
 
-__device__ __forceinline__ void up_load(UpLoads& U, const MlpLayerArgs& L, int o0, int i0, bool use_m, bool use_v) {
+__device__ __forceinline__ void up_load(UpLoads& U, const MlpLayerArgs& L, int o0, int i0, bool use_m, bool use_v,
+                                        bool load_g = true) {
   const int tc = threadIdx.x & 15, tr0 = threadIdx.x >> 4, i = i0 + 4 * tc;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int o = o0 + tr0 + 16 * q;
     const long e = (o < L.out && i < L.in) ? static_cast<long>(o) * L.in + i : 0;  // clamped: loaded, not stored
     U.p[q] = optdev::ld4<1>(L.w + e);
-    U.g[q] = optdev::ld4<1>(L.gw + e);
+    if (load_g) U.g[q] = optdev::ld4<1>(L.gw + e);
     U.m[q] = use_m ? optdev::ld4<1>(L.mw + e) : f32x4{0.f, 0.f, 0.f, 0.f};
     U.v[q] = use_v ? optdev::ld4<1>(L.vw + e) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
@@ -302,15 +307,17 @@ __device__ __forceinline__ void up_load(UpLoads& U, const MlpLayerArgs& L, int o
   U.bp = U.bg = U.bm = U.bv = 0.f;
   if (i0 == 0 && threadIdx.x < 64 && ob < L.out) {
     U.bp = L.b[ob];
-    U.bg = L.gb[ob];
+    if (load_g) U.bg = L.gb[ob];
     if (use_m) U.bm = L.mb[ob];
     if (use_v) U.bv = L.vb[ob];
   }
 }
 
+__device__ __forceinline__ void wt_flush(const MlpLayerArgs& L, int o0, int i0, Smem& sm);
+
 template <int MODE>
 __device__ __forceinline__ void up_finish(UpLoads& U, const MlpLayerArgs& L, const optdev::Hyper& h, int o0, int i0,
-                                          bool use_m, Smem& sm) {
+                                          bool use_m, Smem& sm, bool park = false) {
   const int tc = threadIdx.x & 15, tr0 = threadIdx.x >> 4, i = i0 + 4 * tc;
   float pv[4][4];
 #pragma unroll
@@ -344,6 +351,12 @@ __device__ __forceinline__ void up_finish(UpLoads& U, const MlpLayerArgs& L, con
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int c = 0; c < 4; ++c) sm.tr[4 * tc + c][tr0 + 16 * q] = f2bf(pv[q][c]);
+  if (!park) wt_flush(L, o0, i0, sm);
+}
+
+// The W^T tile in sm.tr (64 input rows x 64 outputs) to L.wtbf: each thread 16 consecutive outputs of one input row
+__device__ __forceinline__ void wt_flush(const MlpLayerArgs& L, int o0, int i0, Smem& sm) {
+  if (L.wtbf == nullptr) return;
   lds_sync();
   const int il = threadIdx.x >> 2, part = threadIdx.x & 3;
   const int ii = i0 + il, ob16 = o0 + 16 * part;
@@ -488,6 +501,53 @@ __device__ __forceinline__ void dgrad_prefetch(const MlpTrainArgs& a, int j, Row
   if (t < g.n) row_load_w(R, L.wtbf, L.ldt, L.in, g.K, (t / mt) * 16);
 }
 
+// The weight + bias gradient of one 64x64 tile from its loaded operands: stored to gw / gb and, `sm` given, also
+// left in sm->gt / sm->gb for the fused update (accumulator layout; read back in the update layout after a sync)
+__device__ __forceinline__ void wgrad_tile(const MlpLayerArgs& L, WgLoads& WW, rsrc_t rg, rsrc_t ra, int B, int o0, int i0, Smem* sm) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wo = w >> 1, wi = w & 1;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+#pragma unroll
+    for (int f = 0; f < 2; ++f) acc[e][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  wg_mma(WW, acc);
+  float bsum = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) bsum += bf2f(WW.g[c][jj]);
+  for (int kb = 128; kb < B; kb += 128) {  // batches beyond 128: further passes (loads not overlapped)
+    wg_load(WW, rg, ra, B, L.out, L.in, o0, i0, kb, false);
+    wg_mma(WW, acc);
+  }
+  if (i0 == 0) {  // bias gradient: 4 threads per row
+    const int o = o0 + (threadIdx.x >> 2), q = threadIdx.x & 3, span = B / 4;
+    for (int b = q * span + 32; b < (q + 1) * span; b += 8) {  // spans beyond the 4 preloaded vectors
+      const u16x8 x = bld16<16>(rg, o < L.out ? (o * B + b) * 2 : OOB);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) bsum += bf2f(x[jj]);
+    }
+    bsum += __shfl_xor(bsum, 1, 64);
+    bsum += __shfl_xor(bsum, 2, 64);
+    if (q == 0 && o < L.out) L.gb[o] = bsum;
+    if (sm != nullptr && q == 0) sm->gb[threadIdx.x >> 2] = bsum;
+  }
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int il = 32 * wi + 16 * f + (lane & 15), i = i0 + il;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int ol = 32 * wo + 16 * e + 4 * (lane >> 4), o = o0 + ol;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (i < L.in && o + r < L.out) L.gw[static_cast<long>(o + r) * L.in + i] = acc[e][f][r];
+        if (sm != nullptr) sm->gt[ol + r][il] = acc[e][f][r];
+      }
+    }
+  }
+}
+
 // Backward phase of layer j: this workgroup's dgrad tile(s) (weights prefetched) and weight-gradient tile(s).
 // `U`: the optimiser state of this workgroup's first update tile of layer j + 1 (`UL`), loaded right behind the
 // GEMM operands so that its HBM traffic overlaps the GEMMs' latency; the update itself runs after the arrive.
@@ -532,46 +592,7 @@ __device__ __forceinline__ void bwd_phase(const MlpTrainArgs& a, int j, int part
     }
     lds_sync();
   };
-  auto wgrad_finish = [&](WgLoads& WW, int o0, int i0) {
-    const int wo = w >> 1, wi = w & 1;
-    f32x4 acc[2][2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e)
-#pragma unroll
-      for (int f = 0; f < 2; ++f) acc[e][f] = f32x4{0.f, 0.f, 0.f, 0.f};
-    wg_mma(WW, acc);
-    float bsum = 0.f;
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) bsum += bf2f(WW.g[c][jj]);
-    for (int kb = 128; kb < B; kb += 128) {  // batches beyond 128: further passes (loads not overlapped)
-      wg_load(WW, rg, ra, B, L.out, L.in, o0, i0, kb, false);
-      wg_mma(WW, acc);
-    }
-    if (i0 == 0) {  // bias gradient: 4 threads per row
-      const int o = o0 + (threadIdx.x >> 2), q = threadIdx.x & 3, span = B / 4;
-      for (int b = q * span + 32; b < (q + 1) * span; b += 8) {  // spans beyond the 4 preloaded vectors
-        const u16x8 x = bld16<16>(rg, o < L.out ? (o * B + b) * 2 : OOB);
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) bsum += bf2f(x[jj]);
-      }
-      bsum += __shfl_xor(bsum, 1, 64);
-      bsum += __shfl_xor(bsum, 2, 64);
-      if (q == 0 && o < L.out) L.gb[o] = bsum;
-    }
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      const int i = i0 + 32 * wi + 16 * f + (lane & 15);
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int o = o0 + 32 * wo + 16 * e + 4 * (lane >> 4);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (i < L.in && o + r < L.out) L.gw[static_cast<long>(o + r) * L.in + i] = acc[e][f][r];
-      }
-    }
-  };
+  auto wgrad_finish = [&](WgLoads& WW, int o0, int i0) { wgrad_tile(L, WW, rg, ra, B, o0, i0, nullptr); };
 
   const int t = blockIdx.x;
   if (part == 0) {
@@ -595,6 +616,50 @@ __device__ __forceinline__ void bwd_phase(const MlpTrainArgs& a, int j, int part
     wg_load(Wg, rg, ra, B, L.out, L.in, o0, i0, 0, i0 == 0);
     wgrad_finish(Wg, o0, i0);
   }
+}
+
+// Fused backward window of layer j (every layer's weight-gradient tiles fit the grid: at most one per workgroup):
+// the weight + bias gradient of this workgroup's 64x64 tile of layer j and, straight from the accumulators (through
+// LDS: no gradient read-back from memory, no extra window), the optimiser update of the same tile -- its state
+// loaded right behind the GEMM operands.  The updated W^T tile cannot be stored yet (other workgroups' dgrads of
+// layer j read W^T until this phase's barrier completes): with `park` it stays in LDS and is stored at the start
+// of this workgroup's next window (`pk`), after that barrier.  j = 0 (no dgrad reads W_0^T): stored at once.
+struct Park {
+  int l, o0, i0;
+};
+
+template <int MODE>
+__device__ __forceinline__ void bwd_fused(const MlpTrainArgs& a, int j, const optdev::Hyper& h, bool use_m, Smem& sm, Park& pk,
+                          bool park) {
+  const MlpLayerArgs& L = a.L[j];
+  const bool last = j == a.nl - 1;
+  const int B = a.B, t = blockIdx.x;
+  const uint16_t* GT = last ? a.dlogT : a.dT[j + 1];
+  const int ot = (L.out + 63) / 64, nwg = ot * ((L.in + 63) / 64);
+  const rsrc_t rg = mkbuf(GT, static_cast<long>(last ? 32 : L.out) * B * 2);
+  const rsrc_t ra = mkbuf(a.actT[j], static_cast<long>(L.in) * B * 2);
+  const bool mine = t < nwg;
+  const int o0 = (t % ot) * 64, i0 = (t / ot) * 64;
+  WgLoads Wg;
+  UpLoads U;
+  if (mine) {
+    wg_load(Wg, rg, ra, B, L.out, L.in, o0, i0, 0, i0 == 0);
+    up_load(U, L, o0, i0, use_m, MODE != 0, false);
+  }
+  if (pk.l >= 0) {  // layer j + 1's parked W^T tile (its dgrads all finished before the last barrier)
+    wt_flush(a.L[j + 1], pk.o0, pk.i0, sm);
+    pk.l = -1;
+  }
+  if (!mine) return;
+  wgrad_tile(L, Wg, rg, ra, B, o0, i0, &sm);
+  lds_sync();
+  const int tc = threadIdx.x & 15, tr0 = threadIdx.x >> 4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) U.g[q] = *reinterpret_cast<const f32x4*>(&sm.gt[tr0 + 16 * q][4 * tc]);
+  if (i0 == 0 && threadIdx.x < 64) U.bg = sm.gb[threadIdx.x];
+  up_finish<MODE>(U, L, h, o0, i0, use_m, sm, park);
+  if (park) pk = Park{j, o0, i0};
+  else lds_sync();  // gt / gb reuse
 }
 
 // The update of layer l (tiles of this workgroup: the ones whose weight gradient it computed)
@@ -695,35 +760,58 @@ __global__ __launch_bounds__(MT) void k_mlp_train(MlpTrainArgs a) {
   dgrad_prefetch(a, nl - 1, R);
   grid_wait(bar, a.err, kb++);
   stamp(a, ks);
-  // B(nl-1) .. B1: the dgrad tiles (the hand-off), then -- between arrive and wait -- the weight-gradient tiles of
-  // layer j, the update of layer j + 1 (its weight-gradient tiles are this workgroup's from B(j+1)'s window; every
-  // dgrad that read its W^T finished before that barrier) and the next dgrad's weight fragments
   UpLoads U;
-  for (int j = nl - 1; j >= 1; --j) {
-    const bool up = j + 1 < nl;
-    const bool pre = up && (a.flags & 1) == 0;
-    bwd_phase(a, j, 0, R, sm, U, false, a.L[j], use_m, MODE != 0);
+  // (SGD keeps the unfused form: with both forms in its body the compiler spills 1.6 KB per lane)
+  bool fuse = MODE != 0 && (a.flags & 2) == 0;
+  for (int l = 0; l < nl; ++l)
+    fuse = fuse && ((a.L[l].out + 63) / 64) * ((a.L[l].in + 63) / 64) <= static_cast<int>(gridDim.x);
+  if (fuse) {
+    // Bj: the dgrad tiles (the hand-off), then -- between arrive and wait -- this workgroup's weight-gradient tile
+    // of layer j updated straight from its accumulators (W^T parked until the next window) and the next dgrad's
+    // weight fragments.  B0: layer 1's parked W^T, layer 0's gradient and update (no barrier left).
+    Park pk{-1, 0, 0};
+    for (int j = nl - 1; j >= 1; --j) {
+      bwd_phase(a, j, 0, R, sm, U, false, a.L[j], use_m, MODE != 0);
+      stamp(a, ks);
+      grid_arrive(bar, kb);
+      bwd_fused<MODE>(a, j, h, use_m, sm, pk, true);
+      dgrad_prefetch(a, j - 1, R);
+      stamp(a, ks);
+      grid_wait(bar, a.err, kb++);
+      stamp(a, ks);
+    }
+    bwd_fused<MODE>(a, 0, h, use_m, sm, pk, false);
+    stamp(a, ks);  // (an empty phase: the boundary count of the unfused form)
+  } else {
+    // B(nl-1) .. B1: the dgrad tiles (the hand-off), then -- between arrive and wait -- the weight-gradient tiles of
+    // layer j, the update of layer j + 1 (its weight-gradient tiles are this workgroup's from B(j+1)'s window; every
+    // dgrad that read its W^T finished before that barrier) and the next dgrad's weight fragments
+    for (int j = nl - 1; j >= 1; --j) {
+      const bool up = j + 1 < nl;
+      const bool pre = up && (a.flags & 1) == 0;
+      bwd_phase(a, j, 0, R, sm, U, false, a.L[j], use_m, MODE != 0);
+      stamp(a, ks);
+      grid_arrive(bar, kb);
+      bwd_phase(a, j, 1, R, sm, U, pre, a.L[up ? j + 1 : j], use_m, MODE != 0);
+      if (up) update_layer<MODE>(a, j + 1, h, use_m, sm, U, pre);
+      dgrad_prefetch(a, j - 1, R);
+      stamp(a, ks);
+      grid_wait(bar, a.err, kb++);
+      stamp(a, ks);
+    }
+    // B0: layer 0's weight gradient and the updates of layers 1 and 0 (no hand-off left: no barrier).  Gradient tiles
+    // stored by OTHER threads of this workgroup earlier (layer 1 in B1's window, layer 0 just below) are drained and
+    // met before the updates read them (the other layers have a grid barrier's arrive in between)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const bool pre0 = nl > 1 && (a.flags & 1) == 0;
+    bwd_phase(a, 0, 1, R, sm, U, pre0, a.L[nl > 1 ? 1 : 0], use_m, MODE != 0);
     stamp(a, ks);
-    grid_arrive(bar, kb);
-    bwd_phase(a, j, 1, R, sm, U, pre, a.L[up ? j + 1 : j], use_m, MODE != 0);
-    if (up) update_layer<MODE>(a, j + 1, h, use_m, sm, U, pre);
-    dgrad_prefetch(a, j - 1, R);
-    stamp(a, ks);
-    grid_wait(bar, a.err, kb++);
-    stamp(a, ks);
+    if (nl > 1) update_layer<MODE>(a, 1, h, use_m, sm, U, pre0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    update_layer<MODE>(a, 0, h, use_m, sm, U, false);
   }
-  // B0: layer 0's weight gradient and the updates of layers 1 and 0 (no hand-off left: no barrier).  Gradient tiles
-  // stored by OTHER threads of this workgroup earlier (layer 1 in B1's window, layer 0 just below) are drained and
-  // met before the updates read them (the other layers have a grid barrier's arrive in between)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const bool pre0 = nl > 1 && (a.flags & 1) == 0;
-  bwd_phase(a, 0, 1, R, sm, U, pre0, a.L[nl > 1 ? 1 : 0], use_m, MODE != 0);
-  stamp(a, ks);
-  if (nl > 1) update_layer<MODE>(a, 1, h, use_m, sm, U, pre0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  update_layer<MODE>(a, 0, h, use_m, sm, U, false);
   stamp(a, ks);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     float s = 0.f;

@@ -1736,9 +1736,10 @@ bool bn_one_launch(int blocks) {
 int bn_lite_sync() {
   static const int lite = !(std::getenv("PDE_BN_LITE") != nullptr && std::getenv("PDE_BN_LITE")[0] == '0');
   static const int allfin = !(std::getenv("PDE_BN_ALLFIN") != nullptr && std::getenv("PDE_BN_ALLFIN")[0] == '0');
-  // bit 3 (PDE_BN_WT=1): the normalised outputs / data gradients stored write-through -- r4m: level (3.256 ms
-  // both ways), so off
-  static const int wt = std::getenv("PDE_BN_WT") != nullptr && std::getenv("PDE_BN_WT")[0] == '1';
+  // bit 3: the normalised outputs / data gradients stored write-through (PDE_BN_WT=0 off) -- r4m: level; r5z, three
+  // alternating pairs: ResNet-50 3.131 -> 3.124 ms, stage 1 g4 1.545 -> 1.516 ms, stage 2 g4 level, stage 2 m8
+  // 1.352 -> 1.359 ms (profiles/r5z_bn_writethrough_ab.txt)
+  static const int wt = !(std::getenv("PDE_BN_WT") != nullptr && std::getenv("PDE_BN_WT")[0] == '0');
   return (lite ? (allfin ? 3 : 1) : 0) | (wt ? 8 : 0);
 }
 // Chunks of 5..8 rows per thread also stay in registers between the passes (RC = 8), r3ac: ResNet-50

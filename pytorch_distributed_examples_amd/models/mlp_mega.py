@@ -16,6 +16,8 @@ step sees the updated weights.  ``kernel_launches_per_step() == 1``.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import _native
@@ -121,14 +123,27 @@ class MegaMLP:
         for l in range(nl - 1):
             names += [f"F{l}", f"bar F{l}"]
         names += ["CE", "bar CE"]
+        fused = self.fused_update()
         for j in range(nl - 1, 0, -1):
-            names += [f"B{j} dgrad", f"B{j} arrive+wgrad+update L{j + 1}" if j + 1 < nl else f"B{j} arrive+wgrad",
-                      f"bar B{j} wait"]
-        names += ["B0 wgrad", "update L1 + L0"]
+            if fused:
+                win = f"B{j} arrive+wgrad+update L{j}" + (f" (+W^T L{j + 1})" if j + 1 < nl else "")
+            else:
+                win = f"B{j} arrive+wgrad+update L{j + 1}" if j + 1 < nl else f"B{j} arrive+wgrad"
+            names += [f"B{j} dgrad", win, f"bar B{j} wait"]
+        names += ["B0 wgrad+update L0 (+W^T L1)", "-"] if fused else ["B0 wgrad", "update L1 + L0"]
         out = []
         for i, n in enumerate(names):
             out.append((n, (t[i + 1] - t[i]) / 100.0, (t[64 + i + 1] - t[64 + i]) / 100.0 if i > 0 else 0.0))
         return out
+
+    def fused_update(self) -> bool:
+        """Whether the kernel updates each weight tile straight from its gradient accumulators, in the same window
+        (Adam / AdamW and every layer's 64x64 gradient tiles within the grid; ``PDE_MLP_FUSE=0`` turns it off) --
+        else one window later, reading the gradient back (the form SGD keeps)."""
+        if self.mode == 0 or os.environ.get("PDE_MLP_FUSE", "1") == "0":
+            return False
+        g = self.grid()
+        return all(-(-L.out_features // 64) * -(-L.in_features // 64) <= g for L in self.layers)
 
     def errors(self) -> int:
         """Non-zero if a grid barrier of a step timed out (a workgroup could not be resident): synchronises.  The

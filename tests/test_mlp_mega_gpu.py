@@ -128,3 +128,50 @@ def test_mega_step_captures_into_a_graph(gpu):
     assert float(last) < first, (first, float(last))  # the same batch: the loss falls
     assert mega.errors() == 0
     assert opt._dev[0]["step"][0].item() == 1 + 31  # the eager warm-up step + 31 replays (capture runs nothing)
+
+
+def test_fused_update_is_bitwise_the_unfused_one(gpu, monkeypatch):
+    """The fused backward window (each weight tile updated straight from its gradient accumulators, its W^T tile
+    parked in LDS until the next window) against the unfused form (update one window later, gradient read back):
+    the same fp32 values through the same update -- weights, their optimiser state, all gradients and both bf16
+    copies bitwise equal after three Adam steps (biases to an ulp)."""
+    from pytorch_distributed_examples_amd.models.mlp import reference_mlp
+    from pytorch_distributed_examples_amd.models.mlp_mega import MegaMLP
+    from pytorch_distributed_examples_amd.ops import functional as OF
+    from pytorch_distributed_examples_amd.ops.optim import FusedAdam
+
+    ma, oa, mb, ob = _pair(reference_mlp, FusedAdam, gpu, lr=1e-3)
+    fa, fb = MegaMLP(ma, oa), MegaMLP(mb, ob)
+    assert fa.fused_update()
+    for step in range(3):
+        x, y = _batch(gpu, seed=step + 11)
+        monkeypatch.setenv("PDE_MLP_FUSE", "1")
+        la = fa.step(x, y)
+        monkeypatch.setenv("PDE_MLP_FUSE", "0")
+        lb = fb.step(x, y)
+        torch.cuda.synchronize()
+        assert float(la) == float(lb), step
+    assert fa.errors() == 0 and fb.errors() == 0
+    bad = []
+    for (n, pa), pb in zip(ma.named_parameters(), mb.parameters()):
+        for what, ta, tb in (("param", pa, pb), ("grad", pa.grad, pb.grad), ("m", oa.state[pa]["exp_avg"],
+                             ob.state[pb]["exp_avg"]), ("v", oa.state[pa]["exp_avg_sq"], ob.state[pb]["exp_avg_sq"])):
+            # biases: the same update, but its scalar instance may be contracted to FMAs differently by the
+            # compiler in the two code paths (r5za: 1-ulp differences, gradients bitwise equal)
+            same = torch.equal(ta, tb) if ta.dim() > 1 or what == "grad" else \
+                torch.allclose(ta, tb, rtol=1e-5, atol=1e-9)
+            if not same:
+                d = (ta - tb).abs()
+                bad.append((n, what, d.max().item(), int((d > 0).sum().item()), int(d.flatten().argmax().item())))
+    assert not bad, bad
+    layers_a = [ma.input_layer, *ma.hidden_layers, ma.final_layer]
+    layers_b = [mb.input_layer, *mb.hidden_layers, mb.final_layer]
+    for i, (La, Lb) in enumerate(zip(layers_a, layers_b)):
+        assert torch.equal(OF._maintained(La.weight, "bf16"), OF._maintained(Lb.weight, "bf16")), i
+        if i > 0:
+            ld = 32 if i == len(layers_a) - 1 else La.out_features
+            ta = OF.maintain_transposed_copy(La.weight, ld)
+            tb = OF.maintain_transposed_copy(Lb.weight, ld)
+            assert torch.equal(ta, tb), i
+            # and it IS the transpose of the updated weights
+            assert torch.equal(ta[:, :La.out_features], La.weight.detach().to(torch.bfloat16).t()), i
