@@ -1,8 +1,8 @@
 """MI355X-native counterpart of the reference's horovod/horovod_mnist_elastic.py (see
 pytorch_distributed_examples_amd/apps/mnist_hvd_elastic.py for the design notes).
 
-Static:   python -m pytorch_distributed_examples_amd.launch.hvdrun -np 8 horovod/horovod_mnist_elastic.py
-Torchrun: torchrun --standalone --nproc_per_node 8 horovod/horovod_mnist_elastic.py
+Static:   python -m pytorch_distributed_examples_amd.launch.hvdrun -np 8 horovod_examples/horovod_mnist_elastic.py
+Torchrun: torchrun --standalone --nproc_per_node 8 horovod_examples/horovod_mnist_elastic.py
 """
 import os
 import sys

@@ -1,8 +1,8 @@
 """MI355X-native counterpart of the reference's horovod/mnist_horovod.py (see
 pytorch_distributed_examples_amd/apps/mnist_hvd.py for the design notes).
 
-Static:   python -m pytorch_distributed_examples_amd.launch.hvdrun -np 8 horovod/mnist_horovod.py
-Torchrun: torchrun --standalone --nproc_per_node 8 horovod/mnist_horovod.py
+Static:   python -m pytorch_distributed_examples_amd.launch.hvdrun -np 8 horovod_examples/mnist_horovod.py
+Torchrun: torchrun --standalone --nproc_per_node 8 horovod_examples/mnist_horovod.py
 """
 import os
 import sys

@@ -10,7 +10,7 @@ epoch=0)`` + ``register_reset_callbacks`` (:104-106).
 Launch (the reference's horovodrun line, :108):
     python -m pytorch_distributed_examples_amd.launch.hvdrun -np 2 --min-np 1 \
         --blacklist-cooldown-range 15 30 --host-discovery-script ./discover_hosts.sh \
-        horovod/horovod_mnist_elastic.py
+        horovod_examples/horovod_mnist_elastic.py
 
 Deliberate differences: skipped batches are not loaded (sampler offset, quirk Q10); the batch index
 bookkeeping keeps the reference's "state.batch updated after the commit check" order.

@@ -68,7 +68,7 @@ def test_hvd_elastic_script_survives_killed_worker_one_gpu(gpu, tmp_path):
     env = dict(os.environ, PDE_FAULT_AT_STEP="40", PDE_FAULT_RANK="1", PDE_FAULT_MODE="exit",
                PDE_FAULT_ONCE=str(tmp_path / "once"), PDE_XGMI_TIMEOUT_S="2.0")
     cmd = [sys.executable, "-m", "pytorch_distributed_examples_amd.launch.hvdrun", "-np", "2", "--min-np", "1",
-           "--verbose", os.path.join(REPO, "horovod", "horovod_mnist_elastic.py"), "--epochs", "2", "--train-size",
+           "--verbose", os.path.join(REPO, "horovod_examples", "horovod_mnist_elastic.py"), "--epochs", "2", "--train-size",
            "16384", "--test-size", "1024", "--batches-per-commit", "10"]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
     out = res.stdout + res.stderr
