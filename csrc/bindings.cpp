@@ -974,7 +974,7 @@ Tensor bn_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, const
 std::vector<Tensor> bn_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, const Tensor& mean,
                            const Tensor& invstd, const optional<Tensor>& gamma, bool relu, bool want_dres,
                            const optional<Tensor>& dg_out, const optional<Tensor>& db_out,
-                           const optional<Tensor>& scale_shift, int64_t groups) {
+                           const optional<Tensor>& scale_shift, int64_t groups, bool accum) {
   CHECK_IN(dy); CHECK_IN(x); CHECK_IN(y); CHECK_BF16(dy);
   resolve_pending(x);
   resolve_pending(y);
@@ -994,7 +994,7 @@ std::vector<Tensor> bn_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, c
   Tensor dres;
   if (want_dres) dres = at::empty_like(x);
   check(pde::bn_bwd(u16(dy), u16(x), u16(y), mean.data_ptr<float>(), invstd.data_ptr<float>(), cf32(gamma), P, C,
-                    relu, dg.data_ptr<float>(), db.data_ptr<float>(), direct ? 1 : 0, ws.data_ptr<float>(),
+                    relu, dg.data_ptr<float>(), db.data_ptr<float>(), direct && accum ? 1 : 0, ws.data_ptr<float>(),
                     coef.data_ptr<float>(), u16(dx), want_dres ? u16(dres) : nullptr, cur_stream(),
                     want_dres ? nullptr : cf32(scale_shift), G, G > 1 ? gs.data_ptr<float>() : nullptr),
         "bn_bwd");
@@ -1404,7 +1404,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("mean"), py::arg("invstd"),
         py::arg("gamma"), py::arg("relu"), py::arg("want_dres"), py::arg("dg_out") = py::none(),
-        py::arg("db_out") = py::none(), py::arg("scale_shift") = py::none(), py::arg("groups") = 1);
+        py::arg("db_out") = py::none(), py::arg("scale_shift") = py::none(), py::arg("groups") = 1,
+        py::arg("accum") = true);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);

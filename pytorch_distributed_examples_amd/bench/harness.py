@@ -139,6 +139,17 @@ def _data_plane_check(ctx, comm) -> int:
     return nranks
 
 
+_UNIT_GRADS: dict = {}
+
+
+def _unit_grad(loss):
+    """A persistent d loss / d loss = 1 (``loss.backward()`` fills a fresh one every step: an ATen fill kernel)."""
+    key = (loss.dtype, loss.device, tuple(loss.shape))
+    if key not in _UNIT_GRADS:
+        _UNIT_GRADS[key] = torch.ones_like(loss)
+    return _UNIT_GRADS[key]
+
+
 def _capture(step_fn, batches, graph_steps, rank):
     """(single-step graph, multi-step graph) or (None, None) when capture is not possible."""
     from ..utils.graph import CapturedStep, CapturedSteps
@@ -257,7 +268,10 @@ def build_data_parallel(args, ctx, batch) -> Workload:
             from ..models.mlp_fused import FusedMLP
 
             fmlp = FusedMLP(model)
-        ddp = DistributedDataParallel(model, overlap=not use_graph and fmlp is None, comm=comm)
+        # ResNet-50 / stages: every gradient's first writer stores (conv / linear weight gradients, BatchNorm's
+        # finalize), so after two checked steps zero_grad stops filling the 100 MB flat gradient
+        ddp = DistributedDataParallel(model, overlap=not use_graph and fmlp is None, comm=comm,
+                                      static_graph=on_gpu and args.model.startswith("resnet50"))
     # world 1, fused MLP, PDE_MLP_FOLD_OPT=1: each layer's Adam update appended to the next backward GEMM launch
     # (default: the separate multi-tensor launch after backward -- measured faster, profiles/README.md r3k)
     fold_opt = fmlp is not None and ctx.world_size == 1 and os.environ.get("PDE_MLP_FOLD_OPT", "0") == "1"
@@ -319,7 +333,7 @@ def build_data_parallel(args, ctx, batch) -> Workload:
             with t.phase("fwd"), OF.bn_groups(bn_groups):
                 loss = loss_fn(ddp(x), y)
             with t.phase("bwd"):
-                loss.backward()
+                loss.backward(_unit_grad(loss))
         if not ddp.overlap:  # graph mode: buckets reduced after backward on the capturing stream
             with t.phase("comm"):
                 ddp.sync_gradients()

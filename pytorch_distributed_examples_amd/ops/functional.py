@@ -346,7 +346,7 @@ class _LinearFn(torch.autograd.Function):
                 dx = _C().linear_dgrad(dy, wb, x if ctx.mask_input_grad else None)
                 _C().linear_wgrad(dy, x, wsink, _sink_accum(wsink))
             if bsink is not None:
-                _C().colsum(dy, -1, bsink, True)
+                _C().colsum(dy, -1, bsink, _sink_accum(bsink))
             elif ctx.has_bias and ctx.needs_input_grad[2]:
                 db = _C().colsum(dy, -1, None, False)
             return dx, None, db, None, None, None, None
@@ -356,7 +356,7 @@ class _LinearFn(torch.autograd.Function):
             with streams.fork(dy, x):
                 _C().linear_wgrad(dy, x, wsink, _sink_accum(wsink))
                 if bsink is not None:
-                    _C().colsum(dy, -1, bsink, True)
+                    _C().colsum(dy, -1, bsink, _sink_accum(bsink))
             dx = _C().linear_dgrad(dy, wb, x if ctx.mask_input_grad else None)
             return dx, None, None, None, None, None, None
         if ctx.needs_input_grad[0]:
@@ -366,7 +366,7 @@ class _LinearFn(torch.autograd.Function):
             if wsink is not None:
                 dw = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = _C().colsum(dy, -1, bsink, bsink is not None)
+            db = _C().colsum(dy, -1, bsink, bsink is not None and _sink_accum(bsink))
             if bsink is not None:
                 db = None
         return dx, dw, db, None, None, None, None
@@ -489,7 +489,7 @@ def _conv_backward(ctx, dy, x, weight, y=None):
                 raise
             pair.__exit__(None, None, None)
             if ctx.has_bias and ctx.needs_input_grad[2]:
-                db = _C().colsum(dy, co, bsink, bsink is not None)
+                db = _C().colsum(dy, co, bsink, bsink is not None and _sink_accum(bsink))
                 if bsink is not None:
                     db = None
             return dx, None, db
@@ -501,7 +501,7 @@ def _conv_backward(ctx, dy, x, weight, y=None):
             if wsink is not None:
                 dw = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = _C().colsum(dy, co, bsink, bsink is not None)
+            db = _C().colsum(dy, co, bsink, bsink is not None and _sink_accum(bsink))
             if bsink is not None:
                 db = None
         return dx, dw, db
@@ -612,10 +612,12 @@ class _BatchNormFn(torch.autograd.Function):
         beta = ctx.beta
         dg_sink, db_sink = _grad_sink(gamma), _grad_sink(beta)
         direct = dg_sink is not None and db_sink is not None
+        # both sinks are first written here or both were written before (pop both marks: no short-circuit)
+        accum = (_sink_accum(dg_sink) | _sink_accum(db_sink)) if direct else True
         dx, dg, db, dres = _C().bn_bwd(dy.contiguous(), x, y, mean, invstd,
                                        gamma.detach() if gamma is not None else None, ctx.relu, ctx.has_res,
                                        dg_sink if direct else None, db_sink if direct else None,
-                                       None if ctx.has_res else ss, ctx.groups)
+                                       None if ctx.has_res else ss, ctx.groups, accum)
         if direct:  # dgamma / dbeta were added into .grad by the finalize kernel
             dg = db = None
         if ctx.has_res and ctx.join is not None:  # the residual fork's conv adds it in its dgrad epilogue
@@ -727,8 +729,10 @@ class _BnConvFn(torch.autograd.Function):
         beta = ctx.beta
         dg_sink, db_sink = _grad_sink(gamma), _grad_sink(beta)
         direct = dg_sink is not None and db_sink is not None
+        accum = (_sink_accum(dg_sink) | _sink_accum(db_sink)) if direct else True
         da, dg, db, _ = _C().bn_bwd(dact, a, act, mean, invstd, gamma.detach(), ctx.relu, False,
-                                    dg_sink if direct else None, db_sink if direct else None, ss, ctx.groups)
+                                    dg_sink if direct else None, db_sink if direct else None, ss, ctx.groups,
+                                    accum)
         if direct:
             dg = db = None
         return da, dg, db, dw, None, None, None, None, None, None

@@ -18,6 +18,10 @@ Mirrors ``torch.nn.parallel.DistributedDataParallel`` as used by the reference
   into the one-shot all-reduce kernel and DDP copies nothing; on RCCL each bucket is cast by our HIP kernel
   into a persistent bf16 buffer, all-reduced in place (bf16, AVG in-collective) and cast back by our kernel
   into the flat fp32 gradient -- no allocation and no ATen kernel per bucket;
+* ``static_graph=True`` (every step writes every gradient through the same kernels): once two consecutive steps
+  saw each gradient view's first writer STORE (``ops.functional._sink_accum`` consumed the view's zero-filled
+  mark), ``zero_grad`` stops filling the flat gradient -- the first writers overwrite it anyway.  The mark is still
+  set and checked every step: a view whose mark survived a step without a fill raises (its gradient was stale);
 * ``comm=`` swaps the c10d group for another communicator (``size``, ``supports_avg``,
   ``allreduce_async(t, avg) -> work``, ``broadcast_(t, src)``), e.g. the per-round RCCL communicator of
   :mod:`..elastic.rewire` that is aborted and rebuilt in-process on a membership change.
@@ -68,7 +72,7 @@ def _cast(src: torch.Tensor, dst: torch.Tensor) -> None:
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float | None = None,
                  broadcast_buffers: bool = True, overlap: bool = True, grad_dtype: torch.dtype | None = None,
-                 src_rank: int = 0, param_order: str = "reverse", comm=None):
+                 src_rank: int = 0, param_order: str = "reverse", comm=None, static_graph: bool = False):
         super().__init__()
         self.module = module
         self.pg = process_group
@@ -128,6 +132,11 @@ class DistributedDataParallel(nn.Module):
         self._bf16_bufs = [torch.empty(e - s, dtype=torch.bfloat16, device=dev) for s, e in self._bucket_ranges] \
             if grad_dtype == torch.bfloat16 else None
         self._sync = True
+        self.static_graph = static_graph
+        self._covered = 0       # consecutive steps whose every gradient view was stored by its first writer
+        self._filled = True     # the last zero_grad filled
+        self._marked = False    # the views carry zero_grad's marks
+        self.fills_skipped = 0
         self._reset_state()
         self._hooks = []
         if overlap and self.world > 1:
@@ -220,13 +229,25 @@ class DistributedDataParallel(nn.Module):
         return self.module(*args, **kwargs)
 
     def zero_grad(self, set_to_none: bool = False):
-        self.flat_grad.zero_()
+        if self.static_graph and self._marked:
+            left = [p for p in self._params if self._views[p].__dict__.get("_pde_fresh", False)]
+            if left and not self._filled:
+                raise RuntimeError(f"DDP(static_graph=True): {len(left)} gradient(s) were not written by a storing "
+                                   "first writer in the last step, whose zero fill was skipped")
+            self._covered = 0 if left else self._covered + 1
+        skip = self.static_graph and self._covered >= 2
+        if skip:
+            self.fills_skipped += 1
+        else:
+            self.flat_grad.zero_()
+        self._filled = not skip
         for p in self._params:
             if p.grad is None or p.grad.data_ptr() != self._views[p].data_ptr():
                 p.grad = self._views[p]
             # zero-filled: the first weight-gradient kernel of the step may store instead of add
             # (ops.functional._sink_accum; bitwise the same as adding to zero, no read-modify-write)
             p.grad.__dict__["_pde_fresh"] = True
+        self._marked = True
 
     def remove_hooks(self):
         """Detach from the parameters (before wrapping the same module in a new DDP, e.g. per round)."""

@@ -99,3 +99,38 @@ def test_ddp_grads_match_full_batch(mode):
 
 def test_ddp_no_sync_accumulation():
     spawn(_ddp_worker, 2, ("no_sync",))
+
+
+def test_static_graph_fill_skip_bookkeeping():
+    """DDP(static_graph=True) stops filling the flat gradient only after two steps in which every view's
+    zero-filled mark was consumed by a storing first writer (simulated here with ops.functional._sink_accum), and
+    raises when a view's mark survives a step whose fill was skipped.  On CPU the ATen path consumes no marks, so
+    the fill is never skipped."""
+    import pytest
+    from torch import nn
+
+    from pytorch_distributed_examples_amd.ops import functional as OF
+    from pytorch_distributed_examples_amd.parallel.ddp import DistributedDataParallel
+
+    m = nn.Sequential(nn.Linear(4, 3), nn.Linear(3, 2))
+    ddp = DistributedDataParallel(m, overlap=False, static_graph=True)
+
+    def first_writes(skip=()):
+        for i, p in enumerate(m.parameters()):
+            if i not in skip:
+                assert OF._sink_accum(p.grad) is False  # the first writer of the step stores
+                assert OF._sink_accum(p.grad) is True   # a later one adds
+
+    for step in range(4):
+        ddp.zero_grad()
+        first_writes()
+    assert ddp.fills_skipped == 2  # steps 3 and 4: the marks of steps 1 and 2 (then 2 and 3) were consumed
+    ddp.zero_grad()
+    first_writes(skip=(1,))  # one gradient not written by a storing kernel in a skipped-fill step
+    with pytest.raises(RuntimeError, match="static_graph"):
+        ddp.zero_grad()
+
+    plain = DistributedDataParallel(nn.Linear(4, 3), overlap=False, static_graph=True)
+    for _ in range(4):
+        plain.zero_grad()  # nothing consumed the marks (the CPU / ATen path): always filled
+    assert plain.fills_skipped == 0

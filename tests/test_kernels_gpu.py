@@ -568,3 +568,40 @@ def test_first_write_after_zero_grad_stores(gpu):
     for p, r in zip(params, ref1):
         if any(p is w for w in weights):
             assert rel_err(p.grad, 2 * r) < 1e-5
+
+
+def test_static_graph_ddp_skips_the_zero_fill(gpu):
+    """DDP(static_graph=True): every gradient of a conv / BatchNorm / linear model is first written by a storing
+    kernel (conv and linear weight + bias gradients, BatchNorm's dgamma / dbeta finalize), so from the third step
+    on zero_grad skips the flat-gradient fill -- and the trained weights are bitwise those of the filling DDP."""
+    from pytorch_distributed_examples_amd.ops import layers as L
+    from pytorch_distributed_examples_amd.ops.optim import FusedSGD
+    from pytorch_distributed_examples_amd.parallel.ddp import DistributedDataParallel
+
+    def make():
+        torch.manual_seed(6)
+        return torch.nn.ModuleList([L.Conv2d(16, 24, 3, stride=1, padding=1), L.BatchNorm2d(24),
+                                    L.Conv2d(24, 32, 1, bias=False), L.BatchNorm2d(32), L.Linear(32, 10)]).to(gpu)
+
+    runs = []
+    for static in (False, True):
+        m = make()
+        ddp = DistributedDataParallel(m, overlap=False, static_graph=static)
+        opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9)
+        for step in range(5):
+            g = torch.Generator(device="cpu").manual_seed(step)
+            x = OF.to_native_image(torch.randn(4, 16, 12, 12, generator=g).to(gpu))
+            ddp.zero_grad()
+            if static and step >= 2:
+                ddp.flat_grad.fill_(77.0)  # what a skipped fill leaves behind must not matter
+            h = m[1](m[0](x), relu=True)
+            h = m[3](m[2](h), relu=True)
+            loss = OF.mse_loss(m[4](OF.global_avg_pool_flat(h), out_f32=True), torch.ones(4, 10, device=gpu))
+            loss.backward()
+            opt.step()
+        torch.cuda.synchronize()
+        runs.append((m, ddp))
+    (ma, _), (mb, db) = runs
+    assert db.fills_skipped == 3, db.fills_skipped
+    for pa, pb in zip(ma.parameters(), mb.parameters()):
+        assert torch.equal(pa, pb) and torch.equal(pa.grad, pb.grad)
