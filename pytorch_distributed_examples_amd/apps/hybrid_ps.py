@@ -176,7 +176,8 @@ class ResNetPipelineDP:
         gd = torch.bfloat16 if (dev.type == "cuda" and os.environ.get("PDE_PIPE_GRAD_DTYPE", "bf16") == "bf16") else None
         self.ddp = DistributedDataParallel(self.module, process_group=self.dp_group,
                                            overlap=self.overlap and self.comm is not None,
-                                           broadcast_buffers=False, comm=self.comm, grad_dtype=gd)
+                                           broadcast_buffers=False, comm=self.comm, grad_dtype=gd,
+                                           static_graph=dev.type == "cuda")  # no zero fill (first writers store)
         self.opt = FusedSGD(self.module.parameters(), lr=lr)
         prev_rank = ctx.rank - 1 if self.stage > 0 else None
         next_rank = ctx.rank + 1 if not self.last else None

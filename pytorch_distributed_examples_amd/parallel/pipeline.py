@@ -240,6 +240,7 @@ class PipelineEngine:
             ch = P2PChannel(peer, tag, device)
             setattr(self, which, ch)
         self._fwd_meta = None  # (shape, dtype) of activations received from prev
+        self._unit = None
         self._bwd_meta = None
         self.timer = NO_PHASES  # utils.log.PhaseTimer: per-stage fwd / bwd / recv-wait times (bench)
         # micro-batches per pipeline unit: each unit passed to train_step is `bn_groups` micro-batches run as
@@ -288,7 +289,9 @@ class PipelineEngine:
         x, y, _ = state["saved"].pop(mb)
         if self.last:
             with self.timer.phase("bwd"):
-                y.backward()
+                if self._unit is None or self._unit.shape != y.shape or self._unit.dtype != y.dtype:
+                    self._unit = torch.ones_like(y)  # persistent d loss = 1: no fill kernel per micro-batch
+                y.backward(self._unit)
         else:
             with self.timer.phase("recv_wait"):
                 g = self.next.recv(y.shape, y.dtype)
