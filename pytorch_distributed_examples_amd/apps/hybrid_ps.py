@@ -30,7 +30,7 @@ from ..data.synthetic import embbag_batches
 from ..ops import functional as OF
 from ..ops import layers as L
 from ..parallel.ddp import DistributedDataParallel
-from ..parallel.dist import free_port
+from ..parallel.dist import free_ports
 from ..rpc import DistributedOptimizer, RemoteModule, dist_autograd
 from ..utils import config as rtconfig
 from ..utils.config import add_runtime_args
@@ -303,5 +303,5 @@ def main(argv=None):
         return
     use_gpu = torch.cuda.is_available() and args.device != "cpu"
     world_size = 4
-    mp.spawn(run_worker, args=(world_size, args.epochs, (free_port(), free_port()), use_gpu), nprocs=world_size,
+    mp.spawn(run_worker, args=(world_size, args.epochs, tuple(free_ports(2)), use_gpu), nprocs=world_size,
              join=True)

@@ -26,7 +26,7 @@ import torch.multiprocessing as mp
 from torch import nn, optim
 
 from ..models.resnet import ResNetShard1, ResNetShard2
-from ..parallel.dist import free_port
+from ..parallel.dist import free_ports
 from ..rpc import DistributedOptimizer, RemotePipeline, dist_autograd
 from ..utils import config as rtconfig
 from ..utils.config import add_runtime_args
@@ -112,7 +112,7 @@ def main(argv=None):
     world_size = 3
     for num_split in args.splits:
         tik = time.time()
-        mp.spawn(run_worker, args=(world_size, num_split, args, free_port(), free_port()), nprocs=world_size,
+        mp.spawn(run_worker, args=(world_size, num_split, args, *free_ports(2)), nprocs=world_size,
                  join=True)
         tok = time.time()
         print(f"number of splits = {num_split}, execution time = {tok - tik}", flush=True)

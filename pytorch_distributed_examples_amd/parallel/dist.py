@@ -40,6 +40,21 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+def free_ports(n: int) -> list:
+    """``n`` DISTINCT free ports: every socket stays bound until all are chosen (two back-to-back
+    ``free_port()`` calls may hand out the same port, and the second server then fails with EADDRINUSE)."""
+    socks = []
+    try:
+        for _ in range(n):
+            s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            s.bind(("127.0.0.1", 0))
+            socks.append(s)
+        return [s.getsockname()[1] for s in socks]
+    finally:
+        for s in socks:
+            s.close()
+
+
 def env_int(name: str, default: int) -> int:
     v = os.environ.get(name)
     return int(v) if v not in (None, "") else default
