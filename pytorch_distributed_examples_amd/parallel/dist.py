@@ -34,10 +34,19 @@ class DistContext:
         return self.rank == 0
 
 
+_HANDED_OUT: set = set()
+
+
 def free_port() -> int:
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """A free port not handed out before by this process (two quick calls can otherwise return the same one)."""
+    for _ in range(64):
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        if port not in _HANDED_OUT:
+            _HANDED_OUT.add(port)
+            return port
+    return port
 
 
 def free_ports(n: int) -> list:
