@@ -1304,6 +1304,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_reserve_headroom", &pde::bn_reserve_headroom, py::arg("blocks"),
         "Reserve (> 0) / release (< 0) CUs for spinning side-stream kernels; returns the one-launch BatchNorm's "
         "resident cap");
+  m.def("bn_headroom_reserved", &pde::bn_headroom_reserved,
+        "CUs currently reserved (bn_reserve_headroom) for kernels spinning on other streams");
   m.def("bn_launch_stats", []() {
     long one = 0, multi = 0;
     int last = 0, cap = 0;

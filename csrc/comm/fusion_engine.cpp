@@ -411,8 +411,10 @@ void FusionEngine::set_graph_mode(bool on, const std::vector<at::Tensor>& tensor
   for (const auto& t : tensors) need += t.numel() * 4;  // fp32 staging covers every wire format
   if (on && !tensors.empty() && tensors.front().is_cuda() && need > 0) {
     c10::hip::HIPGuardMasqueradingAsCUDA guard(tensors.front().device());
-    if (!inline_fused_.defined() || inline_fused_.numel() < need)
+    if (!inline_fused_.defined() || inline_fused_.numel() < need) {
+      if (inline_fused_.defined()) retired_inline_.push_back(inline_fused_);  // an earlier capture may use it
       inline_fused_ = at::empty({need + 4096}, tensors.front().options().dtype(at::kByte));
+    }
   }
   {
     std::lock_guard<std::mutex> g(mu_);

@@ -217,6 +217,9 @@ class FusionEngine {
   std::thread worker_;
   at::Tensor fused_;  // reusable fusion buffer (device or host), engine thread only
   at::Tensor inline_fused_;  // graph mode's staging buffer (caller's stream), sized by set_graph_mode
+  // earlier, smaller staging buffers: a graph captured against one keeps pointing at it, so it lives as long as the
+  // engine (never returned to the allocator while a replay could still write it)
+  std::vector<at::Tensor> retired_inline_;
   bool graph_mode_ = false;
   std::vector<Inflight> inflight_;
 

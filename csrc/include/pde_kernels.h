@@ -250,6 +250,7 @@ int bn_workspace_blocks(int P, int C, int groups = 1);
 // overlapped RCCL all-reduce); returns the resulting resident cap.  Grids shrink to the cap; a BatchNorm whose
 // minimal grid exceeds it is refused up front and runs multi-launch.
 int bn_reserve_headroom(int blocks);
+int bn_headroom_reserved();  // CUs currently reserved for spinning side-stream kernels
 void bn_launch_stats(long* one_launch, long* multi_launch, int* last_grid, int* cap);
 hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, const float* beta, float eps,
                         float momentum, float* running_mean, float* running_var, float* save_mean,

@@ -125,7 +125,8 @@ __device__ __forceinline__ void grid_wait(const Bar& b, int* err, int k) {
     const unsigned groups = gridDim.x < kBarGroups ? gridDim.x : kBarGroups;
     const unsigned target = (b.base + static_cast<unsigned>(k) + 1) * groups;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(b.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    // wrap-safe: the counters run on across launches and wrap after ~2^32 / (groups x nbar) steps
+    while (static_cast<int>(__hip_atomic_load(b.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;

@@ -2011,6 +2011,8 @@ int bn_reserve_headroom(int blocks) {
   return bn_resident_cap();
 }
 
+int bn_headroom_reserved() { return g_bn_headroom.load(); }
+
 void bn_launch_stats(long* one, long* multi, int* last_grid, int* cap) {
   *one = g_bn_one_launches.load();
   *multi = g_bn_multi_launches.load();

@@ -516,10 +516,15 @@ class _FailureWatch:
         self.rnd, self.xa, self.period_s = rnd, xa, period_s
         self.fired_at = None
         self._stop = threading.Event()
-        host, port = os.environ["PDE_ELASTIC_STORE"].rsplit(":", 1)
-        # a client of its own: never interleaves with the main thread's store traffic
-        self._store = dist.TCPStore(host, int(port), is_master=False, timeout=datetime.timedelta(seconds=30),
-                                    wait_for_workers=False)
+        addr = os.environ["PDE_ELASTIC_STORE"]
+        # a client of its own (never interleaves with the main thread's store traffic), reused by the next round's
+        # watcher once this one has stopped: one connection per process, not one per elastic reset
+        self._store = _WATCH_STORES.pop(addr, None)
+        if self._store is None:
+            host, port = addr.rsplit(":", 1)
+            self._store = dist.TCPStore(host, int(port), is_master=False, timeout=datetime.timedelta(seconds=30),
+                                        wait_for_workers=False)
+        self._addr = addr
         self._th = threading.Thread(target=self._run, daemon=True)
         self._th.start()
 
@@ -538,6 +543,13 @@ class _FailureWatch:
     def stop(self):
         self._stop.set()
         self._th.join(timeout=1.0)
+        store, self._store = self._store, None
+        if store is not None and not self._th.is_alive():
+            _WATCH_STORES[self._addr] = store  # idle again: hand it to the next round's watcher
+        # else the thread is still inside a store call: drop our reference, it is released when the call returns
+
+
+_WATCH_STORES: dict = {}  # PDE_ELASTIC_STORE address -> an idle watcher TCPStore client
 
 
 def _fault_time():

@@ -13,6 +13,11 @@ path (:class:`.mlp_fused.FusedMLP` + ``opt.step()``): same bf16 operands, fp32 a
 per-element update (optim_device.h); gradients land in ``p.grad``, the optimiser state in ``opt.state``, the device
 step counter advances, and the bf16 weight copies the layers read are refreshed -- an eager ``model(x)`` after the
 step sees the updated weights.  ``kernel_launches_per_step() == 1``.
+
+The grid barriers need every workgroup resident: ``step`` refuses to run while CUs are reserved for kernels spinning
+on other streams (``bn_reserve_headroom``), and an eager caller's ``step`` reads the barrier error word every
+``check_every`` calls (a device sync; graph replays are checked by :meth:`errors` at the caller's commit / epoch
+boundary) and raises :class:`DeviceBarrierError` -- a timed-out barrier means the step's hand-offs raced.
 """
 from __future__ import annotations
 
@@ -25,8 +30,13 @@ from ..ops import functional as OF
 from ..ops.optim import _MODES
 
 
+class DeviceBarrierError(RuntimeError):
+    """A grid barrier of the one-launch MLP step timed out: not every workgroup was resident, the phase hand-offs
+    raced and the weights / optimiser state written by that step are not trustworthy."""
+
+
 class MegaMLP:
-    def __init__(self, net, opt):
+    def __init__(self, net, opt, check_every: int = 64):
         self.net, self.opt = net, opt
         self.layers = [net.input_layer, *net.hidden_layers, net.final_layer]
         for i, L in enumerate(self.layers):
@@ -39,6 +49,7 @@ class MegaMLP:
         self._bufs: dict = {}
         self._grid = None
         self.calls = 0
+        self.check_every = int(check_every)
         self.stamps = None  # set to a zeroed int64[128] GPU tensor: phase-boundary clocks (100 MHz), see phase_us
 
     def _buffers(self, B: int, dev: torch.device):
@@ -74,6 +85,12 @@ class MegaMLP:
         B = x.shape[0]
         if B % 32:
             raise ValueError(f"MegaMLP: batch {B} must be a multiple of 32")
+        if C.bn_headroom_reserved() > 0:
+            raise RuntimeError("MegaMLP: CUs are reserved for kernels spinning on other streams; the persistent grid "
+                               "(one workgroup per CU) could not be co-resident -- use FusedMLP")
+        capturing = torch.cuda.is_current_stream_capturing()
+        if not capturing and self.check_every > 0 and self.calls and self.calls % self.check_every == 0:
+            self.check()
         for p in self.params:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
@@ -144,6 +161,13 @@ class MegaMLP:
             return False
         g = self.grid()
         return all(-(-L.out_features // 64) * -(-L.in_features // 64) <= g for L in self.layers)
+
+    def check(self, where: str = "") -> None:
+        """Raise :class:`DeviceBarrierError` if a grid barrier timed out since the last check (synchronises)."""
+        n = self.errors()
+        if n:
+            raise DeviceBarrierError(f"MegaMLP: {n} grid-barrier timeout(s){' at ' + where if where else ''}: a "
+                                     "workgroup was not resident, the step's hand-offs raced")
 
     def errors(self) -> int:
         """Non-zero if a grid barrier of a step timed out (a workgroup could not be resident): synchronises.  The

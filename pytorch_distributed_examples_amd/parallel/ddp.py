@@ -21,7 +21,10 @@ Mirrors ``torch.nn.parallel.DistributedDataParallel`` as used by the reference
 * ``static_graph=True`` (every step writes every gradient through the same kernels): once two consecutive steps
   saw each gradient view's first writer STORE (``ops.functional._sink_accum`` consumed the view's zero-filled
   mark), ``zero_grad`` stops filling the flat gradient -- the first writers overwrite it anyway.  The mark is still
-  set and checked every step: a view whose mark survived a step without a fill raises (its gradient was stale);
+  set every step and checked BEFORE the gradients are used: when a bucket is reduced (and in ``sync_gradients`` at
+  world 1) a view whose mark survived a skipped-fill step got no gradient this step, so it is zeroed there (an
+  unused parameter's gradient is zero, as in a filled step) and the next ``zero_grad`` fills again.  A
+  ``zero_grad`` with no backward since the last one consumed no mark: it fills (the buffer may hold an old step);
 * ``comm=`` swaps the c10d group for another communicator (``size``, ``supports_avg``,
   ``allreduce_async(t, avg) -> work``, ``broadcast_(t, src)``), e.g. the per-round RCCL communicator of
   :mod:`..elastic.rewire` that is aborted and rebuilt in-process on a membership change.
@@ -126,6 +129,7 @@ class DistributedDataParallel(nn.Module):
                 off += padded[i]
             self._bucket_ranges.append((start, off))
         self._bucket_sizes = [len(idxs) for idxs in plan]
+        self._bucket_params = [[order[i] for i in idxs] for idxs in plan]
         for p in self._params:
             p.grad = self._views[p]
         self._bucket_flat = [self.flat_grad[s:e] for s, e in self._bucket_ranges]
@@ -137,6 +141,7 @@ class DistributedDataParallel(nn.Module):
         self._filled = True     # the last zero_grad filled
         self._marked = False    # the views carry zero_grad's marks
         self.fills_skipped = 0
+        self.stale_zeroed = 0   # views zeroed at reduction time: unwritten in a skipped-fill step
         self._reset_state()
         self._hooks = []
         if overlap and self.world > 1:
@@ -170,7 +175,20 @@ class DistributedDataParallel(nn.Module):
 
         return hook
 
+    def _repair_stale(self, b: int):
+        """Before bucket ``b``'s gradients are used: in a step whose zero fill was skipped, zero every view that no
+        storing first writer consumed (it still holds an older step's gradient)."""
+        if not self.static_graph or self._filled or not self._marked:
+            return
+        for p in self._bucket_params[b]:
+            v = self._views[p]
+            if v.__dict__.pop("_pde_fresh", False):
+                v.zero_()
+                self.stale_zeroed += 1
+                self._covered = -1  # the next zero_grad fills (and the coverage count restarts)
+
     def _launch(self, b: int):
+        self._repair_stale(b)
         if self.flat_grad.is_cuda:  # weight gradients may still be running on the side stream (ops/streams.py)
             streams.join(self.flat_grad.device)
         fused_wire = getattr(self.comm, "fuses_bf16_wire", None)
@@ -216,6 +234,8 @@ class DistributedDataParallel(nn.Module):
     def sync_gradients(self):
         """Reduce all buckets now (non-overlapped mode / after ``no_sync`` accumulation)."""
         if self.world <= 1:
+            for b in range(len(self._bucket_ranges)):
+                self._repair_stale(b)
             return
         for b in range(len(self._bucket_ranges)):
             self._launch(b)
@@ -229,13 +249,16 @@ class DistributedDataParallel(nn.Module):
         return self.module(*args, **kwargs)
 
     def zero_grad(self, set_to_none: bool = False):
+        skip = False
         if self.static_graph and self._marked:
             left = [p for p in self._params if self._views[p].__dict__.get("_pde_fresh", False)]
-            if left and not self._filled:
-                raise RuntimeError(f"DDP(static_graph=True): {len(left)} gradient(s) were not written by a storing "
-                                   "first writer in the last step, whose zero fill was skipped")
-            self._covered = 0 if left else self._covered + 1
-        skip = self.static_graph and self._covered >= 2
+            if len(left) == len(self._params):
+                pass  # no backward since the last zero_grad: nothing consumed, fill (below) without counting a step
+            elif self._covered < 0:
+                self._covered = 0  # stale views were zeroed at reduction time in the last step
+            else:
+                self._covered = 0 if left else self._covered + 1
+            skip = self._covered >= 2 and len(left) < len(self._params)
         if skip:
             self.fills_skipped += 1
         else:

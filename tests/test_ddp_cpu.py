@@ -103,8 +103,9 @@ def test_ddp_no_sync_accumulation():
 
 def test_static_graph_fill_skip_bookkeeping():
     """DDP(static_graph=True) stops filling the flat gradient only after two steps in which every view's
-    zero-filled mark was consumed by a storing first writer (simulated here with ops.functional._sink_accum), and
-    raises when a view's mark survives a step whose fill was skipped.  On CPU the ATen path consumes no marks, so
+    zero-filled mark was consumed by a storing first writer (simulated here with ops.functional._sink_accum); a
+    view whose mark survives a skipped-fill step is zeroed before the gradients are used (sync_gradients), and a
+    repeated zero_grad with no backward in between fills instead of raising.  On CPU the ATen path consumes no marks, so
     the fill is never skipped."""
     import pytest
     from torch import nn
@@ -126,9 +127,21 @@ def test_static_graph_fill_skip_bookkeeping():
         first_writes()
     assert ddp.fills_skipped == 2  # steps 3 and 4: the marks of steps 1 and 2 (then 2 and 3) were consumed
     ddp.zero_grad()
+    assert ddp.fills_skipped == 3
+    params = list(m.parameters())
+    params[1].grad.fill_(7.0)  # an older step's gradient left in the (unfilled) view
     first_writes(skip=(1,))  # one gradient not written by a storing kernel in a skipped-fill step
-    with pytest.raises(RuntimeError, match="static_graph"):
-        ddp.zero_grad()
+    ddp.sync_gradients()     # BEFORE the optimiser step: the stale view is zeroed (an unused parameter's gradient)
+    assert ddp.stale_zeroed == 1 and float(params[1].grad.abs().sum()) == 0.0
+    ddp.zero_grad()          # ... and the next step fills again, the coverage count restarting
+    assert ddp.fills_skipped == 3
+    first_writes()
+    ddp.zero_grad()
+    first_writes()
+    ddp.zero_grad()          # two covered steps again: skipped
+    assert ddp.fills_skipped == 4
+    ddp.zero_grad()          # no backward since the last zero_grad (allowed): fills, does not raise
+    assert ddp.fills_skipped == 4
 
     plain = DistributedDataParallel(nn.Linear(4, 3), overlap=False, static_graph=True)
     for _ in range(4):
