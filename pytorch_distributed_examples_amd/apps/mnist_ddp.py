@@ -14,11 +14,20 @@ lines, and ``Execution time``.
 
 MI355X-first differences: RCCL (``nccl``) over xGMI on GPUs -- gloo on CPU -- with the xGMI bucket
 policy; bf16 MFMA kernels; HBM-resident synthetic MNIST; atomic snapshot by global rank 0 only;
-``--model cnn`` runs BASELINE config 1's CNN through the same plumbing (``--fused``: the whole-network
-training kernel of csrc/kernels/cnn_fused.hip, gradients straight into the DDP flat buffer; on the xGMI data
-plane of :mod:`..parallel.comm` the all-reduce and the SGD update run inside the slab-reduction kernel, else
-one all-reduce and one fused SGD launch); ``--rewire`` keeps the worker alive
+``--model cnn`` runs BASELINE config 1's CNN through the same plumbing; ``--rewire`` keeps the worker alive
 across membership changes (in-process RCCL communicator re-wire, :mod:`..elastic.rewire`).
+
+GPU training step (default; ``--layers`` keeps the layer-by-layer autograd + DDP-hook path of the CPU config):
+
+* MLP, world 1: the whole step -- forward, cross-entropy, backward, Adam -- as ONE persistent launch
+  (:class:`..models.mlp_mega.MegaMLP`); a short last batch whose size is not a multiple of 32 takes the layer path;
+* MLP, world > 1: :class:`..models.mlp_fused.FusedMLP` (no autograd, dgrad + wgrad paired per layer) + the DDP flat
+  buffer all-reduced by the stream-ordered RCCL / xGMI data plane + the multi-tensor Adam;
+* CNN (``--fused`` is implied): the whole-network training kernel of csrc/kernels/cnn_fused.hip, gradients straight
+  into the DDP flat buffer; on the xGMI data plane the all-reduce and the SGD update run inside its slab-reduction
+  kernel, else one all-reduce and one fused SGD launch;
+* the epoch runs as hipGraph replays of ``--graph_chunk`` steps each over this rank's shard gathered once per epoch
+  (:mod:`..utils.epoch_graph`): no per-step host work.
 """
 from __future__ import annotations
 
@@ -60,7 +69,7 @@ def load_train_objs(model_name: str, device, train_size: int, test_size: int):
 
 class Trainer:
     def __init__(self, ctx, model, train_data, test_data, make_opt, criterion, save_every, snapshot_path,
-                 log, metrics=None, save_optimizer=True, fused=False, ddp_kwargs=None):
+                 log, metrics=None, save_optimizer=True, fused=False, ddp_kwargs=None, fast=None, graph_chunk=50):
         self.ctx = ctx
         self.global_rank = int(os.environ.get("RANK", ctx.rank))
         self.local_rank = int(os.environ.get("LOCAL_RANK", ctx.local_rank))
@@ -79,17 +88,43 @@ class Trainer:
             log.print("Loading snapshot")
             self._load_snapshot(snapshot_path)
         self.fused = None
-        if fused:
+        self.fmlp = self.mega = None
+        self.runner = None
+        on_gpu = ctx.device.type == "cuda"
+        is_cnn = type(self.model).__name__ == "Net"
+        fast = on_gpu if fast is None else fast
+        if fused and not on_gpu:
+            raise SystemExit("--fused runs the gfx950 training kernel: it needs a GPU")
+        if fast and not on_gpu:
+            fast = False
+        if (fused or fast) and is_cnn:
             from ..models.cnn_fused import FusedCNN
             from ..parallel.comm import data_plane
 
-            if ctx.device.type != "cuda":
-                raise SystemExit("--fused runs the gfx950 training kernel: it needs a GPU")
             self.fused = FusedCNN(self.model)
             self.ddp = DistributedDataParallel(self.model, overlap=False, param_order="forward", comm=data_plane(ctx),
                                                **(ddp_kwargs or {}))
+        elif fast:
+            from ..models.mlp_fused import FusedMLP
+            from ..parallel.comm import data_plane
+
+            self.fmlp = FusedMLP(self.model)
+            self.ddp = DistributedDataParallel(self.model, overlap=False, comm=data_plane(ctx), **(ddp_kwargs or {}))
+            if (self.ddp.world == 1 and train_data.batch_size % 32 == 0 and
+                    os.environ.get("PDE_MLP_MEGA", "1") != "0"):
+                from ..models.mlp_mega import MegaMLP
+
+                mega = MegaMLP(self.model, self.optimizer)
+                self.mega = mega if mega.grid() > 0 else None
         else:
             self.ddp = DistributedDataParallel(self.model, **(ddp_kwargs or {}))
+        if (self.fused is not None or self.fmlp is not None) and hasattr(train_data.dataset, "images") and \
+                os.environ.get("PDE_EPOCH_GRAPH", "1") != "0":
+            from ..utils.epoch_graph import ChunkedGraphs, EpochBatches
+
+            self.epoch_batches = EpochBatches(train_data)
+            self.runner = ChunkedGraphs(self._gpu_step, self.epoch_batches, chunk=graph_chunk, eager_first=2,
+                                        tail_step=self._gpu_tail_step)
 
     def _load_snapshot(self, path):
         snap = load_snapshot(path)
@@ -99,20 +134,54 @@ class Trainer:
         self.epochs_run = snap["EPOCHS_RUN"]
         self.log.print(f"Resuming training from snapshot at Epoch {self.epochs_run}")
 
-    def _run_batch(self, source, targets):
-        if self.fused is not None:
-            xgmi = getattr(self.ddp.comm, "xgmi", None)
-            if self.ddp.world == 1:  # SGD + fragment refresh inside the slab reduction
-                loss = self.fused.forward_backward(source, targets, grad_out=self.ddp.flat_grad, sgd=self.optimizer)
-            elif xgmi is not None:  # + the gradient all-reduce, exchanged over xGMI inside that kernel
-                loss = self.fused.forward_backward(source, targets, grad_out=self.ddp.flat_grad, sgd=self.optimizer,
-                                                   xgmi=xgmi)
-            else:
-                loss = self.fused.forward_backward(source, targets, grad_out=self.ddp.flat_grad)
-                self.ddp.sync_gradients()
-                self.fused.sgd_step(self.optimizer, self.ddp.flat_grad)
+    def _gpu_step(self, source, targets):
+        """One full-batch GPU training step (the function the epoch graphs capture)."""
+        if self.mega is not None:
+            return self.mega.step(source, targets)
+        if self.fmlp is not None:
+            loss = self.fmlp.forward_backward(source, targets)  # gradients written into the DDP flat buffer
+            self.ddp.sync_gradients()
+            self.optimizer.step()
+            return loss
+        return self._fused_cnn_step(source, targets)
+
+    def _gpu_tail_step(self, source, targets):
+        """The short last batch (eager): the one-launch MLP step needs a multiple of 32 rows."""
+        if self.mega is not None and source.shape[0] % 32:
+            loss = self.fmlp_for_tail().forward_backward(source, targets)
+            self.optimizer.step()
+            return loss
+        return self._gpu_step(source, targets)
+
+    def fmlp_for_tail(self):
+        if self.fmlp is None:
+            from ..models.mlp_fused import FusedMLP
+
+            self.fmlp = FusedMLP(self.model)
+        return self.fmlp
+
+    def _after_steps(self, idxs, losses):
+        for _ in idxs:
             fault.maybe_fault(self.global_step, self.global_rank)
             self.global_step += 1
+
+    def _fused_cnn_step(self, source, targets):
+        xgmi = getattr(self.ddp.comm, "xgmi", None)
+        if self.ddp.world == 1:  # SGD + fragment refresh inside the slab reduction
+            return self.fused.forward_backward(source, targets, grad_out=self.ddp.flat_grad, sgd=self.optimizer)
+        if xgmi is not None:  # + the gradient all-reduce, exchanged over xGMI inside that kernel
+            return self.fused.forward_backward(source, targets, grad_out=self.ddp.flat_grad, sgd=self.optimizer,
+                                               xgmi=xgmi)
+        loss = self.fused.forward_backward(source, targets, grad_out=self.ddp.flat_grad)
+        self.ddp.sync_gradients()
+        self.fused.sgd_step(self.optimizer, self.ddp.flat_grad)
+        return loss
+
+    def _run_batch(self, source, targets):
+        if self.fused is not None or self.fmlp is not None or self.mega is not None:
+            loss = self._gpu_step(source, targets) if source.shape[0] == self.train_data.batch_size else \
+                self._gpu_tail_step(source, targets)
+            self._after_steps([0], [loss])
             return loss
         self.ddp.zero_grad()
         output = self.ddp(source)
@@ -128,15 +197,21 @@ class Trainer:
         b_sz = self.train_data.batch_size
         self.log.print(f"Local Rank: {self.local_rank} | Global Rank: {self.global_rank} | Epoch {epoch} | "
                        f"Batchsize: {b_sz} | Steps: {len(self.train_data)}", all_ranks=True)
-        self.train_data.set_epoch(epoch)
         t0 = time.perf_counter()
         n = 0
         loss = None
-        for source, targets in self.train_data:
-            loss = self._run_batch(source, targets)
-            n += source.shape[0]
+        if self.runner is not None:  # hipGraph chunks over the epoch's gathered shard (utils/epoch_graph.py)
+            self.epoch_batches.fill(epoch)
+            n, loss = self.runner.run(on_steps=self._after_steps)
+        else:
+            self.train_data.set_epoch(epoch)
+            for source, targets in self.train_data:
+                loss = self._run_batch(source, targets)
+                n += source.shape[0]
         if self.ctx.device.type == "cuda":
             torch.cuda.synchronize()
+            if self.mega is not None:
+                self.mega.check(f"rank {self.global_rank} epoch {epoch}")
             # a one-shot xGMI exchange that timed out drops its result (replicas would silently diverge):
             # read the device error word at this existing sync point, before the test pass and any snapshot
             check = getattr(self.ddp.comm, "check", None)
@@ -188,7 +263,11 @@ def main(argv=None):
     parser.add_argument("save_every", type=int, help="How often to save a snapshot")
     parser.add_argument("--batch_size", default=128, type=int, help="Input batch size on each device (default: 128)")
     parser.add_argument("--model", default="mlp", choices=["mlp", "cnn"])
-    parser.add_argument("--fused", action="store_true", help="cnn: whole-network fused training kernel (GPU)")
+    parser.add_argument("--fused", action="store_true",
+                        help="cnn: whole-network fused training kernel (GPU; the default GPU path, kept for scripts)")
+    parser.add_argument("--layers", action="store_true",
+                        help="GPU: layer-by-layer autograd + DDP hooks instead of the fused / one-launch step")
+    parser.add_argument("--graph_chunk", type=int, default=50, help="GPU: training steps per hipGraph replay")
     parser.add_argument("--device", default="auto", choices=["auto", "cpu", "gpu"])
     parser.add_argument("--snapshot_path", default="snapshot.pt")
     parser.add_argument("--train_size", type=int, default=60000)
@@ -224,7 +303,8 @@ def main(argv=None):
         test_data = ShardedLoader(test_set, args.batch_size, ctx.world_size, ctx.rank, shuffle=False)
         trainer = Trainer(ctx, model, train_data, test_data, make_opt, criterion, args.save_every,
                           args.snapshot_path, log, metrics, fused=args.fused and args.model == "cnn",
-                          ddp_kwargs=cfg.ddp_kwargs())
+                          ddp_kwargs=cfg.ddp_kwargs(), fast=False if args.layers else None,
+                          graph_chunk=args.graph_chunk)
         trainer.train(args.total_epochs)
         pdist.shutdown()
     end = time.time()

@@ -39,6 +39,16 @@ class FusedHvdStep:
         self.opt.step()
         return loss
 
+    def eager_step(self, x, y):
+        """One eager step; the first one negotiates through the engine and turns graph mode on, so every later call
+        is capturable (an epoch-graph runner, utils/epoch_graph.py, captures this function)."""
+        loss = self._eager(x, y)
+        if not self.negotiated:
+            torch.cuda.synchronize()
+            self.opt.enable_graph_mode()
+            self.negotiated = True
+        return loss
+
     def __call__(self, x, y):
         if not self.use_graph or x.shape[0] != self.batch:
             return self._eager(x, y)

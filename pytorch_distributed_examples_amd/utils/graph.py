@@ -81,12 +81,13 @@ class CapturedSteps:
     ``batches`` must stay alive and unchanged in address for the graph's lifetime (dataset slices are).
     ``replay()`` runs the whole group and returns the last step's output."""
 
-    def __init__(self, step_fn, batches, warmup: int = 3):
+    def __init__(self, step_fn, batches, warmup: int = 3, pool=None):
         self.step_fn = step_fn
         self.batches = [tuple(b) for b in batches]
         self.graph = None
         self.outputs = None
         self._warmup = warmup
+        self._pool = pool  # a graph memory pool shared with graphs that never replay concurrently with this one
 
     @property
     def steps(self) -> int:
@@ -102,7 +103,7 @@ class CapturedSteps:
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with OF.recompute_weight_copies():
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, pool=self._pool):
                 self.outputs = [self.step_fn(*b) for b in self.batches]
         torch.cuda.synchronize()
         upload(g)
