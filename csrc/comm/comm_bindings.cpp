@@ -147,6 +147,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              return t;
            },
            py::arg("tensor"), py::arg("scale") = 1.0, py::arg("wire_bf16") = false)
+      .def("allreduce_twoshot_",
+           [](XgmiAllreduce& x, at::Tensor& t, double scale, bool wire_bf16) {
+             check_gpu(t);
+             TORCH_CHECK(t.scalar_type() == at::kFloat, "xgmi allreduce: fp32 tensors");
+             TORCH_CHECK(t.is_contiguous(), "xgmi allreduce: contiguous tensors");
+             x.allreduce_twoshot(t.data_ptr<float>(), t.data_ptr<float>(), t.numel(), static_cast<float>(scale),
+                                 cur(t), wire_bf16);
+             return t;
+           },
+           py::arg("tensor"), py::arg("scale") = 1.0, py::arg("wire_bf16") = false)
       .def("view",
            [](const XgmiAllreduce& x) {  // flat device view for kernels that fold the exchange in (xgmi_view.h)
              const pde::XgmiView v = x.view();

@@ -43,6 +43,10 @@ class XgmiAllreduce {
   // dst[i] = scale * sum_r src_r[i]; fp32; src may alias dst; n * 4 <= max_bytes; stream-ordered.
   // wire_bf16: the exchanged copies are bf16 (cast fused into the staging; fp32 sum and output)
   void allreduce(const float* src, float* dst, int64_t n, float scale, hipStream_t s, bool wire_bf16 = false);
+  // Two-shot form for bandwidth-bound buckets (reduce-scatter + all-gather through the same slots: each link
+  // carries 2/N of the bucket instead of all of it); same contract as allreduce.  An instance runs either form
+  // only (their flag values differ), and a kernel folding the exchange in (view()) uses a one-shot instance.
+  void allreduce_twoshot(const float* src, float* dst, int64_t n, float scale, hipStream_t s, bool wire_bf16 = false);
   XgmiView view() const;  // device view for kernels that fold the exchange in (xgmi_device.h)
   // test hook: every workgroup of this rank stalls `us` microseconds between its flag wait and its peer reads
   void set_read_delay_us(double us) { read_delay_ticks_ = static_cast<uint64_t>(us * 100.0); }
@@ -75,6 +79,7 @@ class XgmiAllreduce {
   uint32_t* host_dev_ = nullptr;  // its device-side address
   std::vector<char*> peers_;    // mapped bases, peers_[rank_] == local_
   bool opened_ = false;
+  int mode_ = 0;  // 0 unused, 1 one-shot, 2 two-shot
   int64_t calls_ = 0;
 };
 

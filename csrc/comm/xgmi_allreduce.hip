@@ -131,6 +131,158 @@ __global__ __launch_bounds__(kThreads) void k_xgmi_oneshot(const float* src, flo
   xgmi_finish(xv, b, epoch);
 }
 
+// ---- two-shot: reduce-scatter + all-gather, for bandwidth-bound buckets ------------------------------------
+// The bucket is cut into NR rank-chunks of `cn` elements and every rank-chunk into gridDim.x pieces of `pc`
+// elements.  Workgroup b of every rank owns piece b of all NR rank-chunks:
+//   1. stages its pieces of its own bucket into its slot (bf16 wire: cast fused into the store), raises flag 2e-1
+//      in every rank's flag array and waits for the peers' 2e-1 (all NR pieces b are staged everywhere);
+//   2. reduces piece b of MY rank-chunk over all NR slots in rank order (the only reader of that range of my slot
+//      in this call is me), scales it and stores the sum in place in my slot and in dst;
+//   3. raises flag 2e, waits for the peers' 2e and copies piece b of every OTHER rank-chunk -- its owner's sum --
+//      from that owner's slot into dst.
+// Each link carries 2/NR of the bucket (the one-shot: all of it), every element is summed by exactly one rank and
+// read back by the others, so the result is bit-identical everywhere; with a bf16 wire the owner keeps the
+// bf16-rounded sum too.  Flags rise monotonically (2e-1, 2e per call, e = the instance's call epoch), so an
+// instance runs two-shot calls only (XgmiAllreduce::allreduce_twoshot refuses a mix with one-shot calls).
+template <bool WIRE_BF16>
+struct Wire;
+template <>
+struct Wire<false> {
+  using T = float;
+  using V = float4;
+  __device__ static float4 load4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+  __device__ static void store4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+  __device__ static float4 round4(float4 v) { return v; }
+  __device__ static float get(const float* p) { return *p; }
+  __device__ static void put(float* p, float v) { *p = v; }
+  __device__ static float round1(float v) { return v; }
+};
+template <>
+struct Wire<true> {
+  using T = uint16_t;
+  __device__ static float4 load4(const uint16_t* p) {
+    const ushort4 u = *reinterpret_cast<const ushort4*>(p);
+    return make_float4(bf16_float(u.x), bf16_float(u.y), bf16_float(u.z), bf16_float(u.w));
+  }
+  __device__ static void store4(uint16_t* p, float4 v) {
+    *reinterpret_cast<ushort4*>(p) = make_ushort4(bf16_bits(v.x), bf16_bits(v.y), bf16_bits(v.z), bf16_bits(v.w));
+  }
+  __device__ static float4 round4(float4 v) {
+    return make_float4(bf16_float(bf16_bits(v.x)), bf16_float(bf16_bits(v.y)), bf16_float(bf16_bits(v.z)),
+                       bf16_float(bf16_bits(v.w)));
+  }
+  __device__ static float get(const uint16_t* p) { return bf16_float(*p); }
+  __device__ static void put(uint16_t* p, float v) { *p = bf16_bits(v); }
+  __device__ static float round1(float v) { return bf16_float(bf16_bits(v)); }
+};
+
+template <int NR, bool VEC, bool WIRE_BF16>
+__global__ __launch_bounds__(kThreads) void k_xgmi_twoshot(const float* src, float* dst, int64_t n, float scale,
+                                                            XgmiView xv, int64_t cn, int64_t pc) {
+  using W = Wire<WIRE_BF16>;
+  using T = typename W::T;
+  __shared__ uint32_t s_epoch;
+  __shared__ int s_fail;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const uint32_t epoch = xgmi_epoch(xv, b, &s_epoch);
+  const int me = xv.rank;
+  auto range = [&](int q, int64_t& lo, int64_t& hi) {
+    const int64_t c0 = static_cast<int64_t>(q) * cn, c1 = c0 + cn < n ? c0 + cn : n;
+    lo = c0 + static_cast<int64_t>(b) * pc;
+    hi = lo + pc < c1 ? lo + pc : c1;
+  };
+  T* mine = reinterpret_cast<T*>(xgmi_slot(xv, me, epoch));
+  // 1. stage my pieces b of all rank-chunks
+#pragma unroll
+  for (int q = 0; q < NR; ++q) {
+    int64_t lo, hi;
+    range(q, lo, hi);
+    if (VEC) {
+      for (int64_t i = lo + 4 * tid; i < hi; i += 4 * kThreads) W::store4(mine + i, *reinterpret_cast<const float4*>(src + i));
+    } else {
+      for (int64_t i = lo + tid; i < hi; i += kThreads) W::put(mine + i, src[i]);
+    }
+  }
+  if (!xgmi_publish_and_wait(xv, b, 2u * epoch - 1u, &s_fail)) {
+    xgmi_finish(xv, b, epoch);
+    return;
+  }
+  xgmi_read_delay(xv);
+  // 2. reduce piece b of my rank-chunk (rank order), keep the sum in my slot for the peers
+  {
+    const T* slots[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) slots[r] = reinterpret_cast<const T*>(xgmi_slot(xv, r, epoch));
+    int64_t lo, hi;
+    range(me, lo, hi);
+    if (VEC) {
+      for (int64_t i = lo + 4 * tid; i < hi; i += 4 * kThreads) {
+        float4 v[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) v[r] = W::load4(slots[r] + i);
+        float4 acc = v[0];
+#pragma unroll
+        for (int r = 1; r < NR; ++r) {
+          acc.x += v[r].x;
+          acc.y += v[r].y;
+          acc.z += v[r].z;
+          acc.w += v[r].w;
+        }
+        acc = W::round4(make_float4(acc.x * scale, acc.y * scale, acc.z * scale, acc.w * scale));
+        W::store4(mine + i, acc);
+        *reinterpret_cast<float4*>(dst + i) = acc;
+      }
+    } else {
+      for (int64_t i = lo + tid; i < hi; i += kThreads) {
+        float v[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) v[r] = W::get(slots[r] + i);
+        float acc = v[0];
+#pragma unroll
+        for (int r = 1; r < NR; ++r) acc += v[r];
+        acc = W::round1(acc * scale);
+        W::put(mine + i, acc);
+        dst[i] = acc;
+      }
+    }
+  }
+  // 3. gather the owners' sums of the other rank-chunks
+  if (xgmi_publish_and_wait(xv, b, 2u * epoch, &s_fail)) {
+#pragma unroll
+    for (int d = 1; d < NR; ++d) {
+      const int q = (me + d) % NR;  // start at a different owner on every rank: the links load evenly
+      const T* theirs = reinterpret_cast<const T*>(xgmi_slot(xv, q, epoch));
+      int64_t lo, hi;
+      range(q, lo, hi);
+      if (VEC) {
+        for (int64_t i = lo + 4 * tid; i < hi; i += 4 * kThreads)
+          *reinterpret_cast<float4*>(dst + i) = W::load4(theirs + i);
+      } else {
+        for (int64_t i = lo + tid; i < hi; i += kThreads) dst[i] = W::get(theirs + i);
+      }
+    }
+  }
+  xgmi_finish(xv, b, epoch);
+}
+
+template <int NR, bool W>
+void launch2_w(bool vec, dim3 grid, hipStream_t s, const float* src, float* dst, int64_t n, float scale,
+               const XgmiView& v, int64_t cn, int64_t pc) {
+  if (vec)
+    hipLaunchKernelGGL((k_xgmi_twoshot<NR, true, W>), grid, dim3(kThreads), 0, s, src, dst, n, scale, v, cn, pc);
+  else
+    hipLaunchKernelGGL((k_xgmi_twoshot<NR, false, W>), grid, dim3(kThreads), 0, s, src, dst, n, scale, v, cn, pc);
+}
+template <int NR>
+void launch2(bool vec, bool wire_bf16, dim3 grid, hipStream_t s, const float* src, float* dst, int64_t n, float scale,
+             const XgmiView& v, int64_t cn, int64_t pc) {
+  if (wire_bf16)
+    launch2_w<NR, true>(vec, grid, s, src, dst, n, scale, v, cn, pc);
+  else
+    launch2_w<NR, false>(vec, grid, s, src, dst, n, scale, v, cn, pc);
+}
+
 __global__ void k_scale(const float* src, float* dst, int64_t n, float scale) {
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x)
@@ -217,6 +369,8 @@ void XgmiAllreduce::allreduce(const float* src, float* dst, int64_t n, float sca
                               bool wire_bf16) {
   if (n <= 0) return;
   if (n * 4 > max_bytes_) throw std::invalid_argument("xgmi allreduce: bucket exceeds max_bytes");
+  if (mode_ == 2) throw std::logic_error("xgmi allreduce: an instance runs one-shot OR two-shot calls, not both");
+  mode_ = 1;
   if (size_ == 1) {
     const int g = static_cast<int>(std::min<int64_t>(1024, (n + kThreads - 1) / kThreads));
     hipLaunchKernelGGL(k_scale, dim3(g), dim3(kThreads), 0, s, src, dst, n, scale);
@@ -242,6 +396,42 @@ void XgmiAllreduce::allreduce(const float* src, float* dst, int64_t n, float sca
     default: launch<8>(vec, wire_bf16, grid, s, src, dst, n, scale, v, chunk); break;
   }
   hip_check(hipGetLastError(), "oneshot launch");
+  ++calls_;
+}
+
+void XgmiAllreduce::allreduce_twoshot(const float* src, float* dst, int64_t n, float scale, hipStream_t s,
+                                      bool wire_bf16) {
+  if (n <= 0) return;
+  if (n * 4 > max_bytes_) throw std::invalid_argument("xgmi allreduce: bucket exceeds max_bytes");
+  if (mode_ == 1) throw std::logic_error("xgmi allreduce: an instance runs one-shot OR two-shot calls, not both");
+  mode_ = 2;
+  if (size_ == 1) {
+    const int g = static_cast<int>(std::min<int64_t>(1024, (n + kThreads - 1) / kThreads));
+    hipLaunchKernelGGL(k_scale, dim3(g), dim3(kThreads), 0, s, src, dst, n, scale);
+    hip_check(hipGetLastError(), "scale launch");
+    return;
+  }
+  if (!opened_) throw std::runtime_error("xgmi allreduce: peers not opened");
+  const XgmiView v = view();
+  // rank-chunks and pieces are multiples of 64 floats (float4 lanes stay aligned); >= 1024 elements per piece
+  // (a piece pays two flag round trips), at most blocks_ pieces per rank-chunk
+  int64_t cn = (n + size_ - 1) / size_;
+  cn = ((cn + 63) / 64) * 64;
+  int64_t pc = std::max<int64_t>((cn + blocks_ - 1) / blocks_, 1024);
+  pc = ((pc + 63) / 64) * 64;
+  const dim3 grid(static_cast<unsigned>((cn + pc - 1) / pc));
+  const bool vec = (n % 4 == 0) && (reinterpret_cast<uintptr_t>(src) % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(dst) % 16 == 0);
+  switch (size_) {
+    case 2: launch2<2>(vec, wire_bf16, grid, s, src, dst, n, scale, v, cn, pc); break;
+    case 3: launch2<3>(vec, wire_bf16, grid, s, src, dst, n, scale, v, cn, pc); break;
+    case 4: launch2<4>(vec, wire_bf16, grid, s, src, dst, n, scale, v, cn, pc); break;
+    case 5: launch2<5>(vec, wire_bf16, grid, s, src, dst, n, scale, v, cn, pc); break;
+    case 6: launch2<6>(vec, wire_bf16, grid, s, src, dst, n, scale, v, cn, pc); break;
+    case 7: launch2<7>(vec, wire_bf16, grid, s, src, dst, n, scale, v, cn, pc); break;
+    default: launch2<8>(vec, wire_bf16, grid, s, src, dst, n, scale, v, cn, pc); break;
+  }
+  hip_check(hipGetLastError(), "twoshot launch");
   ++calls_;
 }
 

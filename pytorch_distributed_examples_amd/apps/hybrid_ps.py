@@ -169,10 +169,20 @@ class ResNetPipelineDP:
         # stage gradients: bf16 on the wire (our cast kernels around RCCL), reduced on a side stream during
         # the last micro-batch's backward (PDE_PIPE_DP_OVERLAP=0: one reduce after the pipeline drains)
         self.overlap = dev.type == "cuda" and self.dp > 1 and os.environ.get("PDE_PIPE_DP_OVERLAP", "1") != "0"
-        if dev.type == "cuda" and self.dp > 1 and ctx.backend == "nccl":
+        dp_comm = os.environ.get("PDE_PIPE_DP_COMM", "rccl" if ctx.backend == "nccl" else "xgmi")
+        if dev.type == "cuda" and self.dp > 1 and dp_comm == "rccl" and ctx.backend == "nccl":
             from ..parallel.rccl import StreamComm
 
             self.comm = StreamComm(dev, group=self.dp_group, side_stream=self.overlap)
+        elif dev.type == "cuda" and self.dp > 1:
+            # the stage gradients over xGMI IPC (one-shot small, two-shot large buckets), no RCCL: the same code
+            # runs with the 2 x dp ranks sharing ONE GPU (RCCL refuses duplicate devices), which is how the
+            # config-4 step is rehearsed on a one-GPU box.  Reduced on the compute stream after the last
+            # micro-batch's backward (the spinning exchange never competes with a one-launch BatchNorm for CUs).
+            from ..parallel.xgmi_allreduce import xgmi_only_comm
+
+            self.overlap = False
+            self.comm = xgmi_only_comm(dev, group=self.dp_group, key=f"{tag}/dp{self.stage}")
         gd = torch.bfloat16 if (dev.type == "cuda" and os.environ.get("PDE_PIPE_GRAD_DTYPE", "bf16") == "bf16") else None
         self.ddp = DistributedDataParallel(self.module, process_group=self.dp_group,
                                            overlap=self.overlap and self.comm is not None,

@@ -203,6 +203,7 @@ class Trainer:
         if self.runner is not None:  # hipGraph chunks over the epoch's gathered shard (utils/epoch_graph.py)
             self.epoch_batches.fill(epoch)
             n, loss = self.runner.run(on_steps=self._after_steps)
+            self.epoch_batches.prepare(epoch + 1)  # host work while the GPU drains this epoch's replays
         else:
             self.train_data.set_epoch(epoch)
             for source, targets in self.train_data:

@@ -90,6 +90,7 @@ def main(argv=None):
             eb.fill()  # no set_epoch, as in the reference (quirk Q8): the permutation repeats, so does no gather
             log = AsyncLossLog(line(epoch), args.log_interval)
             n, _ = runner.run(on_steps=log.add)
+            eb.prepare(loader.sampler.epoch)  # the next epoch's (same, Q8) permutation while the GPU drains
             torch.cuda.synchronize()
             log.poll(wait=True)
         else:

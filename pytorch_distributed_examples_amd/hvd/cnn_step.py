@@ -27,7 +27,15 @@ class FusedHvdStep:
     def __init__(self, model, optimizer, batch: int, graph: bool = True):
         self.model, self.opt, self.batch = model, optimizer, int(batch)
         self.fused = FusedCNN(model)
-        self.fused.always_prep = True
+        from ..ops.optim import FusedSGD
+
+        # plain FusedSGD (the DP script, mnist_horovod.py:50): the update rides in the fused kernel's slab reduction
+        # at world 1, else ONE launch after the engine's synchronize that also refreshes the bf16 fragment image --
+        # the bench's hvd_cnn step.  Other optimisers (AdamW): the multi-tensor update, fragments rebuilt in-kernel.
+        g = optimizer.param_groups[0] if len(optimizer.param_groups) == 1 else None
+        self.sgd_fast = (isinstance(optimizer, FusedSGD) and g is not None and g.get("momentum", 0.0) == 0.0
+                         and g.get("weight_decay", 0.0) == 0.0)
+        self.fused.always_prep = not self.sgd_fast
         self.grads = self.fused.grad_buffer()  # p.grad: views of one flat buffer (never set to None)
         self.use_graph = graph
         self.graph = None
@@ -35,6 +43,17 @@ class FusedHvdStep:
         self.replays = 0
 
     def _eager(self, x, y):
+        if self.sgd_fast:
+            from . import core
+
+            if core.size() == 1:  # all-reduce = identity: SGD inside the reduction kernel
+                self.opt.synchronize()
+                return self.fused.forward_backward(x, y, grad_out=self.grads, sgd=self.opt)
+            loss = self.fused.forward_backward(x, y, grad_out=self.grads)
+            self.opt.synchronize()  # the engine (graph mode: stream-ordered on this stream)
+            with self.opt.skip_synchronize():
+                self.fused.sgd_step(self.opt, self.grads)
+            return loss
         loss = self.fused.forward_backward(x, y, grad_out=self.grads)
         self.opt.step()
         return loss

@@ -5,7 +5,9 @@
 * world 1 or CPU / gloo: ``None`` (DDP uses the c10d group, or nothing at world 1);
 * GPUs over RCCL: a :class:`.rccl.StreamComm` (stream-ordered, hipGraph-capturable RCCL all-reduce) wrapped in
   a :class:`.xgmi_allreduce.RoutedComm` that sends latency-bound buckets (<= ``PDE_XGMI_THRESHOLD``, 1 MiB)
-  through the one-shot xGMI peer all-reduce.  ``PDE_XGMI=0`` keeps every bucket on RCCL.
+  through the one-shot xGMI peer all-reduce and, on a single node, larger ones (<= ``PDE_XGMI_TWOSHOT_MB``, 64 MiB)
+  through the two-shot xGMI all-reduce (every link carries 2/N of the bucket; RCCL remains the fallback for anything
+  larger).  ``PDE_XGMI=0`` keeps every bucket on RCCL; ``PDE_XGMI_TWOSHOT=0`` keeps the large ones there (A/B).
 """
 from __future__ import annotations
 
@@ -22,4 +24,9 @@ def data_plane(ctx, group=None):
         return comm
     from .xgmi_allreduce import RoutedComm, XgmiAllreduce
 
-    return RoutedComm(comm, XgmiAllreduce(ctx.device, group=group))
+    xgmi2 = None
+    single_node = int(os.environ.get("LOCAL_WORLD_SIZE", str(ctx.world_size))) == ctx.world_size
+    if single_node and os.environ.get("PDE_XGMI_TWOSHOT", "1") != "0":
+        mb = float(os.environ.get("PDE_XGMI_TWOSHOT_MB", "64"))
+        xgmi2 = XgmiAllreduce(ctx.device, group=group, max_bytes=int(mb * (1 << 20)), two_shot=True)
+    return RoutedComm(comm, XgmiAllreduce(ctx.device, group=group), xgmi2=xgmi2)

@@ -32,12 +32,19 @@ DEFAULT_THRESHOLD = int(os.environ.get("PDE_XGMI_THRESHOLD", str(1 << 20)))
 
 
 class XgmiAllreduce:
+    """``two_shot=True``: the bandwidth form (reduce-scatter + all-gather through the same IPC slots,
+    ``XgmiAllreduce::allreduce_twoshot``): each rank reduces 1/N of the bucket from all peers and the others read that
+    sum back, so every xGMI link carries 2/N of the bucket instead of all of it -- for large buckets (a pipeline
+    stage's 24M gradients).  An instance runs one form only."""
+
     def __init__(self, device: torch.device, group=None, max_bytes: int = 4 << 20, blocks: int = 256,
-                 timeout_s: float | None = None, read_delay_us: float = 0.0, key: str | None = None):
+                 timeout_s: float | None = None, read_delay_us: float = 0.0, key: str | None = None,
+                 two_shot: bool = False):
         if timeout_s is None:  # PDE_XGMI_TIMEOUT_S: the bounded peer wait (seconds)
             timeout_s = float(os.environ.get("PDE_XGMI_TIMEOUT_S", "5.0"))
         assert device.type == "cuda", "the xGMI all-reduce is a GPU data plane"
         self.device = device
+        self.two_shot = bool(two_shot)
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.size = dist.get_world_size(group) if dist.is_initialized() else 1
         C = _native.comm()
@@ -49,7 +56,8 @@ class XgmiAllreduce:
             ranks = dist.get_process_group_ranks(group) if group is not None else list(range(self.size))
             # ``key``: an explicit handshake key (members that joined at different times -- an elastic
             # round -- have different local counters)
-            key = f"pde/xgmi/{key if key is not None else next(_SEQ)}/{'-'.join(map(str, ranks))}"
+            key = (f"pde/xgmi{'2' if two_shot else ''}/{key if key is not None else next(_SEQ)}/"
+                   f"{'-'.join(map(str, ranks))}")
             store.set(f"{key}/{self.rank}", self.impl.ipc_handle())
             handles = [store.get(f"{key}/{r}") for r in range(self.size)]
             self.impl.open(handles)
@@ -61,7 +69,10 @@ class XgmiAllreduce:
     def allreduce_(self, t: torch.Tensor, avg: bool = False, wire_bf16: bool = False) -> torch.Tensor:
         """In-place fp32 all-reduce; ``wire_bf16``: peers exchange bf16 copies (cast fused into the staging,
         half the xGMI bytes), the sum and the result stay fp32."""
-        self.impl.allreduce_(t, 1.0 / self.size if avg else 1.0, wire_bf16)
+        if self.two_shot:
+            self.impl.allreduce_twoshot_(t, 1.0 / self.size if avg else 1.0, wire_bf16)
+        else:
+            self.impl.allreduce_(t, 1.0 / self.size if avg else 1.0, wire_bf16)
         return t
 
     def view(self) -> list:
@@ -108,20 +119,27 @@ class _Done:
 
 class RoutedComm:
     """DDP communicator plug-in (``size``, ``rank``, ``supports_avg``, ``allreduce_async``, ``broadcast_``):
-    fp32 buckets up to ``threshold_bytes`` take the one-shot xGMI path, the rest go to RCCL."""
+    fp32 buckets up to ``threshold_bytes`` take the one-shot xGMI path; larger fp32 buckets up to the two-shot
+    instance's ``max_bytes`` take the two-shot xGMI path (``xgmi2``, single-node jobs; ``PDE_XGMI_TWOSHOT=0``: RCCL);
+    the rest (and non-fp32 tensors) go to RCCL.  ``rccl=None`` (ranks sharing one GPU: RCCL refuses duplicate
+    devices): every bucket takes an xGMI path and must fit ``xgmi2.max_bytes``."""
 
-    def __init__(self, rccl, xgmi: XgmiAllreduce, threshold_bytes: int = DEFAULT_THRESHOLD):
-        self.rccl, self.xgmi = rccl, xgmi
-        self.size, self.rank = rccl.size, rccl.rank
+    def __init__(self, rccl, xgmi: XgmiAllreduce, threshold_bytes: int = DEFAULT_THRESHOLD, xgmi2=None):
+        self.rccl, self.xgmi, self.xgmi2 = rccl, xgmi, xgmi2
+        self.size, self.rank = xgmi.size, xgmi.rank
         self.supports_avg = True
         self.threshold = min(int(threshold_bytes), xgmi.max_bytes)
-        self.routed = {"xgmi": 0, "rccl": 0}
+        self.routed = {"xgmi": 0, "xgmi2": 0, "rccl": 0}
         self._scratch: dict = {}  # persistent bf16 wire buffers of RCCL-routed fp32 tensors
+
+    def _two_shot(self, t: torch.Tensor) -> bool:
+        return (self.xgmi2 is not None and t.dtype == torch.float32 and t.is_contiguous()
+                and t.numel() * 4 <= self.xgmi2.max_bytes)
 
     def fuses_bf16_wire(self, t: torch.Tensor) -> bool:
         """True when ``allreduce_async(t, wire_bf16=True)`` casts inside the one-shot kernel (the bucket
         takes the xGMI path); DDP casts larger buckets itself into persistent bf16 buffers for RCCL."""
-        return t.dtype == torch.float32 and t.numel() * 4 <= self.threshold
+        return t.dtype == torch.float32 and (t.numel() * 4 <= self.threshold or self._two_shot(t))
 
     def allreduce_async(self, t: torch.Tensor, avg: bool = False, wire_bf16: bool = False):
         """``wire_bf16`` (fp32 ``t``): reduce bf16 copies -- fused into the one-shot kernel on the xGMI path;
@@ -130,6 +148,12 @@ class RoutedComm:
             self.xgmi.allreduce_(t, avg, wire_bf16)
             self.routed["xgmi"] += 1
             return _Done()
+        if self._two_shot(t):
+            self.xgmi2.allreduce_(t, avg, wire_bf16)
+            self.routed["xgmi2"] += 1
+            return _Done()
+        if self.rccl is None:
+            raise RuntimeError(f"xGMI-only communicator: a {t.dtype} bucket of {t.numel()} elements fits no xGMI path")
         self.routed["rccl"] += 1
         if wire_bf16 and t.dtype == torch.float32:
             C = _native.C()
@@ -148,13 +172,42 @@ class RoutedComm:
         return t
 
     def check(self) -> None:
-        """Raise if a one-shot exchange timed out (its result was dropped); synchronises the device -- call
+        """Raise if an xGMI exchange timed out (its result was dropped); synchronises the device -- call
         it at existing sync points (epoch end, before snapshots)."""
         self.xgmi.check()
+        if self.xgmi2 is not None:
+            self.xgmi2.check()
 
     def broadcast_(self, t: torch.Tensor, src: int) -> torch.Tensor:
-        return self.rccl.broadcast_(t, src)
+        if self.rccl is not None:
+            return self.rccl.broadcast_(t, src)
+        # xGMI only: a broadcast is the sum of src's tensor and everyone else's zeros (exact in fp32), chunked
+        # through the two-shot instance (construction time only: parameters and buffers)
+        flat = t.reshape(-1)
+        work = flat.float() if flat.dtype != torch.float32 else flat.clone()
+        if self.rank != src:
+            work.zero_()
+        inst = self.xgmi2 if self.xgmi2 is not None else self.xgmi
+        step = inst.max_bytes // 4
+        for s0 in range(0, work.numel(), step):
+            inst.allreduce_(work[s0:s0 + step], False)  # (1-D slices of a contiguous tensor: in place)
+        with torch.no_grad():
+            t.copy_(work.view_as(t).to(t.dtype))
+        return t
 
     def destroy(self):
         self.xgmi.close()
-        self.rccl.destroy()
+        if self.xgmi2 is not None:
+            self.xgmi2.close()
+        if self.rccl is not None:
+            self.rccl.destroy()
+
+
+def xgmi_only_comm(device: torch.device, group=None, max_bytes: int = 64 << 20, key: str | None = None) -> RoutedComm:
+    """A DDP communicator without RCCL: one-shot xGMI for small buckets, two-shot for the rest (buckets up to
+    ``max_bytes``).  It runs with several ranks sharing one GPU, which is how a pipeline x data-parallel job is
+    rehearsed on a one-GPU box (RCCL refuses two ranks on one device); on a node it is a pure-IPC data plane."""
+    small = XgmiAllreduce(device, group=group, key=None if key is None else key + "/1")
+    big = XgmiAllreduce(device, group=group, max_bytes=max_bytes, blocks=256, two_shot=True,
+                        key=None if key is None else key + "/2")
+    return RoutedComm(None, small, xgmi2=big)

@@ -57,6 +57,7 @@ class EpochBatches:
         self.x = torch.empty((n,) + tuple(self.images.shape[1:]), dtype=self.images.dtype, device=self.images.device)
         self.y = torch.empty((n,) + tuple(self.labels.shape[1:]), dtype=self.labels.dtype, device=self.labels.device)
         self._last = None
+        self._ready: dict = {}  # epoch -> its permutation, computed ahead (prepare)
 
     def __len__(self) -> int:
         return len(self.loader)
@@ -70,13 +71,29 @@ class EpochBatches:
         it, quirk Q8: their permutation repeats and the gather is skipped)."""
         if epoch is not None:
             self.loader.set_epoch(epoch)
-        order = sampler_indices(self.loader.sampler)
+        order = self._ready.pop(self.loader.sampler.epoch, None)
+        self._ready.clear()
+        if order is None:
+            order = sampler_indices(self.loader.sampler)
         if self._last is not None and torch.equal(order, self._last):
             return
-        idx = order.pin_memory().to(self.images.device, non_blocking=True) if self.images.is_cuda else order
+        if self.images.is_cuda:
+            idx = (order if order.is_pinned() else order.pin_memory()).to(self.images.device, non_blocking=True)
+        else:
+            idx = order
         torch.index_select(self.images, 0, idx, out=self.x)
         torch.index_select(self.labels, 0, idx, out=self.y)
         self._last = order
+
+    def prepare(self, epoch: int) -> None:
+        """Compute epoch ``epoch``'s permutation now (host work: call it while the GPU runs the current epoch)."""
+        s = self.loader.sampler
+        cur = s.epoch
+        s.set_epoch(epoch)
+        try:
+            self._ready[epoch] = sampler_indices(s).pin_memory() if self.images.is_cuda else sampler_indices(s)
+        finally:
+            s.set_epoch(cur)
 
     def batch(self, b: int):
         B = self.batch_size

@@ -1,9 +1,6 @@
 """The reference entry scripts on their default GPU paths: the one-launch MLP / fused CNN steps
 replayed as hipGraph chunks over an epoch buffer (utils/epoch_graph.py), against the same steps run eagerly, and
 the scripts' printed lines (pytorch_elastic/mnist_ddp_elastic.py:88,130,213; horovod/mnist_horovod.py:65-67)."""
-import copy
-import os
-
 import pytest
 import torch
 
@@ -29,7 +26,8 @@ def test_chunked_graphs_equal_eager_steps(gpu):
 
     torch.manual_seed(0)
     ma = reference_mlp().to(gpu)
-    mb = copy.deepcopy(ma)
+    mb = reference_mlp().to(gpu)  # (a deepcopy would drop the parameters' layer tags)
+    mb.load_state_dict(ma.state_dict())
     oa, ob = FusedAdam(ma.parameters(), lr=1e-3), FusedAdam(mb.parameters(), lr=1e-3)
     mega_a, mega_b = MegaMLP(ma, oa), MegaMLP(mb, ob)
     fa, fb = FusedMLP(ma), FusedMLP(mb)

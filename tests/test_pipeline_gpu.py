@@ -131,6 +131,78 @@ print("PIPE_OK", r)
 """
 
 
+_PIPE_DP = r"""
+import os, sys, json, time, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["REPO"])
+from pytorch_distributed_examples_amd.parallel import dist as pdist
+from pytorch_distributed_examples_amd.apps.hybrid_ps import ResNetPipelineDP
+from pytorch_distributed_examples_amd.utils.graph import CapturedStep
+ctx = pdist.init_distributed()          # PDE_BACKEND=gloo: 4 ranks = 2 pipelines x 2 stages on ONE GPU
+r, dev, W = ctx.rank, ctx.device, ctx.world_size
+B, M, IMG, STEPS = 8, 2, 64, 3
+torch.manual_seed(0)
+pipe = ResNetPipelineDP(ctx, batch=B, split_size=M, image=IMG, schedule="1f1b", lr=0.05)
+assert pipe.dp == 2 and pipe.comm is not None and pipe.capturable, "xGMI DP communicator: capturable step"
+graph = CapturedStep(pipe.step, [], warmup=1).capture()   # eager warm-up (meta handshake), then ONE hipGraph
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+losses = [float(graph().item()) for _ in range(STEPS)]
+torch.cuda.synchronize()
+dt = (time.perf_counter() - t0) / STEPS
+pipe.check()
+pipe.comm.check()
+flat = torch.cat([p.detach().float().reshape(-1) for p in pipe.module.parameters()]).cpu()
+objs = [None] * W
+dist.all_gather_object(objs, (losses, flat, dict(pipe.comm.routed)))
+# the DP replicas of each stage hold bit-identical weights
+assert torch.equal(objs[0][1], objs[2][1]) and torch.equal(objs[1][1], objs[3][1])
+if r == 0:
+    from pytorch_distributed_examples_amd.data.synthetic import resnet_batch
+    from pytorch_distributed_examples_amd.models.resnet import ResNetShard1, ResNetShard2
+    from pytorch_distributed_examples_amd.ops import functional as OF
+    from pytorch_distributed_examples_amd.ops.optim import FusedSGD
+    torch.manual_seed(0); s1 = ResNetShard1().to(dev)
+    torch.manual_seed(0); s2 = ResNetShard2().to(dev)
+    batches = [resnet_batch(B, IMG, 1000, dev, torch.Generator().manual_seed(1234 + p)) for p in range(2)]
+    opt = FusedSGD(list(s1.parameters()) + list(s2.parameters()), lr=0.05)
+    G = pipe.mb_group
+    ref = []
+    for step in range(1 + STEPS):
+        for q in list(s1.parameters()) + list(s2.parameters()):
+            q.grad = None
+        per = []
+        for x, y in batches:              # the DP average: each pipeline's mean loss / dp
+            tot = 0.0
+            for xm, ym in zip(x.split(M * G), y.split(M * G)):
+                with OF.bn_groups(G):
+                    loss = OF.mse_loss(s2(s1(xm)), ym) / (B // (M * G))
+                (loss / 2).backward()
+                tot += float(loss.item())
+            per.append(tot)
+        opt.step()
+        ref.append(per)
+    for p in range(2):  # pipeline p's loss is reported by its last stage, rank 2p + 1
+        pl = objs[2 * p + 1][0]
+        assert all(abs(a - b[p]) <= 2e-3 * max(1.0, abs(b[p])) for a, b in zip(pl, ref[1:])), (p, pl, ref)
+    for k, mod in ((0, s1), (1, s2)):
+        want = torch.cat([q.detach().float().reshape(-1) for q in mod.parameters()]).cpu()
+        err = ((objs[k][1] - want).norm() / want.norm()).item()
+        assert err < 3e-3, (k, err)
+    rec = dict(config="4 rehearsal: resnet50 pp2 x dp2, 4 ranks sharing ONE MI355X", hipgraph=True,
+               dp_comm="xgmi one-shot + two-shot (no RCCL)", batch_per_pipeline=B, split_size=M, image=IMG,
+               mb_group=G, schedule="1f1b", steps=STEPS, ms_per_step_shared_gpu=round(dt * 1e3, 3),
+               losses=[objs[1][0], objs[3][0]], routed=[o[2] for o in objs],
+               note="4 processes time-share one GPU: a correctness rehearsal, not a throughput number")
+    os.makedirs(os.path.join(os.environ["REPO"], "gpurun_out"), exist_ok=True)
+    with open(os.path.join(os.environ["REPO"], "gpurun_out", "r6_world4_shared_gpu_resnet50_pp.jsonl"), "w") as f:
+        f.write(json.dumps(rec) + "\n")
+dist.barrier()
+pipe.close()
+dist.destroy_process_group()
+print("PIPEDP_OK", r)
+"""
+
+
 def _torchrun(script, n, extra_env=None, timeout=600):
     from pytorch_distributed_examples_amd.parallel.dist import free_port
 
@@ -165,6 +237,13 @@ def test_resnet_pipeline_graph_rehearsal_one_gpu(gpu, schedule, group):
     reference always runs one micro-batch at a time."""
     _check(_torchrun(_PIPE, 2, {"SCHEDULE": schedule, "PDE_PIPE_MB_GROUP": group}), "PIPE_OK", 2,
            f"pipe_{schedule}_g{group}")
+
+
+def test_resnet_pipeline_x_dp_xgmi_graph_rehearsal_one_gpu(gpu):
+    """BASELINE config 4's step, pp2 x dp2 = 4 ranks on one GPU: stage activations over the P2P rings, each stage's
+    gradients all-reduced across its 2 replicas by the xGMI one-/two-shot communicator inside the captured step;
+    losses and final weights against ONE process running both pipelines' micro-batches with averaged gradients."""
+    _check(_torchrun(_PIPE_DP, 4, {"PDE_PIPE_MB_GROUP": "2"}), "PIPEDP_OK", 4, "pipe_dp_xgmi")
 
 
 def test_resnet_rpc_pipeline_one_gpu(gpu):

@@ -1,0 +1,138 @@
+"""Two-shot peer all-reduce (csrc/comm/xgmi_allreduce.hip k_xgmi_twoshot: reduce-scatter + all-gather through
+the IPC slots) rehearsed on ONE GPU with 2 and 4 processes sharing the card, against a CPU sum over 1 KB .. 64 MB,
+fp32 and bf16 wires, averaging, odd sizes, bit-identity across ranks, a late peer and the hipGraph form; then
+the xGMI-only DDP communicator (one-shot small + two-shot large buckets, no RCCL) on a real model's buckets."""
+import os
+import subprocess
+import sys
+import tempfile
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_SCRIPT = r"""
+import os, sys, time, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["REPO"])
+from pytorch_distributed_examples_amd.parallel import dist as pdist
+from pytorch_distributed_examples_amd.parallel.xgmi_allreduce import XgmiAllreduce, xgmi_only_comm
+ctx = pdist.init_distributed()          # PDE_BACKEND=gloo: several ranks on one GPU
+N, r, dev = ctx.world_size, ctx.rank, ctx.device
+
+def rank_data(k, n, seed):
+    g = torch.Generator().manual_seed(seed * 1000 + k)
+    return torch.randn(n, generator=g)
+
+def same_everywhere(x, tag):
+    xs = [torch.empty_like(x) for _ in range(N)]
+    dist.all_gather(xs, x)
+    assert all(torch.equal(v, xs[0]) for v in xs), tag
+
+xa = XgmiAllreduce(dev, max_bytes=64 << 20, timeout_s=30.0, two_shot=True)
+# 1 KB .. 64 MB, plus sizes smaller than the rank count and not a multiple of 4 / 64
+for n in (1, 3, 256, 1001, 65536, 262147, 1 << 20, 4 << 20, 16 << 20):
+    x = rank_data(r, n, n).to(dev)
+    xa.allreduce_(x)
+    torch.cuda.synchronize()
+    ref = torch.zeros(n)
+    for k in range(N):
+        ref += rank_data(k, n, n)
+    assert torch.allclose(x.cpu(), ref, rtol=1e-6, atol=1e-6), (n, (x.cpu() - ref).abs().max())
+    same_everywhere(x.cpu(), n)
+# bf16 wire: bf16 staging, fp32 rank-order sum, the owner's scaled sum rounded to bf16 for everyone
+for n in (1000, 262144, 4 << 20):
+    x = rank_data(r, n, n + 7).to(dev)
+    xa.allreduce_(x, avg=True, wire_bf16=True)
+    torch.cuda.synchronize()
+    ref = torch.zeros(n)
+    for k in range(N):
+        ref += rank_data(k, n, n + 7).bfloat16().float()
+    ref = (ref * (1.0 / N)).bfloat16().float()
+    assert torch.allclose(x.cpu(), ref, rtol=0, atol=0), (n, (x.cpu() - ref).abs().max())
+    same_everywhere(x.cpu(), ("bf16", n))
+# unaligned view (scalar path) + averaging
+big = rank_data(r, 100001, 5).to(dev)
+v = big[1:]
+xa.allreduce_(v, avg=True)
+torch.cuda.synchronize()
+ref = sum(rank_data(k, 100001, 5) for k in range(N))[1:] / N
+assert torch.allclose(v.cpu(), ref, rtol=1e-5, atol=1e-6)
+# a late peer: the others spin (bounded) until it arrives
+if r == N - 1:
+    time.sleep(0.3)
+x = torch.full((3 << 20,), float(r + 1), device=dev)
+xa.allreduce_(x)
+torch.cuda.synchronize()
+assert torch.all(x == N * (N + 1) / 2)
+# hipGraph: 2 all-reduces of different sizes per replay, 3 replays (epochs and slot parities advance)
+t1 = torch.full((1 << 20,), float(r + 1), device=dev)
+t2 = torch.full((5000,), float(r + 1), device=dev)
+torch.cuda.synchronize()
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+    t1.mul_(0.5); xa.allreduce_(t1)
+    t2.mul_(0.5); xa.allreduce_(t2)
+vals = [float(k + 1) for k in range(N)]
+t1.fill_(float(r + 1)); t2.fill_(float(r + 1))
+for _ in range(3):
+    g.replay()
+    s = sum(0.5 * v for v in vals)
+    vals = [s] * N
+torch.cuda.synchronize()
+assert torch.allclose(t1, torch.full_like(t1, vals[0]), rtol=1e-6) and torch.allclose(t2, torch.full_like(t2, vals[0]), rtol=1e-6)
+xa.check()
+try:
+    xa.impl.allreduce_(torch.zeros(8, device=dev), 1.0, False)  # a one-shot call on a two-shot instance
+    raise AssertionError("mixing the one-shot form into a two-shot instance must be refused")
+except RuntimeError as e:
+    assert "not both" in str(e)
+xa.close()
+# the xGMI-only DDP communicator on a model whose buckets straddle the one-shot threshold
+from pytorch_distributed_examples_amd.parallel.ddp import DistributedDataParallel
+comm = xgmi_only_comm(dev, max_bytes=32 << 20)
+torch.manual_seed(r)  # different init per rank: the construction broadcast makes them equal
+m = torch.nn.Sequential(torch.nn.Linear(1024, 2048), torch.nn.Linear(2048, 1024), torch.nn.Linear(1024, 10)).to(dev)
+ddp = DistributedDataParallel(m, overlap=False, comm=comm, bucket_cap_mb=4, grad_dtype=torch.bfloat16)
+same_everywhere(torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu(), "broadcast")
+ddp.zero_grad()
+ddp.flat_grad.copy_(rank_data(r, ddp.flat_grad.numel(), 9).to(dev))
+ddp.sync_gradients()
+torch.cuda.synchronize()
+ref = sum(rank_data(k, ddp.flat_grad.numel(), 9).bfloat16().float() for k in range(N)) / N
+assert torch.allclose(ddp.flat_grad.cpu(), ref, rtol=1e-2, atol=1e-3)
+assert comm.routed["xgmi2"] >= 2, comm.routed
+comm.check()
+same_everywhere(ddp.flat_grad.cpu(), "ddp")
+dist.barrier()
+comm.destroy()
+dist.destroy_process_group()
+print("TWOSHOT_OK", r)
+"""
+
+
+def _run(n):
+    from pytorch_distributed_examples_amd.parallel.dist import free_port
+
+    env = dict(os.environ, REPO=REPO, PDE_BACKEND="gloo")
+    with tempfile.NamedTemporaryFile("w", suffix=".py", delete=False) as f:
+        f.write(_SCRIPT)
+        path = f.name
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), path]
+    try:
+        return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    finally:
+        os.unlink(path)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_xgmi_twoshot_rehearsal_one_gpu(gpu, n):
+    res = _run(n)
+    ranks = "\n".join(l for l in res.stderr.splitlines() if l.startswith("[rank"))
+    if res.returncode != 0:
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(REPO, "gpurun_out", f"xgmi_twoshot_{n}.err"), "w") as f:
+            f.write(res.stdout + "\n----\n" + res.stderr)
+    assert res.returncode == 0 and res.stdout.count("TWOSHOT_OK") == n, (res.stdout[-2000:], ranks[-6000:])
