@@ -353,6 +353,28 @@ void cast_rows_ones(const Tensor& x, Tensor& out) {
   check(pde::cast_rows_bf16(x.data_ptr<float>(), B, K, u16(out), out.stride(0), 1, cur_stream()), "cast_rows_ones");
 }
 
+// Device-counter batch gather (pde::gather_rows_counter): x_out [rows, ...] fp32 / y_out [rows] int64 <- rows
+// counter[0] x rows ... of idx from src / labels; counter (int32 [2], device) advances by one per launch.
+void gather_rows_counter(const Tensor& src, const Tensor& labels, const Tensor& idx, Tensor& counter, Tensor& x_out,
+                         Tensor& y_out) {
+  CHECK_IN(src); CHECK_F32(src); CHECK_IN(labels); CHECK_IN(idx); CHECK_IN(x_out); CHECK_F32(x_out); CHECK_IN(y_out);
+  TORCH_CHECK(labels.scalar_type() == at::kLong && idx.scalar_type() == at::kLong && y_out.scalar_type() == at::kLong,
+              "gather_rows_counter: int64 labels / indices");
+  TORCH_CHECK(counter.is_cuda() && counter.scalar_type() == at::kInt && counter.numel() >= 2,
+              "gather_rows_counter: counter must be a device int32[2]");
+  const int64_t row_elems = src.numel() / std::max<int64_t>(1, src.size(0));
+  const int rows = static_cast<int>(x_out.size(0));
+  TORCH_CHECK(x_out.numel() == rows * row_elems && y_out.numel() == rows, "gather_rows_counter: x_out [rows, row]");
+  TORCH_CHECK(row_elems % 4 == 0 && reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(x_out.data_ptr()) % 16 == 0, "gather_rows_counter: 16-byte rows");
+  TORCH_CHECK(idx.numel() > 0 && labels.numel() == src.size(0), "gather_rows_counter: idx / labels");
+  check(pde::gather_rows_counter(src.data_ptr<float>(), labels.data_ptr<int64_t>(), idx.data_ptr<int64_t>(),
+                                 idx.numel(), reinterpret_cast<uint32_t*>(counter.data_ptr<int>()), rows,
+                                 static_cast<int>(row_elems), x_out.data_ptr<float>(), y_out.data_ptr<int64_t>(),
+                                 cur_stream()),
+        "gather_rows_counter");
+}
+
 // (mean cross-entropy loss, d loss / d logits as bf16) in one launch.  dx_out: a [B, >= V] bf16 row view to
 // write d logits into (its columns past V are left as they are, e.g. the zero padding of a K = 16 operand).
 std::vector<Tensor> ce_fused(const Tensor& x, const Tensor& tgt, const optional<Tensor>& dx_out) {
@@ -1387,6 +1409,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_flush_deferred", &gemm_flush_deferred);
   m.def("gemm_deferred_count", &gemm_deferred_count);
   m.def("cast_rows_ones", &cast_rows_ones);
+  m.def("gather_rows_counter", &gather_rows_counter, py::arg("src"), py::arg("labels"), py::arg("idx"),
+        py::arg("counter"), py::arg("x_out"), py::arg("y_out"));
   m.def("ce_bwd", &ce_bwd);
   m.def("log_softmax_fwd", &log_softmax_fwd);
   m.def("log_softmax_bwd", &log_softmax_bwd);

@@ -250,6 +250,10 @@ int bn_workspace_blocks(int P, int C, int groups = 1);
 // overlapped RCCL all-reduce); returns the resulting resident cap.  Grids shrink to the cap; a BatchNorm whose
 // minimal grid exceeds it is refused up front and runs multi-launch.
 int bn_reserve_headroom(int blocks);
+// rows [c x rows, (c+1) x rows) of idx (c = counter[0], advanced by the launch) gathered from src [N, row_elems]
+// fp32 / labels [N] into dst / ydst (elastic/rewire.py: the per-replay batch gather inside the captured graph)
+hipError_t gather_rows_counter(const float* src, const int64_t* labels, const int64_t* idx, int64_t n_idx,
+                               uint32_t* counter, int rows, int row_elems, float* dst, int64_t* ydst, hipStream_t s);
 int bn_headroom_reserved();  // CUs currently reserved for spinning side-stream kernels
 void bn_launch_stats(long* one_launch, long* multi_launch, int* last_grid, int* cap);
 hipError_t bn_fwd_train(const uint16_t* x, int P, int C, const float* gamma, const float* beta, float eps,

@@ -1,6 +1,8 @@
 // Memory-bound layout / cast / reduction kernels (gfx950).  All loads are vectorised (8 x bf16 or
 // 4 x f32 per lane, cdna_hip_programming.md Guideline 13) and grids are capped grid-stride loops
 // (Guideline 11).
+#include <algorithm>
+
 #include "common.cuh"
 #include "pde_kernels.h"
 
@@ -419,6 +421,56 @@ hipError_t colsum_bf16(const uint16_t* x, float* out, int M, int N, int accum, h
 }
 hipError_t relu_bwd_bf16(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n, hipStream_t s) {
   hipLaunchKernelGGL(k_relu_bwd, dim3(stream_grid(n, 256, 8)), dim3(256), 0, s, dy, y, dx, n);
+  return hipGetLastError();
+}
+
+// Batch gather driven by a DEVICE replay counter (elastic/rewire.py, utils/epoch_graph.py): rows [c x rows,
+// (c + 1) x rows) of the epoch's index list idx (c = counter[0]) are gathered from the HBM-resident dataset into
+// the captured step's static batch slots, and the launch's last workgroup advances the counter -- so a hipGraph
+// replayed k times trains on k different slices of the epoch with no host work between replays (the host sets
+// the counter once per epoch / resume).  Every workgroup reads the counter before it counts itself done, so
+// the increment never races a read; counter[1] is the done count (re-zeroed by the last workgroup).
+__global__ __launch_bounds__(256) void k_gather_rows_counter(const float4* __restrict__ src,
+                                                             const int64_t* __restrict__ labels,
+                                                             const int64_t* __restrict__ idx, int64_t n_idx,
+                                                             uint32_t* counter, int rows, int row4,
+                                                             float4* __restrict__ dst, int64_t* __restrict__ ydst) {
+  __shared__ int64_t s_base;
+  if (threadIdx.x == 0)
+    s_base = static_cast<int64_t>(__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) * rows;
+  __syncthreads();
+  const int64_t base = s_base;
+  const int64_t total = static_cast<int64_t>(rows) * row4;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int64_t row = t / row4, c = t - row * row4;
+    int64_t k = base + row;
+    k = k < n_idx ? k : n_idx - 1;  // (the host only replays whole slices; never read past the list)
+    dst[t] = src[idx[k] * row4 + c];
+  }
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; row < rows; row += stride) {
+    int64_t k = base + row;
+    k = k < n_idx ? k : n_idx - 1;
+    ydst[row] = labels[idx[k]];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t n = __hip_atomic_fetch_add(counter + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (n == gridDim.x - 1) {
+      __hip_atomic_store(counter + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+hipError_t gather_rows_counter(const float* src, const int64_t* labels, const int64_t* idx, int64_t n_idx,
+                               uint32_t* counter, int rows, int row_elems, float* dst, int64_t* ydst, hipStream_t s) {
+  if (rows <= 0 || row_elems % 4 != 0) return hipErrorInvalidValue;
+  const int row4 = row_elems / 4;
+  const int64_t total = static_cast<int64_t>(rows) * row4;
+  const int grid = static_cast<int>(std::min<int64_t>(2048, (total + 255) / 256));
+  hipLaunchKernelGGL(k_gather_rows_counter, dim3(grid), dim3(256), 0, s, reinterpret_cast<const float4*>(src), labels,
+                     idx, n_idx, counter, rows, row4, reinterpret_cast<float4*>(dst), ydst);
   return hipGetLastError();
 }
 

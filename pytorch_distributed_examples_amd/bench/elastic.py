@@ -116,7 +116,7 @@ def worker(args) -> None:
     a = A()
     a.batch_size = args.batch or 1024
     a.graph_steps = args.graph_steps
-    a.commit_every = 2
+    a.commit_every = 10  # replays between commit points (device-side commits: no sync, rewire.py _DeviceCommit)
     a.round_warmup = max(1, args.warmup // max(1, args.graph_steps))
     a.round_replays = max(1, args.steps // max(1, args.graph_steps))
     a.total_steps = 10 ** 9  # the bench ends through report()

@@ -361,6 +361,84 @@ class Commit:
         self.position.update(self._pos)
 
 
+class _DeviceCommit:
+    """Commit points of the fused GPU step without a device synchronisation.
+
+    All trainable state of the fused CNN is ONE flat fp32 tensor (plain SGD keeps no other state).  ``save()``
+    enqueues a copy of it into one of two device buffers and records an event, together with the host-side
+    position; a pending commit is CONFIRMED once its event has completed and the xGMI exchange's host-mapped
+    error word is still clear (a timed-out exchange before the copy would have set it first).  ``throttle()``
+    waits for the previous commit's event only: the host stays at most one commit interval ahead of the device, so
+    failures surface within an interval while the GPU always has an interval of replays queued.
+    ``restore()`` (after a PeerFailure) copies the last confirmed commit back; ``Commit``'s clone of the optimiser
+    state dict is kept for the (tiny) step counter."""
+
+    def __init__(self, flat: torch.Tensor, model, optimizer, position: dict, failed=None):
+        self.flat, self.position = flat, position
+        self.failed = failed or (lambda: False)
+        self.bufs = [torch.empty_like(flat), torch.empty_like(flat)]
+        self.host = Commit(model, optimizer, position)  # synchronous baseline commit (round start)
+        self.bufs[0].copy_(flat)
+        torch.cuda.synchronize()
+        self.confirmed = (0, dict(position))
+        self.pending = None
+        self.last_event = None
+        self.saves = self.skipped = 0
+
+    def _promote(self, wait: bool = False):
+        if self.pending is None:
+            return
+        slot, ev, pos = self.pending
+        if wait:
+            ev.synchronize()
+        elif not ev.query():
+            return
+        if not self.failed():
+            self.confirmed = (slot, pos)
+        self.pending = None
+
+    def throttle(self):
+        if self.last_event is not None:
+            self.last_event.synchronize()
+
+    def save(self):
+        """Non-blocking commit at the current position (no host sync; skipped while the last one is in flight)."""
+        self._promote()
+        if self.pending is not None:
+            self.skipped += 1
+            return
+        slot = 1 - self.confirmed[0]
+        self.bufs[slot].copy_(self.flat)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending = (slot, ev, dict(self.position))
+        self.last_event = ev
+        self.saves += 1
+
+    def save_sync(self):
+        """Commit now and wait for it (epoch end: the device is synchronised there anyway)."""
+        self._promote(wait=True)
+        self.save()
+        self._promote(wait=True)
+
+    def restore(self):
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError:
+            pass
+        self._promote(wait=False)
+        self.pending = None
+        slot, pos = self.confirmed
+        with torch.no_grad():
+            self.flat.copy_(self.bufs[slot])
+        self.position.clear()
+        self.position.update(pos)
+
+    @property
+    def _pos(self):  # (the log line of the failure path reads the restored position)
+        return self.confirmed[1]
+
+
 def _as_peer_failure(fn):
     """Run a data-/control-plane call of the round; its RuntimeError (an xGMI exchange that timed out on a dead
     peer, a gloo collective or store wait whose peer vanished) becomes :class:`PeerFailure`, which the re-wire
@@ -578,10 +656,18 @@ def run_elastic_fused(args, report=None):
     The step is the fused whole-network CNN with the gradient exchange over xGMI INSIDE its reduction kernel
     (``FusedCNN.forward_backward(..., xgmi=...)``: 2 launches per step at any world size) and the SGD update fused
     in.  ``graph_steps`` steps are recorded into ONE hipGraph per round whose inputs are ``graph_steps`` static
-    batch slots: before each replay the next ``graph_steps`` batches of the shard are gathered into the slots
-    (one index-gather per replay), so every replay trains on NEW data; an epoch's tail (fewer batches than a
-    replay, or a short last batch) runs as eager fused steps.  The graph is recaptured after every membership
-    change (xGMI view and world size are baked in).
+    batch slots, preceded by ONE gather node (``gather_rows_counter``) that copies the next ``graph_steps`` batches
+    of the epoch's shard into the slots, at the position of a DEVICE replay counter it advances itself -- every
+    replay trains on new data with no host work between replays (the host writes the counter once per epoch /
+    resume).  The first step of a round, a resumed position inside a replay and an epoch's tail run as eager fused
+    steps.  The graph is recaptured after every membership change (xGMI view and world size are baked in).
+
+    Commit points (every ``commit_every`` replays) never synchronise the device (:class:`_DeviceCommit`): the
+    weights are copied on the stream into one of two device buffers behind an event, and a commit is CONFIRMED
+    once its event has completed with the exchange's host-mapped error word still clear; the host waits only for
+    the PREVIOUS commit's event, so at most one interval of replays is queued and the GPU never idles.  Liveness:
+    the failure watch's abort word (the driver reports a dead member) or the error word turns into PeerFailure at
+    the next commit point, and the survivors restore the last confirmed commit.
 
     Failure handling: a dead peer makes the exchange give up -- at once when the driver reports the failure
     (:class:`_FailureWatch` raises the exchange's host abort word), else at its timeout -- and the next commit
@@ -602,6 +688,7 @@ def run_elastic_fused(args, report=None):
     from ..ops.optim import FusedSGD
     from ..parallel import dist as pdist
     from ..parallel.xgmi_allreduce import XgmiAllreduce
+    from ..utils.epoch_graph import sampler_indices
     from ..utils.graph import CapturedSteps
     from ..utils.log import RankLogger
 
@@ -647,6 +734,9 @@ def run_elastic_fused(args, report=None):
     xbuf = torch.empty(G * batch, 1, 28, 28, device=dev)
     ybuf = torch.zeros(G * batch, dtype=torch.long, device=dev)
     slots = [(xbuf[j * batch:(j + 1) * batch], ybuf[j * batch:(j + 1) * batch]) for j in range(G)]
+    # the graph's gather reads the epoch's index list at a fixed address and the replay position from a device
+    # counter (int32 [replay, done-count]), written by the host once per epoch / resume
+    counter = torch.zeros(2, dtype=torch.int32, device=dev) if on_gpu else None
     pos = {"epoch": 0, "seen": 0, "step": 0}
     commit = Commit(model, opt, pos)
     commit_every = max(1, int(getattr(args, "commit_every", 10)))  # graph replays between commit points
@@ -655,7 +745,7 @@ def run_elastic_fused(args, report=None):
     pid = os.getpid()
 
     def gather(idx, lo, hi, xo, yo):
-        sl = idx[lo:hi] % real_train
+        sl = idx[lo:hi]  # (already reduced modulo the real sample count)
         torch.index_select(train_set.images, 0, sl, out=xo)
         torch.index_select(train_set.labels, 0, sl, out=yo)
 
@@ -667,6 +757,7 @@ def run_elastic_fused(args, report=None):
         log = RankLogger(rank)
         xa = None
         watch = None
+        dcommit = None
         parts = {"rendezvous_s": t_joined - (changed_at if changed_at is not None else t_join),
                  "control_s": comm.timing.get("control_group_s", 0.0)}
         try:
@@ -680,6 +771,7 @@ def run_elastic_fused(args, report=None):
             state = comm.broadcast_object(dict(pos) if rank == 0 else None) if size > 1 else dict(pos)
             pos.clear()
             pos.update(state)
+            round_step0 = pos["step"]  # the round's first step runs eagerly (then the graph is captured)
             sync()
             parts["broadcast_s"] = _time.perf_counter() - tb
             tm = _time.perf_counter()
@@ -692,8 +784,10 @@ def run_elastic_fused(args, report=None):
                 def train_step(x, y):
                     return fused.forward_backward(x, y, grad_out=grads, sgd=opt, xgmi=xa)
 
-                graph = CapturedSteps(train_step, slots, warmup=1).capture()
+                graph = None  # captured at the round's first replay point, after one eager step
                 eager_step = train_step
+                C_ = _native.C()
+                idx_buf = None
             else:
                 from ..ops import functional as OF
                 from ..parallel.ddp import DistributedDataParallel
@@ -725,11 +819,15 @@ def run_elastic_fused(args, report=None):
             rewire_s = _time.perf_counter() - changed_at if changed_at is not None else None
             changed_at = detect = None
             watch = _FailureWatch(rdzv, rnd, xa) if size > 1 else None
+            if on_gpu:
+                dcommit = _DeviceCommit(fused.flat, model, opt, pos,
+                                        failed=(lambda: xa.failed()) if xa is not None else None)
             plane = f"fused CNN + xGMI exchange, {G} steps per graph" if on_gpu else "CPU autograd + gloo DDP"
             log.print(f"[rewire] round {rnd}: rank {rank} of {size} (pid {pid}), {plane}" +
                       (f", re-wired in {rewire_s:.3f}s (" + ", ".join(f"{k[:-2]} {v:.3f}" for k, v in parts.items())
                        + ")" if rewire_s is not None else ""), all_ranks=True)
-            commit.save()
+            if not on_gpu:
+                commit.save()
             train_data = ShardedLoader(train_view, batch, size, rank, shuffle=True)
             test_data = ShardedLoader(test_set, batch, size, rank, shuffle=False)
             per_step = batch * size
@@ -751,8 +849,14 @@ def run_elastic_fused(args, report=None):
                 elif epoch >= total_epochs:
                     break
                 train_data.set_epoch(epoch)
-                idx = torch.tensor(list(iter(train_data.sampler)), dtype=torch.long).to(dev)
+                idx = sampler_indices(train_data.sampler) % real_train
+                if on_gpu:  # the graph's gather reads this buffer: same address every epoch of the round
+                    if idx_buf is None or idx_buf.numel() != idx.numel():
+                        idx_buf, graph = torch.empty(idx.numel(), dtype=torch.long, device=dev), None
+                    idx_buf.copy_(idx)
+                    idx = idx_buf
                 b = min(pos["seen"] // per_step, n_batches)  # resume after the group's consumed batches
+                at = None  # the replay index the device counter holds (None: unknown -> rewritten before a replay)
                 log.print(f"Local Rank: {rdzv.wid} | Global Rank: {rank} | Epoch {epoch} | Batchsize: {batch} | "
                           f"Steps: {n_batches} | start batch {b}", all_ranks=True)
                 # the bench window: whole replays inside this epoch (no test pass or eager tail inside it); a round
@@ -767,12 +871,25 @@ def run_elastic_fused(args, report=None):
                         stop = True
                         break
                     step0 = pos["step"]
-                    if b + G <= n_batches and (b + G) * batch <= idx.numel():
+                    if on_gpu and b % G == 0 and b + G <= n_batches and (b + G) * batch <= idx.numel() and \
+                            (graph is not None or pos["step"] > round_step0):
+                        if graph is None:  # after >= 1 eager step of this round initialised everything
+                            def gather_slots():
+                                C_.gather_rows_counter(train_set.images, train_set.labels, idx_buf, counter, xbuf,
+                                                       ybuf)
+                            graph = CapturedSteps(train_step, slots, warmup=0, prologue=gather_slots).capture()
+                        if at != b // G:
+                            counter.copy_(torch.tensor([b // G, 0], dtype=torch.int32))
+                        loss = graph.replay()  # gather the next G batches at the counter + G fused steps
+                        at = b // G + 1
+                        n = G
+                        replays += 1
+                    elif not on_gpu and b + G <= n_batches and (b + G) * batch <= idx.numel():
                         gather(idx, b * batch, (b + G) * batch, xbuf, ybuf)  # the next G batches -> the slots
                         loss = graph.replay()
                         n = G
                         replays += 1
-                    else:  # epoch tail: fewer batches than a replay, or the short last batch
+                    else:  # round start, resumed mid-replay, epoch tail: eager fused steps
                         lo, hi = b * batch, min((b + 1) * batch, idx.numel())
                         x, y = xbuf[:hi - lo], ybuf[:hi - lo]
                         gather(idx, lo, hi, x, y)
@@ -808,10 +925,15 @@ def run_elastic_fused(args, report=None):
                                 break
                     since += 1
                     if since % commit_every == 0:  # commit point: liveness + membership
-                        sync()
-                        if xa is not None:
-                            _as_peer_failure(xa.check)
-                        commit.save()
+                        if on_gpu:  # no device sync: bounded queue, non-blocking failure words, device copy
+                            dcommit.throttle()
+                            if (watch is not None and watch.fired_at is not None) or (xa is not None and xa.failed()):
+                                raise PeerFailure("xGMI exchange gave up on a peer (driver-reported failure / "
+                                                  "timeout)")
+                            dcommit.save()
+                        else:
+                            sync()
+                            commit.save()
                         if comm.agree(rdzv.hosts_updated()):
                             raise MembershipChanged()
                 if stop:
@@ -821,7 +943,10 @@ def run_elastic_fused(args, report=None):
                 if xa is not None:
                     _as_peer_failure(xa.check)
                 pos["epoch"], pos["seen"] = epoch + 1, 0
-                commit.save()
+                if on_gpu:
+                    dcommit.save_sync()
+                else:
+                    commit.save()
                 _test(model, test_data, dev, comm, log)
                 if rank == 0 and save_every and snapshot_path and epoch % save_every == 0:
                     save_snapshot(snapshot_path, model.state_dict(), epoch, opt.state_dict())
@@ -841,10 +966,13 @@ def run_elastic_fused(args, report=None):
             tf = _fault_time()
             detect = (time.time() - tf) if tf is not None else None
             log.print(f"[rewire] round {rnd}: peer failure ({str(exc).splitlines()[0][:120]}); restoring commit "
-                      f"epoch {commit._pos['epoch']} step {commit._pos['step']}" +
+                      f"epoch {(dcommit or commit)._pos['epoch']} step {(dcommit or commit)._pos['step']}" +
                       (f"; detected {detect:.3f}s after the fault" if detect is not None else ""), all_ranks=True)
             comm.close(abort=True)
-            commit.restore()
+            if on_gpu and dcommit is not None:
+                dcommit.restore()
+            else:
+                commit.restore()
             if fused is not None:
                 fused.invalidate()
         except MembershipChanged:

@@ -28,5 +28,8 @@ def data_plane(ctx, group=None):
     single_node = int(os.environ.get("LOCAL_WORLD_SIZE", str(ctx.world_size))) == ctx.world_size
     if single_node and os.environ.get("PDE_XGMI_TWOSHOT", "1") != "0":
         mb = float(os.environ.get("PDE_XGMI_TWOSHOT_MB", "64"))
-        xgmi2 = XgmiAllreduce(ctx.device, group=group, max_bytes=int(mb * (1 << 20)), two_shot=True)
+        # (a longer peer-wait bound than the one-shot's 5 s: large buckets are first reduced after the first
+        # backward, when ranks may still be far apart from their first-use initialisation)
+        xgmi2 = XgmiAllreduce(ctx.device, group=group, max_bytes=int(mb * (1 << 20)), two_shot=True,
+                              timeout_s=float(os.environ.get("PDE_XGMI_TIMEOUT_S", "30")))
     return RoutedComm(comm, XgmiAllreduce(ctx.device, group=group), xgmi2=xgmi2)

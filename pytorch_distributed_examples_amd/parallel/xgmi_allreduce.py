@@ -207,7 +207,10 @@ def xgmi_only_comm(device: torch.device, group=None, max_bytes: int = 64 << 20, 
     """A DDP communicator without RCCL: one-shot xGMI for small buckets, two-shot for the rest (buckets up to
     ``max_bytes``).  It runs with several ranks sharing one GPU, which is how a pipeline x data-parallel job is
     rehearsed on a one-GPU box (RCCL refuses two ranks on one device); on a node it is a pure-IPC data plane."""
-    small = XgmiAllreduce(device, group=group, key=None if key is None else key + "/1")
+    # the peer-wait bound: ranks sharing one GPU (the rehearsal) start far apart on their first step (every
+    # process loads its code objects at once), so the default here is generous (PDE_XGMI_TIMEOUT_S overrides)
+    t = float(os.environ.get("PDE_XGMI_TIMEOUT_S", "60"))
+    small = XgmiAllreduce(device, group=group, key=None if key is None else key + "/1", timeout_s=t)
     big = XgmiAllreduce(device, group=group, max_bytes=max_bytes, blocks=256, two_shot=True,
-                        key=None if key is None else key + "/2")
+                        key=None if key is None else key + "/2", timeout_s=t)
     return RoutedComm(None, small, xgmi2=big)

@@ -81,8 +81,9 @@ class CapturedSteps:
     ``batches`` must stay alive and unchanged in address for the graph's lifetime (dataset slices are).
     ``replay()`` runs the whole group and returns the last step's output."""
 
-    def __init__(self, step_fn, batches, warmup: int = 3, pool=None):
+    def __init__(self, step_fn, batches, warmup: int = 3, pool=None, prologue=None):
         self.step_fn = step_fn
+        self.prologue = prologue  # recorded before the steps (e.g. a device-counter batch gather into the slots)
         self.batches = [tuple(b) for b in batches]
         self.graph = None
         self.outputs = None
@@ -104,6 +105,8 @@ class CapturedSteps:
         g = torch.cuda.CUDAGraph()
         with OF.recompute_weight_copies():
             with torch.cuda.graph(g, pool=self._pool):
+                if self.prologue is not None:
+                    self.prologue()
                 self.outputs = [self.step_fn(*b) for b in self.batches]
         torch.cuda.synchronize()
         upload(g)
