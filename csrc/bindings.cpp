@@ -1195,7 +1195,8 @@ void mlp_train(const Tensor& x, const Tensor& y, const std::vector<Tensor>& w, c
                const std::vector<Tensor>& wbf, const std::vector<Tensor>& wtbf, const std::vector<Tensor>& act,
                const std::vector<Tensor>& actT, const std::vector<Tensor>& d, const std::vector<Tensor>& dT,
                Tensor& dlog, Tensor& dlogT, Tensor& loss_part, Tensor& loss, const Tensor& hp, Tensor& step, int mode,
-               Tensor& bar, Tensor& err, int grid, const optional<Tensor>& stamps) {
+               Tensor& bar, Tensor& err, int grid, const optional<Tensor>& stamps,
+               const optional<std::vector<int64_t>>& xgmi_view, double xscale) {
   const int nl = static_cast<int>(w.size());
   TORCH_CHECK(nl >= 1 && nl <= pde::kMlpMaxLayers, "mlp_train: 1..8 layers");
   for (const auto* v : {&b, &gw, &gb, &mw, &vw, &mb, &vb, &wbf, &wtbf, &act, &actT, &d, &dT})
@@ -1288,6 +1289,34 @@ void mlp_train(const Tensor& x, const Tensor& y, const std::vector<Tensor>& w, c
     TORCH_CHECK(stamps->is_cuda() && stamps->scalar_type() == at::kLong && stamps->numel() >= 128, "mlp_train: stamps int64[128]");
     a.stamps = reinterpret_cast<long long*>(stamps->data_ptr());
   }
+  a.xchg = 0;
+  a.xscale = 1.f;
+  if (xgmi_view.has_value()) {  // XgmiAllreduce.view(): the in-launch gradient exchange (world > 1, one node)
+    const auto& v = *xgmi_view;
+    TORCH_CHECK(v.size() == pde::kXgmiMaxRanks + 9, "mlp_train: malformed xgmi view");
+    for (int r = 0; r < pde::kXgmiMaxRanks; ++r) a.xv.base[r] = reinterpret_cast<char*>(v[r]);
+    a.xv.state = reinterpret_cast<uint32_t*>(v[8]);
+    a.xv.timeout_ticks = static_cast<uint64_t>(v[9]);
+    a.xv.flag_bytes = v[10];
+    a.xv.slot_bytes = v[11];
+    a.xv.rank = static_cast<int>(v[12]);
+    a.xv.size = static_cast<int>(v[13]);
+    a.xv.blocks = static_cast<int>(v[14]);
+    a.xv.read_delay_ticks = static_cast<uint64_t>(v[15]);
+    a.xv.host = reinterpret_cast<uint32_t*>(v[16]);
+    a.xchg = 1;
+    a.xscale = static_cast<float>(xscale);
+    int ins[pde::kMlpMaxLayers], outs[pde::kMlpMaxLayers];
+    for (int l = 0; l < nl; ++l) {
+      ins[l] = a.L[l].in; outs[l] = a.L[l].out;
+      a.xoff[l] = pde::mlp_xchg_floats(ins, outs, l);  // the tiles of layers 0 .. l-1 come first
+    }
+    TORCH_CHECK(pde::mlp_xchg_floats(ins, outs, nl) * 4 <= a.xv.slot_bytes,
+                "mlp_train: the xGMI instance's slot is smaller than the exchanged gradient tiles (",
+                pde::mlp_xchg_floats(ins, outs, nl) * 4, " B)");
+    TORCH_CHECK(a.xv.blocks >= grid, "mlp_train: the xGMI instance needs >= ", grid, " flag blocks");
+    TORCH_CHECK(mode != 0 && (a.flags & 2) == 0, "mlp_train: the exchange needs the fused Adam / AdamW form");
+  }
   check(pde::mlp_train_step(a, grid, cur_stream()), "mlp_train");
 }
 
@@ -1318,7 +1347,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mw"), py::arg("vw"), py::arg("mb"), py::arg("vb"), py::arg("wbf"), py::arg("wtbf"), py::arg("act"),
         py::arg("actT"), py::arg("d"), py::arg("dT"), py::arg("dlog"), py::arg("dlogT"), py::arg("loss_part"),
         py::arg("loss"), py::arg("hp"), py::arg("step"), py::arg("mode"), py::arg("bar"), py::arg("err"),
-        py::arg("grid"), py::arg("stamps") = py::none());
+        py::arg("grid"), py::arg("stamps") = py::none(), py::arg("xgmi_view") = py::none(),
+        py::arg("xscale") = 1.0);
   m.def("cnn_sgd", &cnn_sgd, py::arg("params"), py::arg("grads"), py::arg("hp"), py::arg("frag"),
         py::arg("step") = py::none());
   m.def("clear_last_error", []() { return static_cast<int>(hipGetLastError()); },

@@ -6,6 +6,8 @@
 
 #include <cstdint>
 
+#include "xgmi_view.h"
+
 namespace pde {
 
 // Whole MLP training step in ONE persistent launch (mlp_fused.hip): forward, mean softmax cross-entropy, backward
@@ -40,7 +42,22 @@ struct MlpTrainArgs {
   long long* stamps;  // optional [128]: workgroup 0's / the latest workgroup's wall clock at each phase boundary
   int flags;          // bit 0: load the update state after the weight-gradient tiles, not with them (PDE_MLP_PRELOAD=0)
                       // bit 1: no fused wgrad + update (PDE_MLP_FUSE=0)
+  // world > 1 (one node): every 64x64 weight-gradient tile (+ its bias slice) is exchanged over xGMI INSIDE the
+  // launch, between its weight-gradient GEMM and its update -- staged into this rank's slot of `xv` at the tile's
+  // offset (kMlpXchgTile floats per tile, layers in order), one flag per (workgroup, exchange), summed over all
+  // ranks in rank order and scaled by xscale (1 / world: DDP's average).  xchg == 0: no exchange.
+  XgmiView xv;
+  float xscale;
+  int xchg;
+  long xoff[kMlpMaxLayers];  // first float of layer l's tiles in the exchange slot (host-computed)
 };
+constexpr int kMlpXchgTile = 64 * 64 + 64;
+// floats of the exchange slot the layers' tiles need (the XgmiAllreduce instance's max_bytes must cover 4x this)
+inline long mlp_xchg_floats(const int* in, const int* out, int nl) {
+  long n = 0;
+  for (int l = 0; l < nl; ++l) n += static_cast<long>((out[l] + 63) / 64) * ((in[l] + 63) / 64) * kMlpXchgTile;
+  return n;
+}
 int mlp_train_grid(int device);  // workgroups of the persistent launch (one per CU), 0 if it cannot be resident
 hipError_t mlp_train_step(const MlpTrainArgs& a, int grid, hipStream_t s);
 

@@ -42,6 +42,7 @@
 #include "mlp_train.h"
 #include "optim_device.h"
 #include "pde_kernels.h"
+#include "xgmi_device.h"
 
 namespace pde {
 
@@ -383,7 +384,7 @@ __device__ __forceinline__ void wt_flush(const MlpLayerArgs& L, int o0, int i0, 
 // Each phase function runs this workgroup's tiles; the FIRST tile's weight fragments were prefetched into `R` by
 // the caller (ahead of the barrier), later tiles (more tiles than workgroups) load their own.
 template <bool AF32>
-__device__ void fwd_phase(const MlpTrainArgs& a, int l, RowLoads& R, Smem& sm) {
+__device__ __forceinline__ void fwd_phase(const MlpTrainArgs& a, int l, RowLoads& R, Smem& sm) {
   const MlpLayerArgs& L = a.L[l];
   const int B = a.B, mt = B / 32, nt = (L.out + 15) / 16, lane = threadIdx.x & 63;
   const void* A = AF32 ? static_cast<const void*>(a.x) : static_cast<const void*>(a.act[l]);
@@ -436,7 +437,7 @@ __device__ __forceinline__ void ce_loads_w(const MlpTrainArgs& a, RowLoads& R, i
 // Last layer (out <= 16) + mean softmax cross-entropy: d logits (both layouts, 16 columns) and one loss partial
 // per 32-row tile.
 template <bool AF32>
-__device__ void ce_phase(const MlpTrainArgs& a, RowLoads& R, Smem& sm) {
+__device__ __forceinline__ void ce_phase(const MlpTrainArgs& a, RowLoads& R, Smem& sm) {
   const int l = a.nl - 1;
   const MlpLayerArgs& L = a.L[l];
   const int B = a.B, mt = B / 32, lane = threadIdx.x & 63;
@@ -629,9 +630,57 @@ struct Park {
   int l, o0, i0;
 };
 
-template <int MODE>
+// In-launch gradient exchange of this workgroup's tile of layer j (world > 1, fused form), on the tile the
+// weight-gradient GEMM left in LDS (sm.gt / sm.gb, read back below in the update layout by the SAME threads, so no
+// extra barrier): stage it (write-through) into my slot at the tile's offset, raise flag value (epoch x nl + exchange
+// index + 1) in every rank's flag array, wait for every rank's, then sum the N ranks' tiles in rank order
+// (bit-identical on every rank), scale by xscale and write the average back to LDS and to gw / gb (DDP's averaged
+// .grad).  Few values are live here (the tile stays in LDS), so the exchange adds no spills to the update's state.
+// A timed-out wait leaves the local gradient (the error words are set; the host raises at its check).
+// Block-collective.
+__device__ __forceinline__ void xchg_tile(const MlpTrainArgs& a, const XgmiView& xv, int j, int t, uint32_t epoch,
+                                          int* s_fail, Smem& sm, int o0, int i0) {
+  const long off = a.xoff[j] + static_cast<long>(t) * kMlpXchgTile;
+  const int tc = threadIdx.x & 15, tr0 = threadIdx.x >> 4;
+  const bool bias = i0 == 0 && threadIdx.x < 64;
+  float* mine = xgmi_slot(xv, xv.rank, epoch) + off;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    st_vec(reinterpret_cast<f32x4*>(mine + (tr0 + 16 * q) * 64 + 4 * tc),
+           *reinterpret_cast<const f32x4*>(&sm.gt[tr0 + 16 * q][4 * tc]), true);
+  if (bias) mine[4096 + threadIdx.x] = sm.gb[threadIdx.x];
+  const uint32_t k = static_cast<uint32_t>(a.nl - 1 - j);
+  // every kernel argument the code below needs is read BEFORE the flag wait: behind its asm memory clobbers a read of
+  // the argument block would make the compiler keep a private copy of the whole block (1.7 KB of scratch per lane)
+  const float xscale = a.xscale;
+  float* const gw = a.L[j].gw;
+  float* const gbp = a.L[j].gb;
+  const int lin = a.L[j].in, lout = a.L[j].out;
+  const uint32_t flag = epoch * static_cast<uint32_t>(a.nl) + k + 1u;
+  if (!xgmi_publish_and_wait(xv, blockIdx.x, flag, s_fail)) return;
+  const int i = i0 + 4 * tc;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = (tr0 + 16 * q) * 64 + 4 * tc;
+    f32x4 acc = *reinterpret_cast<const f32x4*>(xgmi_slot(xv, 0, epoch) + off + row);
+    for (int r = 1; r < xv.size; ++r) acc += *reinterpret_cast<const f32x4*>(xgmi_slot(xv, r, epoch) + off + row);
+    acc *= xscale;
+    *reinterpret_cast<f32x4*>(&sm.gt[tr0 + 16 * q][4 * tc]) = acc;
+    const int o = o0 + tr0 + 16 * q;
+    if (o < lout && i < lin) *reinterpret_cast<f32x4*>(gw + static_cast<long>(o) * lin + i) = acc;
+  }
+  if (bias) {
+    float b = xgmi_slot(xv, 0, epoch)[off + 4096 + threadIdx.x];
+    for (int r = 1; r < xv.size; ++r) b += xgmi_slot(xv, r, epoch)[off + 4096 + threadIdx.x];
+    b *= xscale;
+    sm.gb[threadIdx.x] = b;
+    if (o0 + static_cast<int>(threadIdx.x) < lout) gbp[o0 + threadIdx.x] = b;
+  }
+}
+
+template <int MODE, bool XCHG>
 __device__ __forceinline__ void bwd_fused(const MlpTrainArgs& a, int j, const optdev::Hyper& h, bool use_m, Smem& sm, Park& pk,
-                          bool park) {
+                          bool park, uint32_t xepoch, int* s_fail, const XgmiView* xv) {
   const MlpLayerArgs& L = a.L[j];
   const bool last = j == a.nl - 1;
   const int B = a.B, t = blockIdx.x;
@@ -655,6 +704,7 @@ __device__ __forceinline__ void bwd_fused(const MlpTrainArgs& a, int j, const op
   wgrad_tile(L, Wg, rg, ra, B, o0, i0, &sm);
   lds_sync();
   const int tc = threadIdx.x & 15, tr0 = threadIdx.x >> 4;
+  if constexpr (XCHG) xchg_tile(a, *xv, j, t, xepoch, s_fail, sm, o0, i0);
 #pragma unroll
   for (int q = 0; q < 4; ++q) U.g[q] = *reinterpret_cast<const f32x4*>(&sm.gt[tr0 + 16 * q][4 * tc]);
   if (i0 == 0 && threadIdx.x < 64) U.bg = sm.gb[threadIdx.x];
@@ -705,13 +755,38 @@ __device__ __forceinline__ void write_xT(const MlpTrainArgs& a) {
   }
 }
 
-template <int MODE>
+template <int MODE, bool XCHG>
 __global__ __launch_bounds__(MT) void k_mlp_train(MlpTrainArgs a) {
   __shared__ Smem sm;
   __shared__ int s_step;
   __shared__ unsigned s_launch;
+  __shared__ uint32_t s_xepoch;
+  __shared__ int s_xfail;
+  // the peer view in LDS: its per-lane indexed arrays (base[rank]) must not be indexed in the kernel-argument block
+  // (a divergent index there makes the compiler copy the whole argument block to scratch)
+  __shared__ XgmiView s_xv;
   int ks = 0, kb = 0;
   stamp(a, ks);
+  // world > 1: this launch's exchange epoch (block-collective; the last workgroup to finish advances it)
+  uint32_t xepoch = 0u;
+  if constexpr (XCHG) {
+    if (threadIdx.x == 0) {  // field by field (a struct copy out of the argument block is a memcpy that keeps a
+                             // private copy of the whole block alive)
+#pragma unroll
+      for (int r = 0; r < kXgmiMaxRanks; ++r) s_xv.base[r] = a.xv.base[r];
+      s_xv.state = a.xv.state;
+      s_xv.host = a.xv.host;
+      s_xv.timeout_ticks = a.xv.timeout_ticks;
+      s_xv.read_delay_ticks = a.xv.read_delay_ticks;
+      s_xv.flag_bytes = a.xv.flag_bytes;
+      s_xv.slot_bytes = a.xv.slot_bytes;
+      s_xv.rank = a.xv.rank;
+      s_xv.size = a.xv.size;
+      s_xv.blocks = a.xv.blocks;
+    }
+    __syncthreads();
+    xepoch = xgmi_epoch(s_xv, blockIdx.x, &s_xepoch);
+  }
   if (threadIdx.x == 0) {
     s_step = __hip_atomic_load(a.step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
     s_launch = __hip_atomic_load(a.bar + kBarStride * (kBarGroups + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -775,13 +850,13 @@ __global__ __launch_bounds__(MT) void k_mlp_train(MlpTrainArgs a) {
       bwd_phase(a, j, 0, R, sm, U, false, a.L[j], use_m, MODE != 0);
       stamp(a, ks);
       grid_arrive(bar, kb);
-      bwd_fused<MODE>(a, j, h, use_m, sm, pk, true);
+      bwd_fused<MODE, XCHG>(a, j, h, use_m, sm, pk, true, xepoch, &s_xfail, &s_xv);
       dgrad_prefetch(a, j - 1, R);
       stamp(a, ks);
       grid_wait(bar, a.err, kb++);
       stamp(a, ks);
     }
-    bwd_fused<MODE>(a, 0, h, use_m, sm, pk, false);
+    bwd_fused<MODE, XCHG>(a, 0, h, use_m, sm, pk, false, xepoch, &s_xfail, &s_xv);
     stamp(a, ks);  // (an empty phase: the boundary count of the unfused form)
   } else {
     // B(nl-1) .. B1: the dgrad tiles (the hand-off), then -- between arrive and wait -- the weight-gradient tiles of
@@ -814,6 +889,7 @@ __global__ __launch_bounds__(MT) void k_mlp_train(MlpTrainArgs a) {
     update_layer<MODE>(a, 0, h, use_m, sm, U, false);
   }
   stamp(a, ks);
+  if constexpr (XCHG) xgmi_finish(s_xv, blockIdx.x, xepoch);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     float s = 0.f;
     for (int t = 0; t < B / 32; ++t) s += __hip_atomic_load(a.loss_part + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -830,7 +906,7 @@ int mlp_train_grid(int device) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) return 0;
   int per = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_mlp_train<1>), MT, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_mlp_train<1, false>), MT, 0) !=
           hipSuccess ||
       per < 1)
     return 0;
@@ -839,10 +915,26 @@ int mlp_train_grid(int device) {
 
 hipError_t mlp_train_step(const MlpTrainArgs& a, int grid, hipStream_t s) {
   if (grid <= 0 || a.nl < 1 || a.nl > kMlpMaxLayers || a.B % 32 != 0) return hipErrorInvalidValue;
+  if (a.xchg) {  // the exchange rides on the fused form only, with one flag word per workgroup of the view
+    if (a.mode == 0 || (a.flags & 2) != 0 || a.xv.blocks < grid) return hipErrorInvalidValue;
+    for (int l = 0; l < a.nl; ++l)
+      if (((a.L[l].out + 63) / 64) * ((a.L[l].in + 63) / 64) > grid) return hipErrorInvalidValue;
+    int in[kMlpMaxLayers], out[kMlpMaxLayers];
+    for (int l = 0; l < a.nl; ++l) { in[l] = a.L[l].in; out[l] = a.L[l].out; }
+    if (mlp_xchg_floats(in, out, a.nl) * 4 > a.xv.slot_bytes) return hipErrorInvalidValue;
+  }
+  if (a.xchg) {
+    switch (a.mode) {
+      case 1: hipLaunchKernelGGL((k_mlp_train<1, true>), dim3(grid), dim3(MT), 0, s, a); break;
+      case 2: hipLaunchKernelGGL((k_mlp_train<2, true>), dim3(grid), dim3(MT), 0, s, a); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (a.mode) {
-    case 0: hipLaunchKernelGGL(k_mlp_train<0>, dim3(grid), dim3(MT), 0, s, a); break;
-    case 1: hipLaunchKernelGGL(k_mlp_train<1>, dim3(grid), dim3(MT), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(k_mlp_train<2>, dim3(grid), dim3(MT), 0, s, a); break;
+    case 0: hipLaunchKernelGGL((k_mlp_train<0, false>), dim3(grid), dim3(MT), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((k_mlp_train<1, false>), dim3(grid), dim3(MT), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((k_mlp_train<2, false>), dim3(grid), dim3(MT), 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

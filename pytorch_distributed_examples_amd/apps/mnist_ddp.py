@@ -67,6 +67,12 @@ def load_train_objs(model_name: str, device, train_size: int, test_size: int):
     return train_set, test_set, model, make_opt, loss
 
 
+def _native_grid() -> int:
+    from .. import _native
+
+    return _native.C().mlp_train_grid()
+
+
 class Trainer:
     def __init__(self, ctx, model, train_data, test_data, make_opt, criterion, save_every, snapshot_path,
                  log, metrics=None, save_optimizer=True, fused=False, ddp_kwargs=None, fast=None, graph_chunk=50):
@@ -110,12 +116,18 @@ class Trainer:
 
             self.fmlp = FusedMLP(self.model)
             self.ddp = DistributedDataParallel(self.model, overlap=False, comm=data_plane(ctx), **(ddp_kwargs or {}))
-            if (self.ddp.world == 1 and train_data.batch_size % 32 == 0 and
-                    os.environ.get("PDE_MLP_MEGA", "1") != "0"):
+            # one launch per step at any world size on one node: at world > 1 the gradient average runs inside the
+            # launch over xGMI (MegaMLP.exchange) -- every rank must own its GPU (the persistent grid fills it)
+            world = self.ddp.world
+            own_gpu = torch.cuda.device_count() >= int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+            single_node = int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world
+            if (train_data.batch_size % 32 == 0 and os.environ.get("PDE_MLP_MEGA", "1") != "0" and
+                    (world == 1 or (own_gpu and single_node and getattr(self.optimizer, "KIND", "") != "sgd"))):
                 from ..models.mlp_mega import MegaMLP
 
-                mega = MegaMLP(self.model, self.optimizer)
-                self.mega = mega if mega.grid() > 0 else None
+                if int(_native_grid()) > 0:
+                    xa = MegaMLP.exchange(self.model, ctx.device) if world > 1 else None
+                    self.mega = MegaMLP(self.model, self.optimizer, xgmi=xa)
         else:
             self.ddp = DistributedDataParallel(self.model, **(ddp_kwargs or {}))
         if (self.fused is not None or self.fmlp is not None) and hasattr(train_data.dataset, "images") and \
@@ -149,6 +161,7 @@ class Trainer:
         """The short last batch (eager): the one-launch MLP step needs a multiple of 32 rows."""
         if self.mega is not None and source.shape[0] % 32:
             loss = self.fmlp_for_tail().forward_backward(source, targets)
+            self.ddp.sync_gradients()
             self.optimizer.step()
             return loss
         return self._gpu_step(source, targets)

@@ -99,7 +99,8 @@ def worker(args) -> None:
         if rank == 0:
             rec = dict(event="round", round=rnd, world=size, **{k: (round(v, 4) if isinstance(v, float) else v)
                                                                 for k, v in info.items()})
-            print(json.dumps(rec), flush=True)
+            sys.stdout.write(json.dumps(rec) + "\n")  # ONE write: other ranks' log lines never split the record
+            sys.stdout.flush()
             with open(args.report, "a") as f:
                 f.write(json.dumps(rec) + "\n")
             if size != n_target and not requested[0] and not fault_mode:  # the discovery script reads this file

@@ -1,11 +1,19 @@
 """The elastic-DDP MLP's whole training step as ONE persistent kernel launch (csrc/kernels/mlp_fused.hip).
 
 Reference: pytorch_elastic/mnist_ddp_elastic.py:133-173 (``Model``: Linear + ReLU stack, ``CrossEntropyLoss``,
-``optimizer.step()``); model of :mod:`.mlp`.  Single process (world 1: no gradient all-reduce sits between the
-backward and the update):
+``optimizer.step()``); model of :mod:`.mlp`:
 
     mega = MegaMLP(model, opt)        # opt: FusedAdam / FusedAdamW / FusedSGD over model.parameters() (one group)
     loss = mega.step(x, y)            # forward + cross-entropy + backward + optimiser update: 1 launch
+
+    mega = MegaMLP(model, opt, xgmi=MegaMLP.exchange(model, device))   # world > 1 on one node (collective)
+    loss = mega.step(x, y)            # ... with DDP's gradient average INSIDE the same launch
+
+World > 1 (single node): every 64x64 weight-gradient tile is exchanged with the other ranks over xGMI between its
+GEMM and its update, inside the launch (csrc/kernels/mlp_fused.hip ``xchg_tile``: staged into this rank's IPC slot,
+one flag per workgroup and exchange, summed over the ranks in rank order, x 1/world) -- the gradients of layer j
+cross the links while layer j-1's backward runs, and the step stays ONE launch at any world size.  Adam / AdamW
+(the fused update form) only.
 
 Forward, loss, backward and the update of every layer run phase after phase inside one grid of one workgroup per
 CU (grid barriers between phases), each phase one global round trip.  The results are those of the layer-by-layer
@@ -36,7 +44,18 @@ class DeviceBarrierError(RuntimeError):
 
 
 class MegaMLP:
-    def __init__(self, net, opt, check_every: int = 64):
+    @staticmethod
+    def exchange(net, device, group=None, timeout_s: float | None = None):
+        """The xGMI instance the in-launch exchange of ``net``'s gradient tiles needs (collective over ``group``)."""
+        from ..parallel.xgmi_allreduce import XgmiAllreduce
+
+        layers = [net.input_layer, *net.hidden_layers, net.final_layer]
+        floats = sum(-(-L.out_features // 64) * -(-L.in_features // 64) * (64 * 64 + 64) for L in layers)
+        grid = int(_native.C().mlp_train_grid())
+        return XgmiAllreduce(device, group=group, max_bytes=floats * 4 + (1 << 20), blocks=max(grid, 1),
+                             timeout_s=timeout_s, key=None)
+
+    def __init__(self, net, opt, check_every: int = 64, xgmi=None):
         self.net, self.opt = net, opt
         self.layers = [net.input_layer, *net.hidden_layers, net.final_layer]
         for i, L in enumerate(self.layers):
@@ -50,6 +69,9 @@ class MegaMLP:
         self._grid = None
         self.calls = 0
         self.check_every = int(check_every)
+        self.xgmi = xgmi  # parallel.xgmi_allreduce.XgmiAllreduce: the in-launch gradient exchange (world > 1)
+        if xgmi is not None and self.mode == 0:
+            raise ValueError("MegaMLP: the in-launch gradient exchange needs Adam / AdamW (the fused update form)")
         self.stamps = None  # set to a zeroed int64[128] GPU tensor: phase-boundary clocks (100 MHz), see phase_us
 
     def _buffers(self, B: int, dev: torch.device):
@@ -118,7 +140,9 @@ class MegaMLP:
                     [st_of(L.bias, mkey) for L in self.layers], [st_of(L.bias, "exp_avg_sq") for L in self.layers],
                     wbf, wtbf, bufs["act"], bufs["actT"], bufs["d"], bufs["dT"], bufs["dlog"], bufs["dlogT"],
                     bufs["loss_part"], loss, st["hp"], st["step"], self.mode, bufs["bar"], bufs["err"], self.grid(),
-                    self.stamps)
+                    self.stamps,
+                    self.xgmi.view() if self.xgmi is not None else None,
+                    1.0 / self.xgmi.size if self.xgmi is not None else 1.0)
         # the weights changed on the device: the in-place writes bypass the version counters, so stamp the
         # copies current (they were refreshed by the same kernel) and invalidate generation-keyed caches
         for L in self.layers:
@@ -163,7 +187,10 @@ class MegaMLP:
         return all(-(-L.out_features // 64) * -(-L.in_features // 64) <= g for L in self.layers)
 
     def check(self, where: str = "") -> None:
-        """Raise :class:`DeviceBarrierError` if a grid barrier timed out since the last check (synchronises)."""
+        """Raise :class:`DeviceBarrierError` if a grid barrier timed out since the last check (synchronises), and
+        RuntimeError if an in-launch exchange timed out waiting for a peer."""
+        if self.xgmi is not None:
+            self.xgmi.check()
         n = self.errors()
         if n:
             raise DeviceBarrierError(f"MegaMLP: {n} grid-barrier timeout(s){' at ' + where if where else ''}: a "

@@ -10,6 +10,11 @@ FIELDS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
           "scaling", "vs_baseline", "dtype", "data", "config"}
 
 
+
+def _rec(line):
+    """The JSON record at the start of a line (another rank's log text may follow it on the same line)."""
+    return json.JSONDecoder().raw_decode(line)[0]
+
 def _parse(out):
     lines = [ln for ln in out.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out
@@ -88,8 +93,8 @@ def test_bench_elastic_scale_up_cpu():
                        "--scale-to", "4", "--device", "cpu", "--batch", "32", "--steps", "4", "--warmup", "2",
                        "--graph-steps", "2"], timeout=600)
     assert rc == 0, out
-    rounds = [json.loads(ln) for ln in out.splitlines() if ln.startswith('{"event": "round"')]
-    final = [json.loads(ln) for ln in out.splitlines() if ln.startswith('{"metric"')]
+    rounds = [_rec(ln) for ln in out.splitlines() if ln.startswith('{"event": "round"')]
+    final = [_rec(ln) for ln in out.splitlines() if ln.startswith('{"metric"')]
     assert len(final) == 1 and FIELDS <= set(final[0]), out
     rec = final[0]
     assert [r["world"] for r in rounds] == [2, 4] and rec["n_gpus"] == 4, out
@@ -113,8 +118,8 @@ def test_bench_elastic_survives_killed_worker_cpu():
                        "--scale-to", "1", "--fault-at", "20", "--device", "cpu", "--batch", "32", "--steps", "4",
                        "--warmup", "2", "--graph-steps", "2"], timeout=600)
     assert rc == 0, out[-4000:]
-    rounds = [json.loads(ln) for ln in out.splitlines() if ln.startswith('{"event": "round"')]
-    final = [json.loads(ln) for ln in out.splitlines() if ln.startswith('{"metric"')]
+    rounds = [_rec(ln) for ln in out.splitlines() if ln.startswith('{"event": "round"')]
+    final = [_rec(ln) for ln in out.splitlines() if ln.startswith('{"metric"')]
     assert "[fault-injector] rank 1 step 20" in out and "peer failure" in out, out[-4000:]
     assert [r["world"] for r in rounds] == [2, 1] and len(final) == 1, out[-4000:]
     assert rounds[1]["rewire_s"] > 0 and set(rounds[1]["rewire_parts"]) == {

@@ -16,13 +16,18 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+
+def _rec(line):
+    """The JSON record at the start of a line (another rank's log text may follow it on the same line)."""
+    return json.JSONDecoder().raw_decode(line)[0]
+
 def test_elastic_bench_scale_up_one_gpu(gpu):
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--model", "elastic_cnn", "--gpus", "1", "--scale-to", "2",
            "--steps", "100", "--warmup", "20", "--graph-steps", "10"]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert res.returncode == 0, (res.stdout[-3000:], res.stderr[-3000:])
-    rounds = [json.loads(ln) for ln in res.stdout.splitlines() if ln.startswith('{"event": "round"')]
-    final = [json.loads(ln) for ln in res.stdout.splitlines() if ln.startswith('{"metric"')]
+    rounds = [_rec(ln) for ln in res.stdout.splitlines() if ln.startswith('{"event": "round"')]
+    final = [_rec(ln) for ln in res.stdout.splitlines() if ln.startswith('{"metric"')]
     assert [r["world"] for r in rounds] == [1, 2] and len(final) == 1, res.stdout[-3000:]
     assert rounds[1]["rewire_s"] is not None and rounds[1]["rewire_s"] > 0
     assert all(r["images_per_s"] > 1e6 for r in rounds), rounds  # fused path (millions of images/s)
@@ -42,8 +47,8 @@ def test_elastic_bench_survives_killed_worker_one_gpu(gpu):
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert res.returncode == 0, (res.stdout[-3000:], res.stderr[-3000:])
     out = res.stdout + res.stderr
-    rounds = [json.loads(ln) for ln in res.stdout.splitlines() if ln.startswith('{"event": "round"')]
-    final = [json.loads(ln) for ln in res.stdout.splitlines() if ln.startswith('{"metric"')]
+    rounds = [_rec(ln) for ln in res.stdout.splitlines() if ln.startswith('{"event": "round"')]
+    final = [_rec(ln) for ln in res.stdout.splitlines() if ln.startswith('{"metric"')]
     assert "[fault-injector] rank 1 step 300" in out and "peer failure" in out, out[-3000:]
     assert [r["world"] for r in rounds] == [2, 1] and len(final) == 1, out[-3000:]
     assert rounds[1]["rewire_s"] is not None and rounds[1]["rewire_s"] > 0
