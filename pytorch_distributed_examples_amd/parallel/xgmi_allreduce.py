@@ -211,6 +211,7 @@ def xgmi_only_comm(device: torch.device, group=None, max_bytes: int = 64 << 20, 
     # process loads its code objects at once), so the default here is generous (PDE_XGMI_TIMEOUT_S overrides)
     t = float(os.environ.get("PDE_XGMI_TIMEOUT_S", "60"))
     small = XgmiAllreduce(device, group=group, key=None if key is None else key + "/1", timeout_s=t)
-    big = XgmiAllreduce(device, group=group, max_bytes=max_bytes, blocks=256, two_shot=True,
+    blocks = int(os.environ.get("PDE_XGMI2_BLOCKS", "256"))  # two-shot workgroups (fewer: fewer spinning waves)
+    big = XgmiAllreduce(device, group=group, max_bytes=max_bytes, blocks=blocks, two_shot=True,
                         key=None if key is None else key + "/2", timeout_s=t)
     return RoutedComm(None, small, xgmi2=big)
