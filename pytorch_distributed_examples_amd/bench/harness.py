@@ -442,6 +442,9 @@ def build_hvd_cnn(args, ctx, batch) -> Workload:
         fused = FusedCNN(model)
         grads = fused.grad_buffer()  # p.grad = views of one flat buffer: the engine reduces it in place
         fused.always_prep = elastic  # AdamW updates the weights: fragments rebuilt in-kernel every step
+        if elastic:  # ... so the optimiser need not keep the layer path's bf16 layouts (hvd/cnn_step.py)
+            for p in model.parameters():
+                p.__dict__["_pde_own_copies"] = True
     inner = (FusedAdamW(model.parameters(), lr=0.01 / math.sqrt(hvd.size())) if elastic
              else FusedSGD(model.parameters(), lr=0.01))
     opt = hvd.DistributedOptimizer(inner, named_parameters=model.named_parameters())

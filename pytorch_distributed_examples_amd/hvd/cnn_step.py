@@ -36,6 +36,14 @@ class FusedHvdStep:
         self.sgd_fast = (isinstance(optimizer, FusedSGD) and g is not None and g.get("momentum", 0.0) == 0.0
                          and g.get("weight_decay", 0.0) == 0.0)
         self.fused.always_prep = not self.sgd_fast
+        if not self.sgd_fast:
+            from ..ops import functional as OF
+
+            # the kernel rebuilds its fragment image from the fp32 weights every step: the optimiser need not keep
+            # the layer path's bf16 conv / linear layouts current (an eager model(x) falls back to cached copies)
+            for p in model.parameters():
+                p.__dict__["_pde_own_copies"] = True
+                OF.release_compute_copies(p)
         self.grads = self.fused.grad_buffer()  # p.grad: views of one flat buffer (never set to None)
         self.use_graph = graph
         self.graph = None

@@ -229,8 +229,10 @@ def maintain_compute_copies(p: torch.Tensor):
     multi-tensor launch after the update (``conv_layouts_step``) instead of two conversion kernels per
     conv and step.  Returns the copy dict (or None).  The copies are tied to the weight's version counter:
     an in-place write outside the optimizer (load_state_dict, a broadcast, an elastic restore) is detected
-    by :func:`_maintained` and the copies are re-derived in place."""
-    if not p.is_cuda or p.dtype != torch.float32:
+    by :func:`_maintained` and the copies are re-derived in place.  A parameter marked ``_pde_own_copies`` (its
+    consumer keeps its own operand image, e.g. the fused CNN's bf16 fragment image rebuilt in-kernel) gets none:
+    the optimiser then skips their refresh (the 14 us conv-layout launch of the Horovod-elastic AdamW step)."""
+    if not p.is_cuda or p.dtype != torch.float32 or p.__dict__.get("_pde_own_copies", False):
         return None
     d = {}
     if getattr(p, "_pde_conv", False) and p.dim() == 4:
