@@ -245,6 +245,44 @@ class ResNetPipelineDP:
         self.engine.timer = NO_PHASES
         return loss if loss is not None else self._zero
 
+    def split_step_graphs(self):
+        """Ranks sharing ONE GPU (the config-4 rehearsal): the step as TWO hipGraphs -- the pipelined micro-batch
+        forwards / backwards with their ring sends / receives, then the DP all-reduce + SGD -- with a device sync and
+        a host barrier between them.  On a shared card a grid spinning on its DP peer starves the other pipeline's
+        kernels (profiles/r6f), so no rank may start its DP exchange while another still computes; on a node (one
+        GPU per rank) the step is ONE graph (``step``).  Runs ONE eager warm-up step in the same split form (ring
+        meta handshake, lazy initialisation), then captures.  Returns a callable."""
+        from ..utils.graph import CapturedStep
+
+        def pipeline_part():
+            self.ddp.zero_grad()
+            loss = self.engine.train_step(self.xs if self.stage == 0 else None, self.ys if self.last else None,
+                                          self.n_mb)
+            return loss if loss is not None else self._zero
+
+        def dp_part():
+            self.ddp.sync_gradients()
+            self.opt.step()
+            return self._zero
+
+        pipeline_part()  # the eager warm-up step, split the same way
+        torch.cuda.synchronize()
+        dist.barrier()
+        dp_part()
+        torch.cuda.synchronize()
+        dist.barrier()
+        g1 = CapturedStep(pipeline_part, [], warmup=0).capture()
+        g2 = CapturedStep(dp_part, [], warmup=0).capture()
+
+        def step():
+            loss = g1()
+            torch.cuda.synchronize()
+            dist.barrier()
+            g2()
+            return loss
+
+        return step
+
     def close(self):
         self.engine.close()
         if self.comm is not None:

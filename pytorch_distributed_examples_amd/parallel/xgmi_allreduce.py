@@ -210,11 +210,12 @@ def xgmi_only_comm(device: torch.device, group=None, max_bytes: int = 64 << 20, 
     # the peer-wait bound: ranks sharing one GPU (the rehearsal) start far apart on their first step (every
     # process loads its code objects at once), so the default here is generous (PDE_XGMI_TIMEOUT_S overrides)
     t = float(os.environ.get("PDE_XGMI_TIMEOUT_S", "60"))
-    small = XgmiAllreduce(device, group=group, key=None if key is None else key + "/1", timeout_s=t)
+    shared = torch.cuda.device_count() < int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    small = XgmiAllreduce(device, group=group, key=None if key is None else key + "/1", timeout_s=t,
+                          blocks=8 if shared else 256)
     # two-shot workgroups.  Ranks sharing ONE GPU (the rehearsal): a few -- a 256-workgroup grid spinning on its
     # DP peer starves the other processes' kernels on the card (profiles/r6f: the other pipeline made no progress
     # until the wait timed out; 8 or 1 workgroups: every step and graph replay completes).  A node: 256.
-    shared = torch.cuda.device_count() < int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
     blocks = int(os.environ.get("PDE_XGMI2_BLOCKS", "8" if shared else "256"))
     big = XgmiAllreduce(device, group=group, max_bytes=max_bytes, blocks=blocks, two_shot=True,
                         key=None if key is None else key + "/2", timeout_s=t)
