@@ -1321,6 +1321,30 @@ void mlp_train(const Tensor& x, const Tensor& y, const std::vector<Tensor>& w, c
 }
 
 // Plain SGD on the flat CNN parameters + fragment-image refresh (after the gradient all-reduce).
+}  // namespace
+namespace pde {
+// (declared here, not in pde_kernels.h: cnn_fused.hip is the only definition, bindings.cpp the only caller)
+hipError_t cnn_adamw_fused(float* params, const float* grads, float* m, float* v, const float* hp, void* frag,
+                           int* step, hipStream_t s);
+}  // namespace pde
+namespace {
+
+// AdamW over the flat CNN parameters + fragment refresh, one launch (FusedCNN.adamw_step)
+void cnn_adamw(Tensor& params, const Tensor& grads, Tensor& m, Tensor& v, const Tensor& hp, Tensor& frag,
+               Tensor& step) {
+  CHECK_IN(params); CHECK_IN(grads); CHECK_IN(m); CHECK_IN(v); CHECK_IN(hp); CHECK_IN(frag);
+  CHECK_F32(params); CHECK_F32(grads); CHECK_F32(m); CHECK_F32(v); CHECK_F32(hp);
+  const long n = pde::cnn_num_params();
+  TORCH_CHECK(params.numel() == n && grads.numel() == n && m.numel() == n && v.numel() == n, "cnn_adamw: sizes");
+  TORCH_CHECK(hp.numel() >= pde::HP_COUNT, "cnn_adamw: hp");
+  TORCH_CHECK(frag.nbytes() >= pde::cnn_frag_bytes(), "cnn_adamw: frag size");
+  TORCH_CHECK(step.is_cuda() && step.scalar_type() == at::kInt && step.numel() >= 2, "cnn_adamw: step int32[2]");
+  check(pde::cnn_adamw_fused(params.data_ptr<float>(), grads.data_ptr<float>(), m.data_ptr<float>(),
+                             v.data_ptr<float>(), hp.data_ptr<float>(), frag.data_ptr(), step.data_ptr<int>(),
+                             cur_stream()),
+        "cnn_adamw");
+}
+
 void cnn_sgd(Tensor& params, const Tensor& grads, const Tensor& hp, Tensor& frag, const optional<Tensor>& step) {
   CHECK_IN(params); CHECK_IN(grads); CHECK_IN(hp); CHECK_IN(frag);
   CHECK_F32(params); CHECK_F32(grads); CHECK_F32(hp);
@@ -1349,6 +1373,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("loss"), py::arg("hp"), py::arg("step"), py::arg("mode"), py::arg("bar"), py::arg("err"),
         py::arg("grid"), py::arg("stamps") = py::none(), py::arg("xgmi_view") = py::none(),
         py::arg("xscale") = 1.0);
+  m.def("cnn_adamw", &cnn_adamw, py::arg("params"), py::arg("grads"), py::arg("m"), py::arg("v"), py::arg("hp"),
+        py::arg("frag"), py::arg("step"));
   m.def("cnn_sgd", &cnn_sgd, py::arg("params"), py::arg("grads"), py::arg("hp"), py::arg("frag"),
         py::arg("step") = py::none());
   m.def("clear_last_error", []() { return static_cast<int>(hipGetLastError()); },

@@ -29,6 +29,7 @@
 #include <type_traits>
 
 #include "common.cuh"
+#include "optim_device.h"
 #include "pde_kernels.h"
 #include "xgmi_device.h"
 
@@ -1463,6 +1464,52 @@ hipError_t cnn_sgd_fused(float* params, const float* grads, const float* hp, voi
   if (reinterpret_cast<uintptr_t>(frag) & 15) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_cnn_sgd, dim3(ceil_div(NPARAM, 256)), dim3(256), 0, s, params, grads, hp,
                      static_cast<uint16_t*>(frag), step);
+  return hipGetLastError();
+}
+
+// AdamW (torch.optim.AdamW: the Horovod-elastic script's optimiser, horovod_mnist_elastic.py:41) on the flat
+// parameters, its exp_avg / exp_avg_sq as flat buffers, with the fragment image refreshed in the same pass -- the
+// multi-tensor update launch and the next step's fragment prep launch become ONE launch.  hp / step: the fused
+// optimiser's device hyper-parameters and {steps taken, arrival counter}, read and advanced exactly as its own
+// update kernel does (optim_device.h run_chunks), so its state_dict and later steps stay consistent.
+__global__ __launch_bounds__(256) void k_cnn_adamw(float* __restrict__ params, const float* __restrict__ grads,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   const float* __restrict__ hp, int* __restrict__ step,
+                                                   uint16_t* __restrict__ frag) {
+  __shared__ int s_step;
+  if (threadIdx.x == 0) s_step = step[0] + 1;
+  __syncthreads();
+  optdev::Hyper h;
+  h.lr = hp[HP_LR]; h.b1 = hp[HP_BETA1]; h.b2 = hp[HP_BETA2]; h.eps = hp[HP_EPS];
+  h.wd = hp[HP_WD]; h.mom = hp[HP_MOMENTUM]; h.gscale = hp[HP_GRAD_SCALE];
+  h.step = s_step;
+  const float bc1 = 1.f - __powf(h.b1, static_cast<float>(h.step));
+  const float bc2 = 1.f - __powf(h.b2, static_cast<float>(h.step));
+  h.step_size = h.lr / bc1;
+  h.inv_sqrt_bc2 = rsqrtf(bc2);
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p < NPARAM) {
+    float w = params[p], mm = m[p], vv = v[p];
+    optdev::update<2>(h, w, grads[p], mm, vv);
+    params[p] = w;
+    m[p] = mm;
+    v[p] = vv;
+    write_frag(frag, p, w);
+  }
+  __syncthreads();  // (every block read the old count before its arrival: the last one publishes)
+  if (threadIdx.x == 0) {
+    const int prev = atomicAdd(step + 1, 1);
+    if (prev == static_cast<int>(gridDim.x) - 1) {
+      step[0] = s_step;
+      step[1] = 0;
+    }
+  }
+}
+
+hipError_t cnn_adamw_fused(float* params, const float* grads, float* m, float* v, const float* hp, void* frag,
+                           int* step, hipStream_t s) {
+  hipLaunchKernelGGL(k_cnn_adamw, dim3(ceil_div(NPARAM, 256)), dim3(256), 0, s, params, grads, m, v, hp, step,
+                     static_cast<uint16_t*>(frag));
   return hipGetLastError();
 }
 

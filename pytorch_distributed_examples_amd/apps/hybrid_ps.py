@@ -174,6 +174,8 @@ class ResNetPipelineDP:
             from ..parallel.rccl import StreamComm
 
             self.comm = StreamComm(dev, group=self.dp_group, side_stream=self.overlap)
+        elif dev.type == "cuda" and self.dp > 1 and dp_comm == "gloo":
+            self.overlap = False  # (diagnostic A/B: the c10d gloo group, host-staged; not capturable)
         elif dev.type == "cuda" and self.dp > 1:
             # the stage gradients over xGMI IPC (one-shot small, two-shot large buckets), no RCCL: the same code
             # runs with the 2 x dp ranks sharing ONE GPU (RCCL refuses duplicate devices), which is how the

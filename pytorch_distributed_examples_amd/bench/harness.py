@@ -441,7 +441,7 @@ def build_hvd_cnn(args, ctx, batch) -> Workload:
 
         fused = FusedCNN(model)
         grads = fused.grad_buffer()  # p.grad = views of one flat buffer: the engine reduces it in place
-        fused.always_prep = elastic  # AdamW updates the weights: fragments rebuilt in-kernel every step
+        fused.always_prep = False  # AdamW: fused.adamw_step refreshes the fragments with the update
         if elastic:  # ... so the optimiser need not keep the layer path's bf16 layouts (hvd/cnn_step.py)
             for p in model.parameters():
                 p.__dict__["_pde_own_copies"] = True
@@ -460,9 +460,11 @@ def build_hvd_cnn(args, ctx, batch) -> Workload:
             loss.backward()
             opt.step()
             return loss
-        if elastic:  # AdamW: the engine's all-reduce (graph mode: stream-ordered) + the multi-tensor update
+        if elastic:  # AdamW: the engine's all-reduce (graph mode: stream-ordered) + ONE update + fragment launch
             loss = fused.forward_backward(x, y, grad_out=grads)
-            opt.step()
+            opt.synchronize()
+            with opt.skip_synchronize():
+                fused.adamw_step(opt, grads)
             return loss
         if world == 1:  # all-reduce = identity: the SGD update rides in the reduction kernel
             opt.synchronize()

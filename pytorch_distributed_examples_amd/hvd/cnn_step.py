@@ -32,10 +32,14 @@ class FusedHvdStep:
         # plain FusedSGD (the DP script, mnist_horovod.py:50): the update rides in the fused kernel's slab reduction
         # at world 1, else ONE launch after the engine's synchronize that also refreshes the bf16 fragment image --
         # the bench's hvd_cnn step.  Other optimisers (AdamW): the multi-tensor update, fragments rebuilt in-kernel.
+        from ..ops.optim import FusedAdamW
+
         g = optimizer.param_groups[0] if len(optimizer.param_groups) == 1 else None
         self.sgd_fast = (isinstance(optimizer, FusedSGD) and g is not None and g.get("momentum", 0.0) == 0.0
                          and g.get("weight_decay", 0.0) == 0.0)
-        self.fused.always_prep = not self.sgd_fast
+        # one-group FusedAdamW (the elastic script): update + fragment refresh in ONE launch (FusedCNN.adamw_step)
+        self.adamw_fast = isinstance(optimizer, FusedAdamW) and g is not None
+        self.fused.always_prep = not (self.sgd_fast or self.adamw_fast)
         if not self.sgd_fast:
             from ..ops import functional as OF
 
@@ -63,6 +67,11 @@ class FusedHvdStep:
                 self.fused.sgd_step(self.opt, self.grads)
             return loss
         loss = self.fused.forward_backward(x, y, grad_out=self.grads)
+        if self.adamw_fast:
+            self.opt.synchronize()  # the engine (graph mode: stream-ordered on this stream)
+            with self.opt.skip_synchronize():
+                self.fused.adamw_step(self.opt, self.grads)
+            return loss
         self.opt.step()
         return loss
 

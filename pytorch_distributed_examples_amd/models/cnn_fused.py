@@ -101,6 +101,44 @@ class FusedCNN:
         _native.C().cnn_sgd(self.flat, grads, hp, self.frag, step)
         self._after_update(opt, params)
 
+    def _bind_adamw_state(self, opt):
+        """The FusedAdamW's exp_avg / exp_avg_sq become views of two flat buffers (state_dict keeps working); a state
+        tensor replaced behind our back (load_state_dict of an elastic restore) is copied in and re-bound."""
+        if getattr(self, "_adam_m", None) is None:
+            self._adam_m = torch.zeros_like(self.flat)
+            self._adam_v = torch.zeros_like(self.flat)
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            st = opt.state[p]
+            for key, flat in (("exp_avg", self._adam_m), ("exp_avg_sq", self._adam_v)):
+                view = flat[off:off + k].view_as(p)
+                cur = st.get(key)
+                if cur is None or cur.data_ptr() != view.data_ptr():
+                    with torch.no_grad():
+                        if cur is None:
+                            view.zero_()
+                        else:
+                            view.copy_(cur.reshape(p.shape))
+                    st[key] = view
+            off += k
+
+    @torch.no_grad()
+    def adamw_step(self, opt, grads: torch.Tensor):
+        """``opt.step()`` of a one-group FusedAdamW over the flat parameters fused with the fragment-image refresh:
+        ONE launch (``k_cnn_adamw``) instead of the multi-tensor update plus the next step's prep launch; the update
+        math and the device step counter are the optimiser's own (optim_device.h)."""
+        from ..ops.optim import FusedAdamW
+
+        assert isinstance(opt, FusedAdamW) and len(opt.param_groups) == 1, "adamw_step needs one FusedAdamW group"
+        self._bind_adamw_state(opt)
+        group = opt.param_groups[0]
+        params = [p for p in group["params"] if p.grad is not None]
+        st = opt._group_dev(0, group, params)
+        _native.C().cnn_adamw(self.flat, grads, self._adam_m, self._adam_v, st["hp"], self.frag, st["step"])
+        OF.bump_weight_generation()
+        self._frag_gen = OF.weight_generation()
+
     def _nwg(self, B: int) -> int:
         if self.workgroups:
             return self.workgroups

@@ -566,3 +566,51 @@ def test_fused_cnn_single_launch_tail_matches_two_launches(gpu, monkeypatch):
     (l0, g0, w0), (l1, g1, w1) = runs
     assert l0 == l1, (l0, l1)
     assert torch.equal(g0, g1) and torch.equal(w0, w1)
+
+
+def test_fused_cnn_adamw_step_matches_multi_tensor_adamw(gpu):
+    """FusedCNN.adamw_step (k_cnn_adamw: AdamW over the flat parameters + fragment refresh in ONE launch, the
+    Horovod-elastic step) against (a) an fp32 torch.optim.AdamW step on the same flat gradient, every step, and
+    (b) the multi-tensor FusedAdamW launch + the fragment prep over several steps: same losses, weights and optimiser
+    state to fp32 rounding (the two kernels inline the same update function; the compiler may contract its
+    multiply-adds differently), step counts equal, the state visible in state_dict (eval mode: no dropout)."""
+    from pytorch_distributed_examples_amd.models.cnn_fused import FusedCNN
+    from pytorch_distributed_examples_amd.ops import functional as OF
+    from pytorch_distributed_examples_amd.ops.optim import FusedAdamW
+
+    torch.manual_seed(0)
+    m_ref = Net().to(gpu).eval()
+    m_fus = copy.deepcopy(m_ref).eval()
+    f_ref, f_fus = FusedCNN(m_ref), FusedCNN(m_fus)
+    f_ref.always_prep = True
+    o_ref = FusedAdamW(m_ref.parameters(), lr=0.01, weight_decay=0.01)
+    o_fus = FusedAdamW(m_fus.parameters(), lr=0.01, weight_decay=0.01)
+    g_ref, g_fus = f_ref.grad_buffer(), f_fus.grad_buffer()
+    p_t = f_fus.flat.detach().clone().requires_grad_(True)
+    o_t = torch.optim.AdamW([p_t], lr=0.01, weight_decay=0.01)
+    gen = torch.Generator().manual_seed(3)
+    batches = [(torch.randn(128, 1, 28, 28, generator=gen).to(gpu), torch.randint(0, 10, (128,), generator=gen).to(gpu))
+               for _ in range(4)]
+    ref_losses = []
+    for x, y in batches:  # the reference run first: its optimiser steps bump the global weight generation
+        ref_losses.append(f_ref.forward_backward(x, y, grad_out=g_ref).clone())
+        o_ref.step()
+    for i, (x, y) in enumerate(batches):  # then the fused run: its 2nd..4th steps reuse k_cnn_adamw's fragments
+        l_fus = f_fus.forward_backward(x, y, grad_out=g_fus)
+        if i > 0:
+            assert f_fus._frag_gen == OF.weight_generation()  # no prep launch: the fragments come from k_cnn_adamw
+        with torch.no_grad():
+            p_t.copy_(f_fus.flat)
+        p_t.grad = g_fus.detach().clone()
+        f_fus.adamw_step(o_fus, g_fus)
+        o_t.step()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(f_fus.flat, p_t.detach(), rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(l_fus, ref_losses[i], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(f_ref.flat, f_fus.flat, rtol=1e-5, atol=1e-6)
+    sa, sb = o_ref.state_dict()["state"], o_fus.state_dict()["state"]
+    assert len(sa) == len(sb) == 8
+    for k in sa:
+        torch.testing.assert_close(sa[k]["exp_avg"], sb[k]["exp_avg"], rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(sa[k]["exp_avg_sq"], sb[k]["exp_avg_sq"], rtol=1e-5, atol=1e-9)
+        assert int(sa[k]["step"]) == int(sb[k]["step"]) == 4

@@ -142,18 +142,36 @@ r, dev, W = ctx.rank, ctx.device, ctx.world_size
 B, M, IMG, STEPS = 8, 2, 64, 3
 torch.manual_seed(0)
 pipe = ResNetPipelineDP(ctx, batch=B, split_size=M, image=IMG, schedule="1f1b", lr=0.05)
-assert pipe.dp == 2 and pipe.comm is not None and pipe.capturable, "xGMI DP communicator: capturable step"
-graph = pipe.split_step_graphs()  # one eager warm-up step, then 2 hipGraphs per step with a host barrier between
+if os.environ.get("PDE_PIPE_DP_COMM") != "gloo":
+    assert pipe.dp == 2 and pipe.comm is not None and pipe.capturable, "xGMI DP communicator: capturable step"
+SAME = os.environ.get("PIPE_DP_SAME_BATCH") == "1"  # diagnostic: both pipelines train on pipeline 0's batch
+if SAME:
+    from pytorch_distributed_examples_amd.data.synthetic import resnet_batch as _rb
+    _x, _y = _rb(B, IMG, 1000, dev, torch.Generator().manual_seed(1234))
+    _u = M * pipe.mb_group
+    pipe.xs, pipe.ys = list(_x.split(_u)), list(_y.split(_u))
+if os.environ.get("PIPE_DP_EAGER") == "1":  # the same split step without graphs (diagnostic A/B)
+    def graph():
+        pipe.ddp.zero_grad()
+        loss = pipe.engine.train_step(pipe.xs if pipe.stage == 0 else None, pipe.ys if pipe.last else None, pipe.n_mb)
+        torch.cuda.synchronize(); dist.barrier()
+        pipe.ddp.sync_gradients(); pipe.opt.step()
+        torch.cuda.synchronize(); dist.barrier()
+        return loss if loss is not None else torch.zeros((), device=dev)
+    graph()                       # the warm-up step
+else:
+    graph = pipe.split_step_graphs()  # one eager warm-up step, then 2 hipGraphs per step with a host barrier between
 torch.cuda.synchronize()
 t0 = time.perf_counter()
 losses = [float(graph().item()) for _ in range(STEPS)]
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / STEPS
 pipe.check()
-pipe.comm.check()
+if pipe.comm is not None:
+    pipe.comm.check()
 flat = torch.cat([p.detach().float().reshape(-1) for p in pipe.module.parameters()]).cpu()
 objs = [None] * W
-dist.all_gather_object(objs, (losses, flat, dict(pipe.comm.routed)))
+dist.all_gather_object(objs, (losses, flat, dict(pipe.comm.routed) if pipe.comm is not None else {}))
 # the DP replicas of each stage hold bit-identical weights
 assert torch.equal(objs[0][1], objs[2][1]) and torch.equal(objs[1][1], objs[3][1])
 if r == 0:
@@ -161,26 +179,41 @@ if r == 0:
     from pytorch_distributed_examples_amd.models.resnet import ResNetShard1, ResNetShard2
     from pytorch_distributed_examples_amd.ops import functional as OF
     from pytorch_distributed_examples_amd.ops.optim import FusedSGD
-    torch.manual_seed(0); s1 = ResNetShard1().to(dev)
-    torch.manual_seed(0); s2 = ResNetShard2().to(dev)
-    batches = [resnet_batch(B, IMG, 1000, dev, torch.Generator().manual_seed(1234 + p)) for p in range(2)]
-    opt = FusedSGD(list(s1.parameters()) + list(s2.parameters()), lr=0.05)
+    # one process, one model copy PER PIPELINE (each copy's modules see only their own pipeline's batches, as each
+    # replica does; per-module state such as BatchNorm running statistics evolves the same way), the DP average of
+    # the two copies' gradients applied to both copies with the same SGD
+    copies = []
+    for p in range(2):
+        torch.manual_seed(0); a1 = ResNetShard1().to(dev)
+        torch.manual_seed(0); a2 = ResNetShard2().to(dev)
+        copies.append((a1, a2, FusedSGD(list(a1.parameters()) + list(a2.parameters()), lr=0.05)))
+    s1, s2 = copies[0][0], copies[0][1]
+    batches = [resnet_batch(B, IMG, 1000, dev, torch.Generator().manual_seed(1234 + (0 if SAME else p)))
+               for p in range(2)]
     G = pipe.mb_group
     ref = []
     for step in range(1 + STEPS):
-        for q in list(s1.parameters()) + list(s2.parameters()):
-            q.grad = None
         per = []
-        for x, y in batches:              # the DP average: each pipeline's mean loss / dp
+        for (a1, a2, _), (x, y) in zip(copies, batches):
+            for q in list(a1.parameters()) + list(a2.parameters()):
+                q.grad = None
             tot = 0.0
             for xm, ym in zip(x.split(M * G), y.split(M * G)):
                 with OF.bn_groups(G):
-                    loss = OF.mse_loss(s2(s1(xm)), ym) / (B // (M * G))
-                (loss / 2).backward()
+                    loss = OF.mse_loss(a2(a1(xm)), ym) / (B // (M * G))
+                loss.backward()
                 tot += float(loss.item())
             per.append(tot)
-        opt.step()
+        pa = [q for q in list(copies[0][0].parameters()) + list(copies[0][1].parameters())]
+        pb = [q for q in list(copies[1][0].parameters()) + list(copies[1][1].parameters())]
+        with torch.no_grad():
+            for qa, qb in zip(pa, pb):    # DDP's average (fp32, rank order)
+                avg = (qa.grad + qb.grad) * 0.5
+                qa.grad.copy_(avg); qb.grad.copy_(avg)
+        for _, _, o in copies:
+            o.step()
         ref.append(per)
+    print("PIPEDP losses", [objs[1][0], objs[3][0]], "ref", ref[1:], flush=True)
     for p in range(2):  # pipeline p's loss is reported by its last stage, rank 2p + 1
         pl = objs[2 * p + 1][0]
         assert all(abs(a - b[p]) <= 2e-3 * max(1.0, abs(b[p])) for a, b in zip(pl, ref[1:])), (p, pl, ref)
@@ -188,14 +221,16 @@ if r == 0:
         want = torch.cat([q.detach().float().reshape(-1) for q in mod.parameters()]).cpu()
         err = ((objs[k][1] - want).norm() / want.norm()).item()
         assert err < 3e-3, (k, err)
-    rec = dict(config="4 rehearsal: resnet50 pp2 x dp2, 4 ranks sharing ONE MI355X", hipgraph=True,
+    rec = dict(config="4 rehearsal: resnet50 pp2 x dp2, 4 ranks sharing ONE MI355X",
+               hipgraph=os.environ.get("PIPE_DP_EAGER") != "1",
                graphs_per_step="2 (pipeline part | host barrier | DP all-reduce + SGD: shared-GPU rehearsal only)",
                dp_comm="xgmi one-shot + two-shot (no RCCL), fp32 wire", loss_ref=[r for r in ref[1:]], batch_per_pipeline=B, split_size=M, image=IMG,
                mb_group=G, schedule="1f1b", steps=STEPS, ms_per_step_shared_gpu=round(dt * 1e3, 3),
                losses=[objs[1][0], objs[3][0]], routed=[o[2] for o in objs],
                note="4 processes time-share one GPU: a correctness rehearsal, not a throughput number")
     os.makedirs(os.path.join(os.environ["REPO"], "gpurun_out"), exist_ok=True)
-    with open(os.path.join(os.environ["REPO"], "gpurun_out", "r6_world4_shared_gpu_resnet50_pp.jsonl"), "w") as f:
+    name = "r6_world4_shared_gpu_resnet50_pp" + ("_eager" if os.environ.get("PIPE_DP_EAGER") == "1" else "")
+    with open(os.path.join(os.environ["REPO"], "gpurun_out", name + ".jsonl"), "w") as f:
         f.write(json.dumps(rec) + "\n")
 dist.barrier()
 pipe.close()
@@ -240,14 +275,17 @@ def test_resnet_pipeline_graph_rehearsal_one_gpu(gpu, schedule, group):
            f"pipe_{schedule}_g{group}")
 
 
-def test_resnet_pipeline_x_dp_xgmi_graph_rehearsal_one_gpu(gpu):
+@pytest.mark.parametrize("mode", ["graph", "eager"])
+def test_resnet_pipeline_x_dp_xgmi_graph_rehearsal_one_gpu(gpu, mode):
     """BASELINE config 4's step, pp2 x dp2 = 4 ranks on one GPU: stage activations over the P2P rings, each stage's
     gradients all-reduced across its 2 replicas by the xGMI one-/two-shot communicator inside the captured step;
     losses and final weights against ONE process running both pipelines' micro-batches with averaged gradients."""
     # fp32 gradients on the DP wire: the single-process reference accumulates fp32 gradients (the bf16 wire is the
     # default elsewhere and rounds the averaged gradient: ~1 % loss drift after 3 steps at lr 0.05)
-    _check(_torchrun(_PIPE_DP, 4, {"PDE_PIPE_MB_GROUP": "2", "PDE_PIPE_GRAD_DTYPE": "fp32"}), "PIPEDP_OK", 4,
-           "pipe_dp_xgmi")
+    res = _torchrun(_PIPE_DP, 4, {"PDE_PIPE_MB_GROUP": "2", "PDE_PIPE_GRAD_DTYPE": "fp32",
+                                  "PIPE_DP_EAGER": "1" if mode == "eager" else "0"})
+    print([l for l in res.stdout.splitlines() if l.startswith("PIPEDP losses")])
+    _check(res, "PIPEDP_OK", 4, f"pipe_dp_xgmi_{mode}")
 
 
 def test_resnet_rpc_pipeline_one_gpu(gpu):
