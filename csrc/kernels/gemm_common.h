@@ -673,31 +673,48 @@ __device__ __forceinline__ void write_slab_and_reduce(const GemmArgs& args, cons
   const bool out_vec = vec && !(args.epi & (EPI_OIHW | EPI_OUT_F32)) && args.ldo % 4 == 0 &&
                        (reinterpret_cast<uintptr_t>(args.out) & 7) == 0;
   if (vec) {
-    // the slab loads of QG outputs per thread in flight at once (splits <= kMaxInKernelSplits, host-checked);
-    // groups of QG bound the registers of the big tiles (all 16 outputs of a 128x128 tile would need 512)
+    // the slab loads of QG outputs per thread, ZC slabs at a time, in flight at once (splits <= kMaxInKernelSplits,
+    // host-checked): QG x ZC x 16 B = 64 VGPRs.  (All kMaxInKernelSplits slabs of QG outputs at once -- 128 VGPRs of
+    // loads -- was where every 4-wave tile instantiation spilled: 136-208 B of scratch per lane, r5_gemm_regs.md.)
+    // Summation stays in slab order z = 0, 1, ... (bitwise the reduce launch's order).
     constexpr int QI = BM * BN / 4 / kThreads;
     constexpr int QG = QI < 4 ? QI : 4;
-    static_assert(QI % QG == 0, "output groups");
+    constexpr int ZC = 4;
+    static_assert(QI % QG == 0 && kMaxInKernelSplits % ZC == 0, "output groups / slab chunks");
     const bool stats = out_vec && args.bn_out.sums != nullptr;
     uint16_t* st = smem;  // [BM][BN] bf16 staging for the BatchNorm statistics
     if (stats) __syncthreads();  // every thread has read `last` (aliases st) before anyone stages
 #pragma unroll 1
     for (int i0 = 0; i0 < QI; i0 += QG) {
       f32x4 v[QG];
+      int off[QG];
 #pragma unroll
       for (int ii = 0; ii < QG; ++ii) {
         const int q = threadIdx.x + (i0 + ii) * kThreads;
         const int m = m0 + q / (BN / 4), n = n0 + (q % (BN / 4)) * 4;
         const bool ok = m < args.M && n < args.N;
-        const int off = ok ? static_cast<int>((static_cast<long>(m) * args.N + n) * 4) : 0;
-        u32x4 u[kMaxInKernelSplits];
+        off[ii] = ok ? static_cast<int>((static_cast<long>(m) * args.N + n) * 4) : 0;
+      }
 #pragma unroll
-        for (int z = 0; z < kMaxInKernelSplits; ++z)
-          if (z < splits) u[z] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + static_cast<int>(z * MN * 4), 0, SC1);
-        v[ii] = *reinterpret_cast<const f32x4*>(&u[0]);
+      for (int z0 = 0; z0 < kMaxInKernelSplits; z0 += ZC) {
+        if (z0 >= splits) break;  // block-uniform
+        u32x4 u[QG][ZC];
 #pragma unroll
-        for (int z = 1; z < kMaxInKernelSplits; ++z)
-          if (z < splits) v[ii] += *reinterpret_cast<const f32x4*>(&u[z]);
+        for (int ii = 0; ii < QG; ++ii)
+#pragma unroll
+          for (int zz = 0; zz < ZC; ++zz)
+            if (z0 + zz < splits)
+              u[ii][zz] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off[ii] + static_cast<int>((z0 + zz) * MN * 4), 0,
+                                                                SC1);
+#pragma unroll
+        for (int ii = 0; ii < QG; ++ii)
+#pragma unroll
+          for (int zz = 0; zz < ZC; ++zz) {
+            if (z0 + zz >= splits) continue;
+            const f32x4 x = *reinterpret_cast<const f32x4*>(&u[ii][zz]);
+            if (z0 + zz == 0) v[ii] = x;
+            else v[ii] += x;
+          }
       }
 #pragma unroll
       for (int ii = 0; ii < QG; ++ii) {
