@@ -31,6 +31,7 @@
 //   * Epilogue options: bias, ReLU, ReLU-mask (backward), fp32 / bf16 output, accumulate, and an OIHW
 //     remap that writes a conv weight gradient straight into the parameter's [Co][Ci][R][S] fp32 grad.
 #include "gemm_ring.h"
+#include "gemm_lowk.h"
 
 namespace pde {
 
@@ -567,6 +568,58 @@ hipError_t launch_skinny(const GemmArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(gemm_skinny_kernel<false>, dim3(tm * tn), dim3(kThreads), 0, s, a, tm, tn);
   return hipGetLastError();
 }
+// Low-K path (gemm_lowk.h): dense K-contiguous operands, K <= 64 (<= 128 with PDE_GEMM_LOWK_MAX_K), a bf16 output with at most bias / ReLU in the
+// epilogue, and enough rows for the streamed column strips to pay.  PDE_GEMM_LOWK=0: off; PDE_GEMM_LOWK_MIN_M:
+// fewest rows (default 4096); PDE_GEMM_LOWK_BLOCKS: grid cap (default 256; row tiles beyond it are walked by the
+// same blocks, the next tile's loads overlapping the current one's stores).
+struct LowkPolicy {
+  bool on = true;
+  long min_m = 4096, max_blocks = 256;  // r6q sweep: 256 / 512 / 1024 / 2048 -> 256 (one block per CU)
+  // K <= 64 only by default (r6r, in ResNet-50 b32's eager trace): 32768x256x64 11.75 us vs the tile core's 12.84,
+  // 32768x64x64 6.4 vs 8.2, but 8192x512x128 11.2 vs 8.9 (level in isolation, 7.5 vs 7.4): PDE_GEMM_LOWK_MAX_K
+  int max_k = 64;
+  LowkPolicy() {
+    if (const char* e = std::getenv("PDE_GEMM_LOWK")) on = e[0] != '0';
+    if (const char* e = std::getenv("PDE_GEMM_LOWK_MIN_M")) min_m = std::atol(e);
+    if (const char* e = std::getenv("PDE_GEMM_LOWK_BLOCKS")) max_blocks = std::max(1L, std::atol(e));
+    if (const char* e = std::getenv("PDE_GEMM_LOWK_MAX_K")) max_k = std::min(128, std::atoi(e));
+  }
+};
+const LowkPolicy& lowk_policy() {
+  static const LowkPolicy p;
+  return p;
+}
+bool lowk_ok(const GemmArgs& a) {
+  const LowkPolicy& p = lowk_policy();
+  if (!p.on || generic_only() || a.a.kind != 0 || a.b.kind != 0) return false;
+  if (a.M < p.min_m || a.K > p.max_k || a.K % 8 != 0 || a.N < 64 || a.N % 4 != 0) return false;
+  if ((a.epi & ~(EPI_BIAS | EPI_RELU)) != 0 || a.bias_grad != nullptr || a.bn_out.sums != nullptr ||
+      a.bn_in.ss != nullptr)
+    return false;
+  if (a.a.ld_k != 1 || a.b.ld_k != 1 || a.a.ld_r % 8 != 0 || a.b.ld_r % 8 != 0 || !aligned16(a.a.ptr) ||
+      !aligned16(a.b.ptr))
+    return false;
+  if (a.ldo % 8 != 0 || !aligned16(a.out)) return false;
+  return fast_ok(a, a.a, true, a.M) && fast_ok(a, a.b, true, a.N);
+}
+hipError_t launch_lowk(const GemmArgs& a, hipStream_t s) {
+  const int fn = a.N % 128 == 0 ? 8 : 4;  // column strips of 128 (64 when N is not a multiple of 128)
+  const int tm = ceil_div(a.M, kLowkBM), tn = ceil_div(a.N, 16 * fn);
+  long blocks = static_cast<long>(tm) * tn;
+  const long cap = std::max<long>(tn, lowk_policy().max_blocks / tn * tn);  // a multiple of tn
+  if (blocks > cap) blocks = cap;
+  if (a.splits_out != nullptr) *a.splits_out = 1;
+  gemm_log("lowk", a, kLowkBM, 16 * fn, tm * tn, 1);
+  const dim3 grid(static_cast<unsigned>(blocks));
+  if (a.K <= 64) {
+    if (fn == 8) hipLaunchKernelGGL((gemm_lowk_kernel<2, 8>), grid, dim3(kThreads), 0, s, a, tm, tn);
+    else hipLaunchKernelGGL((gemm_lowk_kernel<2, 4>), grid, dim3(kThreads), 0, s, a, tm, tn);
+  } else {
+    if (fn == 8) hipLaunchKernelGGL((gemm_lowk_kernel<4, 8>), grid, dim3(kThreads), 0, s, a, tm, tn);
+    else hipLaunchKernelGGL((gemm_lowk_kernel<4, 4>), grid, dim3(kThreads), 0, s, a, tm, tn);
+  }
+  return hipGetLastError();
+}
 // skinny problem 0 + 64x64 FAST-tile problem 1 (a weight gradient: dy^T x dense activation)
 bool launch_pair_skinny(const GemmArgs& a0, const GemmArgs& a1, const PairDims& d, hipStream_t s,
                         const OptimSeg& seg) {
@@ -602,6 +655,7 @@ hipError_t gemm_bf16(const GemmArgs& a_in, hipStream_t s) {
   GemmArgs a = a_in;
   a.wt = gemm_wt();
   if (skinny_ok(a)) return launch_skinny(a, s);
+  if (lowk_ok(a)) return launch_lowk(a, s);
   const bool akc = is_kc(a.a), bkc = is_kc(a.b);
   if (akc && bkc) return dispatch_tiles<true, true>(a, s);
   if (akc && !bkc) return dispatch_tiles<true, false>(a, s);

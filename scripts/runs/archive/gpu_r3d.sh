@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 check D: full GPU test suite; benches (cnn / mlp / resnet50 / stages at micro-batch 4, 8, 32, phase
-# timers); hipGraph kernel tables of mlp, resnet50 and both stages (scripts/runs/gpu_r3c.sh).
+# timers); hipGraph kernel tables of mlp, resnet50 and both stages (scripts/runs/archive/gpu_r3c.sh).
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
@@ -17,4 +17,4 @@ for m in "cnn" "mlp" "resnet50" "resnet50_stage --stage 1 --batch 8" "resnet50_s
   tail -1 gpurun_out/r3d_bench_one.log >> gpurun_out/r3d_bench.jsonl
   tail -1 gpurun_out/r3d_bench_one.log | cut -c1-240
 done
-bash scripts/runs/gpu_r3c.sh
+bash scripts/runs/archive/gpu_r3c.sh

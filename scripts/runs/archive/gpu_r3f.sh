@@ -12,4 +12,4 @@ for m in "resnet50_stage --stage 2 --batch 8" "resnet50_stage --stage 1 --batch 
   tail -1 gpurun_out/r3f_one.log >> gpurun_out/r3f_bench.jsonl
   tail -1 gpurun_out/r3f_one.log | cut -c1-200
 done
-bash scripts/runs/gpu_r3c.sh
+bash scripts/runs/archive/gpu_r3c.sh

@@ -5,7 +5,7 @@ R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R"
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-bash scripts/runs/gpu_r5j.sh || exit $?
+bash scripts/runs/archive/gpu_r5j.sh || exit $?
 PDE_BACKEND=gloo timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29541 bench.py --gpus 2 --model hvd_cnn --steps 20 --warmup 5 > gpurun_out/r5l_hvd_w2.log 2>&1 \
   || { tail -30 gpurun_out/r5l_hvd_w2.log; exit 1; }

@@ -21,7 +21,7 @@ for rows in 1024 0 512 2048; do
   BENV="PDE_BN_SINGLE_ROWS=$rows" bench s1_bn$rows resnet50_stage --stage 1 --batch 8 || exit 1
   BENV="PDE_BN_SINGLE_ROWS=$rows" bench s2_bn$rows resnet50_stage --stage 2 --batch 8 || exit 1
 done
-bash scripts/runs/gpu_r5l.sh || exit 1
+bash scripts/runs/archive/gpu_r5l.sh || exit 1
 # the 3-waves/SIMD ring GEMM (built before the BatchNorm change: compare with PDE_BN_SINGLE_ROWS=0)
 cp pytorch_distributed_examples_amd/_C.cpython-310-x86_64-linux-gnu.so /tmp/_C_default.so
 cp variants/_C_wpe3.so pytorch_distributed_examples_amd/_C.cpython-310-x86_64-linux-gnu.so

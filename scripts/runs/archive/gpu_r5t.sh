@@ -12,4 +12,4 @@ for m in "resnet50" "resnet50_stage --stage 1 --batch 8" "resnet50_stage --stage
   tail -1 gpurun_out/r5t_one.log >> gpurun_out/r5t_bench.jsonl
   echo "$m | $(tail -1 gpurun_out/r5t_one.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"])')"
 done
-bash scripts/runs/gpu_r5s.sh
+bash scripts/runs/archive/gpu_r5s.sh

@@ -605,3 +605,55 @@ def test_static_graph_ddp_skips_the_zero_fill(gpu):
     assert db.fills_skipped == 3, db.fills_skipped
     for pa, pb in zip(ma.parameters(), mb.parameters()):
         assert torch.equal(pa, pb) and torch.equal(pa.grad, pb.grad)
+
+
+@pytest.mark.parametrize("M,K,N,bias,relu", [(32768, 64, 256, False, False), (8192, 128, 512, False, False),
+                                             (5000, 64, 64, True, True), (4100, 40, 200, True, False),
+                                             (6000, 56, 384, False, True), (4096, 32, 128, True, True)])
+def test_lowk_gemm_path(gpu, M, K, N, bias, relu):
+    """K <= 64 with dense K-contiguous operands and >= 4096 rows: the streamed low-K kernel (gemm_lowk.h: the B
+    strip through LDS into per-wave registers, A fragments straight from global memory, transposed MFMAs, output
+    staged per wave and stored as 16-byte rows) -- 128- and 64-wide strips, K not a multiple of 32, ragged M / N
+    edges, bias / ReLU epilogues; bitwise deterministic across launches.  (8192x512x128: the tile core, K > 64.)"""
+    C = OF._C()
+    torch.manual_seed(7)
+    x = torch.randn(M, K, device=gpu).bfloat16()
+    w = (torch.randn(N, K, device=gpu) * 0.1).bfloat16()
+    b = torch.randn(N, device=gpu) if bias else None
+    y = C.linear_fwd(x, w, b, relu, False)
+    ref = x.float() @ w.float().t()
+    if bias:
+        ref = ref + b
+    if relu:
+        ref = torch.relu(ref)
+    assert y.shape == (M, N) and y.dtype == torch.bfloat16
+    assert rel_err(y, ref) < 1e-2
+    assert (y.float() - ref).abs().max().item() < 0.05 * ref.abs().max().item() + 1e-2
+    assert torch.equal(y, C.linear_fwd(x, w, b, relu, False))
+
+
+def test_lowk_gemm_path_k128_subprocess(gpu):
+    """The low-K kernel's KT = 3 / 4 instantiations (K up to 128), enabled with PDE_GEMM_LOWK_MAX_K=128 in a child
+    process (the dispatch policy is read once per process)."""
+    import os
+    import subprocess
+    import sys
+
+    code = (
+        "import torch\n"
+        "from pytorch_distributed_examples_amd.ops import functional as OF\n"
+        "C = OF._C(); torch.manual_seed(3)\n"
+        "for M, K, N in ((6000, 96, 384), (8192, 128, 512), (4096, 128, 200)):\n"
+        "    x = torch.randn(M, K, device='cuda').bfloat16(); w = (torch.randn(N, K, device='cuda') * 0.1).bfloat16()\n"
+        "    b = torch.randn(N, device='cuda')\n"
+        "    y = C.linear_fwd(x, w, b, True, False)\n"
+        "    ref = torch.relu(x.float() @ w.float().t() + b)\n"
+        "    e = ((y.float() - ref).norm() / ref.norm()).item()\n"
+        "    assert e < 1e-2, (M, K, N, e)\n"
+        "    assert torch.equal(y, C.linear_fwd(x, w, b, True, False))\n"
+        "print('LOWK128_OK')\n")
+    env = dict(os.environ, PDE_GEMM_LOWK_MAX_K="128", PDE_GEMM_LOG="1")
+    res = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert res.returncode == 0 and "LOWK128_OK" in res.stdout, res.stderr[-3000:]
+    assert res.stderr.count("[gemm] lowk") >= 3, res.stderr[-2000:]
