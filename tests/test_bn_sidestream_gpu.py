@@ -63,7 +63,11 @@ def test_stage_step_beside_spinning_side_stream_kernels(gpu):
     msg_in = torch.zeros_like(msg_out)
     gbuf = torch.ones(1 << 16, device=dev)
     gbuf2 = torch.ones(1 << 14, device=dev)
-    s1, s2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    # the spinning receive gets a HIGH-priority stream: HIP maps streams onto a few hardware queues (4 here) and
+    # serializes the kernels of streams that share one, so a normal-priority pool stream that lands on the main
+    # stream's queue would hold the step -- and the send that ends the spin -- behind the receive (a deadlock
+    # until the ring's 20 s timeout, every iteration; seen when earlier tests had advanced torch's stream pool)
+    s1, s2 = torch.cuda.Stream(device=dev, priority=-1), torch.cuda.Stream(device=dev)
     main = torch.cuda.current_stream(dev)
     torch.cuda.synchronize()
     for it in range(50):

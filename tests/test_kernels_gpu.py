@@ -657,3 +657,34 @@ def test_lowk_gemm_path_k128_subprocess(gpu):
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert res.returncode == 0 and "LOWK128_OK" in res.stdout, res.stderr[-3000:]
     assert res.stderr.count("[gemm] lowk") >= 3, res.stderr[-2000:]
+
+
+@pytest.mark.parametrize("n,h,ci,co,k", [(8, 4, 512, 512, 3), (8, 8, 256, 256, 3), (8, 4, 2048, 512, 1),
+                                          (2, 4, 512, 2048, 1)])
+def test_deferred_conv_slabs_into_batchnorm(gpu, n, h, ci, co, k):
+    """A split-K conv whose slabs the one-launch BatchNorm sums itself (bn_follows: the stage-2 layers at m = 8,
+    where the batched slab loads of k_bn_fwd_fused run) gives the same activation and running statistics as the
+    conv reducing its own slabs first, and matches an fp32 conv + BatchNorm."""
+    torch.manual_seed(11)
+    x = OF.to_native_image(torch.randn(n, ci, h, h, device=gpu))
+    w = torch.randn(co, ci, k, k, device=gpu) * (1.0 / (ci * k * k) ** 0.5)
+    g = torch.rand(co, device=gpu) + 0.5
+    b = torch.randn(co, device=gpu) * 0.1
+    outs = []
+    for defer in (True, False):
+        rm, rv = torch.zeros(co, device=gpu), torch.ones(co, device=gpu)
+        y = OF.conv2d(x, w, None, 1, k // 2, bn_follows=defer)
+        z = OF.batch_norm(y, g, b, rm, rv, True, relu=True)
+        torch.cuda.synchronize()
+        outs.append((z.clone(), rm.clone(), rv.clone()))
+    OF.check_device_errors("deferred slabs")
+    # (the standalone slab reduction sums with several slab lanes per column for > 2 slabs, the BatchNorm in slab
+    # order: the bf16 activations may differ in the last bit, the statistics by fp32 rounding)
+    assert (outs[0][0].float() - outs[1][0].float()).abs().max().item() <= 2e-2 * outs[1][0].float().abs().max().item()
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(outs[0][2], outs[1][2], rtol=1e-3, atol=1e-4)
+    ref = torch.relu(torch.nn.functional.batch_norm(
+        torch.nn.functional.conv2d(x[..., :ci].permute(0, 3, 1, 2).float(), w.bfloat16().float(), padding=k // 2),
+        None, None, g, b, True, 0.1, 1e-5))
+    got = outs[0][0][..., :co].permute(0, 3, 1, 2).float()
+    assert rel_err(got, ref) < 2e-2
