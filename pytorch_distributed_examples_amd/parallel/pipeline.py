@@ -147,7 +147,9 @@ class P2PChannel:
             self._pending.append((dist.isend(src, self.peer, tag=self._tag(True)), src))
             return
         if self._send_stream is None:
-            self._send_stream = torch.cuda.Stream(device=self.device)
+            # high priority: sends spin waiting for the peer's credit; on a hardware queue shared with the compute
+            # stream they would hold back the compute stream's own receives (a cross-rank wait cycle in 1F1B)
+            self._send_stream = torch.cuda.Stream(device=self.device, priority=-1)
         cur = torch.cuda.current_stream(self.device)
         self._send_stream.wait_stream(cur)
         with torch.cuda.stream(self._send_stream):

@@ -74,7 +74,9 @@ class StreamComm:
         uid = store.get(key)
         self.rccl = C.RcclComm()
         self.rccl.init(uid, self.rank, self.size, device.index, True)
-        self.side = torch.cuda.Stream(device=device) if side_stream else None
+        # high priority: a separate hardware queue class, so the spinning all-reduce never shares (and serializes)
+        # a queue with the compute stream whose later kernels its peers may be waiting for
+        self.side = torch.cuda.Stream(device=device, priority=-1) if side_stream else None
         self._bn_headroom = None
         if self.side is not None:
             # an overlapped all-reduce spins on its side stream while compute (a one-launch BatchNorm) runs:
