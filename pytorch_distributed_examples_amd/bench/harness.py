@@ -275,16 +275,23 @@ def build_data_parallel(args, ctx, batch) -> Workload:
     # world 1, fused MLP, PDE_MLP_FOLD_OPT=1: each layer's Adam update appended to the next backward GEMM launch
     # (default: the separate multi-tensor launch after backward -- measured faster, profiles/README.md r3k)
     fold_opt = fmlp is not None and ctx.world_size == 1 and os.environ.get("PDE_MLP_FOLD_OPT", "0") == "1"
-    # world 1, fused MLP: the whole step (forward, loss, backward, Adam) as ONE persistent launch
-    # (models/mlp_mega.py; PDE_MLP_MEGA=0: the layer-by-layer launches)
+    # fused MLP: the whole step (forward, loss, backward, Adam) as ONE persistent launch (models/mlp_mega.py;
+    # PDE_MLP_MEGA=0: the layer-by-layer launches) -- at world > 1 on one node with a GPU per rank the gradient
+    # average runs inside that launch over xGMI (MegaMLP.exchange), as in the entry script (apps/mnist_ddp.py)
     mega = None
-    if (fmlp is not None and ctx.world_size == 1 and not fold_opt and os.environ.get("PDE_MLP_MEGA", "1") != "0"
-            and batch % 32 == 0):
-        from ..models.mlp_mega import MegaMLP
+    mega_xchg = False
+    if fmlp is not None and not fold_opt and os.environ.get("PDE_MLP_MEGA", "1") != "0" and batch % 32 == 0:
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", str(ctx.world_size)))
+        own_gpu = torch.cuda.device_count() >= local
+        mega_xchg = (ctx.world_size > 1 and own_gpu and local == ctx.world_size and
+                     getattr(opt, "KIND", "") != "sgd" and os.environ.get("PDE_MLP_MEGA_XCHG", "1") != "0")
+        if ctx.world_size == 1 or mega_xchg:
+            from ..models.mlp_mega import MegaMLP
 
-        mega = MegaMLP(model, opt)
-        if mega.grid() <= 0:
-            mega = None
+            if int(OF._C().mlp_train_grid()) > 0:
+                xa = MegaMLP.exchange(model, ctx.device) if ctx.world_size > 1 else None
+                mega = MegaMLP(model, opt, xgmi=xa)
+        mega_xchg = mega_xchg and mega is not None
     # world > 1 on the xGMI data plane: the fused CNN exchanges its gradients inside the slab reduction
     # (PDE_CNN_XCHG=0: all-reduce through the DDP communicator + a separate SGD launch instead)
     xgmi = getattr(comm, "xgmi", None) if fused is not None and os.environ.get("PDE_CNN_XCHG", "1") != "0" else None
@@ -361,7 +368,8 @@ def build_data_parallel(args, ctx, batch) -> Workload:
                  **({"mega_kernel": True, "launches_per_step": mega.kernel_launches_per_step(),
                      "optimizer": "adam inside the step's single launch"} if mega is not None else {}),
                  steps_per_graph=group.steps if group is not None else (1 if one is not None else 0),
-                 allreduce=("xgmi-in-reduce-kernel" if xgmi is not None else
+                 allreduce=("xgmi-in-mega-kernel" if mega_xchg else
+                            "xgmi-in-reduce-kernel" if xgmi is not None else
                             "xgmi-oneshot<=%dB+rccl" % comm.threshold) if routed is not None else
                  ("rccl" if comm is not None else ("gloo" if ctx.world_size > 1 else "none")))
     w.group = group
