@@ -94,6 +94,7 @@ int split_cap(const pde::GemmArgs& a) {
 struct PendingGemm {
   pde::GemmArgs args;
   Tensor ws;
+  bool defer_out = false;  // problem 0 of a pair: leave its split-K slabs for the BatchNorm backward (conv_dgrad)
 };
 thread_local bool g_collect = false;
 thread_local std::vector<PendingGemm> g_pending;
@@ -143,6 +144,8 @@ void resolve_pending(const optional<Tensor>& t) {
   if (t.has_value()) resolve_pending(*t);
 }
 int pending_conv_count() { return static_cast<int>(g_pending_conv.size()); }
+long g_bn_bwd_slab_uses = 0;  // BatchNorm backwards that summed a deferred dgrad's slabs (tests / diagnostics)
+long bn_bwd_slab_uses() { return g_bn_bwd_slab_uses; }
 
 void gemm_pair_begin() {
   TORCH_CHECK(!g_collect && g_pending.empty(), "gemm_pair_begin: a pair is already being collected");
@@ -187,9 +190,14 @@ bool gemm_pair_end(bool abort, bool defer) {
   g_seg_pending = false;
   if (abort) return false;
   if (q.size() == 2) {
-    int sp1 = 0;
-    check(pde::gemm_bf16_pair(q[0].args, q[1].args, cur_stream(), defer ? &sp1 : nullptr, has_seg ? &seg : nullptr),
+    int sp1 = 0, sp0 = 0;
+    check(pde::gemm_bf16_pair(q[0].args, q[1].args, cur_stream(), defer ? &sp1 : nullptr, has_seg ? &seg : nullptr,
+                              q[0].defer_out ? &sp0 : nullptr),
           "gemm_pair");
+    if (sp0 > 1) {  // the dgrad output stays unreduced: the BatchNorm backward sums its slabs (bn_bwd)
+      std::lock_guard<std::mutex> lk(g_pending_mu);
+      g_pending_conv[q[0].args.out] = PendingConv{q[0].ws, sp0, q[0].args.M, q[0].args.N};
+    }
     if (sp1 > 1) {
       const pde::GemmArgs& a = q[1].args;
       pde::ReduceJob j{};
@@ -571,7 +579,7 @@ std::vector<Tensor> conv_fwd_bn(const Tensor& x, const Tensor& wf, int R, int S,
 // aux: with add_aux, a bf16 [N*H*W, Ci] gradient added in the epilogue (the other branch of a residual
 // fork); otherwise the saved post-ReLU activation whose mask multiplies the result.
 Tensor conv_dgrad(const Tensor& dy, const Tensor& wd, int H, int W, int R, int S, int stride, int pad,
-                  const optional<Tensor>& aux, bool w_fwd_layout, bool add_aux) {
+                  const optional<Tensor>& aux, bool w_fwd_layout, bool add_aux, bool defer) {
   CHECK_IN(dy); CHECK_IN(wd); CHECK_BF16(dy); CHECK_BF16(wd);
   resolve_pending(aux);
   const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
@@ -599,6 +607,9 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wd, int H, int W, int R, int S
   }
   a.epi = a.aux ? (add_aux ? pde::EPI_ADD_AUX : pde::EPI_DRELU) : 0;
   run_gemm(a, dy, -1);
+  // defer (a dgrad collected as problem 0 of a pair, plain epilogue): its split-K slabs are left for the
+  // BatchNorm backward that consumes dx (registered as pending by gemm_pair_end if it did split)
+  if (defer && g_collect && a.epi == 0 && g_pending.size() == 1) g_pending.back().defer_out = true;
   return dx;
 }
 
@@ -1002,6 +1013,20 @@ std::vector<Tensor> bn_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, c
   resolve_pending(y);
   const int C = x.size(-1);
   const int P = x.numel() / C;
+  // dy left as split-K slabs by the conv dgrad that produced it (conv_dgrad(defer=true)): summed by the kernel
+  Tensor dyws;
+  int dysp = 1;
+  {
+    std::lock_guard<std::mutex> lk(g_pending_mu);
+    auto it = g_pending_conv.find(dy.data_ptr());
+    if (it != g_pending_conv.end() && it->second.M == P && it->second.N == C && dy.numel() == x.numel()) {
+      dyws = it->second.ws;
+      dysp = it->second.splits;
+      g_pending_conv.erase(it);
+    }
+  }
+  if (!dyws.defined()) resolve_pending(dy);
+  else ++g_bn_bwd_slab_uses;
   const int G = static_cast<int>(groups);
   TORCH_CHECK(G >= 1 && x.size(0) % G == 0 && mean.numel() == static_cast<long>(G) * C,
               "bn_bwd: groups / statistics shape mismatch");
@@ -1018,7 +1043,8 @@ std::vector<Tensor> bn_bwd(const Tensor& dy, const Tensor& x, const Tensor& y, c
   check(pde::bn_bwd(u16(dy), u16(x), u16(y), mean.data_ptr<float>(), invstd.data_ptr<float>(), cf32(gamma), P, C,
                     relu, dg.data_ptr<float>(), db.data_ptr<float>(), direct && accum ? 1 : 0, ws.data_ptr<float>(),
                     coef.data_ptr<float>(), u16(dx), want_dres ? u16(dres) : nullptr, cur_stream(),
-                    want_dres ? nullptr : cf32(scale_shift), G, G > 1 ? gs.data_ptr<float>() : nullptr),
+                    want_dres ? nullptr : cf32(scale_shift), G, G > 1 ? gs.data_ptr<float>() : nullptr,
+                    dyws.defined() ? dyws.data_ptr<float>() : nullptr, dysp),
         "bn_bwd");
   return {dx, dg, db, dres};
 }
@@ -1422,9 +1448,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pad"), py::arg("groups"), py::arg("stats_sums"), py::arg("stats_ticket"), py::arg("gamma"),
         py::arg("beta"), py::arg("running_mean"), py::arg("running_var"), py::arg("eps"), py::arg("momentum"),
         py::arg("fold_ss"), py::arg("relu"), py::arg("defer") = false);
+  m.def("bn_bwd_slab_uses", &bn_bwd_slab_uses);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wd"), py::arg("H"), py::arg("W"), py::arg("R"),
         py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("aux") = py::none(), py::arg("w_fwd_layout") = false,
-        py::arg("add_aux") = false);
+        py::arg("add_aux") = false, py::arg("defer") = false);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),
         py::arg("pad"), py::arg("Co"), py::arg("Ci"), py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("cast_bf16", &cast_bf16);

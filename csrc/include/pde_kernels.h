@@ -129,8 +129,10 @@ hipError_t gemm_bf16(const GemmArgs& args, hipStream_t stream);
 struct OptimSeg;
 // seg (optional): optimiser blocks appended to the launch (their own chunk range; run as a separate launch when
 // the two problems cannot be paired)
+// defer_split0 != nullptr: problem 0's split-K slab reduction is NOT launched either; its split count is returned
+// there (0 / 1: nothing deferred, the output is written) and a consumer sums the slabs itself (bn_bwd's dys).
 hipError_t gemm_bf16_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t stream, int* defer_split1 = nullptr,
-                          const OptimSeg* seg = nullptr);
+                          const OptimSeg* seg = nullptr, int* defer_split0 = nullptr);
 bool gemm_pair_enabled();
 // A deferred split-K slab reduction (vector form: N % 4 == 0, 16-B aligned slabs) with the fp32 epilogue of
 // its GEMM (accumulate, OIHW remap, ones-column bias gradient).
@@ -271,7 +273,9 @@ hipError_t bn_apply(const uint16_t* x, int P, int C, const float* scale, const f
 hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
                   const float* gamma, int P, int C, int relu, float* dgamma, float* dbeta, int accum_params, float* ws,
                   float* coef, uint16_t* dx, uint16_t* dres, hipStream_t s, const float* ss = nullptr, int groups = 1,
-                  float* gscratch = nullptr);
+                  float* gscratch = nullptr, const float* dys = nullptr, int dysplits = 1);
+// (dys / dysplits > 1: dy's values are still the unreduced split-K slabs [dysplits][P][C] fp32 of the conv dgrad
+// that produced it -- summed by the BatchNorm itself, or reduced into dy first where its kernel cannot)
 hipError_t maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
                        int k, int st, int p, int relu, hipStream_t s);
 hipError_t maxpool_bwd(const uint16_t* dy, const uint16_t* y, const uint8_t* idx, uint16_t* dx, int N, int H, int W,

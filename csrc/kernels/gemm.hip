@@ -702,10 +702,11 @@ bool gemm_pair_enabled() {
 }
 
 hipError_t gemm_bf16_pair(const GemmArgs& a0_in, const GemmArgs& a1_in, hipStream_t s, int* defer_split1,
-                          const OptimSeg* seg_in) {
+                          const OptimSeg* seg_in, int* defer_split0) {
   GemmArgs a0 = a0_in, a1 = a1_in;
   a0.wt = a1.wt = gemm_wt();
   if (defer_split1 != nullptr) *defer_split1 = 0;
+  if (defer_split0 != nullptr) *defer_split0 = 0;
   OptimSeg seg{};  // blocks = 0: no optimiser segment
   if (seg_in != nullptr && seg_in->c1 > seg_in->c0 && seg_in->blocks > 0) seg = *seg_in;
   PairDims d{};
@@ -788,6 +789,10 @@ hipError_t gemm_bf16_pair(const GemmArgs& a0_in, const GemmArgs& a1_in, hipStrea
   if (defer_split1 != nullptr && sp1 > 1) {  // problem 1's slabs are reduced later by gemm_reduce_jobs
     *defer_split1 = sp1;
     sp1 = 1;
+  }
+  if (defer_split0 != nullptr && sp0 > 1) {  // problem 0's slabs are summed by their consumer (bn_bwd's dys)
+    *defer_split0 = sp0;
+    sp0 = 1;
   }
   if (sp0 > 1 && sp1 > 1) {
     const int l0 = reduce_lanes(sp0), l1 = reduce_lanes(sp1);

@@ -1121,7 +1121,7 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
     const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta, int accum,
     float* __restrict__ coef, uint16_t* __restrict__ dx, uint16_t* __restrict__ dres,
     const float* __restrict__ ss, float* __restrict__ gdgb, int* __restrict__ gtickets, int lite,
-    uint64_t* __restrict__ parts) {
+    uint64_t* __restrict__ parts, const float* __restrict__ dys, int dysplits, long dyzs) {
   __shared__ float red[2][kBnRows][kBnCG + 1];
   __shared__ float tot1[kBnCG], tot2[kBnCG], s_coef[3][kBnCG];
   __shared__ int s_last;
@@ -1130,10 +1130,13 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
   const int c0 = blockIdx.y * kBnCG + tv * 8;
   const bool cok = c0 < C;
   const bool from_x = relu && ss != nullptr;
+  // dys (RC > 0 only, host-checked): dy is the unreduced split-K slabs of the conv dgrad that produced it; the
+  // thread's rows are summed here in slab order and rounded to bf16, the value the slab reduction would store
   const int gz = blockIdx.z, G = gridDim.z;  // group (see bn_group_last)
   {
     const long xo = static_cast<long>(gz) * P * C;
     dy += xo;
+    if (dys) dys += xo;
     x += xo;
     if (y) y += xo;
     dx += xo;
@@ -1166,8 +1169,20 @@ __global__ __launch_bounds__(kBnThreads) void k_bn_bwd_fused(
         const int r = r0 + k * kBnRows;
         if (r < r1) {
           const long off = static_cast<long>(r) * C + c0;
-          cd[k] = *reinterpret_cast<const u16x8*>(dy + off);
+          if (dys == nullptr) cd[k] = *reinterpret_cast<const u16x8*>(dy + off);
           cx[k] = *reinterpret_cast<const u16x8*>(x + off);
+        }
+      }
+      if (dys != nullptr) {
+#pragma unroll
+        for (int k = 0; k < RC; ++k) {
+          const int r = r0 + k * kBnRows;
+          if (r < r1) {
+            float v[8];
+            slab_row8(dys, dyzs, dysplits, static_cast<long>(r) * C + c0, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) cd[k][j] = f2bf(v[j]);
+          }
         }
       }
 #pragma unroll
@@ -1944,14 +1959,22 @@ hipError_t bn_apply(const uint16_t* x, int P, int C, const float* scale, const f
 hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean, const float* invstd,
                   const float* gamma, int P, int C, int relu, float* dgamma, float* dbeta, int accum_params, float* ws,
                   float* coef, uint16_t* dx, uint16_t* dres, hipStream_t s, const float* ss, int groups,
-                  float* gscratch) {
+                  float* gscratch, const float* dys, int dysplits) {
   int rpb;
   const int ncg = ceil_div(C, kBnCG);
   int* err = nullptr;
   if (groups < 1 || P % groups != 0) return hipErrorInvalidValue;
   const int Pg = P / groups;
   const int nrb1 = bn_fin_grid(Pg, C, rpb, groups);
-  if (bn_one_launch(nrb1 * ncg * groups) && bn_ticket_base(s, &err) != nullptr) {
+  if (dysplits <= 1) dys = nullptr;
+  const bool one = bn_one_launch(nrb1 * ncg * groups) && bn_ticket_base(s, &err) != nullptr;
+  if (dys != nullptr && !(one && ceil_div(rpb, kBnRows) <= 4)) {
+    // only the register-resident one-launch kernel sums dy from the slabs: reduce them into dy first
+    const hipError_t e = gemm_reduce_slabs_bf16(const_cast<float*>(dys), dysplits, P, C, const_cast<uint16_t*>(dy), s);
+    if (e != hipSuccess) return e;
+    dys = nullptr;
+  }
+  if (one) {
     int* tk = bn_tickets(ncg * groups, s);
     uint32_t* fl = bn_flags(ncg * groups, s);
     int* gt = groups > 1 ? bn_tickets(ncg, s) : nullptr;
@@ -1970,18 +1993,27 @@ hipError_t bn_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, cons
       // rows per thread of a chunk: small enough -> kept in registers for the apply pass
       if (ceil_div(rpb, kBnRows) <= 4)
         hipLaunchKernelGGL(k_bn_bwd_fused<4>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
-                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, mode, parts);
+                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, mode, parts,
+                           dys, dysplits, static_cast<long>(P) * C);
       else if (bn_rc8_on() && ceil_div(rpb, kBnRows) <= 8)
         hipLaunchKernelGGL(k_bn_bwd_fused<8>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
-                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, mode, parts);
+                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, mode, parts,
+                           nullptr, 1, 0L);
       else if (bn_rc16_on() && ceil_div(rpb, kBnRows) <= 16)
         hipLaunchKernelGGL(k_bn_bwd_fused<16>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
-                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, mode, parts);
+                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, mode, parts,
+                           nullptr, 1, 0L);
       else
         hipLaunchKernelGGL(k_bn_bwd_fused<0>, grid, dim3(kBnThreads), 0, s, dy, x, y, mean, invstd, Pg, C, rpb, relu,
-                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, mode, parts);
+                           ws, tk, fl, err, gamma, dgamma, dbeta, accum_params, coef, dx, dres, ss, gscratch, gt, mode, parts,
+                           nullptr, 1, 0L);
       return hipGetLastError();
     }
+  }
+  if (dys != nullptr) {  // (the one-launch kernel could not be launched after all)
+    const hipError_t e = gemm_reduce_slabs_bf16(const_cast<float*>(dys), dysplits, P, C, const_cast<uint16_t*>(dy), s);
+    if (e != hipSuccess) return e;
+    dys = nullptr;
   }
   if (groups > 1) {  // grouped, multi-launch: group 0 writes / adds the parameter gradients, the rest add
     for (int g = 0; g < groups; ++g) {

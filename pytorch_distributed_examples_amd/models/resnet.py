@@ -76,11 +76,13 @@ class Bottleneck(nn.Module):
             a2 = OF.bn_relu_conv(a1, st1, self.conv2, stats_out=st2, bn_follows=t)
         else:
             out = self.bn1(self.conv1(x, grad_join=join, bn_follows=t), relu=True)
-            a2 = self.conv2(out, bn_follows=t, bn_stats=st2)
+            # bn1's output feeds conv2 alone (and bn2's conv3): their dgrads' split-K slabs go to the BatchNorm
+            # backward unreduced (dx_bn)
+            a2 = self.conv2(out, bn_follows=t, bn_stats=st2, dx_bn=t)
         if f2:
             out = OF.bn_relu_conv(a2, st2, self.conv3, bn_follows=t)
         else:
-            out = self.conv3(self.bn2(a2, relu=True), bn_follows=t)
+            out = self.conv3(self.bn2(a2, relu=True), bn_follows=t, dx_bn=t)
         if self.downsample is not None:
             conv, bn = self.downsample[0], self.downsample[1]
             identity = bn(conv(x, grad_to=join, bn_follows=t))

@@ -412,9 +412,11 @@ class _ConvBwdCtx:
 
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, relu, join=None, grad_to=None, defer=False, stats=None):
+    def forward(ctx, x, weight, bias, stride, pad, relu, join=None, grad_to=None, defer=False, stats=None,
+                dx_defer=False):
         ctx.join = join
         ctx.grad_to = grad_to
+        ctx.dx_defer = dx_defer
         co, ci, r, s = weight.shape
         cp = x.shape[3]
         cop = pad8(co)
@@ -438,7 +440,7 @@ class _Conv2dFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, weight, y = ctx.saved_tensors
         dx, dw, db = _conv_backward(ctx, dy, x, weight, y)
-        return dx, dw, db, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None
 
 
 def _conv_backward(ctx, dy, x, weight, y=None):
@@ -470,16 +472,20 @@ def _conv_backward(ctx, dy, x, weight, y=None):
             # residual fork: the other branch's gradient (stored by the block's last BatchNorm) is added in the
             # dgrad epilogue instead of by a separate autograd add
             other = ctx.join.take() if ctx.join is not None else None
+            # dx_defer (the conv's input is a BatchNorm + ReLU output consumed by this conv alone): a split-K
+            # dgrad leaves its slabs for that BatchNorm's backward, which sums them itself (no reduce launch)
+            defer = (paired and other is None and ctx.grad_to is None and getattr(ctx, "dx_defer", False)
+                     and _BN_BWD_DEFER[0])
             wf = _maintained(weight, "conv_fwd") if (r == 1 and s == 1 and pad == 0) else None
             if wf is not None and weight.__dict__["_pde_maint"].get("kxk") is None:
                 # 1x1 (stride 1 or 2): the dgrad GEMM reads the forward copy [Co, Ci] transposed
-                dx = _C().conv_dgrad(dy, wf, h, w, r, s, stride, pad, other, True, other is not None)
+                dx = _C().conv_dgrad(dy, wf, h, w, r, s, stride, pad, other, True, other is not None, defer)
             else:
                 wd = _maintained(weight, "conv_dgrad") if cp == pad8(ci) else None
                 if wd is None:
                     wd = _cached(weight, ("conv_dgrad", cp, cop),
                                  lambda: _C().conv_w_dgrad(weight.detach().contiguous(), cp, cop))
-                dx = _C().conv_dgrad(dy, wd, h, w, r, s, stride, pad, other, False, other is not None)
+                dx = _C().conv_dgrad(dy, wd, h, w, r, s, stride, pad, other, False, other is not None, defer)
             if ctx.grad_to is not None:  # the other consumer of x adds this gradient in its dgrad epilogue
                 ctx.grad_to.put(dx)
                 dx = None
@@ -540,24 +546,28 @@ class GradJoin:
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, relu=False, grad_join=None, grad_to=None, bn_follows=False,
-           bn_stats=None):
+           bn_stats=None, dx_bn=False):
     """2-D convolution.  GPU: ``x`` is NHWC bf16 with C padded to a multiple of 8; output NHWC with
     Cout padded to a multiple of 8 (padded channels are exactly zero).  CPU: NCHW fp32 F.conv2d.
     ``grad_join`` (this conv's dgrad adds the join's gradient) / ``grad_to`` (this conv's input gradient
     goes to the join instead of autograd): see :class:`GradJoin` (GPU only; ignored on CPU).
     ``bn_follows``: a training-mode batch_norm consumes the output next -- a split-K GEMM then skips its
-    slab reduction and the one-launch BatchNorm sums the slabs itself (any other reader resolves them)."""
+    slab reduction and the one-launch BatchNorm sums the slabs itself (any other reader resolves them).
+    ``dx_bn``: ``x`` is a training BatchNorm(+ReLU) output that ONLY this conv consumes -- the backward's split-K
+    dgrad then leaves its slabs for that BatchNorm's backward in the same way (the caller vouches for the
+    single consumer: an autograd accumulation of the pending gradient would read it unreduced)."""
     if not x.is_cuda:
         y = F.conv2d(_emu(x), _emu(weight), bias, stride=stride, padding=padding)
         return _emu(F.relu(y) if relu else y)
     defer = bool(bn_follows) and bias is None and not relu and _DEFER_CONV[0]
     return _Conv2dFn.apply(x.contiguous(), weight, bias, int(stride), int(padding), relu, grad_join, grad_to, defer,
-                           bn_stats)
+                           bn_stats, bool(dx_bn))
 
 
 import os as _os
 
 _DEFER_CONV = [_os.environ.get("PDE_CONV_BN_DEFER", "1") != "0"]  # A/B switch
+_BN_BWD_DEFER = [_os.environ.get("PDE_BN_BWD_DEFER", "1") != "0"]  # A/B switch: dgrad slabs summed by bn_bwd
 
 
 def to_native_image(x: torch.Tensor) -> torch.Tensor:

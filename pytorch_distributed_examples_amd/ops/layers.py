@@ -58,9 +58,9 @@ class Conv2d(nn.Module):
             bound = 1 / math.sqrt(fan_in)
             nn.init.uniform_(self.bias, -bound, bound)
 
-    def forward(self, x, grad_join=None, grad_to=None, bn_follows=False, bn_stats=None):
+    def forward(self, x, grad_join=None, grad_to=None, bn_follows=False, bn_stats=None, dx_bn=False):
         return OF.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.relu, grad_join, grad_to,
-                         bn_follows, bn_stats)
+                         bn_follows, bn_stats, dx_bn)
 
     def extra_repr(self):
         return (f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}, stride={self.stride}, "

@@ -614,3 +614,45 @@ def test_fused_cnn_adamw_step_matches_multi_tensor_adamw(gpu):
         torch.testing.assert_close(sa[k]["exp_avg"], sb[k]["exp_avg"], rtol=1e-5, atol=1e-7)
         torch.testing.assert_close(sa[k]["exp_avg_sq"], sb[k]["exp_avg_sq"], rtol=1e-5, atol=1e-9)
         assert int(sa[k]["step"]) == int(sb[k]["step"]) == 4
+
+
+@pytest.mark.parametrize("grouped", [1, 2])
+def test_bottleneck_backward_dgrad_slabs_into_batchnorm(gpu, grouped):
+    """conv2 / conv3 dgrads of a Bottleneck (inputs: bn1 / bn2 + ReLU outputs, consumed by that conv alone,
+    ``dx_bn``) leave their split-K slabs unreduced and the BatchNorm backward sums them itself: at the stage-2
+    micro-batch (layer3 / layer4, 8 images; grouped BatchNorm too) the block's input and parameter gradients match
+    the path with the dgrads' own reduce launches (PDE_BN_BWD_DEFER=0) to bf16 rounding, the BatchNorm backward
+    really took slabs, and no deferred output is left behind."""
+    C = OF._C()
+    torch.manual_seed(5)
+    s2 = ResNetShard2()
+    for blk, (c, hw) in ((s2.seq[0][1], (1024, 8)), (s2.seq[1][1], (2048, 4))):
+        x = torch.randn(8, hw, hw, c).to(torch.bfloat16).to(gpu)
+        gen = torch.Generator().manual_seed(c)
+        outs = []
+        for defer in (True, False):
+            OF._BN_BWD_DEFER[0] = defer
+            try:
+                b = copy.deepcopy(blk).to(gpu).train()
+                for it in range(2):  # the 2nd backward has .grad sinks: dgrad + wgrad paired (the deferring path)
+                    for p in b.parameters():
+                        if p.grad is not None:
+                            p.grad.zero_()
+                    xg = x.clone().requires_grad_()
+                    before = C.bn_bwd_slab_uses()
+                    with OF.bn_groups(grouped):
+                        y = b(xg)
+                    gy = torch.randn(y.shape, generator=gen.manual_seed(c)).to(torch.bfloat16).to(gpu)
+                    y.backward(gy)
+                    torch.cuda.synchronize()
+                    used = C.bn_bwd_slab_uses() - before
+            finally:
+                OF._BN_BWD_DEFER[0] = True
+            assert C.pending_conv_count() == 0
+            grads = torch.cat([p.grad.float().reshape(-1) for p in b.parameters()])
+            outs.append((xg.grad.float(), grads, used))
+        (da, ga, ua), (db, gb, ub) = outs
+        assert ua >= 1 and ub == 0, (c, ua, ub)
+        assert rel_err(da, db) < 2e-2, (c, rel_err(da, db))
+        assert rel_err(ga, gb) < 2e-2, (c, rel_err(ga, gb))
+    OF.check_device_errors("dgrad slabs into bn_bwd")
