@@ -609,10 +609,22 @@ __device__ __forceinline__ void slab_row8(const float* __restrict__ slabs, long 
       b += q[u][1];
     }
   }
-  for (; z < splits; ++z) {
-    const f32x4* q = reinterpret_cast<const f32x4*>(slabs + z * zs + off);
-    a += q[0];
-    b += q[1];
+  {  // the last 0..3 slabs: their loads issued together too (one more round trip, not up to three)
+    const int rem = splits - z;
+    f32x4 q[3][2];
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (u < rem) {
+        const f32x4* r = reinterpret_cast<const f32x4*>(slabs + (z + u) * zs + off);
+        q[u][0] = r[0];
+        q[u][1] = r[1];
+      }
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (u < rem) {
+        a += q[u][0];
+        b += q[u][1];
+      }
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -648,13 +660,27 @@ __device__ __forceinline__ void slab_2rows8(const float* __restrict__ slabs, lon
       b1 += q[u][3];
     }
   }
-  for (; z < splits; ++z) {
-    const f32x4* r0 = reinterpret_cast<const f32x4*>(slabs + z * zs + off0);
-    const f32x4* r1 = reinterpret_cast<const f32x4*>(slabs + z * zs + (ok1 ? off1 : off0));
-    a0 += r0[0];
-    b0 += r0[1];
-    a1 += r1[0];
-    b1 += r1[1];
+  {  // the last 0..3 slabs of both rows in one more round trip
+    const int rem = splits - z;
+    f32x4 q[3][4];
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (u < rem) {
+        const f32x4* r0 = reinterpret_cast<const f32x4*>(slabs + (z + u) * zs + off0);
+        const f32x4* r1 = reinterpret_cast<const f32x4*>(slabs + (z + u) * zs + (ok1 ? off1 : off0));
+        q[u][0] = r0[0];
+        q[u][1] = r0[1];
+        q[u][2] = r1[0];
+        q[u][3] = r1[1];
+      }
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (u < rem) {
+        a0 += q[u][0];
+        b0 += q[u][1];
+        a1 += q[u][2];
+        b1 += q[u][3];
+      }
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
