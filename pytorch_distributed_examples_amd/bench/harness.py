@@ -96,12 +96,21 @@ def parse_args(argv=None):
     ap.add_argument("--no-graph", action="store_true", help="run the step eagerly (no hipGraph capture)")
     ap.add_argument("--graph-steps", type=int, default=0,
                     help="consecutive training steps recorded into one hipGraph (each reads its own batch); "
-                         "0 = auto: the largest divisor of --steps up to 50, so the timed steps are whole replays")
+                         "0 = auto: the largest divisor of --steps up to 50 -- and up to --warmup when that still "
+                         "leaves >= 4 steps per graph -- so the timed steps are whole replays of a graph the warmup "
+                         "already replayed")
     ap.add_argument("--generic", action="store_true", help="CNN / MLP: layer-by-layer autograd kernels instead of the fused step")
     ap.add_argument("--device", default="auto", choices=["auto", "cpu"], help="cpu: contract/plumbing check only")
     args = ap.parse_args(argv)
     if args.graph_steps <= 0:
-        args.graph_steps = max(d for d in range(1, min(50, max(1, args.steps)) + 1) if args.steps % d == 0)
+        def divisor_upto(cap):
+            return max(d for d in range(1, max(1, min(cap, args.steps)) + 1) if args.steps % d == 0)
+        # a group the warmup replays at least once: the FIRST replay of a freshly captured multi-step graph ran
+        # ~0.1 ms slow in half of the processes (driver config, 20 / 5: 0.0325 vs 0.0286 ms/step when the 20-step
+        # graph was first replayed inside the timed region, 0.0285-0.0288 with a 5-step graph the warmup had
+        # replayed; profiles/README.md r6ae)
+        g = divisor_upto(min(50, args.warmup))
+        args.graph_steps = g if g >= 4 else divisor_upto(50)
     if args.model == "resnet50_hybrid":
         args.model = "resnet50_pp"
     return args
