@@ -241,7 +241,9 @@ def test_hvd_cnn_world2_one_gpu_rehearsal(gpu):
     rec = _bench_json(res.stdout)
     eng = rec["config"]["engine"]
     assert rec["n_gpus"] == 2 and rec["config"]["hipgraph"], rec
-    assert eng["xgmi_batches"] >= 1 and eng["inplace_batches"] >= 1 and eng["inline_calls"] >= 20, eng
+    # (inline calls are recorded once per captured step: the multi-step graph's steps + the single-step graph)
+    assert eng["xgmi_batches"] >= 1 and eng["inplace_batches"] >= 1, eng
+    assert eng["inline_calls"] >= rec["config"]["steps_per_graph"] + 1, (eng, rec["config"]["steps_per_graph"])
     assert eng["string_gathers"] <= 3, eng  # broadcast_parameters + the first step only
     os.makedirs(os.path.join(repo, "gpurun_out"), exist_ok=True)
     with open(os.path.join(repo, "gpurun_out", "hvd_world2_rehearsal.json"), "w") as f:
