@@ -1,6 +1,8 @@
 // Stage-to-stage P2P channel over xGMI: see p2p_ring.h for the protocol.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <thread>
 #include <cstdlib>
 
 #include <algorithm>
@@ -179,7 +181,16 @@ P2PRing::~P2PRing() {
 
 std::string P2PRing::ipc_handle() const {
   hipIpcMemHandle_t h;
-  hip_check(hipIpcGetMemHandle(&h, local_), "hipIpcGetMemHandle");
+  // (the export has been seen to fail once, transiently, with "invalid argument" while several ranks shared one
+  // card and exported at the same moment: a few spaced attempts before giving up -- a host call, no GPU work)
+  hipError_t e = hipErrorUnknown;
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    e = hipIpcGetMemHandle(&h, local_);
+    if (e == hipSuccess) break;
+    (void)hipGetLastError();
+    std::this_thread::sleep_for(std::chrono::milliseconds(50 * (attempt + 1)));
+  }
+  hip_check(e, "hipIpcGetMemHandle");
   return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
 }
 

@@ -1,6 +1,8 @@
 // One-shot peer all-reduce over xGMI: see xgmi_allreduce.h for the protocol.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <thread>
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
@@ -346,7 +348,16 @@ XgmiAllreduce::~XgmiAllreduce() {
 
 std::string XgmiAllreduce::ipc_handle() const {
   hipIpcMemHandle_t h;
-  hip_check(hipIpcGetMemHandle(&h, local_), "hipIpcGetMemHandle");
+  // (the export has been seen to fail once, transiently, with "invalid argument" while several ranks shared one
+  // card and exported at the same moment: a few spaced attempts before giving up -- a host call, no GPU work)
+  hipError_t e = hipErrorUnknown;
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    e = hipIpcGetMemHandle(&h, local_);
+    if (e == hipSuccess) break;
+    (void)hipGetLastError();
+    std::this_thread::sleep_for(std::chrono::milliseconds(50 * (attempt + 1)));
+  }
+  hip_check(e, "hipIpcGetMemHandle");
   return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
 }
 
