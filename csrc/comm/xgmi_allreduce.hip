@@ -2,7 +2,10 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <deque>
+#include <mutex>
 #include <thread>
+#include <utility>
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
@@ -492,6 +495,27 @@ bool XgmiAllreduce::aborted() const {
   return host_ != nullptr && __atomic_load_n(host_ + kXgmiHostAbort, __ATOMIC_ACQUIRE) != 0u;
 }
 
+namespace {
+// Exported slot buffers of closed instances, freed only a few closes later: a peer may still have the buffer
+// mapped when this rank closes (the ranks close one after another, with no barrier -- a failure path must not
+// wait for dead peers), and a new instance allocated right away could reuse the freed range and export it while
+// that stale mapping is alive (observed: hipIpcGetMemHandle "invalid argument" on the next export, 4 ranks on one
+// card closing one communicator and opening the next).  Bounded: at most kRetired buffers stay allocated.
+constexpr size_t kRetired = 4;
+std::mutex g_retired_mu;
+std::deque<std::pair<int, void*>> g_retired;  // (device, buffer)
+void retire(int device, void* p) {
+  std::lock_guard<std::mutex> lk(g_retired_mu);
+  g_retired.emplace_back(device, p);
+  while (g_retired.size() > kRetired) {
+    (void)hipSetDevice(g_retired.front().first);
+    (void)hipFree(g_retired.front().second);
+    g_retired.pop_front();
+  }
+  (void)hipSetDevice(device);
+}
+}  // namespace
+
 void XgmiAllreduce::close() {
   if (local_ == nullptr) return;
   (void)hipSetDevice(device_);
@@ -499,7 +523,7 @@ void XgmiAllreduce::close() {
   for (int r = 0; r < size_; ++r)
     if (r != rank_ && peers_[r] != nullptr) (void)hipIpcCloseMemHandle(peers_[r]);
   peers_.clear();
-  (void)hipFree(local_);
+  retire(device_, local_);
   (void)hipFree(state_);
   if (host_ != nullptr) (void)hipHostFree(host_);
   local_ = nullptr;
