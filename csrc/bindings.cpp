@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -144,8 +145,8 @@ void resolve_pending(const optional<Tensor>& t) {
   if (t.has_value()) resolve_pending(*t);
 }
 int pending_conv_count() { return static_cast<int>(g_pending_conv.size()); }
-long g_bn_bwd_slab_uses = 0;  // BatchNorm backwards that summed a deferred dgrad's slabs (tests / diagnostics)
-long bn_bwd_slab_uses() { return g_bn_bwd_slab_uses; }
+std::atomic<long> g_bn_bwd_slab_uses{0};  // BatchNorm backwards that summed a deferred dgrad's slabs (tests)
+long bn_bwd_slab_uses() { return g_bn_bwd_slab_uses.load(); }
 
 void gemm_pair_begin() {
   TORCH_CHECK(!g_collect && g_pending.empty(), "gemm_pair_begin: a pair is already being collected");
