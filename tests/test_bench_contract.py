@@ -133,3 +133,16 @@ def test_bench_elastic_survives_killed_worker_cpu():
             rnd = int(ln.split()[2].rstrip(":"))
             pids.setdefault(rnd, set()).add(int(re.match(r"\d+", ln.split("(pid ")[1]).group(0)))
     assert pids[1] < pids[0], pids  # the survivor kept its process
+
+
+def test_auto_graph_group_is_replayed_by_the_warmup():
+    """The auto hipGraph step group is the largest divisor of --steps up to --warmup (when that keeps >= 4 steps per
+    graph), so the timed region never holds a graph's first replay; otherwise the largest divisor up to 50."""
+    from pytorch_distributed_examples_amd.bench.harness import parse_args
+
+    cases = {(20, 5): 5, (100, 20): 20, (300, 30): 30, (500, 50): 50, (7, 5): 7, (20, 2): 20, (20, 0): 20, (64, 12): 8}
+    for (steps, warmup), want in cases.items():
+        a = parse_args(["--steps", str(steps), "--warmup", str(warmup)])
+        assert a.graph_steps == want, (steps, warmup, a.graph_steps)
+        assert steps % a.graph_steps == 0
+    assert parse_args(["--steps", "20", "--warmup", "5", "--graph-steps", "10"]).graph_steps == 10
