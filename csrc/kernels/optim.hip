@@ -45,9 +45,13 @@ int optim_segment_blocks(int nchunks) {
 hipError_t multi_tensor_optim_range(int mode, const OptimEntry* dev_table, const OptimChunk* dev_chunks, int c_begin,
                                     int c_end, const float* dev_hparams, int* dev_step, int publish, hipStream_t s) {
   if (c_end <= c_begin) return hipSuccess;
-  // PDE_OPTIM_NT: 0 plain (default), 1 non-temporal loads + stores, 2 non-temporal loads + write-through stores
-  // (ld4/st4).  r4x, MLP Adam on its vector path: plain 31.2 us, write-through 35.1, non-temporal 37.9
-  static const int nt = std::getenv("PDE_OPTIM_NT") ? std::atoi(std::getenv("PDE_OPTIM_NT")) : 0;
+  // PDE_OPTIM_NT: 0 plain, 1 non-temporal loads + stores, 2 non-temporal loads + write-through stores (ld4/st4).
+  // Default by size: non-temporal from 8M elements per launch up (the state streams through once and would only
+  // evict the next step's operands from L2 / MALL), plain below.  r4x, MLP Adam (6M): plain 31.2 us, write-through
+  // 35.1, non-temporal 37.9; r6ah, ResNet stage 2 SGD (24M): non-temporal 1.2439 vs plain 1.2626 ms per step,
+  // ResNet-50 b32 (25.5M, write-through) level
+  static const int nt_env = std::getenv("PDE_OPTIM_NT") ? std::atoi(std::getenv("PDE_OPTIM_NT")) : -1;
+  const int nt = nt_env >= 0 ? nt_env : (static_cast<long>(c_end - c_begin) * kOptChunk >= (8L << 20) ? 1 : 0);
   dim3 grid(static_cast<unsigned>(optim_segment_blocks(c_end - c_begin)));
 #define PDE_OPT(M)                                                                                            \
   if (nt == 2)                                                                                                \
