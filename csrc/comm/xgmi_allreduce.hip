@@ -498,9 +498,9 @@ bool XgmiAllreduce::aborted() const {
 namespace {
 // Exported slot buffers of closed instances, freed only a few closes later: a peer may still have the buffer
 // mapped when this rank closes (the ranks close one after another, with no barrier -- a failure path must not
-// wait for dead peers), and a new instance allocated right away could reuse the freed range and export it while
-// that stale mapping is alive (observed: hipIpcGetMemHandle "invalid argument" on the next export, 4 ranks on one
-// card closing one communicator and opening the next).  Bounded: at most kRetired buffers stay allocated.
+// wait for dead peers), so a new instance allocated right away must not reuse the range while that stale mapping
+// is alive.  A precaution: the intermittent hipIpcGetMemHandle "invalid argument" seen with 4 processes sharing
+// one card after a close (tests/test_xgmi_twoshot_gpu.py) persisted with it.  At most kRetired buffers stay.
 constexpr size_t kRetired = 4;
 std::mutex g_retired_mu;
 std::deque<std::pair<int, void*>> g_retired;  // (device, buffer)
