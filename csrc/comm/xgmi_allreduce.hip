@@ -351,8 +351,8 @@ XgmiAllreduce::~XgmiAllreduce() {
 
 std::string XgmiAllreduce::ipc_handle() const {
   hipIpcMemHandle_t h;
-  // (the export has been seen to fail once, transiently, with "invalid argument" while several ranks shared one
-  // card and exported at the same moment: a few spaced attempts before giving up -- a host call, no GPU work)
+  // (a few spaced attempts before giving up -- a host call, no GPU work; the "invalid argument" seen with several
+  // processes sharing one card right after a close did not clear this way: see tests/test_xgmi_twoshot_gpu.py)
   hipError_t e = hipErrorUnknown;
   for (int attempt = 0; attempt < 4; ++attempt) {
     e = hipIpcGetMemHandle(&h, local_);
