@@ -108,8 +108,9 @@ class Trainer:
             from ..parallel.comm import data_plane
 
             self.fused = FusedCNN(self.model)
-            self.ddp = DistributedDataParallel(self.model, overlap=False, param_order="forward", comm=data_plane(ctx),
-                                               **(ddp_kwargs or {}))
+            # (the CNN's 87 KB of gradients is one one-shot bucket: no two-shot instance)
+            self.ddp = DistributedDataParallel(self.model, overlap=False, param_order="forward",
+                                               comm=data_plane(ctx, two_shot=False), **(ddp_kwargs or {}))
         elif fast:
             from ..models.mlp_fused import FusedMLP
             from ..parallel.comm import data_plane

@@ -258,7 +258,7 @@ def build_data_parallel(args, ctx, batch) -> Workload:
     # CNN's single 87 KB bucket)
     from ..parallel.comm import data_plane
 
-    comm = data_plane(ctx)
+    comm = data_plane(ctx, two_shot=args.model.startswith("resnet50"))  # (the MNIST nets' buckets are one-shot sized)
     nranks = _data_plane_check(ctx, getattr(comm, "rccl", comm))
     fused = None
     if args.model == "cnn" and not args.generic and on_gpu:

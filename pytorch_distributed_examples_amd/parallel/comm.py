@@ -14,7 +14,9 @@ from __future__ import annotations
 import os
 
 
-def data_plane(ctx, group=None):
+def data_plane(ctx, group=None, two_shot: bool = True):
+    """``two_shot=False``: no two-shot instance (a workload whose gradients all fit the one-shot's 1 MiB buckets --
+    the MNIST nets -- would only allocate and hand-shake it)."""
     if ctx.device.type != "cuda" or ctx.world_size <= 1 or ctx.backend != "nccl":
         return None
     from .rccl import StreamComm
@@ -26,7 +28,7 @@ def data_plane(ctx, group=None):
 
     xgmi2 = None
     single_node = int(os.environ.get("LOCAL_WORLD_SIZE", str(ctx.world_size))) == ctx.world_size
-    if single_node and os.environ.get("PDE_XGMI_TWOSHOT", "1") != "0":
+    if two_shot and single_node and os.environ.get("PDE_XGMI_TWOSHOT", "1") != "0":
         mb = float(os.environ.get("PDE_XGMI_TWOSHOT_MB", "64"))
         # (a longer peer-wait bound than the one-shot's 5 s: large buckets are first reduced after the first
         # backward, when ranks may still be far apart from their first-use initialisation)
